@@ -1,0 +1,244 @@
+// pybind11 module `_atpu`: the Python face of the native MI355X runtime.
+//
+// Device buffers are owned by PyTorch (caching allocator); kernels receive raw
+// device pointers and the hipStream_t of torch's current stream as integers,
+// so every launch is graph-capturable through torch.cuda.CUDAGraph (hipGraph).
+// Python-side wrappers with shape/dtype checks live in agent_tpu_amd/ops/.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "atpu/common.h"
+#include "atpu/csv.h"
+#include "atpu/kernels.h"
+#include "atpu/runtime.h"
+
+namespace py = pybind11;
+using namespace atpu;
+
+namespace {
+
+template <typename T>
+T* P(uintptr_t p) {
+  return reinterpret_cast<T*>(p);
+}
+hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+py::str decode(const std::string& s) {
+  PyObject* o = PyUnicode_DecodeUTF8(s.data(), static_cast<Py_ssize_t>(s.size()), "strict");
+  if (!o) throw py::error_already_set();
+  return py::reinterpret_steal<py::str>(o);
+}
+
+py::dict make_row(const std::vector<std::string>& header, const std::vector<std::string>& row) {
+  // csv.DictReader semantics: zip(fieldnames, row); extra -> key None (list);
+  // missing -> value None.
+  py::dict d;
+  const size_t nf = header.size(), nr = row.size();
+  for (size_t i = 0; i < std::min(nf, nr); ++i)
+    d[py::str(header[i])] = decode(row[i]);
+  if (nr > nf) {
+    py::list extra;
+    for (size_t i = nf; i < nr; ++i) extra.append(decode(row[i]));
+    d[py::none()] = extra;
+  } else {
+    for (size_t i = nr; i < nf; ++i) d[py::str(header[i])] = py::none();
+  }
+  return d;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_atpu, m) {
+  m.doc() = "agent_tpu_amd native runtime: gfx950 HIP kernels + C++ host runtime";
+  m.attr("ARCH") = "gfx950";
+
+  // ------------------------------------------------------------- kernels
+  m.def(
+      "gemm",
+      [](uintptr_t A, int lda, uintptr_t Bt, int ldb, uintptr_t C, int ldc, uintptr_t bias, uintptr_t R, int ldr, int M,
+         int N, int K, int epi, uintptr_t stream) {
+        GemmArgs g;
+        g.A = P<const bf16>(A); g.lda = lda; g.Bt = P<const bf16>(Bt); g.ldb = ldb; g.C = P<bf16>(C); g.ldc = ldc;
+        g.bias = P<const float>(bias); g.R = P<const bf16>(R); g.ldr = ldr; g.M = M; g.N = N; g.K = K; g.epi = epi;
+        gemm_bf16(g, S(stream));
+      },
+      "bf16 MFMA GEMM C = epi(A @ Bt^T)");
+  m.attr("EPI_BIAS") = static_cast<int>(kEpiBias);
+  m.attr("EPI_GELU") = static_cast<int>(kEpiGelu);
+  m.attr("EPI_TANH") = static_cast<int>(kEpiTanh);
+  m.attr("EPI_RESIDUAL") = static_cast<int>(kEpiResidual);
+
+  m.def("attention", [](uintptr_t qkv, uintptr_t lens, uintptr_t bias, uintptr_t out, int B, int Sq, int H, int D,
+                        float scale, uintptr_t stream) {
+    attention_fwd(P<const bf16>(qkv), P<const int32_t>(lens), P<const float>(bias), P<bf16>(out), B, Sq, H, D, scale,
+                  S(stream));
+  });
+  m.def("attention_strided", [](uintptr_t q, int ldq, uintptr_t k, int ldk, uintptr_t v, int ldv, uintptr_t out,
+                                int ldo, uintptr_t lens, uintptr_t bias, int B, int Sq, int Skv, int H, int D,
+                                float scale, int causal, uintptr_t stream) {
+    attention_fwd_strided(P<const bf16>(q), ldq, P<const bf16>(k), ldk, P<const bf16>(v), ldv, P<bf16>(out), ldo,
+                          P<const int32_t>(lens), P<const float>(bias), B, Sq, Skv, H, D, scale, causal, S(stream));
+  });
+  m.def("layernorm", [](uintptr_t x, uintptr_t res, uintptr_t g, uintptr_t b, uintptr_t out, int rows, int N,
+                        float eps, uintptr_t stream) {
+    layernorm_bf16(P<const bf16>(x), P<const bf16>(res), P<const float>(g), P<const float>(b), P<bf16>(out), rows, N,
+                   eps, S(stream));
+  });
+  m.def("rmsnorm", [](uintptr_t x, uintptr_t g, uintptr_t out, int rows, int N, float eps, uintptr_t stream) {
+    rmsnorm_bf16(P<const bf16>(x), P<const float>(g), P<bf16>(out), rows, N, eps, S(stream));
+  });
+  m.def("embed_layernorm", [](uintptr_t ids, uintptr_t tt, uintptr_t word, uintptr_t pos, uintptr_t type, uintptr_t g,
+                              uintptr_t b, uintptr_t out, int B, int Sq, int N, int vocab, float eps, uintptr_t stream) {
+    embed_layernorm(P<const int32_t>(ids), P<const int32_t>(tt), P<const bf16>(word), P<const bf16>(pos),
+                    P<const bf16>(type), P<const float>(g), P<const float>(b), P<bf16>(out), B, Sq, N, vocab, eps,
+                    S(stream));
+  });
+  m.def("embed_gather", [](uintptr_t ids, uintptr_t table, uintptr_t out, int tokens, int N, int vocab,
+                           uintptr_t stream) {
+    embed_gather(P<const int32_t>(ids), P<const bf16>(table), P<bf16>(out), tokens, N, vocab, S(stream));
+  });
+  m.def("tokenize", [](uintptr_t text, uintptr_t offsets, uintptr_t ids, uintptr_t lens, int B, int Sq, int vocab,
+                       int max_row_bytes, uintptr_t stream) {
+    tokenize_hash(P<const uint8_t>(text), P<const int32_t>(offsets), P<int32_t>(ids), P<int32_t>(lens), B, Sq, vocab,
+                  max_row_bytes, S(stream));
+  });
+  m.def("head_topk", [](uintptr_t pooled, int ldp, uintptr_t Wc, uintptr_t bc, uintptr_t logits, uintptr_t idx,
+                        uintptr_t score, int B, int N, int C, int k, uintptr_t stream) {
+    classify_head_topk(P<const bf16>(pooled), ldp, P<const bf16>(Wc), P<const float>(bc), P<float>(logits),
+                       P<int32_t>(idx), P<float>(score), B, N, C, k, S(stream));
+  });
+  m.def("reduce_stats_blocks", &reduce_stats_blocks);
+  m.def("reduce_stats_f64", [](uintptr_t x, int64_t n, uintptr_t partial, int blocks, uintptr_t stream) {
+    reduce_stats_f64(P<const double>(x), n, P<double>(partial), blocks, S(stream));
+  });
+  m.def("reduce_stats_f32", [](uintptr_t x, int64_t n, uintptr_t partial, int blocks, uintptr_t stream) {
+    reduce_stats_f32(P<const float>(x), n, P<double>(partial), blocks, S(stream));
+  });
+  m.def("reduce_stats_finalize", [](uintptr_t partial, int blocks, uintptr_t out, uintptr_t stream) {
+    reduce_stats_finalize(P<const double>(partial), blocks, P<double>(out), S(stream));
+  });
+
+  // ------------------------------------------------------- host runtime
+  m.def(
+      "tokenize_host",
+      [](py::array_t<uint8_t, py::array::c_style> text, py::array_t<int32_t, py::array::c_style> offsets, int Sq,
+         int vocab, int max_row_bytes) {
+        const int B = static_cast<int>(offsets.size()) - 1;
+        ATPU_CHECK(B >= 0, "tokenize_host: offsets must have B+1 entries");
+        py::array_t<int32_t> ids({B, Sq});
+        py::array_t<int32_t> lens(B);
+        {
+          py::gil_scoped_release nogil;
+          tokenize_host(text.data(), offsets.data(), ids.mutable_data(), lens.mutable_data(), B, Sq, vocab,
+                        max_row_bytes);
+        }
+        return py::make_tuple(ids, lens);
+      },
+      py::arg("text"), py::arg("offsets"), py::arg("seq_len"), py::arg("vocab"), py::arg("max_row_bytes"));
+
+  m.def("device_query", [] {
+    py::list out;
+    for (const auto& d : device_query()) {
+      py::dict x;
+      x["index"] = d.index; x["name"] = d.name; x["arch"] = d.arch; x["total_memory_bytes"] = d.total_bytes;
+      x["free_memory_bytes"] = d.free_bytes; x["compute_units"] = d.cus; x["clock_khz"] = d.clock_khz;
+      out.append(x);
+    }
+    return out;
+  });
+
+  py::class_<CsvTable, std::shared_ptr<CsvTable>>(m, "CsvTable")
+      .def(py::init([](const std::string& path) {
+             py::gil_scoped_release nogil;
+             return std::make_shared<CsvTable>(path);
+           }),
+           py::arg("path"))
+      .def_property_readonly("path", &CsvTable::path)
+      .def_property_readonly("num_rows", &CsvTable::num_rows)
+      .def_property_readonly("file_size", &CsvTable::file_size)
+      .def_property_readonly("mtime_ns", &CsvTable::mtime_ns)
+      .def_property_readonly("header",
+                             [](const CsvTable& t) {
+                               py::list h;
+                               for (const auto& s : t.header()) h.append(decode(s));
+                               return h;
+                             })
+      .def("column_index", &CsvTable::column_index)
+      .def("row",
+           [](const CsvTable& t, size_t i) {
+             std::vector<std::string> f;
+             t.parse_row(i, f);
+             py::list out;
+             for (const auto& s : f) out.append(decode(s));
+             return out;
+           })
+      .def("dict_rows",
+           [](const CsvTable& t, size_t start, size_t n) {
+             py::list out;
+             if (start >= t.num_rows()) return out;
+             n = std::min(n, t.num_rows() - start);
+             std::vector<std::string> f;
+             for (size_t r = start; r < start + n; ++r) {
+               t.parse_row(r, f);
+               out.append(make_row(t.header(), f));
+             }
+             return out;
+           })
+      .def("float_column",
+           [](const CsvTable& t, size_t start, size_t n, int col, int threads) {
+             if (start > t.num_rows()) start = t.num_rows();
+             n = std::min(n, t.num_rows() - start);
+             py::array_t<double> out(n);
+             {
+               py::gil_scoped_release nogil;
+               t.extract_doubles(start, n, col, out.mutable_data(), threads);
+             }
+             return out;
+           },
+           py::arg("start"), py::arg("n"), py::arg("col"), py::arg("threads") = 8)
+      .def("extract_column",
+           [](const CsvTable& t, size_t start, size_t n, int col, size_t max_bytes, int threads) {
+             if (start > t.num_rows()) start = t.num_rows();
+             n = std::min(n, t.num_rows() - start);
+             py::array_t<int32_t> offs(n + 1);
+             // capacity bound: each value is at most max_bytes
+             std::vector<uint8_t> buf(std::max<size_t>(1, n * max_bytes));
+             int64_t bytes;
+             {
+               py::gil_scoped_release nogil;
+               bytes = t.extract_column(start, n, col, buf.data(), buf.size(), offs.mutable_data(), max_bytes, threads);
+             }
+             py::array_t<uint8_t> text(bytes);
+             std::memcpy(text.mutable_data(), buf.data(), bytes);
+             return py::make_tuple(text, offs);
+           },
+           py::arg("start"), py::arg("n"), py::arg("col"), py::arg("max_bytes"), py::arg("threads") = 8);
+
+  py::class_<HostStager>(m, "HostStager")
+      .def(py::init<int, size_t, int>(), py::arg("slots"), py::arg("text_capacity"), py::arg("max_rows"))
+      .def("submit",
+           [](HostStager& s, int slot, std::shared_ptr<CsvTable> t, size_t start, size_t n, int col, size_t max_bytes,
+              int threads) { s.submit(slot, t.get(), start, n, col, max_bytes, threads); },
+           py::keep_alive<1, 3>())
+      .def("upload",
+           [](HostStager& s, int slot, uintptr_t dev_text, size_t cap, uintptr_t dev_off, uintptr_t copy_stream,
+              uintptr_t compute_stream) {
+             py::gil_scoped_release nogil;
+             return s.upload(slot, P<void>(dev_text), cap, P<void>(dev_off), S(copy_stream), S(compute_stream));
+           })
+      .def("wait",
+           [](HostStager& s, int slot) {
+             py::gil_scoped_release nogil;
+             return s.wait(slot);
+           })
+      .def("release", [](HostStager& s, int slot, uintptr_t stream) { s.release(slot, S(stream)); })
+      .def_property_readonly("slots", &HostStager::slots)
+      .def_property_readonly("text_capacity", &HostStager::text_capacity);
+}

@@ -1,0 +1,75 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+namespace atpu {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kWave = 64;  // CDNA wavefront width (never 32)
+
+#define ATPU_GLOBAL_AS __attribute__((address_space(1)))
+#define ATPU_LDS_AS __attribute__((address_space(3)))
+
+// Async 16-byte global -> LDS copy (global_load_lds_dwordx4). `lds` must be
+// wave-uniform: lane i lands at lds + 16*i.
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds) {
+  __builtin_amdgcn_global_load_lds((const ATPU_GLOBAL_AS void*)gsrc, (ATPU_LDS_AS void*)lds, 16, 0, 0);
+}
+
+__device__ __forceinline__ void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+__device__ __forceinline__ float bf2f(bf16 x) { return static_cast<float>(x); }
+__device__ __forceinline__ bf16 f2bf(float x) { return static_cast<bf16>(x); }
+
+// Bijective XCD-aware block remap (guide §5 "XCD swizzle must be bijective"):
+// blocks that the dispatcher places on one XCD (b % 8 equal) get a contiguous
+// range of logical tile ids, so neighbouring tiles share that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int b, int nblocks) {
+  const int q = nblocks / 8, r = nblocks % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+}  // namespace atpu
+
+#define ATPU_HIP_CHECK(expr)                                                              \
+  do {                                                                                    \
+    hipError_t _e = (expr);                                                               \
+    if (_e != hipSuccess)                                                                 \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__));                \
+  } while (0)
+
+#define ATPU_CHECK(cond, msg)                                                   \
+  do {                                                                          \
+    if (!(cond)) throw std::invalid_argument(std::string("atpu: ") + (msg));    \
+  } while (0)

@@ -1,0 +1,88 @@
+// Host-side launch API for every hand-written gfx950 kernel in csrc/kernels.
+// All launchers are asynchronous on the given stream and graph-capturable
+// (no allocation, no synchronisation inside).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace atpu {
+
+typedef __bf16 bf16;
+
+// ---------------------------------------------------------------- GEMM (K3/K5/K6)
+enum GemmEpilogue : int {
+  kEpiBias = 1,
+  kEpiGelu = 2,
+  kEpiTanh = 4,
+  kEpiResidual = 8,
+};
+
+struct GemmArgs {
+  const bf16* A = nullptr;  // [M, K] row-major, leading dim lda
+  int lda = 0;
+  const bf16* Bt = nullptr;  // [N, K] row-major (nn.Linear.weight layout)
+  int ldb = 0;
+  bf16* C = nullptr;  // [M, N], leading dim ldc
+  int ldc = 0;
+  const float* bias = nullptr;  // [N] fp32
+  const bf16* R = nullptr;      // residual [M, N], leading dim ldr
+  int ldr = 0;
+  int M = 0, N = 0, K = 0;
+  int epi = 0;
+};
+void gemm_bf16(const GemmArgs& g, hipStream_t stream);
+
+// ------------------------------------------------------------- attention (K4)
+// qkv: [B*S, 3*H*D] packed per token as [q(H*D) | k(H*D) | v(H*D)];
+// lens: [B] valid key count per row (keys >= len masked); bias: optional
+// additive fp32 [H, S, S] (T5 relative-position bias), may be null.
+// out: [B*S, H*D]. D must be 64; S <= 512.
+void attention_fwd(const bf16* qkv, const int32_t* lens, const float* bias, bf16* out, int B, int S, int H,
+                   int D, float scale, hipStream_t stream);
+
+// ------------------------------------------------------- normalisation (K2/K6b)
+// out = LN(x (+ res)) * gamma + beta, rows of width N; fp32 statistics.
+void layernorm_bf16(const bf16* x, const bf16* res, const float* gamma, const float* beta, bf16* out, int rows,
+                    int N, float eps, hipStream_t stream);
+// out = x * rsqrt(mean(x^2) + eps) * gamma (T5 RMSNorm, no mean subtraction)
+void rmsnorm_bf16(const bf16* x, const float* gamma, bf16* out, int rows, int N, float eps,
+                  hipStream_t stream);
+// Fused BERT embedding: out[t] = LN(word[ids[t]] + pos[t % S] + type[tt[t]]).
+void embed_layernorm(const int32_t* ids, const int32_t* type_ids, const bf16* word, const bf16* pos,
+                     const bf16* type, const float* gamma, const float* beta, bf16* out, int B, int S, int N,
+                     int vocab, float eps, hipStream_t stream);
+// Plain embedding gather (T5 encoder/decoder input): out[t] = table[ids[t]] * scale
+void embed_gather(const int32_t* ids, const bf16* table, bf16* out, int tokens, int N, int vocab,
+                  hipStream_t stream);
+
+// ----------------------------------------------------------- tokenizer (K1)
+// Deterministic hash word-piece tokenizer (see agent_tpu_amd/tokenizer.py for
+// the exact spec and the CPU twin). text: packed UTF-8 bytes; offsets[B+1].
+void tokenize_hash(const uint8_t* text, const int32_t* offsets, int32_t* ids, int32_t* lens, int B, int S,
+                   int vocab, int max_row_bytes, hipStream_t stream);
+
+// ------------------------------------------------ classify head + top-k (K7)
+// logits[b, c] = pooled[b] · Wc[c] + bc[c]; probs = softmax(logits);
+// writes top-k (descending prob, ties -> lower index) and the full logits.
+void classify_head_topk(const bf16* pooled, int ldp, const bf16* Wc, const float* bc, float* logits,
+                        int32_t* topk_idx, float* topk_score, int B, int N, int C, int k, hipStream_t stream);
+
+// ---------------------------------------------------- streaming reduce (K12)
+// partial[4*blocks] doubles {count, sum, min, max}; finalize on host or via
+// reduce_stats_finalize into out[4].
+int reduce_stats_blocks(int64_t n);
+void reduce_stats_f64(const double* x, int64_t n, double* partial, int blocks, hipStream_t stream);
+void reduce_stats_f32(const float* x, int64_t n, double* partial, int blocks, hipStream_t stream);
+void reduce_stats_finalize(const double* partial, int blocks, double* out, hipStream_t stream);
+
+}  // namespace atpu
+
+namespace atpu {
+// General strided form (T5 cross/causal attention): q rows b*Sq+t, k/v rows
+// b*Skv+t; head h at column h*D of each row.
+void attention_fwd_strided(const bf16* q, int ldq, const bf16* k, int ldk, const bf16* v, int ldv, bf16* out,
+                           int ldo, const int32_t* lens, const float* bias, int B, int Sq, int Skv, int H, int D,
+                           float scale, int causal, hipStream_t stream);
+}  // namespace atpu

@@ -1,0 +1,86 @@
+// Host runtime pieces: tokenizer twin, device query, CSV -> pinned -> device
+// staging pipeline.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <condition_variable>
+#include <cstdint>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "atpu/csv.h"
+
+namespace atpu {
+
+// Host twin of the K1 GPU tokenizer (identical output, see tokenize.hip).
+void tokenize_host(const uint8_t* text, const int32_t* offsets, int32_t* ids, int32_t* lens, int B, int S, int vocab,
+                   int max_row_bytes);
+
+struct DeviceInfo {
+  int index;
+  std::string name;
+  std::string arch;
+  size_t total_bytes;
+  size_t free_bytes;
+  int cus;
+  int clock_khz;
+};
+std::vector<DeviceInfo> device_query();
+
+// Double-buffered CSV column -> pinned host -> device pipeline.
+//  submit(slot, ...)  : background thread extracts rows into slot's pinned
+//                       buffer (after the slot's previous H2D has finished).
+//  upload(slot, ...)  : waits for extraction, hipMemcpyAsync's text+offsets on
+//                       the copy stream (after the compute stream released the
+//                       slot's device buffers), and makes the compute stream
+//                       wait for the copy.
+//  release(slot, s)   : records on the compute stream that the device buffers
+//                       of `slot` have been consumed.
+class HostStager {
+ public:
+  HostStager(int slots, size_t text_capacity, int max_rows);
+  ~HostStager();
+  HostStager(const HostStager&) = delete;
+  HostStager& operator=(const HostStager&) = delete;
+
+  void submit(int slot, const CsvTable* table, size_t start, size_t n, int col, size_t max_bytes, int threads);
+  // returns {rows, bytes}
+  std::pair<int64_t, int64_t> upload(int slot, void* dev_text, size_t dev_text_cap, void* dev_offsets,
+                                     hipStream_t copy_stream, hipStream_t compute_stream);
+  void release(int slot, hipStream_t compute_stream);
+  int slots() const { return static_cast<int>(slots_.size()); }
+  size_t text_capacity() const { return text_cap_; }
+  // host view of a slot's staged data (valid after upload/wait)
+  const uint8_t* host_text(int slot) const { return slots_[slot].text; }
+  const int32_t* host_offsets(int slot) const { return slots_[slot].offsets; }
+  std::pair<int64_t, int64_t> wait(int slot);
+
+ private:
+  struct Slot {
+    uint8_t* text = nullptr;
+    int32_t* offsets = nullptr;
+    hipEvent_t copied = nullptr;    // H2D done -> pinned buffer reusable
+    hipEvent_t consumed = nullptr;  // compute done with device buffers
+    bool has_copy = false;
+    bool has_consume = false;
+    int64_t rows = 0, bytes = 0;
+    bool pending = false;
+    std::string error;
+  };
+  void worker();
+
+  std::vector<Slot> slots_;
+  size_t text_cap_;
+  int max_rows_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<std::function<void()>> queue_;
+  bool stop_ = false;
+  std::thread thread_;
+};
+
+}  // namespace atpu

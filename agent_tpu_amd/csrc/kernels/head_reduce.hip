@@ -1,0 +1,171 @@
+// Classify head + softmax + top-k and the streaming
+// count/sum/min/max reduction behind risk_accumulate (K12).
+#include "atpu/common.h"
+#include "atpu/kernels.h"
+
+#include <algorithm>
+#include <cfloat>
+
+namespace atpu {
+namespace {
+
+constexpr int kMaxClasses = 4096;
+constexpr int kMaxK = 64;
+
+// One wave per row. pooled row staged in LDS; lane j owns classes j, j+64, ...
+// Top-k = k rounds of a wave-wide argmax on (prob desc, index asc), so ties
+// resolve to the lower class index deterministically (ref _topk:
+// /root/reference/ops/map_classify_tpu.py:15-19 orders by descending score).
+__global__ __launch_bounds__(64) void head_topk_kernel(const bf16* __restrict__ pooled, int ldp,
+                                                       const bf16* __restrict__ Wc, const float* __restrict__ bc,
+                                                       float* __restrict__ logits, int32_t* __restrict__ topk_idx,
+                                                       float* __restrict__ topk_score, int N, int C, int k) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* x = reinterpret_cast<float*>(smem);       // [N]
+  float* z = x + N;                                 // [C]
+  const int lane = threadIdx.x, row = blockIdx.x;
+  const bf16* p = pooled + (size_t)row * ldp;
+  for (int i = lane; i < N; i += 64) x[i] = bf2f(p[i]);
+  __syncthreads();
+  float mx = -FLT_MAX;
+  for (int c = lane; c < C; c += 64) {
+    const bf16* w = Wc + (size_t)c * N;
+    float acc = bc ? bc[c] : 0.f;
+    for (int i = 0; i < N; i += 8) {
+      const bf16x8 wv = *reinterpret_cast<const bf16x8*>(w + i);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc += x[i + e] * bf2f(wv[e]);
+    }
+    z[c] = acc;
+    logits[(size_t)row * C + c] = acc;
+    mx = fmaxf(mx, acc);
+  }
+  mx = wave_max(mx);
+  float se = 0.f;
+  for (int c = lane; c < C; c += 64) se += __expf(z[c] - mx);
+  se = wave_sum(se);
+  const float inv = 1.f / se;
+  __syncthreads();
+  for (int r = 0; r < k; ++r) {
+    float best = -FLT_MAX;
+    int bi = 0x7fffffff;
+    for (int c = lane; c < C; c += 64) {
+      const float v = z[c];
+      if (v > best || (v == best && c < bi)) { best = v; bi = c; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+    }
+    if (lane == 0) {
+      topk_idx[(size_t)row * k + r] = bi;
+      topk_score[(size_t)row * k + r] = __expf(best - mx) * inv;
+      z[bi] = -FLT_MAX;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- K12
+constexpr int kRedThreads = 256;
+
+template <typename T>
+__global__ __launch_bounds__(kRedThreads) void reduce_stats_kernel(const T* __restrict__ x, int64_t n,
+                                                                   double* __restrict__ partial) {
+  __shared__ double sh[4][kRedThreads / 64];
+  double cnt = 0, sum = 0, comp = 0, lo = DBL_MAX, hi = -DBL_MAX;
+  const int64_t stride = (int64_t)gridDim.x * kRedThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kRedThreads + threadIdx.x; i < n; i += stride) {
+    const double v = (double)x[i];
+    // Neumaier-compensated running sum: keeps fp64 sums within an ulp or two of
+    // the reference's sequential Python sum for well-conditioned data
+    const double t = sum + v;
+    comp += fabs(sum) >= fabs(v) ? (sum - t) + v : (v - t) + sum;
+    sum = t;
+    lo = fmin(lo, v);
+    hi = fmax(hi, v);
+    cnt += 1;
+  }
+  sum += comp;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    cnt += __shfl_xor(cnt, o, 64);
+    sum += __shfl_xor(sum, o, 64);
+    lo = fmin(lo, __shfl_xor(lo, o, 64));
+    hi = fmax(hi, __shfl_xor(hi, o, 64));
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[0][w] = cnt; sh[1][w] = sum; sh[2][w] = lo; sh[3][w] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < kRedThreads / 64; ++i) {
+      sh[0][0] += sh[0][i]; sh[1][0] += sh[1][i];
+      sh[2][0] = fmin(sh[2][0], sh[2][i]); sh[3][0] = fmax(sh[3][0], sh[3][i]);
+    }
+    partial[4 * blockIdx.x + 0] = sh[0][0];
+    partial[4 * blockIdx.x + 1] = sh[1][0];
+    partial[4 * blockIdx.x + 2] = sh[2][0];
+    partial[4 * blockIdx.x + 3] = sh[3][0];
+  }
+}
+
+__global__ __launch_bounds__(64) void reduce_finalize_kernel(const double* __restrict__ partial, int blocks,
+                                                             double* __restrict__ out) {
+  double cnt = 0, sum = 0, lo = DBL_MAX, hi = -DBL_MAX;
+  for (int i = threadIdx.x; i < blocks; i += 64) {
+    cnt += partial[4 * i];
+    sum += partial[4 * i + 1];
+    lo = fmin(lo, partial[4 * i + 2]);
+    hi = fmax(hi, partial[4 * i + 3]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    cnt += __shfl_xor(cnt, o, 64);
+    sum += __shfl_xor(sum, o, 64);
+    lo = fmin(lo, __shfl_xor(lo, o, 64));
+    hi = fmax(hi, __shfl_xor(hi, o, 64));
+  }
+  if (threadIdx.x == 0) {
+    out[0] = cnt; out[1] = sum; out[2] = lo; out[3] = hi;
+  }
+}
+
+}  // namespace
+
+void classify_head_topk(const bf16* pooled, int ldp, const bf16* Wc, const float* bc, float* logits,
+                        int32_t* topk_idx, float* topk_score, int B, int N, int C, int k, hipStream_t stream) {
+  ATPU_CHECK(C >= 1 && C <= kMaxClasses, "head: 1 <= classes <= 4096");
+  ATPU_CHECK(k >= 1 && k <= C && k <= kMaxK, "head: 1 <= k <= min(C, 64)");
+  ATPU_CHECK(N % 8 == 0, "head: hidden size must be a multiple of 8");
+  if (B <= 0) return;
+  const size_t shm = (size_t)(N + C) * sizeof(float);
+  hipLaunchKernelGGL(head_topk_kernel, dim3(B), dim3(64), shm, stream, pooled, ldp, Wc, bc, logits, topk_idx,
+                     topk_score, N, C, k);
+  ATPU_HIP_CHECK(hipGetLastError());
+}
+
+int reduce_stats_blocks(int64_t n) {
+  const int64_t want = (n + kRedThreads * 16 - 1) / (kRedThreads * 16);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(want, 2048));
+}
+
+void reduce_stats_f64(const double* x, int64_t n, double* partial, int blocks, hipStream_t stream) {
+  hipLaunchKernelGGL(reduce_stats_kernel<double>, dim3(blocks), dim3(kRedThreads), 0, stream, x, n, partial);
+  ATPU_HIP_CHECK(hipGetLastError());
+}
+
+void reduce_stats_f32(const float* x, int64_t n, double* partial, int blocks, hipStream_t stream) {
+  hipLaunchKernelGGL(reduce_stats_kernel<float>, dim3(blocks), dim3(kRedThreads), 0, stream, x, n, partial);
+  ATPU_HIP_CHECK(hipGetLastError());
+}
+
+void reduce_stats_finalize(const double* partial, int blocks, double* out, hipStream_t stream) {
+  hipLaunchKernelGGL(reduce_finalize_kernel, dim3(1), dim3(64), 0, stream, partial, blocks, out);
+  ATPU_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace atpu

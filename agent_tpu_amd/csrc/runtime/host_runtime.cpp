@@ -1,0 +1,196 @@
+// Host runtime: tokenizer twin, HIP device query, pinned double-buffer stager.
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+
+#include "atpu/common.h"
+#include "atpu/runtime.h"
+
+namespace atpu {
+
+// ------------------------------------------------------------ tokenizer twin
+namespace {
+constexpr uint32_t kBasis = 2166136261u, kPrime = 16777619u;
+constexpr int kPieceBytes = 24;
+inline int cls_of(uint32_t c) {
+  if (c == 0x20 || (c >= 0x09 && c <= 0x0D) || c < 0x20 || c == 0x7F) return 0;
+  if ((c >= 0x21 && c <= 0x2F) || (c >= 0x3A && c <= 0x40) || (c >= 0x5B && c <= 0x60) || (c >= 0x7B && c <= 0x7E))
+    return 1;
+  return 2;
+}
+inline uint32_t step(uint32_t h, uint32_t c) {
+  if (c >= 'A' && c <= 'Z') c += 32;
+  return (h ^ c) * kPrime;
+}
+}  // namespace
+
+void tokenize_host(const uint8_t* text, const int32_t* offsets, int32_t* ids, int32_t* lens, int B, int S, int vocab,
+                   int max_row_bytes) {
+  if (S < 2 || vocab <= 1000) throw std::invalid_argument("tokenize_host: bad S/vocab");
+  const uint32_t mod = static_cast<uint32_t>(vocab - 1000);
+  const uint32_t cont = step(step(kBasis, '#'), '#');
+  const int cap = S - 2;
+  for (int r = 0; r < B; ++r) {
+    const uint8_t* p = text + offsets[r];
+    const int n = std::min(offsets[r + 1] - offsets[r], max_row_bytes);
+    int32_t* out = ids + static_cast<size_t>(r) * S;
+    int nt = 0;
+    for (int i = 0; i < n && nt < cap;) {
+      const int c = cls_of(p[i]);
+      if (c == 0) { ++i; continue; }
+      if (c == 1) {
+        out[1 + nt++] = static_cast<int32_t>(1000u + step(kBasis, p[i]) % mod);
+        ++i;
+        continue;
+      }
+      int j = i;
+      while (j < n && cls_of(p[j]) == 2) ++j;
+      for (int b0 = i, piece = 0; b0 < j && nt < cap; b0 += kPieceBytes, ++piece) {
+        uint32_t h = piece == 0 ? kBasis : cont;
+        for (int k = b0; k < std::min(j, b0 + kPieceBytes); ++k) h = step(h, p[k]);
+        out[1 + nt++] = static_cast<int32_t>(1000u + h % mod);
+      }
+      i = j;
+    }
+    out[0] = 101;
+    out[1 + nt] = 102;
+    for (int j = nt + 2; j < S; ++j) out[j] = 0;
+    lens[r] = nt + 2;
+  }
+}
+
+// -------------------------------------------------------------- device query
+std::vector<DeviceInfo> device_query() {
+  std::vector<DeviceInfo> out;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return out;
+  }
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  for (int i = 0; i < n; ++i) {
+    hipDeviceProp_t prop{};
+    if (hipGetDeviceProperties(&prop, i) != hipSuccess) continue;
+    DeviceInfo d{};
+    d.index = i;
+    d.name = prop.name;
+    d.arch = prop.gcnArchName;
+    d.total_bytes = prop.totalGlobalMem;
+    d.cus = prop.multiProcessorCount;
+    d.clock_khz = prop.clockRate;
+    size_t fr = 0, tot = 0;
+    if (hipSetDevice(i) == hipSuccess && hipMemGetInfo(&fr, &tot) == hipSuccess) d.free_bytes = fr;
+    out.push_back(d);
+  }
+  (void)hipSetDevice(cur);
+  return out;
+}
+
+// --------------------------------------------------------------- HostStager
+HostStager::HostStager(int slots, size_t text_capacity, int max_rows)
+    : slots_(slots), text_cap_(text_capacity), max_rows_(max_rows) {
+  ATPU_CHECK(slots >= 1 && slots <= 8, "stager: 1..8 slots");
+  for (auto& s : slots_) {
+    ATPU_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&s.text), text_cap_, hipHostMallocDefault));
+    ATPU_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&s.offsets), sizeof(int32_t) * (max_rows_ + 1),
+                                 hipHostMallocDefault));
+    ATPU_HIP_CHECK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
+    ATPU_HIP_CHECK(hipEventCreateWithFlags(&s.consumed, hipEventDisableTiming));
+  }
+  thread_ = std::thread([this] { worker(); });
+}
+
+HostStager::~HostStager() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  if (thread_.joinable()) thread_.join();
+  for (auto& s : slots_) {
+    if (s.copied) (void)hipEventSynchronize(s.copied), (void)hipEventDestroy(s.copied);
+    if (s.consumed) (void)hipEventDestroy(s.consumed);
+    if (s.text) (void)hipHostFree(s.text);
+    if (s.offsets) (void)hipHostFree(s.offsets);
+  }
+}
+
+void HostStager::worker() {
+  for (;;) {
+    std::function<void()> job;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [this] { return stop_ || !queue_.empty(); });
+      if (stop_ && queue_.empty()) return;
+      job = std::move(queue_.front());
+      queue_.erase(queue_.begin());
+    }
+    job();
+  }
+}
+
+void HostStager::submit(int slot, const CsvTable* table, size_t start, size_t n, int col, size_t max_bytes,
+                        int threads) {
+  ATPU_CHECK(slot >= 0 && slot < slots(), "stager: bad slot");
+  ATPU_CHECK(n <= static_cast<size_t>(max_rows_), "stager: too many rows for slot");
+  std::lock_guard<std::mutex> g(mu_);
+  Slot& s = slots_[slot];
+  ATPU_CHECK(!s.pending, "stager: slot already pending");
+  s.pending = true;
+  s.error.clear();
+  queue_.push_back([this, slot, table, start, n, col, max_bytes, threads] {
+    Slot& sl = slots_[slot];
+    std::string err;
+    int64_t rows = 0, bytes = 0;
+    try {
+      if (sl.has_copy) ATPU_HIP_CHECK(hipEventSynchronize(sl.copied));  // pinned buffer free again
+      const size_t have = table->num_rows() > start ? table->num_rows() - start : 0;
+      rows = static_cast<int64_t>(std::min(n, have));
+      bytes = table->extract_column(start, rows, col, sl.text, text_cap_, sl.offsets, max_bytes, threads);
+      if (bytes < 0) err = "stager: text capacity exceeded";
+    } catch (const std::exception& e) {
+      err = e.what();
+    }
+    {
+      std::lock_guard<std::mutex> g2(mu_);
+      sl.rows = rows;
+      sl.bytes = bytes;
+      sl.error = err;
+      sl.pending = false;
+    }
+    cv_.notify_all();
+  });
+  cv_.notify_all();
+}
+
+std::pair<int64_t, int64_t> HostStager::wait(int slot) {
+  ATPU_CHECK(slot >= 0 && slot < slots(), "stager: bad slot");
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_.wait(lk, [&] { return !slots_[slot].pending; });
+  if (!slots_[slot].error.empty()) throw std::runtime_error(slots_[slot].error);
+  return {slots_[slot].rows, slots_[slot].bytes};
+}
+
+std::pair<int64_t, int64_t> HostStager::upload(int slot, void* dev_text, size_t dev_text_cap, void* dev_offsets,
+                                               hipStream_t copy_stream, hipStream_t compute_stream) {
+  auto [rows, bytes] = wait(slot);
+  Slot& s = slots_[slot];
+  ATPU_CHECK(static_cast<size_t>(bytes) <= dev_text_cap, "stager: device text buffer too small");
+  if (s.has_consume) ATPU_HIP_CHECK(hipStreamWaitEvent(copy_stream, s.consumed, 0));
+  if (bytes > 0) ATPU_HIP_CHECK(hipMemcpyAsync(dev_text, s.text, bytes, hipMemcpyHostToDevice, copy_stream));
+  ATPU_HIP_CHECK(
+      hipMemcpyAsync(dev_offsets, s.offsets, sizeof(int32_t) * (rows + 1), hipMemcpyHostToDevice, copy_stream));
+  ATPU_HIP_CHECK(hipEventRecord(s.copied, copy_stream));
+  s.has_copy = true;
+  if (compute_stream != copy_stream) ATPU_HIP_CHECK(hipStreamWaitEvent(compute_stream, s.copied, 0));
+  return {rows, bytes};
+}
+
+void HostStager::release(int slot, hipStream_t compute_stream) {
+  ATPU_CHECK(slot >= 0 && slot < slots(), "stager: bad slot");
+  ATPU_HIP_CHECK(hipEventRecord(slots_[slot].consumed, compute_stream));
+  slots_[slot].has_consume = true;
+}
+
+}  // namespace atpu

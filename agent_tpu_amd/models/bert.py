@@ -1,0 +1,200 @@
+"""BERT sequence classifier on the hand-written gfx950 kernels.
+
+Replaces the reference's opaque Edge-TPU ``interpreter.invoke()``
+(``/root/reference/ops/map_classify_tpu.py:71-74``) with an explicit encoder:
+
+    ids --K2 embed+LN--> h
+    repeat L: qkv = h·Wqkvᵀ+b (K3) -> ctx = attn(qkv, lens) (K4)
+              h1  = LN(ctx·Woᵀ+b+h)  (K5 + K6b)
+              h   = LN(gelu(h1·W1ᵀ+b1)·W2ᵀ+b2+h1)  (K6, K5 + K6b)
+    pooled = tanh(h[:,0]·Wpᵀ+bp) (GEMM, tanh epilogue, strided CLS rows)
+    logits/top-k = head (K7)
+
+Parameter names/layouts mirror HF ``BertForSequenceClassification`` (Linear
+weights are ``[out, in]``, exactly the GEMM's ``Bt`` operand), so
+:func:`from_hf_state_dict` is a rename plus the Q/K/V concat — used by the
+parity test against transformers with identical random weights.
+"""
+from __future__ import annotations
+
+import dataclasses
+from dataclasses import dataclass
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from .. import ops
+from .params import ParamPack
+
+
+@dataclass(frozen=True)
+class BertConfig:
+    vocab_size: int = 30522
+    hidden: int = 768
+    layers: int = 12
+    heads: int = 12
+    intermediate: int = 3072
+    max_positions: int = 512
+    type_vocab: int = 2
+    num_labels: int = 2
+    eps: float = 1e-12
+
+    @property
+    def head_dim(self) -> int:
+        return self.hidden // self.heads
+
+    def param_count(self) -> int:
+        H, I, L = self.hidden, self.intermediate, self.layers
+        emb = (self.vocab_size + self.max_positions + self.type_vocab) * H + 2 * H
+        layer = 4 * H * H + 4 * H + 2 * H * I + I + H + 4 * H
+        head = H * H + H + self.num_labels * H + self.num_labels
+        return emb + L * layer + head
+
+    def flops_per_row(self, seq_len: int) -> float:
+        """Forward FLOPs for one row of ``seq_len`` tokens (GEMMs + attention)."""
+        H, I, L, S = self.hidden, self.intermediate, self.layers, seq_len
+        gemm = 2 * S * (4 * H * H + 2 * H * I) * L
+        attn = 4 * S * S * H * L
+        head = 2 * (H * H + H * self.num_labels)
+        return float(gemm + attn + head)
+
+
+PRESETS: Dict[str, BertConfig] = {
+    "bert-base": BertConfig(),
+    "bert-large": BertConfig(hidden=1024, layers=24, heads=16, intermediate=4096),
+    "bert-tiny": BertConfig(vocab_size=4096, hidden=256, layers=2, heads=4, intermediate=1024, max_positions=512),
+}
+
+
+def config_for(name: str, **overrides) -> BertConfig:
+    if name not in PRESETS:
+        raise ValueError(f"unknown BERT preset {name!r}; known: {sorted(PRESETS)}")
+    return dataclasses.replace(PRESETS[name], **overrides)
+
+
+def param_specs(cfg: BertConfig):
+    H, I, C = cfg.hidden, cfg.intermediate, cfg.num_labels
+    bf, f32 = torch.bfloat16, torch.float32
+    yield "emb.word", (cfg.vocab_size, H), bf
+    yield "emb.pos", (cfg.max_positions, H), bf
+    yield "emb.type", (cfg.type_vocab, H), bf
+    yield "emb.ln_g", (H,), f32
+    yield "emb.ln_b", (H,), f32
+    for i in range(cfg.layers):
+        p = f"l{i}."
+        yield p + "qkv_w", (3 * H, H), bf
+        yield p + "qkv_b", (3 * H,), f32
+        yield p + "o_w", (H, H), bf
+        yield p + "o_b", (H,), f32
+        yield p + "ln1_g", (H,), f32
+        yield p + "ln1_b", (H,), f32
+        yield p + "f1_w", (I, H), bf
+        yield p + "f1_b", (I,), f32
+        yield p + "f2_w", (H, I), bf
+        yield p + "f2_b", (H,), f32
+        yield p + "ln2_g", (H,), f32
+        yield p + "ln2_b", (H,), f32
+    yield "pool_w", (H, H), bf
+    yield "pool_b", (H,), f32
+    yield "cls_w", (C, H), bf
+    yield "cls_b", (C,), f32
+
+
+def init_random(cfg: BertConfig, seed: int = 0, std: float = 0.02, bias_std: float = 0.0) -> ParamPack:
+    """Seeded random init on the CPU (bit-identical on every host/rank).
+
+    Matches HF's BERT init scheme (N(0, 0.02) weights, LN γ=1/β=0, zero biases)
+    unless ``bias_std`` > 0, which tests use to exercise the bias epilogues.
+    """
+    pack = ParamPack(param_specs(cfg))
+    g = torch.Generator().manual_seed(int(seed))
+    for name in pack.names():
+        t = pack[name]
+        if name.endswith("ln_g") or name.endswith("ln1_g") or name.endswith("ln2_g"):
+            t.fill_(1.0)
+        elif name.endswith("ln_b") or name.endswith("ln1_b") or name.endswith("ln2_b"):
+            t.zero_()
+        elif name.endswith("_b"):
+            if bias_std > 0:
+                t.copy_(torch.randn(t.shape, generator=g) * bias_std)
+            else:
+                t.zero_()
+        else:
+            t.copy_((torch.randn(t.shape, generator=g) * std).to(t.dtype))
+    return pack
+
+
+def from_hf_state_dict(cfg: BertConfig, sd: Dict[str, torch.Tensor]) -> ParamPack:
+    """Build a pack from a transformers ``BertForSequenceClassification`` state dict."""
+    pack = ParamPack(param_specs(cfg))
+
+    def put(name, t):
+        pack[name].copy_(t.to(pack[name].dtype).view(pack[name].shape))
+
+    put("emb.word", sd["bert.embeddings.word_embeddings.weight"])
+    put("emb.pos", sd["bert.embeddings.position_embeddings.weight"])
+    put("emb.type", sd["bert.embeddings.token_type_embeddings.weight"])
+    put("emb.ln_g", sd["bert.embeddings.LayerNorm.weight"])
+    put("emb.ln_b", sd["bert.embeddings.LayerNorm.bias"])
+    for i in range(cfg.layers):
+        b = f"bert.encoder.layer.{i}."
+        a = b + "attention."
+        put(f"l{i}.qkv_w", torch.cat([sd[a + f"self.{n}.weight"] for n in ("query", "key", "value")], 0))
+        put(f"l{i}.qkv_b", torch.cat([sd[a + f"self.{n}.bias"] for n in ("query", "key", "value")], 0))
+        put(f"l{i}.o_w", sd[a + "output.dense.weight"])
+        put(f"l{i}.o_b", sd[a + "output.dense.bias"])
+        put(f"l{i}.ln1_g", sd[a + "output.LayerNorm.weight"])
+        put(f"l{i}.ln1_b", sd[a + "output.LayerNorm.bias"])
+        put(f"l{i}.f1_w", sd[b + "intermediate.dense.weight"])
+        put(f"l{i}.f1_b", sd[b + "intermediate.dense.bias"])
+        put(f"l{i}.f2_w", sd[b + "output.dense.weight"])
+        put(f"l{i}.f2_b", sd[b + "output.dense.bias"])
+        put(f"l{i}.ln2_g", sd[b + "output.LayerNorm.weight"])
+        put(f"l{i}.ln2_b", sd[b + "output.LayerNorm.bias"])
+    put("pool_w", sd["bert.pooler.dense.weight"])
+    put("pool_b", sd["bert.pooler.dense.bias"])
+    put("cls_w", sd["classifier.weight"])
+    put("cls_b", sd["classifier.bias"])
+    return pack
+
+
+class BertClassifier:
+    """Encoder + pooler + classifier over a :class:`ParamPack`.
+
+    ``params`` may live on a ROCm device (native kernels) or on the CPU (the
+    PyTorch reference path of every op; pass ``fp32=True`` for an fp32 oracle).
+    """
+
+    def __init__(self, cfg: BertConfig, pack: ParamPack, fp32: bool = False):
+        self.cfg = cfg
+        self.pack = pack
+        self.p = pack.with_dtype(torch.float32) if fp32 else {n: pack[n] for n in pack.names()}
+        self.device = pack.buffer.device
+
+    def encode(self, ids: torch.Tensor, lens: torch.Tensor, type_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
+        cfg, p = self.cfg, self.p
+        B, S = ids.shape
+        h = ops.embed_layernorm(ids, p["emb.word"], p["emb.pos"], p["emb.type"], p["emb.ln_g"], p["emb.ln_b"],
+                                cfg.eps, type_ids=type_ids)
+        for i in range(cfg.layers):
+            q = f"l{i}."
+            qkv = ops.linear(h, p[q + "qkv_w"], p[q + "qkv_b"])
+            ctx = ops.attention_packed(qkv, lens, B, S, cfg.heads)
+            h1 = ops.linear(ctx, p[q + "o_w"], p[q + "o_b"], residual=h)
+            h1 = ops.layernorm(h1, p[q + "ln1_g"], p[q + "ln1_b"], cfg.eps)
+            f = ops.linear(h1, p[q + "f1_w"], p[q + "f1_b"], act="gelu")
+            h2 = ops.linear(f, p[q + "f2_w"], p[q + "f2_b"], residual=h1)
+            h = ops.layernorm(h2, p[q + "ln2_g"], p[q + "ln2_b"], cfg.eps)
+        return h
+
+    def pooled(self, h: torch.Tensor, B: int, S: int) -> torch.Tensor:
+        cls_rows = h.view(B, S, self.cfg.hidden)[:, 0, :]  # strided view: row stride S*H
+        return ops.linear(cls_rows, self.p["pool_w"], self.p["pool_b"], act="tanh")
+
+    def forward(self, ids: torch.Tensor, lens: torch.Tensor, k: int = 5,
+                type_ids: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """Returns ``(logits[B,C] fp32, topk_idx[B,k] int32, topk_prob[B,k] fp32)``."""
+        B, S = ids.shape
+        h = self.encode(ids, lens, type_ids)
+        pooled = self.pooled(h, B, S)
+        return ops.classify_head_topk(pooled, self.p["cls_w"], self.p["cls_b"], k)

@@ -1,0 +1,13 @@
+"""Device ops: thin, shape-checked wrappers over the gfx950 HIP kernels.
+
+Every op runs the native kernel for CUDA (ROCm) tensors and a plain PyTorch
+reference for CPU tensors; the reference doubles as the numerics oracle in
+``tests/kernels``. There is no silent fallback for device tensors: if the
+extension cannot load on a GPU, the call raises.
+"""
+from .linear import linear, EPI_BIAS, EPI_GELU, EPI_TANH, EPI_RESIDUAL  # noqa: F401
+from .attention import attention_packed, attention  # noqa: F401
+from .norm import layernorm, rmsnorm, embed_layernorm, embed_gather  # noqa: F401
+from .tokenize import tokenize  # noqa: F401
+from .head import classify_head_topk  # noqa: F401
+from .reduce import risk_stats, reduce_stats_tensor  # noqa: F401

@@ -1,0 +1,65 @@
+"""Fused linear layer on the bf16 MFMA GEMM (K3/K5/K6).
+
+``y = act(x @ w.T + bias) + residual`` with ``w`` in ``nn.Linear.weight``
+layout ``[N, K]``. Native kernel: ``csrc/kernels/gemm_bf16.hip``.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from .._native import native, ptr, stream_handle
+from ._util import check, check_bf16_dev, row_stride, same_device
+
+EPI_BIAS, EPI_GELU, EPI_TANH, EPI_RESIDUAL = 1, 2, 4, 8
+_ACTS = {None: 0, "none": 0, "gelu": EPI_GELU, "tanh": EPI_TANH}
+
+
+def linear_ref(x, w, bias=None, act=None, residual=None):
+    y = x.float() @ w.float().t()
+    if bias is not None:
+        y = y + bias.float()
+    if act == "gelu":
+        y = F.gelu(y)
+    elif act == "tanh":
+        y = torch.tanh(y)
+    if residual is not None:
+        y = y + residual.float()
+    return y.to(x.dtype)
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: Optional[str] = None,
+           residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    check(act in _ACTS, f"unknown activation {act!r}")
+    if not x.is_cuda:
+        y = linear_ref(x, w, bias, act, residual)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    check_bf16_dev(x, "x")
+    check_bf16_dev(w, "w")
+    same_device(x, w, bias, residual, out)
+    M, K = x.shape
+    N, K2 = w.shape
+    check(K == K2, f"inner dims differ: x {tuple(x.shape)} w {tuple(w.shape)}")
+    lda, ldb = row_stride(x, "x"), row_stride(w, "w")
+    epi = _ACTS[act]
+    if bias is not None:
+        check(bias.dtype == torch.float32 and bias.is_contiguous() and bias.numel() == N, "bias must be fp32 [N]")
+        epi |= EPI_BIAS
+    ldr = 0
+    if residual is not None:
+        check_bf16_dev(residual, "residual")
+        check(tuple(residual.shape) == (M, N), "residual must be [M, N]")
+        ldr = row_stride(residual, "residual")
+        epi |= EPI_RESIDUAL
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    check(tuple(out.shape) == (M, N), "out must be [M, N]")
+    ldc = row_stride(out, "out")
+    native().gemm(ptr(x), lda, ptr(w), ldb, ptr(out), ldc, ptr(bias), ptr(residual), ldr, M, N, K, epi,
+                  stream_handle())
+    return out

@@ -1,0 +1,89 @@
+"""Row normalisation and embedding ops (K2, K6b, T5 RMSNorm).
+
+Native kernels: ``csrc/kernels/norm_embed.hip`` (one wave per row, fp32 stats).
+Row width must be a multiple of 256 (768 / 1024 for BERT, 768 for T5-base).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from .._native import native, ptr, stream_handle
+from ._util import check, check_bf16_dev
+
+
+def _f32(t: torch.Tensor, n: int, name: str) -> None:
+    check(t.dtype == torch.float32 and t.is_contiguous() and t.numel() == n, f"{name} must be fp32 [{n}]")
+
+
+def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-12,
+              residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    rows, N = x.shape
+    if not x.is_cuda:
+        y = x.float() + (residual.float() if residual is not None else 0.0)
+        y = F.layer_norm(y, (N,), gamma.float(), beta.float(), eps).to(x.dtype)
+        return out.copy_(y) if out is not None else y
+    check_bf16_dev(x, "x")
+    check(x.is_contiguous(), "x must be contiguous")
+    _f32(gamma, N, "gamma")
+    _f32(beta, N, "beta")
+    if residual is not None:
+        check_bf16_dev(residual, "residual")
+        check(residual.is_contiguous() and residual.shape == x.shape, "residual must match x")
+    out = torch.empty_like(x) if out is None else out
+    native().layernorm(ptr(x), ptr(residual), ptr(gamma), ptr(beta), ptr(out), rows, N, float(eps), stream_handle())
+    return out
+
+
+def rmsnorm(x: torch.Tensor, gamma: torch.Tensor, eps: float = 1e-6, out: Optional[torch.Tensor] = None):
+    rows, N = x.shape
+    if not x.is_cuda:
+        xf = x.float()
+        y = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * gamma.float()).to(x.dtype)
+        return out.copy_(y) if out is not None else y
+    check_bf16_dev(x, "x")
+    check(x.is_contiguous(), "x must be contiguous")
+    _f32(gamma, N, "gamma")
+    out = torch.empty_like(x) if out is None else out
+    native().rmsnorm(ptr(x), ptr(gamma), ptr(out), rows, N, float(eps), stream_handle())
+    return out
+
+
+def embed_layernorm(ids: torch.Tensor, word: torch.Tensor, pos: torch.Tensor, type_: torch.Tensor,
+                    gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-12,
+                    type_ids: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``LN(word[ids] + pos[s] + type[type_ids])`` for ``ids[B, S]`` -> ``[B*S, N]``."""
+    B, S = ids.shape
+    V, N = word.shape
+    if not ids.is_cuda:
+        tt = type_ids if type_ids is not None else torch.zeros_like(ids)
+        x = word.float()[ids.long().clamp(0, V - 1)] + pos.float()[:S].unsqueeze(0) + type_.float()[tt.long()]
+        y = F.layer_norm(x, (N,), gamma.float(), beta.float(), eps).to(word.dtype).view(B * S, N)
+        return out.copy_(y) if out is not None else y
+    check(ids.dtype == torch.int32 and ids.is_contiguous(), "ids must be contiguous int32")
+    check(pos.shape[0] >= S, "sequence longer than the position table")
+    for t, n in ((word, "word"), (pos, "pos"), (type_, "type")):
+        check_bf16_dev(t, n)
+    _f32(gamma, N, "gamma")
+    _f32(beta, N, "beta")
+    if type_ids is not None:
+        check(type_ids.dtype == torch.int32 and type_ids.shape == ids.shape, "type_ids must be int32 [B,S]")
+    out = torch.empty((B * S, N), dtype=torch.bfloat16, device=ids.device) if out is None else out
+    native().embed_layernorm(ptr(ids), ptr(type_ids), ptr(word), ptr(pos), ptr(type_), ptr(gamma), ptr(beta),
+                             ptr(out), B, S, N, V, float(eps), stream_handle())
+    return out
+
+
+def embed_gather(ids: torch.Tensor, table: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    V, N = table.shape
+    flat = ids.reshape(-1)
+    if not ids.is_cuda:
+        y = table[flat.long().clamp(0, V - 1)]
+        return out.copy_(y) if out is not None else y
+    check(ids.dtype == torch.int32 and ids.is_contiguous(), "ids must be contiguous int32")
+    check_bf16_dev(table, "table")
+    out = torch.empty((flat.numel(), N), dtype=torch.bfloat16, device=ids.device) if out is None else out
+    native().embed_gather(ptr(flat), ptr(table), ptr(out), flat.numel(), N, V, stream_handle())
+    return out

@@ -1,0 +1,210 @@
+"""Collective job execution: rank 0 leases, every rank computes its shard.
+
+Process model (one process per GPU, ``torchrun --nproc-per-node N app.py``):
+rank 0 runs the HTTP agent loop; ranks 1..N-1 sit in :func:`worker_loop`.
+For a DP-capable job rank 0 calls :func:`dispatch`, which broadcasts the task
+descriptor (C4) and then runs the same registered ``@dp_task`` body as every
+worker. Bodies do their local (collective-free) work first; the per-rank
+errors are then exchanged, so a failure on ANY rank fails the job on rank 0
+with that rank's id in the message instead of hanging the others in a
+collective. ``MI355X_FAULT=rank:K`` injects a failure on rank
+K for tests.
+
+Registered bodies: ``map_classify_csv`` (C2 all-gather of top-k) and
+``risk_accumulate`` (C3 all-reduce of {count,sum,min,max}).
+"""
+from __future__ import annotations
+
+import os
+import time
+import traceback
+from typing import Any, Callable, Dict, Tuple
+
+import torch
+import torch.distributed as dist
+
+from .dp import all_gather_rows, broadcast_task, comm_device, is_dist, split_range, world
+
+_TASKS: Dict[str, Callable[[Dict[str, Any]], Any]] = {}
+_SHUTDOWN = "__shutdown__"
+
+
+def dp_task(name: str):
+    def wrap(fn):
+        _TASKS[name] = fn
+        return fn
+
+    return wrap
+
+
+def init_from_env() -> None:
+    """Join the node's process group (RCCL on GPUs, gloo otherwise)."""
+    if is_dist():
+        return
+    local = int(os.getenv("LOCAL_RANK", "0"))
+    if torch.cuda.is_available() and os.getenv("ATPU_DP_BACKEND", "nccl") == "nccl":
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group("gloo")
+
+
+def maybe_inject_fault(stage: str) -> None:
+    spec = os.getenv("MI355X_FAULT", "")
+    if not spec.startswith("rank:"):
+        return
+    rank, _ = world()
+    parts = spec.split(":")
+    if int(parts[1]) == rank and (len(parts) < 3 or parts[2] == stage):
+        raise RuntimeError(f"injected fault ({spec}) at {stage}")
+
+
+def _check_errors(err: str) -> None:
+    if not is_dist():
+        if err:
+            raise RuntimeError(err)
+        return
+    rank, ws = world()
+    errs = [None] * ws
+    dist.all_gather_object(errs, err)
+    bad = [(r, e) for r, e in enumerate(errs) if e]
+    if bad:
+        raise RuntimeError("; ".join(f"rank {r}: {e}" for r, e in bad))
+
+
+def run_collective(name: str, payload: Dict[str, Any]) -> Any:
+    fn = _TASKS[name]
+    return fn(payload)
+
+
+def dispatch(name: str, payload: Dict[str, Any]) -> Any:
+    """Rank 0: broadcast ``(name, payload)`` then execute it with every rank."""
+    if is_dist():
+        broadcast_task({"op": name, "payload": payload})
+    return run_collective(name, payload)
+
+
+def worker_loop() -> int:
+    """Ranks != 0: execute broadcast task descriptors until shutdown."""
+    rank, _ = world()
+    print(f"[agent-mi355x] dp worker rank={rank} ready", flush=True)
+    while True:
+        desc = broadcast_task(None)
+        if not isinstance(desc, dict) or desc.get("op") == _SHUTDOWN:
+            break
+        try:
+            run_collective(desc["op"], desc["payload"])
+        except Exception as exc:  # rank 0 reports; keep serving
+            print(f"[agent-mi355x] dp worker rank={rank} task {desc.get('op')} failed: {exc}", flush=True)
+    if is_dist():
+        dist.destroy_process_group()
+    return 0
+
+
+def shutdown_workers() -> None:
+    if is_dist() and world()[0] == 0:
+        broadcast_task({"op": _SHUTDOWN})
+
+
+# ------------------------------------------------------------ map_classify
+def _open_table(path: str):
+    from ..io.csv import open_csv
+
+    return open_csv(path)
+
+
+@dp_task("map_classify_csv")
+def classify_csv_task(payload: Dict[str, Any]) -> Any:
+    from ops._gpu_runtime import get_gpu_handle, get_model_path  # agent-level registry
+
+    t0 = time.perf_counter()
+    rank, ws = world()
+    # model load is itself collective (C1 broadcast), so it happens on every rank
+    h = get_gpu_handle(get_model_path(payload.get("model_path")))
+    timing: Dict[str, float] = {"load_ms": (time.perf_counter() - t0) * 1000.0}
+    err, idx, sc, meta = "", None, None, {}
+    try:
+        start = int(payload.get("start_row", 0))
+        size = int(payload.get("shard_size", 100))
+        if start < 0 or size <= 0:
+            raise ValueError("start_row must be >= 0 and shard_size > 0")
+        table = _open_table(payload["source_uri"])
+        col = table.native.column_index(str(payload.get("text_column", "text")))
+        if col < 0:
+            raise ValueError(f"text_column {payload.get('text_column', 'text')!r} not in header {table.header}")
+        total = max(0, min(size, table.num_rows - start))
+        s_r, n_r = split_range(start, total, ws, rank)
+        maybe_inject_fault("classify")
+        t1 = time.perf_counter()
+        idx, sc, st = h.engine.classify_table(table.native, s_r, n_r, col)
+        timing["classify_ms"] = (time.perf_counter() - t1) * 1000.0
+        meta = {"start_row": start, "end_row": start + total, "world": ws}
+    except Exception as exc:
+        err = f"{type(exc).__name__}: {exc}"
+        if os.getenv("ATPU_DEBUG"):
+            traceback.print_exc()
+    _check_errors(err)
+    t2 = time.perf_counter()
+    idx, sc = all_gather_rows(idx, sc)
+    timing["allgather_ms"] = (time.perf_counter() - t2) * 1000.0
+    if rank != 0:
+        return None
+    meta["timing_ms"] = timing
+    from ops.map_classify import csv_result
+
+    return csv_result(h, idx.cpu(), sc.cpu(), meta, payload)
+
+
+# ---------------------------------------------------------- risk_accumulate
+def _local_values(payload: Dict[str, Any], rank: int, ws: int) -> Tuple[torch.Tensor, int]:
+    """This rank's slice of the values, as fp64."""
+    if "source_uri" in payload:
+        table = _open_table(payload["source_uri"])
+        col = table.native.column_index(str(payload.get("field", "risk")))
+        if col < 0:
+            raise ValueError(f"field {payload.get('field', 'risk')!r} not in header {table.header}")
+        start = int(payload.get("start_row", 0))
+        total = max(0, min(int(payload.get("shard_size", table.num_rows)), table.num_rows - start))
+        s_r, n_r = split_range(start, total, ws, rank)
+        return torch.from_numpy(table.native.float_column(s_r, n_r, col)), total
+    from ops.risk_accumulate import _gather  # same validation/messages as the CPU op
+
+    vals = _gather(payload)
+    s_r, n_r = split_range(0, len(vals), ws, rank)
+    return torch.tensor(vals[s_r:s_r + n_r], dtype=torch.float64), len(vals)
+
+
+@dp_task("risk_accumulate")
+def risk_task(payload: Dict[str, Any]) -> Any:
+    from ..ops.reduce import reduce_stats_tensor, stats_dict
+
+    t0 = time.perf_counter()
+    rank, ws = world()
+    err, stats = "", torch.tensor([0.0, 0.0, float("inf"), float("-inf")], dtype=torch.float64)
+    try:
+        maybe_inject_fault("risk")
+        x, _ = _local_values(payload, rank, ws)
+        if torch.cuda.is_available():
+            dev = torch.device("cuda", torch.cuda.current_device())
+            x = x.to(dev, non_blocking=True)
+        if x.numel():
+            stats = reduce_stats_tensor(x)
+    except Exception as exc:
+        err = f"{type(exc).__name__}: {exc}"
+    _check_errors(err)
+    if is_dist():
+        cdev = comm_device()
+        s = stats.to(cdev)
+        sums = s[:2].clone()
+        ext = torch.stack([s[3], -s[2]])  # max, -min -> one MAX all-reduce
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+        dist.all_reduce(ext, op=dist.ReduceOp.MAX)
+        stats = torch.stack([sums[0], sums[1], -ext[1], ext[0]]).cpu()
+    else:
+        stats = stats.cpu()
+    if rank != 0:
+        return None
+    out = stats_dict(stats.tolist())
+    out["compute_time_ms"] = (time.perf_counter() - t0) * 1000.0
+    out["dp_world_size"] = ws
+    return out

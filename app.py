@@ -1,0 +1,348 @@
+#!/usr/bin/env python3
+"""MI355X job agent: lease -> execute -> report.
+
+Wire protocol and env contract of the reference agent
+(``/root/reference/app.py``): ``POST /v1/leases`` with
+``{agent, capabilities:{ops}, max_tasks, timeout_ms, labels, worker_profile,
+metrics}`` (ref ``app.py:161-195``); ``POST /v1/results`` with
+``{lease_id, job_id, job_epoch, status, result, error}`` (ref ``:198-218``);
+error objects ``{type, message, trace}`` (ref ``:288-294``); exit code 2 when
+``TASKS`` is empty, 0 after SIGINT/SIGTERM (ref ``:245-316``).
+
+Fixes over the reference:
+
+* ops are resolved through the ``ops`` registry / ``ops_loader`` (the
+  reference's ``app.py`` had a private two-entry table, §2.4.1-2);
+* the worker profile is built dynamically by ``worker_sizing`` (AMD GPUs,
+  HBM-derived batch sizing) plus the reference's ``tier``/``limits`` (§2.4.3);
+* EVERY task of a multi-task lease is executed and resulted (§2.4.8);
+* one keep-alive HTTP session instead of a TCP connect per request (§2.4.11);
+* failed result posts get a bounded retry on transport/5xx errors, never on
+  4xx (a 409 stale epoch is final); ``job_epoch`` is passed through verbatim;
+* metrics add GPU/HBM use, completed jobs and a rolling rows/s (§5.5).
+
+Data parallel: launched under ``torchrun`` (WORLD_SIZE>1), rank 0 runs this
+loop and the other ranks run :func:`agent_tpu_amd.parallel.dp_ops.worker_loop`,
+executing their shard of every DP-capable job (map_classify, risk_accumulate).
+"""
+from __future__ import annotations
+
+import os
+import signal
+import socket
+import sys
+import threading
+import time
+import traceback
+from typing import Any, Dict, List, Optional, Tuple
+
+try:
+    import requests
+except Exception:  # pragma: no cover
+    requests = None
+
+try:
+    import psutil  # type: ignore
+except Exception:  # pragma: no cover
+    psutil = None
+
+LOG = "[agent-mi355x]"
+
+# ------------------------------------------------------------------ config
+# identical names and defaults to the reference (app.py:21-41)
+CONTROLLER_URL = os.getenv("CONTROLLER_URL", "").rstrip("/") or "http://10.11.12.54:8080"
+AGENT_NAME = os.getenv("AGENT_NAME", socket.gethostname())
+HTTP_TIMEOUT_SEC = float(os.getenv("HTTP_TIMEOUT_SEC", "10"))
+IDLE_SLEEP_SEC = float(os.getenv("IDLE_SLEEP_SEC", "0.25"))
+MAX_TASKS = int(os.getenv("MAX_TASKS", "1"))
+LEASE_TIMEOUT_MS = int(os.getenv("LEASE_TIMEOUT_MS", "3000"))
+ERROR_LOG_EVERY_SEC = float(os.getenv("ERROR_LOG_EVERY_SEC", "10"))
+ERROR_BACKOFF_SEC = float(os.getenv("ERROR_BACKOFF_SEC", "1.0"))
+TASKS_RAW = os.getenv("TASKS", "echo,map_classify_tpu")
+AGENT_LABELS_RAW = os.getenv("AGENT_LABELS", "")
+# new knobs
+RESULT_RETRIES = int(os.getenv("RESULT_RETRIES", "2"))
+FAIL_ON_NOT_OK = os.getenv("FAIL_ON_NOT_OK", "0").strip().lower() in ("1", "true", "yes")
+
+_running = True
+_last_log: Dict[str, float] = {}
+
+
+def parse_labels(raw: str) -> Dict[str, Any]:
+    """``"k=v,flag,x=1=2"`` -> ``{"k": "v", "flag": True, "x": "1=2"}`` (ref app.py:49-63)."""
+    labels: Dict[str, Any] = {}
+    for part in (raw or "").split(","):
+        part = part.strip()
+        if not part:
+            continue
+        key, sep, val = part.partition("=")
+        labels[key.strip()] = val.strip() if sep else True
+    return labels
+
+
+def capabilities(raw: str) -> List[str]:
+    """Comma list -> de-duplicated names in first-seen order (ref app.py:86-96)."""
+    seen: Dict[str, None] = {}
+    for tok in (raw or "").split(","):
+        tok = tok.strip()
+        if tok:
+            seen.setdefault(tok, None)
+    return list(seen)
+
+
+def log_every(key: str, msg: str) -> None:
+    """Print ``msg`` at most once per ERROR_LOG_EVERY_SEC for ``key``."""
+    now = time.time()
+    if now - _last_log.get(key, 0.0) >= ERROR_LOG_EVERY_SEC:
+        _last_log[key] = now
+        print(msg, flush=True)
+
+
+CAPS_LIST = capabilities(TASKS_RAW)
+BASE_LABELS = parse_labels(AGENT_LABELS_RAW)
+
+
+# ----------------------------------------------------------------- metrics
+class Metrics:
+    """Piggy-backed on every lease (ref app.py:74-83 keys + GPU/throughput)."""
+
+    def __init__(self) -> None:
+        self.jobs_completed = 0
+        self.jobs_failed = 0
+        self._rows: List[Tuple[float, int]] = []
+        self._lock = threading.Lock()
+
+    def job_done(self, ok: bool, result: Any) -> None:
+        with self._lock:
+            if ok:
+                self.jobs_completed += 1
+            else:
+                self.jobs_failed += 1
+            rows = result.get("row_count") if isinstance(result, dict) and ok else None
+            if isinstance(rows, int) and result.get("rows_per_sec") is not None:
+                self._rows.append((time.time(), rows))
+                cut = time.time() - 60.0
+                self._rows = [r for r in self._rows if r[0] >= cut]
+
+    def rows_per_sec(self) -> float:
+        with self._lock:
+            if not self._rows:
+                return 0.0
+            span = max(1.0, time.time() - self._rows[0][0])
+            return sum(n for _, n in self._rows) / span
+
+    def snapshot(self) -> Dict[str, Any]:
+        out: Dict[str, Any] = {}
+        if psutil is not None:
+            try:
+                out["cpu_util"] = float(psutil.cpu_percent(interval=None)) / 100.0
+                out["ram_mb"] = float(psutil.virtual_memory().used) / (1024 * 1024)
+            except Exception:
+                out = {}
+        out.update(gpu_metrics())
+        out["jobs_completed"] = self.jobs_completed
+        out["jobs_failed"] = self.jobs_failed
+        out["rows_per_sec"] = round(self.rows_per_sec(), 2)
+        return out
+
+
+def gpu_metrics() -> Dict[str, Any]:
+    """HBM use per device, only if this process already initialised the GPU."""
+    try:
+        import torch
+
+        if not torch.cuda.is_available() or not torch.cuda.is_initialized():
+            return {}
+        used, total = [], []
+        for i in range(torch.cuda.device_count()):
+            free_b, tot_b = torch.cuda.mem_get_info(i)
+            used.append(round((tot_b - free_b) / 2**30, 2))
+            total.append(round(tot_b / 2**30, 2))
+        return {"hbm_used_gb": used, "hbm_total_gb": total}
+    except Exception:
+        return {}
+
+
+METRICS = Metrics()
+
+
+# --------------------------------------------------------------- profile
+def worker_profile() -> Dict[str, Any]:
+    from worker_sizing import build_worker_profile
+
+    prof = build_worker_profile()
+    prof["tier"] = "mi355x" if prof.get("gpu", {}).get("gpu_present") else "cpu"
+    prof["limits"] = {"max_payload_bytes": int(os.getenv("MAX_PAYLOAD_BYTES", "262144")),
+                      "max_tokens": int(os.getenv("MAX_TOKENS", "2048"))}
+    return prof
+
+
+# ------------------------------------------------------------------- http
+class Controller:
+    def __init__(self, base: str, timeout: float) -> None:
+        self.base = base
+        self.timeout = timeout
+        self.http = requests.Session() if requests is not None else None
+
+    def post(self, path: str, body: Dict[str, Any]) -> Tuple[int, Any]:
+        url = self.base + path
+        try:
+            r = self.http.post(url, json=body, timeout=self.timeout)
+        except Exception as exc:
+            return 0, {"error": str(exc), "url": url}
+        if r.status_code == 204:
+            return 204, None
+        try:
+            return r.status_code, r.json()
+        except Exception:
+            return r.status_code, r.text
+
+    def lease(self, caps: List[str], profile: Dict[str, Any]) -> Optional[Tuple[str, List[Any]]]:
+        body = {"agent": AGENT_NAME, "capabilities": {"ops": caps}, "max_tasks": MAX_TASKS,
+                "timeout_ms": LEASE_TIMEOUT_MS, "labels": BASE_LABELS, "worker_profile": profile,
+                "metrics": METRICS.snapshot()}
+        code, resp = self.post("/v1/leases", body)
+        if code == 204:
+            return None
+        if code == 0:
+            raise RuntimeError(f"lease failed: {resp}")
+        if code >= 400:
+            raise RuntimeError(f"lease HTTP {code}: {resp}")
+        if not isinstance(resp, dict):
+            raise RuntimeError(f"lease body not dict: {resp!r}")
+        lease_id, tasks = resp.get("lease_id"), resp.get("tasks")
+        if not isinstance(lease_id, str) or not lease_id:
+            raise RuntimeError(f"lease missing lease_id: {resp!r}")
+        if not isinstance(tasks, list) or not tasks:
+            return None
+        return lease_id, tasks
+
+    def result(self, lease_id: str, job_id: str, epoch: Any, status: str, result: Any, error: Any) -> None:
+        body = {"lease_id": lease_id, "job_id": job_id, "job_epoch": epoch, "status": status,
+                "result": result, "error": error}
+        for attempt in range(RESULT_RETRIES + 1):
+            code, resp = self.post("/v1/results", body)
+            if 0 < code < 400:
+                return
+            retryable = code == 0 or code >= 500
+            if not retryable or attempt == RESULT_RETRIES:
+                if code == 0:
+                    raise RuntimeError(f"result failed: {resp}")
+                raise RuntimeError(f"result HTTP {code}: {resp}")
+            time.sleep(min(2.0, 0.1 * 2**attempt))
+
+
+def extract_task(task: Any) -> Tuple[str, str, Dict[str, Any], Any]:
+    """-> (job_id, op, payload, job_epoch) with the reference's checks (app.py:221-234)."""
+    if not isinstance(task, dict):
+        raise RuntimeError(f"task not dict: {task!r}")
+    job_id = task.get("id") or task.get("job_id")
+    op = task.get("op")
+    payload = task.get("payload") or {}
+    if not isinstance(job_id, str) or not job_id:
+        raise RuntimeError(f"task missing job id: {task!r}")
+    if not isinstance(op, str) or not op:
+        raise RuntimeError(f"task missing op: {task!r}")
+    if not isinstance(payload, dict):
+        raise RuntimeError(f"task payload not dict: {task!r}")
+    return job_id, op, payload, task.get("job_epoch")
+
+
+# ---------------------------------------------------------------- agent
+class Agent:
+    def __init__(self) -> None:
+        from ops_loader import load_ops_lenient
+
+        self.handlers, errors = load_ops_lenient(CAPS_LIST)
+        for name, msg in errors:
+            print(f"{LOG} op unavailable: {name}: {msg}", flush=True)
+        # advertise only what can run: a leased-but-unloadable op would fail every job
+        self.caps = [c for c in CAPS_LIST if c in self.handlers] if errors and self.handlers else list(CAPS_LIST)
+        self.ctl = Controller(CONTROLLER_URL, HTTP_TIMEOUT_SEC)
+        self.profile = worker_profile()
+
+    def run_task(self, lease_id: str, task: Any) -> None:
+        try:
+            job_id, op, payload, epoch = extract_task(task)
+        except Exception as exc:
+            log_every("task:bad", f"{LOG} bad task: {exc} task={repr(task)[:300]}")
+            return
+        t0 = time.time()
+        out, err = None, None
+        try:
+            fn = self.handlers.get(op)
+            if fn is None:
+                raise RuntimeError(f"Unknown op '{op}'")
+            out = fn(payload)  # inline: one job at a time per agent (ref app.py:286-287)
+            if FAIL_ON_NOT_OK and isinstance(out, dict) and out.get("ok") is False:
+                raise RuntimeError(str(out.get("error", "op returned ok=false")))
+        except Exception as exc:
+            err = {"type": type(exc).__name__, "message": str(exc), "trace": traceback.format_exc(limit=12)}
+        ok = err is None
+        ms = (time.time() - t0) * 1000.0
+        METRICS.job_done(ok, out)
+        try:
+            self.ctl.result(lease_id, job_id, epoch, "succeeded" if ok else "failed",
+                            out if ok else None, None if ok else err)
+        except Exception as exc:
+            log_every("result", f"{LOG} post result error: {exc}")
+        if ok:
+            print(f"{LOG} ok job={job_id} op={op} ms={ms:.1f}", flush=True)
+        else:
+            log_every("exec", f"{LOG} FAIL job={job_id} op={op} ms={ms:.1f} err={err}")
+
+    def loop(self) -> None:
+        while _running:
+            try:
+                leased = self.ctl.lease(self.caps, self.profile)
+            except Exception as exc:
+                log_every("lease", f"{LOG} lease error: {exc}")
+                time.sleep(ERROR_BACKOFF_SEC)
+                continue
+            if not leased:
+                time.sleep(IDLE_SLEEP_SEC)
+                continue
+            lease_id, tasks = leased
+            for task in tasks:
+                self.run_task(lease_id, task)
+
+
+def _on_signal(signum: int, _frame: Any) -> None:
+    global _running
+    _running = False
+    print(f"{LOG} shutdown signal {signum}", flush=True)
+
+
+def main() -> int:
+    global _running
+    _running = True
+    signal.signal(signal.SIGINT, _on_signal)
+    signal.signal(signal.SIGTERM, _on_signal)
+    if not CAPS_LIST:
+        print(f"{LOG} no TASKS configured; exiting", flush=True)
+        return 2
+
+    world = int(os.getenv("WORLD_SIZE", "1"))
+    rank = int(os.getenv("RANK", "0"))
+    if world > 1:
+        from agent_tpu_amd.parallel import dp_ops
+
+        dp_ops.init_from_env()
+        if rank != 0:
+            return dp_ops.worker_loop()
+
+    agent = Agent()
+    print(f"{LOG} starting name={AGENT_NAME} controller={CONTROLLER_URL} ops={agent.caps}", flush=True)
+    try:
+        agent.loop()
+    finally:
+        if world > 1:
+            from agent_tpu_amd.parallel import dp_ops
+
+            dp_ops.shutdown_workers()
+    print(f"{LOG} stopped", flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

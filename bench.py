@@ -1,0 +1,151 @@
+#!/usr/bin/env python3
+"""Headline benchmark: classified rows/sec (whole node), map_classify BERT-base.
+
+Metric/config from BASELINE.json: "classified rows/sec (whole node)
+map_classify BERT-base at 1/2/4/8 MI355X". One process per GPU (torchrun);
+each rank streams its own row range of a synthetic CSV through the full
+map_classify device pipeline:
+
+  C++ CSV row index -> pinned double-buffer -> hipMemcpyAsync (side stream)
+  -> GPU tokenizer (K1) -> BERT-base bf16 encoder (K2..K6) -> pooler + head/top-k (K7)
+  -> RCCL all-gather of every rank's per-row top-k (C2)
+
+A "step" = one batch of ``--batch-rows`` rows per GPU (S=128 tokens each,
+random-init weights broadcast from rank 0 with RCCL, C1). W warmup steps,
+then exactly K timed steps bracketed by barrier + synchronize; the time is the
+max over ranks. Weak scaling: per-GPU work is fixed as N grows.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "classified rows/sec (whole node) map_classify BERT-base at 1/2/4/8 MI355X"
+# reference-compute proxy, BERT-base S=128 batch 32 = 35.2 rows/s
+BASELINE_ROWS_PER_SEC = 35.2
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch-rows", type=int, default=int(os.environ.get("BENCH_BATCH_ROWS", "1024")))
+    ap.add_argument("--seq-len", type=int, default=128)
+    ap.add_argument("--model", default="bert-base")
+    ap.add_argument("--topk", type=int, default=5)
+    ap.add_argument("--num-labels", type=int, default=2)
+    ap.add_argument("--words-per-row", type=int, default=150)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--csv", default="")
+    return ap.parse_args()
+
+
+def main() -> int:
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus and rank == 0:
+        print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from agent_tpu_amd._native import native
+    from agent_tpu_amd.models.bert import config_for, init_random
+    from agent_tpu_amd.parallel.dp import broadcast_pack, all_gather_rows
+    from agent_tpu_amd.runtime.classify import ClassifyEngine
+    from agent_tpu_amd.utils.synthetic import write_csv
+
+    nat = native()
+    cfg = config_for(a.model, num_labels=a.num_labels)
+    B = a.batch_rows
+    rows_needed = (a.warmup + a.steps) * B
+    csv_path = a.csv or f"/tmp/atpu_bench_r{rank}_{rows_needed}_{a.words_per_row}.csv"
+    if not os.path.exists(csv_path):
+        write_csv(csv_path, rows_needed, a.words_per_row, seed=1234 + rank)
+    table = nat.CsvTable(csv_path)
+    col = table.column_index("text")
+
+    # weights: rank 0 initialises, RCCL broadcast to every rank (C1)
+    pack = init_random(cfg, seed=0) if rank == 0 else None
+    t_b = time.perf_counter()
+    pack = broadcast_pack(pack, cfg, dev) if world > 1 else pack.to(dev)
+    torch.cuda.synchronize(dev)
+    bcast_ms = (time.perf_counter() - t_b) * 1000.0
+
+    eng = ClassifyEngine(cfg, pack, dev, batch_rows=B, seq_len=a.seq_len, topk=a.topk, use_graph=not a.no_graph)
+
+    def run(start_batch: int, nbatches: int):
+        idx, score, _ = eng.classify_table(table, start_batch * B, nbatches * B, col)
+        if world > 1:
+            idx, score = all_gather_rows(idx, score)
+        return idx, score
+
+    run(0, a.warmup)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    idx, score = run(a.warmup, a.steps)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_rows = world * B * a.steps
+    assert idx.shape[0] == total_rows, (idx.shape, total_rows)
+    value = total_rows / elapsed
+    if rank == 0:
+        flops = cfg.flops_per_row(a.seq_len) * total_rows / elapsed
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed * 1000.0 / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_ROWS_PER_SEC, 2),
+            "dtype": "bf16",
+            "data": "synthetic CSV rows (random words), random-init weights",
+            "config": {
+                "model": a.model,
+                "global_batch": B * world,
+                "seq_len": a.seq_len,
+                "parallelism": f"dp{world}",
+                "rows_per_gpu_per_step": B,
+                "num_labels": cfg.num_labels,
+                "topk": min(a.topk, cfg.num_labels),
+                "hipgraph": not a.no_graph,
+                "weight_broadcast_ms": round(bcast_ms, 2),
+                "achieved_tflops_per_gpu": round(flops / world / 1e12, 1),
+            },
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,125 @@
+"""``map_classify`` (alias ``map_classify_tpu``) — BERT text classification on MI355X.
+
+Replaces the reference's Edge-TPU op (``/root/reference/ops/map_classify_tpu.py``).
+Three payload forms (see map_classify.CONTRACT.md):
+
+1. reference form ``{"input": [token ids], "topk"?, "model_path"?,
+   "allow_fallback"?}`` — one pre-tokenized row; returns exactly the
+   reference keys ``{op, model_path, topk:[{index,score}], elapsed_ms}``, and on
+   any error with ``allow_fallback`` (default True) the reference's stub
+   ``{op, fallback:"cpu", reason, topk:[], elapsed_ms}`` (``:22-28,84-89``).
+2. text rows ``{"texts": [...]}`` — tokenized on the GPU (K1).
+3. CSV shard ``{"source_uri", "start_row", "shard_size", "text_column"?}`` —
+   rows streamed from the native CSV index through pinned double buffers;
+   under ``torchrun`` the shard is split over every GPU of the node and the
+   per-rank top-k is all-gathered over RCCL.
+
+``score`` is the softmax probability of the class (the reference returned raw
+quantized outputs cast to float; see CONTRACT "Notes").
+"""
+from __future__ import annotations
+
+import time
+from typing import Any, Dict, List
+
+from . import register_op
+from ._gpu_runtime import get_gpu_handle, get_model_path
+
+OP_NAME = "map_classify_tpu"
+
+
+def _topk_list(idx_row, score_row) -> List[Dict[str, Any]]:
+    return [{"index": int(i), "score": float(s)} for i, s in zip(idx_row, score_row)]
+
+
+def _fallback(payload: Dict[str, Any], reason: str, t0: float, op: str) -> Dict[str, Any]:
+    return {"op": op, "fallback": "cpu", "reason": payload.get("fallback_reason", reason), "topk": [],
+            "elapsed_ms": (time.time() - t0) * 1000.0}
+
+
+def _classify_ids(h, payload: Dict[str, Any], k: int, op: str, t0: float) -> Dict[str, Any]:
+    import torch
+
+    S = h.engine.S
+    raw = payload["input"]
+    ids = torch.tensor(raw, dtype=torch.int64)
+    if ids.numel() != S:
+        raise ValueError(f"Input size mismatch. Got {ids.numel()}, expected {S} for shape (1, {S}).")
+    if int(ids.min()) < 0 or int(ids.max()) >= h.cfg.vocab_size:
+        raise ValueError(f"token id out of range [0, {h.cfg.vocab_size})")
+    nz = (ids != 0).nonzero()
+    n = int(nz[-1]) + 1 if nz.numel() else 1
+    dev = h.engine.device
+    _, idx, sc = h.engine.model.forward(ids.view(1, S).to(torch.int32).to(dev),
+                                         torch.tensor([max(1, n)], dtype=torch.int32, device=dev), k)
+    return {"op": op, "model_path": h.model_path, "topk": _topk_list(idx[0].tolist(), sc[0].tolist()),
+            "elapsed_ms": (time.time() - t0) * 1000.0}
+
+
+def csv_result(h, idx, sc, meta: Dict[str, Any], payload: Dict[str, Any]) -> Dict[str, Any]:
+    k = max(1, min(int(payload.get("topk", 5)), h.cfg.num_labels))
+    return _rows_result(h, idx[:, :k], sc[:, :k], int(meta["start_row"]), k, payload.get("_op", OP_NAME),
+                        float(payload.get("_t0", time.time())),
+                        {"dataset_id": payload.get("dataset_id", "unknown_dataset"),
+                         "start_row": meta["start_row"], "end_row": meta["end_row"],
+                         "dp_world_size": meta["world"], "timing_ms": meta["timing_ms"],
+                         "_summary": payload.get("output", "rows") == "summary"})
+
+
+def _rows_result(h, idx, sc, start: int, k: int, op: str, t0: float, extra: Dict[str, Any]) -> Dict[str, Any]:
+    summary = bool(extra.pop("_summary", False))
+    idx_l, sc_l = idx.tolist(), sc.tolist()
+    rows = [{"row": start + i, "topk": _topk_list(a, b)} for i, (a, b) in enumerate(zip(idx_l, sc_l))]
+    dt = time.time() - t0
+    out = {"ok": True, "op": op, "model_path": h.model_path, "row_count": len(rows),
+           "topk": rows[0]["topk"] if rows else [], "elapsed_ms": dt * 1000.0,
+           "rows_per_sec": (len(rows) / dt) if dt > 0 else None}
+    out.update(extra)
+    if summary:
+        hist: Dict[int, int] = {}
+        for r in idx_l:
+            hist[r[0]] = hist.get(r[0], 0) + 1
+        out.pop("topk", None)
+        out["top1_histogram"] = {str(c): n for c, n in sorted(hist.items())}
+    else:
+        out["rows"] = rows
+    return out
+
+
+def run(payload: Dict[str, Any], ctx: Dict[str, Any] = None, op: str = OP_NAME) -> Dict[str, Any]:
+    payload = payload or {}
+    t0 = time.time()
+    allow_fallback = payload.get("allow_fallback", True)
+    try:
+        if "source_uri" in payload and "input" not in payload:
+            # DP path: every rank (not only this one) must load the model, so
+            # the task descriptor is broadcast before anything touches the GPU
+            from agent_tpu_amd.parallel.dp_ops import dispatch
+
+            out = dispatch("map_classify_csv", dict(payload, _op=op, _t0=t0))
+            return out
+        h = get_gpu_handle(get_model_path(payload.get("model_path")))
+        k = max(1, min(int(payload.get("topk", 5)), h.cfg.num_labels))
+        if "input" in payload:
+            return _classify_ids(h, payload, k, op, t0)
+        if "texts" in payload:
+            texts = payload["texts"]
+            if not isinstance(texts, list):
+                raise ValueError("payload.texts must be a list of strings")
+            res = h.engine.classify_texts(["" if t is None else str(t) for t in texts], k)
+            return _rows_result(h, res.idx[:, :k], res.score[:, :k], 0, k, op, t0, {})
+        raise ValueError('payload missing required key: "input" (or "texts" / "source_uri")')
+    except Exception as exc:
+        if allow_fallback:
+            return _fallback(payload, str(exc), t0, op)
+        raise
+
+
+@register_op("map_classify_tpu")
+def map_classify_tpu(payload: Dict[str, Any], ctx: Dict[str, Any] = None) -> Dict[str, Any]:
+    return run(payload, ctx, op="map_classify_tpu")
+
+
+@register_op("map_classify")
+def map_classify(payload: Dict[str, Any], ctx: Dict[str, Any] = None) -> Dict[str, Any]:
+    return run(payload, ctx, op="map_classify")

@@ -1,0 +1,100 @@
+"""``risk_accumulate`` — streaming count/sum/mean/min/max.
+
+Parity with ``/root/reference/ops/risk_accumulate.py:10-77`` (same output keys,
+same raised ``ValueError`` messages, float64 accumulation, ``bool`` accepted as
+numeric). Large ``values`` lists go through the GPU reduction kernel (K12) when
+a device is present (``RISK_DEVICE=auto|gpu|cpu``); the DP-over-8-GPU variant
+with an RCCL all-reduce lives in :mod:`agent_tpu_amd.parallel.risk`.
+
+Sums are taken with ``math.fsum``-free sequential float64 addition on the CPU
+path so that results are bit-identical to the reference's ``sum()``; the GPU
+path accumulates in fp64 per lane and is exact to rounding order (documented in
+risk_accumulate.CONTRACT.md).
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Any, Dict, List
+
+from . import register_op
+
+GPU_MIN_VALUES = int(os.getenv("RISK_GPU_MIN_VALUES", "1000000"))
+
+
+def to_float(value: Any) -> float:
+    if isinstance(value, (int, float)):
+        return float(value)
+    if isinstance(value, str):
+        return float(value.strip())
+    raise ValueError("value must be numeric")
+
+
+def _gather(payload: Dict[str, Any]) -> List[float]:
+    if "values" in payload:
+        raw = payload.get("values")
+        if not isinstance(raw, list):
+            raise ValueError("payload.values must be a list")
+        return [to_float(v) for v in raw]
+    if "items" in payload:
+        items = payload.get("items")
+        if not isinstance(items, list):
+            raise ValueError("payload.items must be a list")
+        field = payload.get("field", "risk")
+        out: List[float] = []
+        for it in items:
+            if not isinstance(it, dict):
+                raise ValueError("payload.items must contain dict objects")
+            if field in it:
+                out.append(to_float(it[field]))
+        return out
+    raise ValueError("payload must include either 'values' or 'items'")
+
+
+def _stats_cpu(values: List[float]) -> Dict[str, Any]:
+    total = 0.0
+    lo = hi = values[0]
+    for v in values:
+        total += v
+        if v < lo:
+            lo = v
+        if v > hi:
+            hi = v
+    return {"count": len(values), "sum": total, "mean": total / len(values), "min": lo, "max": hi}
+
+
+def _use_gpu(n: int) -> bool:
+    mode = os.getenv("RISK_DEVICE", "auto").strip().lower()
+    if mode == "cpu":
+        return False
+    if mode == "gpu":
+        return True
+    return n >= GPU_MIN_VALUES and _gpu_available()
+
+
+def _gpu_available() -> bool:
+    try:
+        import torch
+
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@register_op("risk_accumulate")
+def risk_accumulate(payload: Dict[str, Any]) -> Dict[str, Any]:
+    t0 = time.time()
+    payload = payload if payload is not None else {}
+    values = _gather(payload)
+    if not values:
+        return {"count": 0, "sum": 0.0, "mean": 0.0, "min": None, "max": None,
+                "compute_time_ms": (time.time() - t0) * 1000.0}
+    if _use_gpu(len(values)):
+        from agent_tpu_amd.ops.reduce import risk_stats
+
+        stats = risk_stats(values)
+        stats["device"] = "gpu"
+    else:
+        stats = _stats_cpu(values)
+    stats["compute_time_ms"] = (time.time() - t0) * 1000.0
+    return stats

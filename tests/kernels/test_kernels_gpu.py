@@ -1,0 +1,197 @@
+"""Numerics of every hand-written HIP kernel vs a plain PyTorch fp32 reference.
+
+Run on a MI355X (``pytest -m gpu``). Tolerances: bf16 I/O with fp32
+accumulation -> compare relative to the output scale.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from agent_tpu_amd import ops
+from agent_tpu_amd.ops.attention import attention_ref
+from agent_tpu_amd.ops.linear import linear_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel_err(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-6)).item()
+
+
+def _rand(shape, dev, scale=1.0, dtype=torch.bfloat16, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(shape, generator=g) * scale).to(dtype).to(dev)
+
+
+# ------------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("M,N,K", [(256, 768, 768), (300, 2304, 768), (128, 100, 64), (512, 768, 3072),
+                                   (1000, 3072, 768)])
+@pytest.mark.parametrize("act,use_bias,use_res", [(None, True, False), ("gelu", True, False),
+                                                  ("tanh", True, False), (None, True, True), (None, False, False)])
+def test_gemm_epilogues(gpu, M, N, K, act, use_bias, use_res):
+    x = _rand((M, K), gpu, seed=1)
+    w = _rand((N, K), gpu, 0.05, seed=2)
+    b = _rand((N,), gpu, 0.1, torch.float32, seed=3) if use_bias else None
+    r = _rand((M, N), gpu, seed=4) if use_res else None
+    y = ops.linear(x, w, b, act=act, residual=r)
+    ref = linear_ref(x.cpu(), w.cpu(), None if b is None else b.cpu(), act, None if r is None else r.cpu())
+    assert _rel_err(y, ref) < 2e-2
+
+
+def test_gemm_exact_integers_asymmetric(gpu):
+    # {-1,0,1} operands: every partial sum is an exact small integer in fp32 and bf16
+    g = torch.Generator().manual_seed(7)
+    M, N, K = 256, 384, 192
+    x = torch.randint(-1, 2, (M, K), generator=g).to(torch.bfloat16)
+    w = torch.randint(-1, 2, (N, K), generator=g).to(torch.bfloat16)
+    y = ops.linear(x.to(gpu), w.to(gpu)).cpu().float()
+    assert torch.equal(y, x.float() @ w.float().t())
+    # A = I picks rows of W^T: catches row/col swaps in the C write
+    eye = torch.eye(128).to(torch.bfloat16)
+    w2 = torch.arange(256 * 128).remainder(17).sub(8).view(256, 128).to(torch.bfloat16)
+    y2 = ops.linear(eye.to(gpu), w2.to(gpu)).cpu().float()
+    assert torch.equal(y2, w2.float().t())
+
+
+def test_gemm_strided_rows(gpu):
+    # pooler case: A rows taken every S rows (CLS tokens) of a [B*S, H] tensor
+    B, S, H = 37, 128, 768
+    h = _rand((B * S, H), gpu, seed=5)
+    cls = h.view(B, S, H)[:, 0, :]
+    w = _rand((H, H), gpu, 0.05, seed=6)
+    b = _rand((H,), gpu, 0.1, torch.float32, seed=7)
+    y = ops.linear(cls, w, b, act="tanh")
+    ref = linear_ref(cls.cpu(), w.cpu(), b.cpu(), "tanh")
+    assert _rel_err(y, ref) < 2e-2
+
+
+# -------------------------------------------------------------- attention
+@pytest.mark.parametrize("B,S,H", [(3, 128, 12), (2, 64, 4), (2, 200, 2), (1, 512, 2)])
+def test_attention_packed(gpu, B, S, H):
+    qkv = _rand((B * S, 3 * H * 64), gpu, seed=11)
+    lens = torch.tensor([S - 7 * i for i in range(B)], dtype=torch.int32).clamp(min=2)
+    out = ops.attention_packed(qkv, lens.to(gpu), B, S, H)
+    hd = H * 64
+    qc = qkv.cpu()
+    ref = attention_ref(qc[:, :hd], qc[:, hd:2 * hd], qc[:, 2 * hd:], lens, B, S, S, H, 1 / math.sqrt(64))
+    assert _rel_err(out, ref) < 2e-2
+
+
+def test_attention_spike_forces_rescale(gpu):
+    # one huge key late in the sequence forces the online-softmax rescale branch
+    B, S, H = 1, 256, 1
+    qkv = _rand((B * S, 3 * 64), gpu, 0.5, seed=12).float()
+    qkv[:, :64] = 1.0
+    qkv[200, 64:128] = 8.0  # key 200 dominates every query in chunk 2
+    qkv = qkv.to(torch.bfloat16)
+    lens = torch.tensor([S], dtype=torch.int32)
+    out = ops.attention_packed(qkv, lens.to(gpu), B, S, H)
+    qc = qkv.cpu()
+    ref = attention_ref(qc[:, :64], qc[:, 64:128], qc[:, 128:], lens, B, S, S, H, 1 / 8)
+    assert _rel_err(out, ref) < 2e-2
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_attention_strided_bias_causal(gpu, causal):
+    B, Sq, Skv, H = 2, 96, 160, 3
+    q = _rand((B * Sq, H * 64), gpu, seed=13)
+    kv = _rand((B * Skv, 2 * H * 64), gpu, seed=14)
+    k, v = kv[:, :H * 64], kv[:, H * 64:]
+    bias = _rand((H, Sq, Skv), gpu, 1.0, torch.float32, seed=15)
+    lens = torch.tensor([Skv, 100], dtype=torch.int32)
+    out = ops.attention(q, k, v, lens.to(gpu), B, Sq, Skv, H, scale=1.0, bias=bias, causal=causal)
+    ref = attention_ref(q.cpu(), k.cpu(), v.cpu(), lens, B, Sq, Skv, H, 1.0, bias.cpu(), causal)
+    assert _rel_err(out, ref) < 2e-2
+
+
+# ------------------------------------------------------------ norms/embed
+@pytest.mark.parametrize("N", [256, 768, 1024])
+def test_layernorm_residual(gpu, N):
+    x = _rand((1000, N), gpu, 2.0, seed=21)
+    r = _rand((1000, N), gpu, seed=22)
+    g = _rand((N,), gpu, 1.0, torch.float32, seed=23)
+    b = _rand((N,), gpu, 1.0, torch.float32, seed=24)
+    y = ops.layernorm(x, g, b, 1e-12, residual=r)
+    ref = torch.nn.functional.layer_norm(x.cpu().float() + r.cpu().float(), (N,), g.cpu(), b.cpu(), 1e-12)
+    assert _rel_err(y, ref) < 1e-2
+
+
+def test_rmsnorm(gpu):
+    x = _rand((333, 768), gpu, 3.0, seed=25)
+    g = _rand((768,), gpu, 1.0, torch.float32, seed=26)
+    y = ops.rmsnorm(x, g, 1e-6)
+    xf = x.cpu().float()
+    ref = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-6) * g.cpu()
+    assert _rel_err(y, ref) < 1e-2
+
+
+def test_embed_layernorm_and_gather(gpu):
+    V, N, B, S = 1000, 768, 4, 128
+    word, pos, typ = _rand((V, N), gpu, seed=31), _rand((512, N), gpu, seed=32), _rand((2, N), gpu, seed=33)
+    g = _rand((N,), gpu, 1.0, torch.float32, seed=34)
+    b = _rand((N,), gpu, 1.0, torch.float32, seed=35)
+    ids = torch.randint(0, V, (B, S), dtype=torch.int32)
+    y = ops.embed_layernorm(ids.to(gpu), word, pos, typ, g, b, 1e-12)
+    ref = ops.embed_layernorm(ids, word.cpu().float(), pos.cpu().float(), typ.cpu().float(), g.cpu(), b.cpu(), 1e-12)
+    assert _rel_err(y, ref) < 1e-2
+    e = ops.embed_gather(ids.to(gpu), word)
+    assert torch.equal(e.cpu(), word.cpu()[ids.view(-1).long()])
+
+
+# -------------------------------------------------------------- tokenizer
+def test_tokenizer_gpu_matches_python_and_host(gpu, nat):
+    from agent_tpu_amd import tokenizer as T
+    from agent_tpu_amd.utils.synthetic import make_text_rows
+
+    rows = make_text_rows(300, words_per_row=40, seed=3)
+    rows += ["", "   ", "Hello, WORLD!!", "x" * 100, "naïve café — 東京 ok", "a\tb\nc\x01d", "(" * 300]
+    text, offs = T.pack_rows(rows)
+    for S in (8, 128):
+        ids_py, lens_py = T.tokenize_rows([r.encode() for r in rows], S, 30522, 2048)
+        ids_h, lens_h = nat.tokenize_host(text, offs, S, 30522, 2048)
+        ids_g, lens_g = ops.tokenize(torch.from_numpy(text).to(gpu), torch.from_numpy(offs).to(gpu), S, 30522, 2048)
+        np.testing.assert_array_equal(ids_h, ids_py)
+        np.testing.assert_array_equal(lens_h, lens_py)
+        np.testing.assert_array_equal(ids_g.cpu().numpy(), ids_py)
+        np.testing.assert_array_equal(lens_g.cpu().numpy(), lens_py)
+
+
+# ------------------------------------------------------------------- head
+@pytest.mark.parametrize("C,k", [(2, 2), (10, 5), (1000, 5), (3, 1)])
+def test_head_topk(gpu, C, k):
+    B, N = 50, 768
+    pooled = _rand((B, N), gpu, seed=41)
+    Wc = _rand((C, N), gpu, 0.05, seed=42)
+    bc = _rand((C,), gpu, 0.1, torch.float32, seed=43)
+    logits, idx, sc = ops.classify_head_topk(pooled, Wc, bc, k)
+    rl, ri, rs = ops.classify_head_topk(pooled.cpu(), Wc.cpu(), bc.cpu(), k)
+    assert _rel_err(logits, rl) < 1e-3
+    torch.testing.assert_close(sc.cpu(), rs, atol=2e-4, rtol=1e-3)
+    # indices equal wherever the top-k scores are well separated
+    gap_ok = (rs[:, :-1] - rs[:, 1:]).abs().min(dim=1).values > 1e-3 if k > 1 else torch.ones(B, dtype=torch.bool)
+    assert torch.equal(idx.cpu()[gap_ok], ri[gap_ok])
+
+
+def test_head_ties_lower_index_first(gpu):
+    B, N, C = 2, 64, 6
+    pooled = torch.zeros((B, N), dtype=torch.bfloat16, device=gpu)
+    Wc = torch.zeros((C, N), dtype=torch.bfloat16, device=gpu)
+    bc = torch.tensor([0.0, 1.0, 1.0, 0.5, 1.0, 0.0], device=gpu)
+    _, idx, _ = ops.classify_head_topk(pooled, Wc, bc, 4)
+    assert idx.cpu().tolist() == [[1, 2, 4, 3]] * 2
+
+
+# ----------------------------------------------------------------- reduce
+@pytest.mark.parametrize("n", [1, 1000, 3_000_001])
+def test_reduce_stats(gpu, n):
+    g = torch.Generator().manual_seed(n)
+    x = torch.randn(n, generator=g, dtype=torch.float64) * 10 + 3
+    out = ops.reduce_stats_tensor(x.to(gpu)).cpu()
+    assert out[0].item() == n
+    assert math.isclose(out[1].item(), x.sum().item(), rel_tol=1e-12, abs_tol=1e-9)
+    assert out[2].item() == x.min().item() and out[3].item() == x.max().item()
+    out32 = ops.reduce_stats_tensor(x.float().to(gpu)).cpu()
+    assert math.isclose(out32[1].item(), x.float().double().sum().item(), rel_tol=1e-10, abs_tol=1e-6)
