@@ -26,6 +26,10 @@
 #include "atpu/common.h"
 #include "atpu/kernels.h"
 
+#include <cstdlib>
+#include <string>
+#include <type_traits>
+
 namespace atpu {
 namespace {
 
@@ -143,7 +147,7 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
       }
       if constexpr (EPI & kEpiGelu) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+        for (int e = 0; e < 4; ++e) v[e] = gelu_fast(v[e]);
       }
       if constexpr (EPI & kEpiTanh) {
 #pragma unroll
@@ -161,6 +165,221 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
     }
   }
 }
+
+// ============================================================================
+// 256x256 tile, 8 waves, FULL-LINE staging (kernel "256b").
+//
+// The ablation of the ring kernel showed the LDS-DMA instructions themselves
+// costing ~40 % of the MFMA rate; its k-half chunks had 64-byte rows, so every
+// 1 KiB DMA instruction touched 16 half-used 128-byte lines. Here a K-tile
+// (BK = 64) is split by ROWS into four 16 KiB chunks [A rows 0-127 | A rows
+// 128-255 | B rows 0-127 | B rows 128-255] of 128-byte rows: one DMA
+// instruction = 8 full lines. Row swizzle c ^ ((r>>1)&7) (conflict-free for the
+// ds_read_b128 lane groups, see gemm_bf16 128x128 kernel). Wave (wm, wn) reads
+// only chunk A[wm] and chunk B[wn>>1].
+// Schedule per K-tile t (buffer t&1, two 64 KiB buffers):
+//   SYNC(t): vmcnt(0) + barrier  -> tile t landed, every wave done with t-1
+//   issue tile t+1 (8 DMA/wave) into the other buffer, interleaved into R1
+//   R1..R4: 4 MFMA clusters of 16 with the next cluster's fragment reads
+//           interleaved (k32 step x row half of the wave tile)
+// ============================================================================
+namespace g2 {
+constexpr int kChunk = 16384;    // 128 rows x 128 B
+constexpr int kTile = 4 * kChunk;
+__device__ __forceinline__ int sw(int r, int c) { return c ^ ((r >> 1) & 7); }
+}  // namespace g2
+
+// DBG: timing-only ablation builds (results are WRONG): 1 = no vmcnt/barrier
+// waits, 2 = no global->LDS DMA. See docs/PERF_NOTES.md.
+template <int EPI, int DBG = 0>
+__global__ __launch_bounds__(512, 2) void gemm256b_kernel(
+    const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C, int ldc,
+    const float* __restrict__ bias, const bf16* __restrict__ R, int ldr, int M, int N, int K) {
+  using namespace g2;
+  __shared__ __attribute__((aligned(16))) char lds[2 * kTile];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntn = N / 256, ntm = (M + 255) / 256;
+  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
+  const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 256;
+
+  // staging: chunk q (0..3) = (A|B) x (row half); this wave issues
+  // instructions i = wave, wave + 8 of each chunk (8 rows x 128 B each)
+  const int srow = lane >> 3, spos = lane & 7;
+  const int lr0 = wave * 8 + srow, lr1 = (wave + 8) * 8 + srow;  // local rows 0..127
+  const bf16* src[4][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    src[h][0] = A + (size_t)min(m0 + h * 128 + lr0, M - 1) * lda + sw(lr0, spos) * 8;
+    src[h][1] = A + (size_t)min(m0 + h * 128 + lr1, M - 1) * lda + sw(lr1, spos) * 8;
+    src[2 + h][0] = Bt + (size_t)(n0 + h * 128 + lr0) * ldb + sw(lr0, spos) * 8;
+    src[2 + h][1] = Bt + (size_t)(n0 + h * 128 + lr1) * ldb + sw(lr1, spos) * 8;
+  }
+  auto issue_tile = [&](int kt, int buf) {
+    if constexpr (DBG & 2) return;
+    char* base = lds + buf * kTile;
+    const int koff = kt * 64;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      glds16(src[q][0] + koff, base + q * kChunk + wave * 1024);
+      glds16(src[q][1] + koff, base + q * kChunk + (wave + 8) * 1024);
+    }
+  };
+
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr = lane & 15, fc = lane >> 4;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto load_b = [&](bf16x8 (&f)[4], int buf, int ks) {
+    const char* img = lds + buf * kTile + (2 + (wn >> 1)) * kChunk;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = (wn & 1) * 64 + j * 16 + fr;
+      f[j] = *reinterpret_cast<const bf16x8*>(img + r * 128 + sw(r, ks * 4 + fc) * 16);
+    }
+  };
+  auto load_a = [&](bf16x8 (&f)[4], int buf, int ks, int qm) {
+    const char* img = lds + buf * kTile + wm * kChunk;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = qm * 64 + i * 16 + fr;
+      f[i] = *reinterpret_cast<const bf16x8*>(img + r * 128 + sw(r, ks * 4 + fc) * 16);
+    }
+  };
+  auto mma = [&](const bf16x8 (&bfr)[4], const bf16x8 (&afr)[4], int qm) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[qm * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], afr[i], acc[qm * 4 + i][j], 0, 0, 0);
+  };
+#define ATPU_INTERLEAVE(NREAD)                                           \
+  _Pragma("unroll") for (int q = 0; q < (NREAD); ++q) {                  \
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                   \
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                   \
+  }                                                                      \
+  __builtin_amdgcn_sched_group_barrier(0x008, 16 - (NREAD), 0)
+
+  const int nk = K / 64;
+  bf16x8 b0[4], b1[4], a00[4], a01[4], a10[4], a11[4];
+  issue_tile(0, 0);
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    if constexpr (!(DBG & 1)) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    load_b(b0, cur, 0);
+    load_a(a00, cur, 0, 0);
+    if (t + 1 < nk) issue_tile(t + 1, cur ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(b0, a00, 0);
+    load_a(a01, cur, 0, 1);
+    ATPU_INTERLEAVE(4);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(b0, a01, 1);
+    load_b(b1, cur, 1);
+    load_a(a10, cur, 1, 0);
+    ATPU_INTERLEAVE(8);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(b1, a10, 0);
+    load_a(a11, cur, 1, 1);
+    ATPU_INTERLEAVE(4);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(b1, a11, 1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#undef ATPU_INTERLEAVE
+
+  f32x4 bv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wn * 64 + j * 16 + fc * 4;
+    if constexpr (EPI & kEpiBias) bv[j] = *reinterpret_cast<const f32x4*>(bias + n);
+    else bv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    bf16x4 res[4][4];
+    if constexpr (EPI & kEpiResidual) {
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int m = min(m0 + wm * 128 + (half * 4 + ii) * 16 + fr, M - 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          res[ii][j] = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + n0 + wn * 64 + j * 16 + fc * 4);
+      }
+    }
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const int i = half * 4 + ii;
+      const int m = m0 + wm * 128 + i * 16 + fr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + fc * 4;
+        f32x4 v = acc[i][j] + bv[j];
+        if constexpr (EPI & kEpiGelu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = gelu_fast(v[e]);
+        }
+        if constexpr (EPI & kEpiTanh) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
+        }
+        if constexpr (EPI & kEpiResidual) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += bf2f(res[ii][j][e]);
+        }
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+        if (m < M) *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
+      }
+    }
+  }
+}
+
+
+void launch_256b(const GemmArgs& g, hipStream_t s) {
+  const int nb = ((g.M + 255) / 256) * (g.N / 256);
+  static const int ablate = [] {
+    const char* f = std::getenv("ATPU_GEMM_ABLATE");
+    return f ? std::atoi(f) : 0;
+  }();
+  if (ablate && g.epi == (kEpiBias | kEpiResidual)) {
+#define ATPU_ABL(D)                                                                                              \
+  case D:                                                                                                        \
+    hipLaunchKernelGGL((gemm256b_kernel<kEpiBias | kEpiResidual, D>), dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, \
+                       g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K);                                   \
+    return;
+    switch (ablate) {
+      ATPU_ABL(1) ATPU_ABL(2) ATPU_ABL(3)
+      default: break;
+    }
+#undef ATPU_ABL
+  }
+#define ATPU_G256B(E)                                                                                     \
+  case E:                                                                                                 \
+    hipLaunchKernelGGL((gemm256b_kernel<E>), dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, \
+                       g.bias, g.R, g.ldr, g.M, g.N, g.K);                                                \
+    break;
+  switch (g.epi) {
+    ATPU_G256B(0)
+    ATPU_G256B(kEpiBias)
+    ATPU_G256B(kEpiBias | kEpiGelu)
+    ATPU_G256B(kEpiBias | kEpiTanh)
+    ATPU_G256B(kEpiBias | kEpiResidual)
+    ATPU_G256B(kEpiResidual)
+    ATPU_G256B(kEpiGelu)
+    default:
+      throw std::invalid_argument("atpu: unsupported GEMM epilogue " + std::to_string(g.epi));
+  }
+#undef ATPU_G256B
+}
+
+
 
 template <int BM, int BN, int WM, int WN>
 void launch_tile(const GemmArgs& g, hipStream_t s) {
@@ -196,7 +415,21 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
              "gemm: A/Bt must be 16-byte aligned");
   ATPU_CHECK(!(g.epi & kEpiBias) || g.bias, "gemm: bias epilogue without bias");
   ATPU_CHECK(!(g.epi & kEpiResidual) || (g.R && g.ldr % 4 == 0), "gemm: residual epilogue without R");
-  launch_tile<128, 128, 2, 2>(g, stream);
+  // 256x256 tiles once the grid fills the chip several times over; the 128x128
+  // kernel (2 blocks/CU) covers small M (pooler, decode) and odd N.
+  // 256x256 full-line-staged kernel once the grid fills the chip several
+  // times over; the 128x128 kernel (2 blocks/CU) covers small M and odd N.
+  // ATPU_GEMM_TILE=128|256 forces one (benchmarks/tests).
+  static const int forced = [] {
+    const char* f = std::getenv("ATPU_GEMM_TILE");
+    return f ? std::atoi(f) : 0;
+  }();
+  const bool big_ok = g.N % 256 == 0;
+  const bool use_big = forced ? (forced == 256 && big_ok) : (g.M >= 2048 && big_ok);
+  if (use_big)
+    launch_256b(g, stream);
+  else
+    launch_tile<128, 128, 2, 2>(g, stream);
   ATPU_HIP_CHECK(hipGetLastError());
 }
 

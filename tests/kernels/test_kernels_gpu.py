@@ -28,7 +28,8 @@ def _rand(shape, dev, scale=1.0, dtype=torch.bfloat16, seed=0):
 
 # ------------------------------------------------------------------- GEMM
 @pytest.mark.parametrize("M,N,K", [(256, 768, 768), (300, 2304, 768), (128, 100, 64), (512, 768, 3072),
-                                   (1000, 3072, 768)])
+                                   (1000, 3072, 768), (4096, 768, 768), (2500, 2304, 768), (2048, 768, 3072),
+                                   (3000, 3072, 768), (2304, 256, 128)])
 @pytest.mark.parametrize("act,use_bias,use_res", [(None, True, False), ("gelu", True, False),
                                                   ("tanh", True, False), (None, True, True), (None, False, False)])
 def test_gemm_epilogues(gpu, M, N, K, act, use_bias, use_res):
@@ -54,6 +55,19 @@ def test_gemm_exact_integers_asymmetric(gpu):
     w2 = torch.arange(256 * 128).remainder(17).sub(8).view(256, 128).to(torch.bfloat16)
     y2 = ops.linear(eye.to(gpu), w2.to(gpu)).cpu().float()
     assert torch.equal(y2, w2.float().t())
+
+
+def test_gemm256_exact_integers(gpu):
+    # the 256x256 pipelined kernel on exact data: M not a multiple of 256, many K-tiles
+    g = torch.Generator().manual_seed(8)
+    M, N, K = 2600, 512, 1024
+    x = torch.randint(-1, 2, (M, K), generator=g).to(torch.bfloat16)
+    w = torch.randint(-1, 2, (N, K), generator=g).to(torch.bfloat16)
+    b = torch.randint(-4, 5, (N,), generator=g).float()
+    r = torch.randint(-3, 4, (M, N), generator=g).to(torch.bfloat16)
+    y = ops.linear(x.to(gpu), w.to(gpu), b.to(gpu), residual=r.to(gpu)).cpu().float()
+    ref = (x.float() @ w.float().t() + b + r.float()).to(torch.bfloat16).float()
+    assert torch.equal(y, ref)
 
 
 def test_gemm_strided_rows(gpu):

@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Per-kernel microbenchmarks at the BERT-base S=128 shapes (random data).
+
+Interleaved rounds in one process (guide §5.4 rule 24): each variant is timed
+with hipEvents over `iters` launches, the round order alternates, and the
+median is reported. Compares the hand-written kernels against the library
+(hipBLASLt via torch.matmul, torch SDPA) on identical inputs.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import statistics
+import sys
+import os
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from agent_tpu_amd import ops  # noqa: E402
+
+
+def timeit(fn, iters=20):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=1024)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    M = a.rows * 128
+    H, I = 768, 3072
+    g = torch.Generator(device=dev).manual_seed(0)
+
+    def r(*shape, scale=1.0, dtype=torch.bfloat16):
+        return (torch.randn(*shape, generator=g, device=dev) * scale).to(dtype)
+
+    x768, x3072 = r(M, H), r(M, I)
+    wqkv, wo, w1, w2 = r(3 * H, H, scale=0.03), r(H, H, scale=0.03), r(I, H, scale=0.03), r(H, I, scale=0.03)
+    bqkv, bo, b1, b2 = (r(n, scale=0.1, dtype=torch.float32) for n in (3 * H, H, I, H))
+    res = r(M, H)
+    out = {}
+    cases = {
+        "gemm_qkv": (lambda: ops.linear(x768, wqkv, bqkv), lambda: torch.addmm(bqkv.bfloat16(), x768, wqkv.t()),
+                     2 * M * H * 3 * H),
+        "gemm_o_res": (lambda: ops.linear(x768, wo, bo, residual=res),
+                       lambda: torch.addmm(bo.bfloat16(), x768, wo.t()).add_(res), 2 * M * H * H),
+        "gemm_ffn1_gelu": (lambda: ops.linear(x768, w1, b1, act="gelu"),
+                           lambda: torch.nn.functional.gelu(torch.addmm(b1.bfloat16(), x768, w1.t())), 2 * M * H * I),
+        "gemm_ffn2_res": (lambda: ops.linear(x3072, w2, b2, residual=res),
+                          lambda: torch.addmm(b2.bfloat16(), x3072, w2.t()).add_(res), 2 * M * I * H),
+    }
+    qkv = r(M, 3 * H)
+    lens = torch.full((a.rows,), 128, dtype=torch.int32, device=dev)
+    q4 = qkv[:, :H].view(a.rows, 128, 12, 64).transpose(1, 2)
+    k4 = qkv[:, H:2 * H].view(a.rows, 128, 12, 64).transpose(1, 2)
+    v4 = qkv[:, 2 * H:].view(a.rows, 128, 12, 64).transpose(1, 2)
+    cases["attention"] = (lambda: ops.attention_packed(qkv, lens, a.rows, 128, 12),
+                          lambda: torch.nn.functional.scaled_dot_product_attention(q4, k4, v4),
+                          4 * a.rows * 12 * 128 * 128 * 64)
+    gam, bet = r(H, dtype=torch.float32), r(H, dtype=torch.float32)
+    cases["layernorm"] = (lambda: ops.layernorm(x768, gam, bet, 1e-12),
+                          lambda: torch.nn.functional.layer_norm(x768, (H,), gam.bfloat16(), bet.bfloat16(), 1e-12),
+                          0)
+    sel = [k for k in cases if not a.only or k in a.only.split(",")]
+    times = {k: {"ours": [], "lib": []} for k in sel}
+    for rd in range(a.rounds):
+        for k in (sel if rd % 2 == 0 else list(reversed(sel))):
+            ours, lib, _ = cases[k]
+            times[k]["ours"].append(timeit(ours, a.iters))
+            times[k]["lib"].append(timeit(lib, a.iters))
+    for k in sel:
+        fl = cases[k][2]
+        o, l = statistics.median(times[k]["ours"]), statistics.median(times[k]["lib"])
+        out[k] = {"ours_ms": round(o, 4), "lib_ms": round(l, 4), "speedup_vs_lib": round(l / o, 3)}
+        if fl:
+            out[k]["ours_tflops"] = round(fl / o / 1e9, 1)
+            out[k]["lib_tflops"] = round(fl / l / 1e9, 1)
+        print(k, json.dumps(out[k]), flush=True)
+    print("JSON", json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
