@@ -74,6 +74,30 @@ PYBIND11_MODULE(_atpu, m) {
   m.attr("EPI_GELU") = static_cast<int>(kEpiGelu);
   m.attr("EPI_TANH") = static_cast<int>(kEpiTanh);
   m.attr("EPI_RESIDUAL") = static_cast<int>(kEpiResidual);
+  m.attr("EPI_RELU") = static_cast<int>(kEpiRelu);
+  m.attr("EPI_OUT_F32") = static_cast<int>(kEpiOutF32);
+  m.def("decode_attention", [](uintptr_t q, int ldq, uintptr_t k, uintptr_t v, int ldkv, int seq_stride, int group,
+                               uintptr_t lens, uintptr_t step_dev, uintptr_t bias, int bias_stride, uintptr_t out,
+                               int ldo, int rows, int H, float scale, uintptr_t stream) {
+    decode_attention(P<const bf16>(q), ldq, P<const bf16>(k), P<const bf16>(v), ldkv, seq_stride, group,
+                     P<const int32_t>(lens), P<const int32_t>(step_dev), P<const float>(bias), bias_stride, P<bf16>(out),
+                     ldo, rows, H, scale, S(stream));
+  });
+  m.def("kv_append", [](uintptr_t src, int lds, int col0, int ncols, uintptr_t cache, int seq_stride, int ldc,
+                        uintptr_t step_dev, int rows, uintptr_t stream) {
+    kv_append(P<const bf16>(src), lds, col0, ncols, P<bf16>(cache), seq_stride, ldc, P<const int32_t>(step_dev), rows,
+              S(stream));
+  });
+  m.def("gather_rows", [](uintptr_t src, uintptr_t dst, uintptr_t parent, int nrows, int seq_stride, int ldc,
+                          uintptr_t step_dev, int slabs, size_t slab_elems, uintptr_t stream) {
+    gather_rows(P<const bf16>(src), P<bf16>(dst), P<const int32_t>(parent), nrows, seq_stride, ldc,
+                P<const int32_t>(step_dev), slabs, slab_elems, S(stream));
+  });
+  m.def("beam_topk_rows", [](uintptr_t logits, int rows, int V, uintptr_t beam_scores, int eos, int mask_eos, int K,
+                             uintptr_t out_score, uintptr_t out_token, uintptr_t stream) {
+    beam_topk_rows(P<const float>(logits), rows, V, P<const float>(beam_scores), eos, mask_eos, K, P<float>(out_score),
+                   P<int32_t>(out_token), S(stream));
+  });
 
   m.def("attention", [](uintptr_t qkv, uintptr_t lens, uintptr_t bias, uintptr_t out, int B, int Sq, int H, int D,
                         float scale, uintptr_t stream) {

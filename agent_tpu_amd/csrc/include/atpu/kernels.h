@@ -17,6 +17,8 @@ enum GemmEpilogue : int {
   kEpiGelu = 2,
   kEpiTanh = 4,
   kEpiResidual = 8,
+  kEpiRelu = 16,
+  kEpiOutF32 = 32,  // C is float* (128x128 kernel only; LM-head logits)
 };
 
 struct GemmArgs {
@@ -33,6 +35,21 @@ struct GemmArgs {
   int epi = 0;
 };
 void gemm_bf16(const GemmArgs& g, hipStream_t stream);
+
+// ------------------------------------------------------------ decode (K9-K11)
+// One query row per (row, head) against a KV cache. Key j of row r lives at
+// k/v + ((r / group) * seq_stride + j) * ldkv + h*64. Length: lens[r / group],
+// or *step_dev + 1 when lens is null. bias_dist (fp32 [H, bias_stride]) adds
+// bias_dist[h][len-1-j] (T5 decoder relative position bias).
+void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int ldkv, int seq_stride, int group,
+                      const int32_t* lens, const int32_t* step_dev, const float* bias_dist, int bias_stride, bf16* out,
+                      int ldo, int rows, int H, float scale, hipStream_t stream);
+void kv_append(const bf16* src, int lds, int col0, int ncols, bf16* cache, int seq_stride, int ldc,
+               const int32_t* step_dev, int rows, hipStream_t stream);
+void gather_rows(const bf16* src, bf16* dst, const int32_t* parent, int nrows, int seq_stride, int ldc,
+                 const int32_t* step_dev, int slabs, size_t slab_elems, hipStream_t stream);
+void beam_topk_rows(const float* logits, int rows, int V, const float* beam_scores, int eos, int mask_eos, int K,
+                    float* out_score, int32_t* out_token, hipStream_t stream);
 
 // ------------------------------------------------------------- attention (K4)
 // qkv: [B*S, 3*H*D] packed per token as [q(H*D) | k(H*D) | v(H*D)];

@@ -153,15 +153,23 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
       }
+      if constexpr (EPI & kEpiRelu) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
       if constexpr (EPI & kEpiResidual) {
         const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + n);
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] += bf2f(r[e]);
       }
-      bf16x4 o;
+      if constexpr (EPI & kEpiOutF32) {
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + (size_t)m * ldc + n) = v;
+      } else {
+        bf16x4 o;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
-      *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
+        for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+        *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
+      }
     }
   }
 }
@@ -328,6 +336,10 @@ __global__ __launch_bounds__(512, 2) void gemm256b_kernel(
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
         }
+        if constexpr (EPI & kEpiRelu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
         if constexpr (EPI & kEpiResidual) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] += bf2f(res[ii][j][e]);
@@ -373,6 +385,7 @@ void launch_256b(const GemmArgs& g, hipStream_t s) {
     ATPU_G256B(kEpiBias | kEpiResidual)
     ATPU_G256B(kEpiResidual)
     ATPU_G256B(kEpiGelu)
+    ATPU_G256B(kEpiRelu)
     default:
       throw std::invalid_argument("atpu: unsupported GEMM epilogue " + std::to_string(g.epi));
   }
@@ -398,6 +411,9 @@ void launch_tile(const GemmArgs& g, hipStream_t s) {
     ATPU_GEMM_CASE(kEpiBias | kEpiResidual)
     ATPU_GEMM_CASE(kEpiResidual)
     ATPU_GEMM_CASE(kEpiGelu)
+    ATPU_GEMM_CASE(kEpiRelu)
+    ATPU_GEMM_CASE(kEpiOutF32)
+    ATPU_GEMM_CASE(kEpiBias | kEpiOutF32)
     default:
       throw std::invalid_argument("atpu: unsupported GEMM epilogue " + std::to_string(g.epi));
   }
@@ -411,6 +427,7 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
   ATPU_CHECK(g.K % kBK == 0, "gemm: K must be a multiple of 64");
   ATPU_CHECK(g.N % 4 == 0, "gemm: N must be a multiple of 4");
   ATPU_CHECK(g.lda % 8 == 0 && g.ldb % 8 == 0 && g.ldc % 4 == 0, "gemm: leading dims must keep 16-B rows");
+  ATPU_CHECK(!((g.epi & kEpiRelu) && (g.epi & (kEpiGelu | kEpiTanh))), "gemm: one activation at most");
   ATPU_CHECK((reinterpret_cast<uintptr_t>(g.A) & 15) == 0 && (reinterpret_cast<uintptr_t>(g.Bt) & 15) == 0,
              "gemm: A/Bt must be 16-byte aligned");
   ATPU_CHECK(!(g.epi & kEpiBias) || g.bias, "gemm: bias epilogue without bias");
@@ -425,7 +442,7 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
     return f ? std::atoi(f) : 0;
   }();
   const bool big_ok = g.N % 256 == 0;
-  const bool use_big = forced ? (forced == 256 && big_ok) : (g.M >= 2048 && big_ok);
+  const bool use_big = !(g.epi & kEpiOutF32) && (forced ? (forced == 256 && big_ok) : (g.M >= 2048 && big_ok));
   if (use_big)
     launch_256b(g, stream);
   else

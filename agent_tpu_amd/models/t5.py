@@ -1,0 +1,275 @@
+"""T5 encoder-decoder on the gfx950 kernels (map_summarize, BASELINE config 4).
+
+Replaces the reference's CPU ``BartForConditionalGeneration.generate``
+(``/root/reference/ops/map_summarize.py:52-59``) with an explicit HIP path:
+
+  encoder  : gather (K8) -> L x [RMSNorm, fused QKV GEMM, attention with the
+             T5 bidirectional relative-position bias (K4 bias path), O-proj +
+             residual (GEMM epilogue), RMSNorm, FFN ReLU (epilogue), FFN2 +
+             residual] -> RMSNorm -> ONE GEMM producing every decoder layer's
+             cross-attention K/V ([B*S, L*2d]).
+  decoder  : per generated token, L x [RMSNorm, QKV GEMM, KV-cache append,
+             single-query attention over the cache with the causal distance
+             bias (K9), O-proj + residual, RMSNorm, cross Q GEMM, single-query
+             cross attention over the encoder K/V (beams share their item's
+             rows), O-proj + residual, RMSNorm, FFN] -> RMSNorm -> LM-head GEMM
+             with fp32 logits -> fused log-softmax/top-k (K10).
+
+Parameter names follow HF ``T5ForConditionalGeneration`` (Linear weights are
+``[out, in]``) so :func:`from_hf_state_dict` is a rename + concat; T5 uses no
+Linear biases, unscaled attention and RMSNorm (eps 1e-6). The tied LM head is
+stored pre-scaled by ``d_model**-0.5`` (what HF applies at run time).
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+
+from .. import ops
+from .params import ParamPack
+
+
+@dataclass(frozen=True)
+class T5Config:
+    vocab_size: int = 32128
+    d_model: int = 768
+    d_kv: int = 64
+    d_ff: int = 3072
+    heads: int = 12
+    enc_layers: int = 12
+    dec_layers: int = 12
+    buckets: int = 32
+    max_distance: int = 128
+    eps: float = 1e-6
+    pad_id: int = 0
+    eos_id: int = 1
+    decoder_start_id: int = 0
+    tie_embeddings: bool = True
+
+    def param_count(self) -> int:
+        d, f = self.d_model, self.d_ff
+        enc = self.enc_layers * (4 * d * d + 2 * d * f + 2 * d)
+        dec = self.dec_layers * (8 * d * d + 2 * d * f + 3 * d)
+        return self.vocab_size * d + enc + dec + 2 * d + 2 * self.buckets * self.heads
+
+
+PRESETS: Dict[str, T5Config] = {
+    "t5-base": T5Config(),
+    "t5-small": T5Config(d_model=512, d_ff=2048, heads=8, enc_layers=6, dec_layers=6),
+    "t5-tiny": T5Config(vocab_size=4096, d_model=256, d_ff=1024, heads=4, enc_layers=2, dec_layers=2),
+}
+
+
+def config_for(name: str, **overrides) -> T5Config:
+    if name not in PRESETS:
+        raise ValueError(f"unknown T5 preset {name!r}; known: {sorted(PRESETS)}")
+    return dataclasses.replace(PRESETS[name], **overrides)
+
+
+def param_specs(cfg: T5Config):
+    d, f, bf, f32 = cfg.d_model, cfg.d_ff, torch.bfloat16, torch.float32
+    yield "shared", (cfg.vocab_size, d), bf
+    yield "enc.rel", (cfg.buckets, cfg.heads), f32
+    for i in range(cfg.enc_layers):
+        p = f"enc.l{i}."
+        yield p + "ln1", (d,), f32
+        yield p + "qkv", (3 * d, d), bf
+        yield p + "o", (d, d), bf
+        yield p + "ln2", (d,), f32
+        yield p + "wi", (f, d), bf
+        yield p + "wo", (d, f), bf
+    yield "enc.ln_f", (d,), f32
+    yield "dec.rel", (cfg.buckets, cfg.heads), f32
+    for i in range(cfg.dec_layers):
+        p = f"dec.l{i}."
+        yield p + "ln1", (d,), f32
+        yield p + "qkv", (3 * d, d), bf
+        yield p + "o", (d, d), bf
+        yield p + "ln2", (d,), f32
+        yield p + "cq", (d, d), bf
+        yield p + "co", (d, d), bf
+        yield p + "ln3", (d,), f32
+        yield p + "wi", (f, d), bf
+        yield p + "wo", (d, f), bf
+    yield "dec.ckv", (cfg.dec_layers * 2 * d, d), bf  # every layer's cross K|V, one GEMM
+    yield "dec.ln_f", (d,), f32
+    yield "lm", (cfg.vocab_size, d), bf
+
+
+def init_random(cfg: T5Config, seed: int = 0) -> ParamPack:
+    """Seeded random init (HF T5 scheme: factor 1.0 normal with fan-in scaling)."""
+    pack = ParamPack(param_specs(cfg))
+    g = torch.Generator().manual_seed(int(seed))
+    d, f = cfg.d_model, cfg.d_ff
+    for name in pack.names():
+        t = pack[name]
+        base = name.split(".")[-1]
+        if base.startswith("ln"):
+            t.fill_(1.0)
+        elif base == "rel":
+            t.copy_(torch.randn(t.shape, generator=g) * d ** -0.5)
+        elif name == "shared":
+            t.copy_(torch.randn(t.shape, generator=g).to(t.dtype))
+        elif base in ("wo",):
+            t.copy_((torch.randn(t.shape, generator=g) * f ** -0.5).to(t.dtype))
+        elif base == "qkv":
+            w = torch.randn(t.shape, generator=g) * d ** -0.5
+            w[:d] *= cfg.d_kv ** -0.5  # T5 folds the 1/sqrt(d_kv) attention scale into q
+            t.copy_(w.to(t.dtype))
+        elif base == "cq":
+            t.copy_((torch.randn(t.shape, generator=g) * d ** -0.5 * cfg.d_kv ** -0.5).to(t.dtype))
+        else:
+            t.copy_((torch.randn(t.shape, generator=g) * d ** -0.5).to(t.dtype))
+    if cfg.tie_embeddings:
+        pack["lm"].copy_((pack["shared"].float() * d ** -0.5).to(torch.bfloat16))
+    return pack
+
+
+def from_hf_state_dict(cfg: T5Config, sd: Dict[str, torch.Tensor]) -> ParamPack:
+    pack = ParamPack(param_specs(cfg))
+    d = cfg.d_model
+
+    def put(name, t):
+        pack[name].copy_(t.to(pack[name].dtype).view(pack[name].shape))
+
+    put("shared", sd["shared.weight"])
+    put("enc.rel", sd["encoder.block.0.layer.0.SelfAttention.relative_attention_bias.weight"])
+    for i in range(cfg.enc_layers):
+        b = f"encoder.block.{i}.layer."
+        put(f"enc.l{i}.ln1", sd[b + "0.layer_norm.weight"])
+        put(f"enc.l{i}.qkv", torch.cat([sd[b + f"0.SelfAttention.{n}.weight"] for n in "qkv"], 0))
+        put(f"enc.l{i}.o", sd[b + "0.SelfAttention.o.weight"])
+        put(f"enc.l{i}.ln2", sd[b + "1.layer_norm.weight"])
+        put(f"enc.l{i}.wi", sd[b + "1.DenseReluDense.wi.weight"])
+        put(f"enc.l{i}.wo", sd[b + "1.DenseReluDense.wo.weight"])
+    put("enc.ln_f", sd["encoder.final_layer_norm.weight"])
+    put("dec.rel", sd["decoder.block.0.layer.0.SelfAttention.relative_attention_bias.weight"])
+    ckv = []
+    for i in range(cfg.dec_layers):
+        b = f"decoder.block.{i}.layer."
+        put(f"dec.l{i}.ln1", sd[b + "0.layer_norm.weight"])
+        put(f"dec.l{i}.qkv", torch.cat([sd[b + f"0.SelfAttention.{n}.weight"] for n in "qkv"], 0))
+        put(f"dec.l{i}.o", sd[b + "0.SelfAttention.o.weight"])
+        put(f"dec.l{i}.ln2", sd[b + "1.layer_norm.weight"])
+        put(f"dec.l{i}.cq", sd[b + "1.EncDecAttention.q.weight"])
+        put(f"dec.l{i}.co", sd[b + "1.EncDecAttention.o.weight"])
+        ckv += [sd[b + "1.EncDecAttention.k.weight"], sd[b + "1.EncDecAttention.v.weight"]]
+        put(f"dec.l{i}.ln3", sd[b + "2.layer_norm.weight"])
+        put(f"dec.l{i}.wi", sd[b + "2.DenseReluDense.wi.weight"])
+        put(f"dec.l{i}.wo", sd[b + "2.DenseReluDense.wo.weight"])
+    put("dec.ckv", torch.cat(ckv, 0))
+    put("dec.ln_f", sd["decoder.final_layer_norm.weight"])
+    lm = sd.get("lm_head.weight", sd["shared.weight"])
+    put("lm", lm.float() * (d ** -0.5 if cfg.tie_embeddings else 1.0))
+    return pack
+
+
+def relative_bucket(rel: torch.Tensor, bidirectional: bool, buckets: int, max_distance: int) -> torch.Tensor:
+    """T5 relative-position bucketing (same function as HF ``_relative_position_bucket``)."""
+    out = torch.zeros_like(rel)
+    if bidirectional:
+        buckets //= 2
+        out += (rel > 0).to(rel.dtype) * buckets
+        rel = rel.abs()
+    else:
+        rel = -torch.clamp(rel, max=0)
+    exact = buckets // 2
+    small = rel < exact
+    large = exact + (torch.log(rel.float().clamp(min=1) / exact) / math.log(max_distance / exact)
+                     * (buckets - exact)).to(rel.dtype)
+    large = torch.clamp(large, max=buckets - 1)
+    return out + torch.where(small, rel, large)
+
+
+class T5Model:
+    """Device-agnostic T5: ``pack`` on a ROCm device runs the HIP kernels; on CPU
+    (with ``fp32=True``) every op's PyTorch reference, used as the oracle."""
+
+    def __init__(self, cfg: T5Config, pack: ParamPack, fp32: bool = False):
+        self.cfg, self.pack = cfg, pack
+        self.p = pack.with_dtype(torch.float32) if fp32 else {n: pack[n] for n in pack.names()}
+        self.device = pack.buffer.device
+        self._enc_bias: Dict[int, torch.Tensor] = {}
+        self._dec_bias: Optional[torch.Tensor] = None
+
+    # ------------------------------------------------------------- biases
+    def enc_bias(self, S: int) -> torch.Tensor:
+        if S not in self._enc_bias:
+            pos = torch.arange(S)
+            b = relative_bucket(pos.view(1, S) - pos.view(S, 1), True, self.cfg.buckets, self.cfg.max_distance)
+            rel = self.p["enc.rel"].float().cpu()  # [buckets, H]
+            self._enc_bias[S] = rel[b].permute(2, 0, 1).contiguous().to(self.device)  # [H, S, S]
+        return self._enc_bias[S]
+
+    def dec_bias(self, T: int) -> torch.Tensor:
+        if self._dec_bias is None or self._dec_bias.shape[1] < T:
+            dist = torch.arange(T)
+            b = relative_bucket(-dist, False, self.cfg.buckets, self.cfg.max_distance)
+            rel = self.p["dec.rel"].float().cpu()
+            self._dec_bias = rel[b].t().contiguous().to(self.device)  # [H, T] by distance q-k
+        return self._dec_bias
+
+    # ------------------------------------------------------------- encoder
+    def encode(self, ids: torch.Tensor, lens: torch.Tensor):
+        """ids [B, S] int32 (S % 4 == 0), lens [B] -> (enc [B*S, d], cross K|V [B*S, L*2d])."""
+        cfg, p = self.cfg, self.p
+        B, S = ids.shape
+        d, H = cfg.d_model, cfg.heads
+        bias = self.enc_bias(S)
+        h = ops.embed_gather(ids, p["shared"])
+        if h.dtype != p["enc.l0.qkv"].dtype:
+            h = h.to(p["enc.l0.qkv"].dtype)
+        for i in range(cfg.enc_layers):
+            q = f"enc.l{i}."
+            x = ops.rmsnorm(h, p[q + "ln1"], cfg.eps)
+            qkv = ops.linear(x, p[q + "qkv"])
+            ctx = ops.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], lens, B, S, S, H, scale=1.0, bias=bias)
+            h = ops.linear(ctx, p[q + "o"], residual=h)
+            x = ops.rmsnorm(h, p[q + "ln2"], cfg.eps)
+            f = ops.linear(x, p[q + "wi"], act="relu")
+            h = ops.linear(f, p[q + "wo"], residual=h)
+        enc = ops.rmsnorm(h, p["enc.ln_f"], cfg.eps)
+        return enc, ops.linear(enc, p["dec.ckv"])
+
+    # ------------------------------------------------------------- decoder
+    def new_cache(self, rows: int, T: int) -> torch.Tensor:
+        """Self-attention K|V cache [L, rows*T, 2d]."""
+        dt = self.p["dec.l0.qkv"].dtype
+        return torch.zeros((self.cfg.dec_layers, rows * T, 2 * self.cfg.d_model), dtype=dt, device=self.device)
+
+    def step(self, tokens: torch.Tensor, step: torch.Tensor, cache: torch.Tensor, T: int, ckv: torch.Tensor,
+             src_lens: torch.Tensor, S: int, group: int) -> torch.Tensor:
+        """One decoder position for ``rows`` sequences -> fp32 logits [rows, V].
+
+        ``step`` is a 1-element int32 device tensor (position of ``tokens``);
+        cache rows of sequence r are r*T .. r*T+T-1; encoder rows of batch item
+        r // group are (r//group)*S ...
+        """
+        cfg, p = self.cfg, self.p
+        d, H = cfg.d_model, cfg.heads
+        dbias = self.dec_bias(T)
+        x = ops.embed_gather(tokens, p["shared"])
+        if x.dtype != p["dec.l0.qkv"].dtype:
+            x = x.to(p["dec.l0.qkv"].dtype)
+        for i in range(cfg.dec_layers):
+            q = f"dec.l{i}."
+            c = cache[i]
+            y = ops.rmsnorm(x, p[q + "ln1"], cfg.eps)
+            qkv = ops.linear(y, p[q + "qkv"])
+            ops.kv_append(qkv, d, 2 * d, c, T, step)
+            ctx = ops.decode_attention(qkv[:, :d], c[:, :d], c[:, d:], H, T, 1, step=step, bias_dist=dbias)
+            x = ops.linear(ctx, p[q + "o"], residual=x)
+            y = ops.rmsnorm(x, p[q + "ln2"], cfg.eps)
+            cq = ops.linear(y, p[q + "cq"])
+            kv = ckv[:, i * 2 * d:(i + 1) * 2 * d]
+            ctx = ops.decode_attention(cq, kv[:, :d], kv[:, d:], H, S, group, lens=src_lens)
+            x = ops.linear(ctx, p[q + "co"], residual=x)
+            y = ops.rmsnorm(x, p[q + "ln3"], cfg.eps)
+            f = ops.linear(y, p[q + "wi"], act="relu")
+            x = ops.linear(f, p[q + "wo"], residual=x)
+        y = ops.rmsnorm(x, p["dec.ln_f"], cfg.eps)
+        return ops.linear(y, p["lm"], out_f32=True)

@@ -5,7 +5,8 @@ reference for CPU tensors; the reference doubles as the numerics oracle in
 ``tests/kernels``. There is no silent fallback for device tensors: if the
 extension cannot load on a GPU, the call raises.
 """
-from .linear import linear, EPI_BIAS, EPI_GELU, EPI_TANH, EPI_RESIDUAL  # noqa: F401
+from .linear import linear, EPI_BIAS, EPI_GELU, EPI_TANH, EPI_RESIDUAL, EPI_RELU  # noqa: F401
+from .decode import decode_attention, kv_append, gather_rows, beam_topk_rows  # noqa: F401
 from .attention import attention_packed, attention  # noqa: F401
 from .norm import layernorm, rmsnorm, embed_layernorm, embed_gather  # noqa: F401
 from .tokenize import tokenize  # noqa: F401

@@ -1,0 +1,106 @@
+"""Seq2seq decode ops (K9-K11). Native kernels: ``csrc/kernels/decode.hip``.
+
+* :func:`decode_attention` — one query row per (row, head) vs a KV cache
+  (self: the row's own cache up to step t; cross: the encoder K/V of batch item
+  ``row // group`` masked by its source length), optional T5 distance bias.
+* :func:`kv_append` — write step t's K/V into the cache (t on device).
+* :func:`gather_rows` — beam reorder of cache slabs.
+* :func:`beam_topk_rows` — log-softmax + beam score (+ EOS mask) + top-k per row.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+
+from .._native import native, ptr, stream_handle
+from ._util import check, check_bf16_dev, row_stride
+
+HEAD_DIM = 64
+
+
+def decode_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, H: int, seq_stride: int, group: int = 1,
+                     lens: Optional[torch.Tensor] = None, step: Optional[torch.Tensor] = None,
+                     bias_dist: Optional[torch.Tensor] = None, scale: float = 1.0,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """q [R, >=H*64]; k/v 2-D row views with ``seq_stride`` rows per sequence."""
+    R = q.shape[0]
+    if not q.is_cuda:
+        return _decode_attention_ref(q, k, v, H, seq_stride, group, lens, step, bias_dist, scale, out)
+    check_bf16_dev(q, "q")
+    check_bf16_dev(k, "k")
+    check(lens is not None or step is not None, "need lens or step")
+    if bias_dist is not None:
+        check(bias_dist.dtype == torch.float32 and bias_dist.is_contiguous() and bias_dist.dim() == 2,
+              "bias_dist must be fp32 [H, T]")
+    out = torch.empty((R, H * HEAD_DIM), dtype=torch.bfloat16, device=q.device) if out is None else out
+    native().decode_attention(ptr(q), row_stride(q, "q"), ptr(k), ptr(v), row_stride(k, "k"), seq_stride, group,
+                              ptr(lens), ptr(step), ptr(bias_dist), 0 if bias_dist is None else bias_dist.shape[1],
+                              ptr(out), row_stride(out, "out"), R, H, float(scale), stream_handle())
+    return out
+
+
+def _decode_attention_ref(q, k, v, H, seq_stride, group, lens, step, bias_dist, scale, out):
+    R = q.shape[0]
+    D = HEAD_DIM
+    res = torch.zeros((R, H * D), dtype=torch.float32)
+    for r in range(R):
+        s = r // group
+        n = int(lens[s]) if lens is not None else int(step.reshape(-1)[0]) + 1
+        kk = k[s * seq_stride:s * seq_stride + n, :H * D].float().view(n, H, D)
+        vv = v[s * seq_stride:s * seq_stride + n, :H * D].float().view(n, H, D)
+        qq = q[r, :H * D].float().view(H, D) * scale
+        sc = torch.einsum("hd,nhd->hn", qq, kk)
+        if bias_dist is not None:
+            dist = (n - 1 - torch.arange(n))
+            sc = sc + bias_dist.float()[:, dist]
+        p = torch.softmax(sc, dim=-1)
+        res[r] = torch.einsum("hn,nhd->hd", p, vv).reshape(-1)
+    y = res.to(q.dtype)
+    return out.copy_(y) if out is not None else y
+
+
+def kv_append(src: torch.Tensor, col0: int, ncols: int, cache: torch.Tensor, seq_stride: int,
+              step: torch.Tensor) -> None:
+    """cache rows (r*seq_stride + t) <- src[r, col0:col0+ncols]; cache is 2-D [R*seq_stride, ncols]."""
+    R = src.shape[0]
+    if not src.is_cuda:
+        t = int(step.reshape(-1)[0])
+        cache.view(R, seq_stride, -1)[:, t, :ncols] = src[:, col0:col0 + ncols]
+        return
+    native().kv_append(ptr(src), row_stride(src, "src"), col0, ncols, ptr(cache), seq_stride,
+                       row_stride(cache, "cache"), ptr(step), R, stream_handle())
+
+
+def gather_rows(src: torch.Tensor, dst: torch.Tensor, parent: torch.Tensor, nrows: int, seq_stride: int,
+                step: torch.Tensor, slabs: int = 1) -> None:
+    """dst[slab, r, :t+1] = src[slab, parent[r], :t+1]; tensors [slabs, nrows*seq_stride, C]."""
+    if not src.is_cuda:
+        t = int(step.reshape(-1)[0]) + 1
+        s4 = src.view(slabs, nrows, seq_stride, -1)
+        dst.view(slabs, nrows, seq_stride, -1)[:, :, :t] = s4[:, parent.long(), :t]
+        return
+    check(parent.dtype == torch.int32 and parent.is_cuda, "parent must be int32 on device")
+    C = src.shape[-1]
+    native().gather_rows(ptr(src), ptr(dst), ptr(parent), nrows, seq_stride, C, ptr(step), slabs,
+                         nrows * seq_stride * C, stream_handle())
+
+
+def beam_topk_rows(logits: torch.Tensor, beam_scores: torch.Tensor, k: int, eos: int, mask_eos: bool
+                   ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per row: top-k of ``log_softmax(logits) + beam_score`` (EOS masked if asked)."""
+    R, V = logits.shape
+    if not logits.is_cuda:
+        lp = torch.log_softmax(logits.float(), dim=-1)
+        if mask_eos:
+            lp[:, eos] = float("-inf")
+        lp = lp + beam_scores.float().view(-1, 1)
+        sc, idx = torch.topk(lp, k, dim=-1)
+        return sc, idx.to(torch.int32)
+    check(logits.dtype == torch.float32 and logits.is_contiguous(), "logits must be contiguous fp32")
+    sc = torch.empty((R, k), dtype=torch.float32, device=logits.device)
+    idx = torch.empty((R, k), dtype=torch.int32, device=logits.device)
+    native().beam_topk_rows(ptr(logits), R, V, ptr(beam_scores), int(eos), int(mask_eos), int(k), ptr(sc), ptr(idx),
+                            stream_handle())
+    return sc, idx

@@ -13,11 +13,11 @@ import torch.nn.functional as F
 from .._native import native, ptr, stream_handle
 from ._util import check, check_bf16_dev, row_stride, same_device
 
-EPI_BIAS, EPI_GELU, EPI_TANH, EPI_RESIDUAL = 1, 2, 4, 8
-_ACTS = {None: 0, "none": 0, "gelu": EPI_GELU, "tanh": EPI_TANH}
+EPI_BIAS, EPI_GELU, EPI_TANH, EPI_RESIDUAL, EPI_RELU, EPI_OUT_F32 = 1, 2, 4, 8, 16, 32
+_ACTS = {None: 0, "none": 0, "gelu": EPI_GELU, "tanh": EPI_TANH, "relu": EPI_RELU}
 
 
-def linear_ref(x, w, bias=None, act=None, residual=None):
+def linear_ref(x, w, bias=None, act=None, residual=None, out_f32=False):
     y = x.float() @ w.float().t()
     if bias is not None:
         y = y + bias.float()
@@ -25,16 +25,20 @@ def linear_ref(x, w, bias=None, act=None, residual=None):
         y = F.gelu(y)
     elif act == "tanh":
         y = torch.tanh(y)
+    elif act == "relu":
+        y = torch.relu(y)
     if residual is not None:
         y = y + residual.float()
-    return y.to(x.dtype)
+    return y if out_f32 else y.to(x.dtype)
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: Optional[str] = None,
-           residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+           residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+           out_f32: bool = False) -> torch.Tensor:
+    """``act(x @ w.T + bias) + residual``; ``out_f32`` returns fp32 (LM-head logits)."""
     check(act in _ACTS, f"unknown activation {act!r}")
     if not x.is_cuda:
-        y = linear_ref(x, w, bias, act, residual)
+        y = linear_ref(x, w, bias, act, residual, out_f32)
         if out is not None:
             out.copy_(y)
             return out
@@ -56,9 +60,12 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         check(tuple(residual.shape) == (M, N), "residual must be [M, N]")
         ldr = row_stride(residual, "residual")
         epi |= EPI_RESIDUAL
+    if out_f32:
+        epi |= EPI_OUT_F32
+    odt = torch.float32 if out_f32 else torch.bfloat16
     if out is None:
-        out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
-    check(tuple(out.shape) == (M, N), "out must be [M, N]")
+        out = torch.empty((M, N), dtype=odt, device=x.device)
+    check(tuple(out.shape) == (M, N) and out.dtype == odt, "out must be [M, N] of the output dtype")
     ldc = row_stride(out, "out")
     native().gemm(ptr(x), lda, ptr(w), ldb, ptr(out), ldc, ptr(bias), ptr(residual), ldr, M, N, K, epi,
                   stream_handle())

@@ -1,0 +1,198 @@
+"""Batched beam-search summarisation on the T5 HIP path (map_summarize).
+
+Semantics follow HF transformers' (5.x) vectorised beam search, which the
+reference invokes through ``model.generate(num_beams=4, max_length=130,
+min_length=30, early_stopping=True)`` (``/root/reference/ops/map_summarize.py:53-59``):
+
+* per step keep the top ``2*num_beams`` continuations of every batch item over
+  ``num_beams x vocab`` accumulated log-probs (the fused K10 kernel returns
+  each beam row's top ``2*num_beams``; their union holds the item's global top);
+* a continuation "hits" when it emits EOS or reaches ``max_length``; the best
+  ``num_beams`` non-hit continuations keep running, and hits among the top
+  ``num_beams`` candidates enter the finished set scored
+  ``logprob / generated_len ** length_penalty``;
+* ``early_stopping=True`` freezes an item once ``num_beams`` hypotheses have
+  finished; the loop ends when no item can improve;
+* EOS is masked (after log-softmax) while the sequence is shorter than
+  ``min_length``.
+
+Device work per step: the decoder step (L layers of GEMMs, KV-cache appends,
+single-query attention), the LM-head GEMM and K10. Host work: bookkeeping on
+``[B, 2*num_beams]`` tensors and one gather of the KV caches by parent beam.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.t5 import T5Config, T5Model
+from ..tokenizer import pack_rows
+
+NEG = -1.0e9
+
+
+@dataclass
+class GenConfig:
+    num_beams: int = 4
+    max_length: int = 130
+    min_length: int = 30
+    length_penalty: float = 1.0
+    early_stopping: bool = True
+
+
+@dataclass
+class GenResult:
+    sequences: List[List[int]]
+    scores: List[float]
+    steps: int
+    timing_ms: Dict[str, float] = field(default_factory=dict)
+
+
+def generate(model: T5Model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfig) -> GenResult:
+    """Beam search for a batch. ``src_ids`` [B, S] int32 (on the model device)."""
+    cfg: T5Config = model.cfg
+    dev = model.device
+    B, S = src_ids.shape
+    nb = max(1, int(gen.num_beams))
+    K2 = 2 * nb
+    V = cfg.vocab_size
+    T = int(gen.max_length)
+    rows = B * nb
+    t0 = time.perf_counter()
+
+    _, ckv = model.encode(src_ids, src_lens)
+    t_enc = time.perf_counter()
+    cache = model.new_cache(rows, T)
+    cache_alt = torch.empty_like(cache)
+    step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    run_seq = torch.full((B, nb, T), cfg.pad_id, dtype=torch.long)
+    run_seq[:, :, 0] = cfg.decoder_start_id
+    run_scores = torch.zeros((B, nb), dtype=torch.float32)
+    run_scores[:, 1:] = NEG
+    fin_seq = run_seq.clone()
+    fin_scores = torch.full((B, nb), NEG, dtype=torch.float32)
+    fin_done = torch.zeros((B, nb), dtype=torch.bool)
+    fin_len = torch.ones((B, nb), dtype=torch.long)
+    unsat = torch.ones((B, 1), dtype=torch.bool)
+    top_mask = torch.cat([torch.ones(nb, dtype=torch.bool), torch.zeros(K2 - nb, dtype=torch.bool)])
+    tokens = torch.full((rows,), cfg.decoder_start_id, dtype=torch.int32, device=dev)
+    lp = float(gen.length_penalty)
+
+    cur = 1  # sequence length so far (decoder start token included)
+    steps = 0
+    while cur < T:
+        step_dev.fill_(cur - 1)
+        logits = model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb)
+        sc, tk = ops.beam_topk_rows(logits, run_scores.view(-1).to(dev), K2, cfg.eos_id, cur < gen.min_length)
+        sc, tk = sc.cpu().view(B, nb * K2), tk.cpu().view(B, nb * K2).long()
+        steps += 1
+        # global top-K2 per item; ties -> lower flat index (beam * V + token) like torch.topk over [nb*V]
+        beam_of = torch.arange(nb).repeat_interleave(K2).view(1, -1).expand(B, -1)
+        flat = beam_of * V + tk
+        order = torch.argsort(flat, dim=1)
+        sc, tk, beam_of, flat = (torch.gather(x, 1, order) for x in (sc, tk, beam_of, flat))
+        top_sc, pos = torch.sort(sc, dim=1, descending=True, stable=True)
+        pos = pos[:, :K2]
+        top_sc = top_sc[:, :K2]
+        top_tok = torch.gather(tk, 1, pos)
+        top_beam = torch.gather(beam_of, 1, pos)
+        cand_seq = torch.gather(run_seq, 1, top_beam.unsqueeze(-1).expand(-1, -1, T)).clone()
+        cand_seq[:, :, cur] = top_tok
+        hits = (top_tok == cfg.eos_id) | (cur + 1 >= T)
+
+        # running beams for the next step: best nb non-hit continuations
+        run_cand = top_sc + hits.float() * NEG
+        nxt = torch.topk(run_cand, nb, dim=1).indices
+        new_run_seq = torch.gather(cand_seq, 1, nxt.unsqueeze(-1).expand(-1, -1, T))
+        new_run_scores = torch.gather(run_cand, 1, nxt)
+        parent = torch.gather(top_beam, 1, nxt)  # beam index within the item
+
+        # finished hypotheses: hits among the top nb candidates
+        did = hits & top_mask.view(1, -1)
+        fin_cand = top_sc / float(cur) ** lp  # generated length = cur + 1 - prompt(1)
+        full = fin_done.all(dim=1, keepdim=True) & gen.early_stopping
+        fin_cand = fin_cand + full.float() * NEG + (~unsat).float() * NEG + (~did).float() * NEG
+        m_seq = torch.cat([fin_seq, cand_seq], 1)
+        m_sc = torch.cat([fin_scores, fin_cand], 1)
+        m_done = torch.cat([fin_done, did], 1)
+        m_len = torch.cat([fin_len, torch.full((B, K2), cur + 1, dtype=torch.long)], 1)
+        keep = torch.topk(m_sc, nb, dim=1).indices
+        fin_seq = torch.gather(m_seq, 1, keep.unsqueeze(-1).expand(-1, -1, T))
+        fin_scores = torch.gather(m_sc, 1, keep)
+        fin_done = torch.gather(m_done, 1, keep)
+        fin_len = torch.gather(m_len, 1, keep)
+
+        run_seq, run_scores = new_run_seq, new_run_scores
+        # KV caches follow their parent beams
+        par_rows = (torch.arange(B).view(-1, 1) * nb + parent).view(-1).to(torch.int32).to(dev)
+        ops.gather_rows(cache, cache_alt, par_rows, rows, T, step_dev, slabs=cfg.dec_layers)
+        cache, cache_alt = cache_alt, cache
+        tokens = run_seq[:, :, cur].reshape(-1).to(torch.int32).to(dev)
+        cur += 1
+        # early-stop heuristic (early_stopping=True: best running at current length)
+        best_run = run_scores[:, :1] / float(cur - 1) ** lp
+        worst_fin = torch.where(fin_done, fin_scores.min(dim=1, keepdim=True).values, torch.full_like(fin_scores, NEG))
+        unsat = unsat & (best_run > worst_fin).any(dim=1, keepdim=True)
+        open_beam = ~(fin_done.all() & gen.early_stopping)
+        if not (bool(unsat.any()) and bool(open_beam) and not bool(hits.all())):
+            break
+    t_dec = time.perf_counter()
+    seqs, scores = [], []
+    for b in range(B):
+        n = int(fin_len[b, 0])
+        seqs.append(fin_seq[b, 0, :n].tolist())
+        scores.append(float(fin_scores[b, 0]))
+    return GenResult(seqs, scores, steps, {"encode_ms": (t_enc - t0) * 1e3, "decode_ms": (t_dec - t_enc) * 1e3})
+
+
+class SummarizeEngine:
+    """Texts -> summaries with a device-resident T5 (batched beam search)."""
+
+    def __init__(self, cfg: T5Config, pack, device: torch.device, max_source_len: int = 512):
+        self.cfg = cfg
+        self.model = T5Model(cfg, pack if pack.buffer.device == device else pack.to(device))
+        self.device = device
+        self.max_src = int(max_source_len)
+
+    def encode_texts(self, texts: Sequence[str]) -> Tuple[torch.Tensor, torch.Tensor, List[Dict[int, str]]]:
+        """Hash-tokenize (same spec as K1, vocab = T5's), append EOS, pad to S % 8 == 0."""
+        from .. import tokenizer as T
+        from .._native import native
+
+        text, offs = pack_rows(texts)
+        ids, lens = native().tokenize_host(text, offs, self.max_src + 1, self.cfg.vocab_size, 1 << 16)
+        rows = []
+        for r in range(len(texts)):
+            toks = [int(x) for x in ids[r, 1:lens[r] - 1]]  # strip [CLS]/[SEP]
+            rows.append(toks[: self.max_src - 1] + [self.cfg.eos_id])
+        S = max(8, (max(len(r) for r in rows) + 7) // 8 * 8)
+        arr = np.full((len(rows), S), self.cfg.pad_id, dtype=np.int32)
+        for r, toks in enumerate(rows):
+            arr[r, :len(toks)] = toks
+        lens_t = torch.tensor([len(r) for r in rows], dtype=torch.int32)
+        vocab_maps = [self._reverse_map(t) for t in texts]
+        return torch.from_numpy(arr).to(self.device), lens_t.to(self.device), vocab_maps
+
+    def _reverse_map(self, text: str) -> Dict[int, str]:
+        from .. import tokenizer as T
+
+        out: Dict[int, str] = {}
+        for word in text.split():
+            for tok_id in T.token_ids(word.encode("utf-8"), self.cfg.vocab_size, 64):
+                out.setdefault(tok_id, word)
+        return out
+
+    def detokenize(self, seq: List[int], vmap: Dict[int, str]) -> str:
+        special = {self.cfg.pad_id, self.cfg.eos_id, self.cfg.decoder_start_id}
+        return " ".join(vmap.get(t, f"<{t}>") for t in seq if t not in special)
+
+    def summarize(self, texts: Sequence[str], gen: GenConfig) -> Tuple[List[str], GenResult]:
+        ids, lens, maps = self.encode_texts(texts)
+        res = generate(self.model, ids, lens, gen)
+        return [self.detokenize(s, m) for s, m in zip(res.sequences, maps)], res

@@ -41,14 +41,17 @@ def make_text_rows(n: int, words_per_row: int = 150, seed: int = 0):
 
 def write_csv(path: str, n: int, words_per_row: int = 150, seed: int = 0, quote_every: int = 7) -> str:
     """Write ``n`` rows; every ``quote_every``-th text is quoted with an embedded comma/quote/newline."""
+    import csv
+
     rows = make_text_rows(n, words_per_row, seed)
     tmp = f"{path}.tmp{os.getpid()}"
     with open(tmp, "w", encoding="utf-8", newline="") as f:
-        f.write("id,text,risk\n")
+        w = csv.writer(f, lineterminator="\n")  # excel dialect, QUOTE_MINIMAL
+        w.writerow(["id", "text", "risk"])
         for i, t in enumerate(rows):
             if quote_every and i % quote_every == 3:
-                t = '"' + t.replace('"', '""') + ', said "x"\nend"'
-            f.write(f"{i},{t},{(i % 1000) / 1000.0}\n")
+                t = t + ', said "x"\nend'
+            w.writerow([i, t, (i % 1000) / 1000.0])
     os.replace(tmp, path)
     return path
 

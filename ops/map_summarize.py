@@ -1,0 +1,101 @@
+"""``map_summarize`` — abstractive summarisation on the T5 encoder-decoder HIP path.
+
+Reference: ``/root/reference/ops/map_summarize.py`` (HF BART-large-CNN on CPU,
+one document per call, ``generate(num_beams=4, max_length=130, min_length=30,
+early_stopping=True)``). Here (BASELINE config 4): T5 with random-init weights
+on the hand-written kernels (agent_tpu_amd/models/t5.py), batched beam search
+with HF's semantics (agent_tpu_amd/runtime/summarize.py), documents tokenised
+with the same hash tokenizer as map_classify (no SentencePiece model is
+available offline; see map_summarize.CONTRACT.md).
+
+Output keys are the reference's ``{ok, summary, device, model}``; ``texts``
+(a list) returns ``summaries``. Fix: the payload is
+validated BEFORE the model is built. ``SUMMARIZE_FORCE_CPU=1`` runs the fp32
+PyTorch reference path (the reference defaulted to CPU; here the GPU is the
+default).
+"""
+from __future__ import annotations
+
+import os
+import threading
+import time
+from typing import Any, Dict, List, Optional
+
+from . import register_op
+
+MODEL_NAME = os.getenv("SUMMARIZE_MODEL", "t5-base")
+FORCE_CPU = os.getenv("SUMMARIZE_FORCE_CPU", "0").strip().lower() in ("1", "true", "yes")
+MAX_SOURCE_TOKENS = int(os.getenv("SUMMARIZE_MAX_SOURCE_TOKENS", "512"))
+
+_lock = threading.Lock()
+_engine = None
+_device = "cpu"
+
+
+def _init_engine():
+    global _engine, _device
+    if _engine is not None:
+        return _engine
+    with _lock:
+        if _engine is not None:
+            return _engine
+        import torch
+
+        from agent_tpu_amd.models.t5 import config_for, init_random
+        from agent_tpu_amd.runtime.summarize import SummarizeEngine
+
+        cfg = config_for(MODEL_NAME)
+        pack = init_random(cfg, seed=int(os.getenv("MODEL_SEED", "0")))
+        if not FORCE_CPU and torch.cuda.is_available():
+            dev = torch.device("cuda", int(os.getenv("LOCAL_RANK", "0")))
+        else:
+            dev = torch.device("cpu")
+        eng = SummarizeEngine(cfg, pack, dev, MAX_SOURCE_TOKENS)
+        if dev.type == "cpu":
+            from agent_tpu_amd.models.t5 import T5Model
+
+            eng.model = T5Model(cfg, pack, fp32=True)
+        _engine, _device = eng, ("cuda" if dev.type == "cuda" else "cpu")
+        print(f"[map_summarize] {MODEL_NAME} ready on {_device}", flush=True)
+        return _engine
+
+
+def _gen_config(payload: Dict[str, Any]):
+    from agent_tpu_amd.runtime.summarize import GenConfig
+
+    return GenConfig(num_beams=int(payload.get("num_beams", 4)), max_length=int(payload.get("max_length", 130)),
+                     min_length=int(payload.get("min_length", 30)),
+                     length_penalty=float(payload.get("length_penalty", 1.0)), early_stopping=True)
+
+
+@register_op("map_summarize")
+def handle(payload: Optional[Dict[str, Any]]) -> Dict[str, Any]:
+    if not payload:
+        return {"ok": False, "error": "empty payload"}
+    texts: Optional[List[str]] = None
+    if "texts" in payload:
+        raw = payload.get("texts")
+        if not isinstance(raw, list) or not raw or not all(isinstance(t, str) and t.strip() for t in raw):
+            return {"ok": False, "error": "payload.texts must be a non-empty list of non-empty strings"}
+        texts = [t.strip() for t in raw]
+    else:
+        text = payload.get("text", "")
+        text = text.strip() if isinstance(text, str) else ""
+        if not text:
+            return {"ok": False, "error": "no text provided"}
+        texts = [text]
+    try:
+        gen = _gen_config(payload)
+    except (TypeError, ValueError) as exc:
+        return {"ok": False, "error": f"bad generation parameter: {exc}"}
+    t0 = time.time()
+    eng = _init_engine()
+    summaries, res = eng.summarize(texts, gen)
+    out: Dict[str, Any] = {"ok": True, "device": _device, "model": MODEL_NAME,
+                           "elapsed_ms": (time.time() - t0) * 1000.0, "decode_steps": res.steps,
+                           "timing_ms": res.timing_ms}
+    if "texts" in payload:
+        out["summaries"] = summaries
+    else:
+        out["summary"] = summaries[0]
+    return out

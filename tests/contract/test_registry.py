@@ -1,0 +1,79 @@
+"""Registry semantics (ref /root/reference/ops/__init__.py)."""
+import pytest
+
+import ops
+import ops_loader
+
+
+@pytest.fixture(autouse=True)
+def _clean_tasks(monkeypatch):
+    monkeypatch.delenv("TASKS", raising=False)
+    ops._reset_for_tests()
+    yield
+    ops._reset_for_tests()
+
+
+def test_unset_all_star_enable_default_ops(monkeypatch):
+    base = ops.list_ops()
+    assert base == sorted(n for n in ops.OP_TO_MODULE if n not in ops.OPT_IN_OPS)
+    for kw in ("*", "all", "ALL", " all , "):
+        monkeypatch.setenv("TASKS", kw)
+        assert ops.list_ops() == base
+
+
+def test_none_and_exact_names_case_sensitive(monkeypatch):
+    monkeypatch.setenv("TASKS", "none")
+    assert ops.list_ops() == []
+    monkeypatch.setenv("TASKS", "echo,csv_shard")
+    assert ops.list_ops() == ["csv_shard", "echo"]
+    monkeypatch.setenv("TASKS", "ECHO")
+    assert ops.list_ops() == []
+
+
+def test_get_op_error_messages(monkeypatch):
+    with pytest.raises(ValueError, match=r"Unknown op 'nonexistent'\. Allowed ops: \["):
+        ops.get_op("nonexistent")
+    monkeypatch.setenv("TASKS", "echo")
+    with pytest.raises(ValueError, match=r"Op 'map_tokenize' is not enabled by TASKS\. Enabled ops: \['echo'\]"):
+        ops.get_op("map_tokenize")
+
+
+def test_failed_import_reported_once(monkeypatch, capsys):
+    monkeypatch.setitem(ops.OP_TO_MODULE, "ghost", "ghost_module_does_not_exist")
+    for _ in range(3):
+        with pytest.raises(ValueError, match=r"Unknown or failed op 'ghost'.*Also saw op import errors: "
+                                             r"ghost_module_does_not_exist => ModuleNotFoundError"):
+            ops.get_op("ghost")
+    assert len(ops.OPS_LOAD_ERRORS) == 1  # the reference appended on every call
+    assert capsys.readouterr().out.count("[ops] ERROR: failed to import ops.ghost_module_does_not_exist") == 1
+
+
+def test_aliases_resolve_to_same_handler():
+    assert ops.get_op("csv_shard") is ops.get_op("read_csv_shard")
+    assert ops.get_op("map_classify_tpu").__name__ == "map_classify_tpu"
+    assert ops.get_op("map_classify").__name__ == "map_classify"
+
+
+def test_opt_in_triggers(monkeypatch):
+    assert "trigger_oracle" not in ops.list_ops()
+    with pytest.raises(ValueError, match="not enabled"):
+        ops.get_op("trigger_sap")
+    monkeypatch.setenv("TASKS", "all,trigger_sap")
+    assert "trigger_sap" in ops.list_ops() and "trigger_oracle" not in ops.list_ops()
+    assert callable(ops.get_op("trigger_sap"))
+
+
+def test_every_mapped_module_exists():
+    import importlib.util
+
+    for name, mod in ops.OP_TO_MODULE.items():
+        assert importlib.util.find_spec(f"ops.{mod}") is not None, name
+
+
+def test_ops_loader(monkeypatch):
+    got = ops_loader.load_ops(["echo", "map_tokenize"])
+    assert set(got) == {"echo", "map_tokenize"}
+    with pytest.raises(ValueError):
+        ops_loader.load_ops(["echo", "nope"])
+    ok, bad = ops_loader.load_ops_lenient(["echo", "nope"])
+    assert list(ok) == ["echo"] and bad[0][0] == "nope"

@@ -1,0 +1,117 @@
+"""Decode kernels (K9-K11) and the T5 HIP path vs the fp32 CPU references."""
+import pytest
+import torch
+
+from agent_tpu_amd import ops
+from agent_tpu_amd.ops.decode import _decode_attention_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _r(shape, dev, scale=1.0, dtype=torch.bfloat16, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(shape, generator=g) * scale).to(dtype).to(dev)
+
+
+def _rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-6)).item()
+
+
+@pytest.mark.parametrize("rows,group,S,H", [(8, 4, 37, 12), (3, 1, 130, 4), (16, 4, 512, 12)])
+def test_decode_attention_cross(gpu, rows, group, S, H):
+    nseq = rows // group
+    q = _r((rows, H * 64), gpu, seed=1)
+    kv = _r((nseq * S, 2 * H * 64), gpu, seed=2)
+    lens = torch.tensor([S - 5 * i for i in range(nseq)], dtype=torch.int32).clamp(min=1)
+    out = ops.decode_attention(q, kv[:, :H * 64], kv[:, H * 64:], H, S, group, lens=lens.to(gpu))
+    ref = _decode_attention_ref(q.cpu(), kv.cpu()[:, :H * 64], kv.cpu()[:, H * 64:], H, S, group, lens, None, None,
+                                1.0, None)
+    assert _rel(out, ref) < 2e-2
+
+
+def test_decode_self_with_bias_append_gather(gpu):
+    rows, H, T = 6, 4, 20
+    d = H * 64
+    cache = torch.zeros((rows * T, 2 * d), dtype=torch.bfloat16, device=gpu)
+    step = torch.zeros(1, dtype=torch.int32, device=gpu)
+    bias = _r((H, T), gpu, 1.0, torch.float32, seed=3)
+    for t in range(7):
+        step.fill_(t)
+        qkv = _r((rows, 3 * d), gpu, seed=10 + t)
+        ops.kv_append(qkv, d, 2 * d, cache, T, step)
+        out = ops.decode_attention(qkv[:, :d], cache[:, :d], cache[:, d:], H, T, 1, step=step, bias_dist=bias)
+        ref = _decode_attention_ref(qkv.cpu(), cache.cpu()[:, :d], cache.cpu()[:, d:], H, T, 1, None,
+                                    step.cpu(), bias.cpu(), 1.0, None)
+        assert _rel(out, ref) < 2e-2
+    parent = torch.tensor([2, 2, 0, 5, 1, 3], dtype=torch.int32, device=gpu)
+    dst = torch.zeros_like(cache)
+    ops.gather_rows(cache.view(1, rows * T, 2 * d), dst.view(1, rows * T, 2 * d), parent, rows, T, step)
+    c3, d3 = cache.view(rows, T, 2 * d).cpu(), dst.view(rows, T, 2 * d).cpu()
+    assert torch.equal(d3[:, :7], c3[parent.long().cpu(), :7])
+
+
+@pytest.mark.parametrize("V,k,mask", [(4096, 8, False), (32128, 8, True), (50, 2, False)])
+def test_beam_topk_rows(gpu, V, k, mask):
+    R = 12
+    logits = _r((R, V), gpu, 3.0, torch.float32, seed=4)
+    bs = _r((R,), gpu, 1.0, torch.float32, seed=5)
+    sc, idx = ops.beam_topk_rows(logits, bs, k, eos=1, mask_eos=mask)
+    rsc, ridx = ops.beam_topk_rows(logits.cpu(), bs.cpu(), k, eos=1, mask_eos=mask)
+    torch.testing.assert_close(sc.cpu(), rsc, atol=2e-4, rtol=1e-5)
+    assert torch.equal(idx.cpu(), ridx)
+    if mask:
+        assert not (idx == 1).any()
+
+
+def test_gemm_relu_and_f32_out(gpu):
+    x = _r((96, 256), gpu, seed=6)
+    w = _r((512, 256), gpu, 0.1, seed=7)
+    y = ops.linear(x, w, act="relu")
+    ref = torch.relu(x.cpu().float() @ w.cpu().float().t())
+    assert _rel(y, ref) < 2e-2 and (y >= 0).all()
+    y32 = ops.linear(x, w, out_f32=True)
+    assert y32.dtype == torch.float32 and _rel(y32, x.cpu().float() @ w.cpu().float().t()) < 1e-3
+    big = _r((4096, 768), gpu, seed=8)
+    w2 = _r((1024, 768), gpu, 0.05, seed=9)
+    assert _rel(ops.linear(big, w2, act="relu"), torch.relu(big.cpu().float() @ w2.cpu().float().t())) < 2e-2
+
+
+def test_t5_step_and_generate_gpu(gpu):
+    from agent_tpu_amd.models.t5 import T5Model, config_for, init_random
+    from agent_tpu_amd.runtime.summarize import GenConfig, generate
+
+    cfg = config_for("t5-tiny")
+    pack = init_random(cfg, seed=1)
+    cpu_m, gpu_m = T5Model(cfg, pack, fp32=True), T5Model(cfg, pack.to(gpu))
+    B, S = 2, 24
+    g = torch.Generator().manual_seed(2)
+    ids = torch.randint(2, cfg.vocab_size, (B, S), generator=g, dtype=torch.int32)
+    lens = torch.tensor([24, 17], dtype=torch.int32)
+    ec, kc = cpu_m.encode(ids, lens)
+    eg, kg = gpu_m.encode(ids.to(gpu), lens.to(gpu))
+    assert _rel(eg[:S], ec[:S]) < 3e-2
+    T = 8
+    cc, cg = cpu_m.new_cache(B, T), gpu_m.new_cache(B, T)
+    tok = torch.zeros(B, dtype=torch.int32)
+    step = torch.zeros(1, dtype=torch.int32)
+    lc = cpu_m.step(tok, step, cc, T, kc, lens, S, 1)
+    lg = gpu_m.step(tok.to(gpu), step.to(gpu), cg, T, kg, lens.to(gpu), S, 1)
+    assert _rel(lg, lc) < 5e-2
+    r1 = generate(gpu_m, ids.to(gpu), lens.to(gpu), GenConfig(num_beams=4, max_length=16, min_length=4))
+    r2 = generate(gpu_m, ids.to(gpu), lens.to(gpu), GenConfig(num_beams=4, max_length=16, min_length=4))
+    assert r1.sequences == r2.sequences
+    assert all(2 <= len(s) <= 16 and s[0] == 0 for s in r1.sequences)
+
+
+def test_map_summarize_op_gpu(gpu, monkeypatch):
+    import importlib
+
+    monkeypatch.setenv("SUMMARIZE_MODEL", "t5-tiny")
+    import ops.map_summarize as ms
+
+    ms = importlib.reload(ms)
+    out = ms.handle({"texts": ["the quick brown fox jumps over the lazy dog " * 5, "MI355X summarize test."],
+                     "max_length": 20, "min_length": 5})
+    assert out["ok"] and out["device"] == "cuda" and len(out["summaries"]) == 2
+    assert ms.handle({}) == {"ok": False, "error": "empty payload"}
