@@ -63,13 +63,17 @@ PYBIND11_MODULE(_atpu, m) {
   m.def(
       "gemm",
       [](uintptr_t A, int lda, uintptr_t Bt, int ldb, uintptr_t C, int ldc, uintptr_t bias, uintptr_t R, int ldr, int M,
-         int N, int K, int epi, uintptr_t stream) {
+         int N, int K, int epi, uintptr_t stream, int splits, uintptr_t ws) {
         GemmArgs g;
         g.A = P<const bf16>(A); g.lda = lda; g.Bt = P<const bf16>(Bt); g.ldb = ldb; g.C = P<bf16>(C); g.ldc = ldc;
         g.bias = P<const float>(bias); g.R = P<const bf16>(R); g.ldr = ldr; g.M = M; g.N = N; g.K = K; g.epi = epi;
+        g.splits = splits; g.ws = P<float>(ws);
         gemm_bf16(g, S(stream));
       },
-      "bf16 MFMA GEMM C = epi(A @ Bt^T)");
+      "bf16 MFMA GEMM C = epi(A @ Bt^T)", py::arg("A"), py::arg("lda"), py::arg("Bt"), py::arg("ldb"), py::arg("C"),
+      py::arg("ldc"), py::arg("bias"), py::arg("R"), py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"),
+      py::arg("epi"), py::arg("stream"), py::arg("splits") = 1, py::arg("ws") = 0);
+  m.def("gemm_splitk_splits", &gemm_splitk_splits, "split-K factor chosen for an [M,N,K] GEMM");
   m.attr("EPI_BIAS") = static_cast<int>(kEpiBias);
   m.attr("EPI_GELU") = static_cast<int>(kEpiGelu);
   m.attr("EPI_TANH") = static_cast<int>(kEpiTanh);
@@ -77,11 +81,16 @@ PYBIND11_MODULE(_atpu, m) {
   m.attr("EPI_RELU") = static_cast<int>(kEpiRelu);
   m.attr("EPI_OUT_F32") = static_cast<int>(kEpiOutF32);
   m.def("decode_attention", [](uintptr_t q, int ldq, uintptr_t k, uintptr_t v, int ldkv, int seq_stride, int group,
-                               uintptr_t lens, uintptr_t step_dev, uintptr_t bias, int bias_stride, uintptr_t out,
-                               int ldo, int rows, int H, float scale, uintptr_t stream) {
+                               uintptr_t lens, uintptr_t step_dev, uintptr_t hist, int hist_stride, uintptr_t bias,
+                               int bias_stride, uintptr_t out, int ldo, int rows, int H, float scale, uintptr_t stream) {
     decode_attention(P<const bf16>(q), ldq, P<const bf16>(k), P<const bf16>(v), ldkv, seq_stride, group,
-                     P<const int32_t>(lens), P<const int32_t>(step_dev), P<const float>(bias), bias_stride, P<bf16>(out),
-                     ldo, rows, H, scale, S(stream));
+                     P<const int32_t>(lens), P<const int32_t>(step_dev), P<const int32_t>(hist), hist_stride,
+                     P<const float>(bias), bias_stride, P<bf16>(out), ldo, rows, H, scale, S(stream));
+  });
+  m.def("beam_reorder_hist", [](uintptr_t src, uintptr_t dst, uintptr_t parent, int rows, int stride,
+                                uintptr_t step_dev, uintptr_t stream) {
+    beam_reorder_hist(P<const int32_t>(src), P<int32_t>(dst), P<const int32_t>(parent), rows, stride,
+                      P<const int32_t>(step_dev), S(stream));
   });
   m.def("kv_append", [](uintptr_t src, int lds, int col0, int ncols, uintptr_t cache, int seq_stride, int ldc,
                         uintptr_t step_dev, int rows, uintptr_t stream) {

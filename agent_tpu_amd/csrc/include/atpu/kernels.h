@@ -33,17 +33,29 @@ struct GemmArgs {
   int ldr = 0;
   int M = 0, N = 0, K = 0;
   int epi = 0;
+  // split-K (skinny M): splits > 1 needs ws = fp32 [splits, M, N]
+  int splits = 1;
+  float* ws = nullptr;
 };
 void gemm_bf16(const GemmArgs& g, hipStream_t stream);
+// split count the library picks for an [M,N,K] problem (1 = no split-K)
+int gemm_splitk_splits(int M, int N, int K);
 
 // ------------------------------------------------------------ decode (K9-K11)
-// One query row per (row, head) against a KV cache. Key j of row r lives at
-// k/v + ((r / group) * seq_stride + j) * ldkv + h*64. Length: lens[r / group],
-// or *step_dev + 1 when lens is null. bias_dist (fp32 [H, bias_stride]) adds
+// One query row per (row, head) against a KV cache. Cross attention (lens set):
+// key j of row r lives at k/v + ((r / group) * seq_stride + j) * ldkv + h*64,
+// length lens[r / group]; one workgroup serves the `group` rows of a sequence.
+// Self attention (step_dev set, group 1): length *step_dev + 1; key j < len-1
+// of row r lives in physical row hist[r * hist_stride + j] when hist is given
+// (beam backpointers), else in row r. bias_dist (fp32 [H, bias_stride]) adds
 // bias_dist[h][len-1-j] (T5 decoder relative position bias).
 void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int ldkv, int seq_stride, int group,
-                      const int32_t* lens, const int32_t* step_dev, const float* bias_dist, int bias_stride, bf16* out,
-                      int ldo, int rows, int H, float scale, hipStream_t stream);
+                      const int32_t* lens, const int32_t* step_dev, const int32_t* hist, int hist_stride,
+                      const float* bias_dist, int bias_stride, bf16* out, int ldo, int rows, int H, float scale,
+                      hipStream_t stream);
+// dst[r][j] = src[parent[r]][j] (j < t), dst[r][t] = parent[r]; t = *step_dev
+void beam_reorder_hist(const int32_t* src, int32_t* dst, const int32_t* parent, int rows, int stride,
+                       const int32_t* step_dev, hipStream_t stream);
 void kv_append(const bf16* src, int lds, int col0, int ncols, bf16* cache, int seq_stride, int ldc,
                const int32_t* step_dev, int rows, hipStream_t stream);
 void gather_rows(const bf16* src, bf16* dst, const int32_t* parent, int nrows, int seq_stride, int ldc,

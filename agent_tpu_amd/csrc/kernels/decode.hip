@@ -1,20 +1,27 @@
 // Seq2seq decode kernels for map_summarize.
 //
-//  * decode_attention: one query token per row against a KV cache. Self
-//    attention reads the beam's own cache rows [0, t]; cross attention reads
-//    the ENCODER K/V of the row's batch item (rows / group), masked by the
-//    source length. Optional T5 relative-position bias indexed by distance.
-//    One 64-wide wave per (row, head): q lives in registers, lane j scores key
-//    j of each 64-key chunk (128-B row reads), the softmax is a wave
-//    reduction, and lane d accumulates output dim d over keys (coalesced V
-//    rows).
+//  * decode_attention: one query token per row against a KV cache.
+//      - cross attention (lens != null): ONE workgroup per (batch item, head)
+//        serves all `group` beam rows of that item, so the encoder K/V of the
+//        item is streamed from HBM once per step instead of once per beam
+//        (it is the dominant byte stream of a decode step).
+//      - self attention (step_dev != null): key j of row r lives in the cache
+//        of physical row hist[r][j] (beam backpointers, see beam_reorder_hist)
+//        except the current position, which is the row's own; no cache copy
+//        on beam reorder. Optional T5 relative-position bias by distance.
+//    Scores: lane = key (full 128-B K row per lane, queries broadcast from
+//    LDS); softmax with block reductions; P·V with lane = (key-sub, 8 dims):
+//    one 16-B load per lane covers 8 keys x 128 B, fully coalesced.
 //  * kv_append: write the new token's K/V (from the fused QKV GEMM output)
 //    into the cache at step t (t read from device memory -> graph friendly).
-//  * gather_rows: beam reorder, dst[r] = src[parent[r]] for the first n rows
-//    of every cache slab.
-//  * beam_topk_rows: per beam row, log-softmax(logits) + beam score (+ EOS
-//    mask while below min_length) and its top-k candidates; the union over a
-//    batch item's beams contains that item's global top-k (merge on host).
+//  * beam_reorder_hist: hist'[r][j] = hist[parent[r]][j] (j < t), hist'[r][t]
+//    = parent[r]; the O(rows*T) int gather replaces an O(rows*T*L*2d) copy.
+//  * gather_rows: explicit cache reorder (kept for callers without hist).
+//  * beam_topk_rows: per beam row, ONE pass over the logits computes the
+//    online max / sum-exp (log-softmax normaliser) and a per-thread top-K
+//    (register lists with compile-time indexing only -> no scratch), then
+//    wave-level argmax rounds merge them; the union over an item's beams
+//    contains the item's global top-k (merged on the host).
 #include "atpu/common.h"
 #include "atpu/kernels.h"
 
@@ -26,67 +33,152 @@ namespace {
 constexpr int kD = 64;
 constexpr int kMaxKeys = 2048;
 
-__global__ __launch_bounds__(64) void decode_attention_kernel(
+template <int GM, int NW>
+__global__ __launch_bounds__(NW * 64) void decode_attention_kernel(
     const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k, const bf16* __restrict__ v, int ldkv,
-    int seq_stride, int group, const int32_t* __restrict__ lens, const int32_t* __restrict__ step_dev,
-    const float* __restrict__ bias_dist, int bias_stride, bf16* __restrict__ out, int ldo, float scale) {
-  __shared__ float p[kMaxKeys];
-  const int row = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
-  const int seq = row / group;
+    int seq_stride, int group, int nrows, const int32_t* __restrict__ lens, const int32_t* __restrict__ step_dev,
+    const int32_t* __restrict__ hist, int hist_stride, const float* __restrict__ bias_dist, int bias_stride,
+    bf16* __restrict__ out, int ldo, float scale) {
+  __shared__ float p[GM][kMaxKeys];
+  __shared__ float po[NW][GM][kD];
+  __shared__ float red[NW][16];
+  const int seq = blockIdx.x, h = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int G = min(group, nrows - seq * group);
   int len = lens ? lens[seq] : (*step_dev + 1);
   len = min(len, kMaxKeys);
-  // q row -> registers (fp32)
-  float qv[kD];
-  const bf16* qr = q + (size_t)row * ldq + h * kD;
+  auto phys = [&](int j) -> size_t {
+    const int r = (hist && j < len - 1) ? hist[(size_t)seq * hist_stride + j] : seq;
+    return ((size_t)r * seq_stride + j) * ldkv + h * kD;
+  };
+  // ---- scores on MFMA: S^T[16 keys x 16 queries] = K[16 x 64] . Q^T[64 x 16] ----
+  // A operand = K rows (lane&15 = key, (lane>>4)*8 = dims), B operand = the
+  // group's queries zero-padded to 16 (loop invariant, 8 VGPRs). Lane l gets
+  // S[key (l>>4)*4 + e][query l&15].
+  const int li = lane & 15, kq = (lane >> 4) * 8;
+  bf16x8 qb0, qb1;
+  if (li < G) {
+    const bf16* qr = q + (size_t)(seq * group + li) * ldq + h * kD;
+    qb0 = *reinterpret_cast<const bf16x8*>(qr + kq);
+    qb1 = *reinterpret_cast<const bf16x8*>(qr + 32 + kq);
+  } else {
 #pragma unroll
-  for (int c = 0; c < kD / 8; ++c) {
-    const bf16x8 x = *reinterpret_cast<const bf16x8*>(qr + c * 8);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) qv[c * 8 + e] = bf2f(x[e]) * scale;
+    for (int e = 0; e < 8; ++e) { qb0[e] = f2bf(0.f); qb1[e] = f2bf(0.f); }
   }
-  const size_t base = (size_t)seq * seq_stride;
-  float mx = -FLT_MAX;
-  for (int j0 = 0; j0 < len; j0 += 64) {
-    const int j = j0 + lane;
-    float s = -FLT_MAX;
-    if (j < len) {
-      const bf16* kr = k + (base + j) * ldkv + h * kD;
-      float acc = 0.f;
+  float mxl = -FLT_MAX;
+  for (int t = w; t * 16 < len; t += NW) {
+    const bf16* kr = k + phys(min(t * 16 + li, len - 1));
+    const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(kr + kq);
+    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(kr + 32 + kq);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, qb0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, qb1, acc, 0, 0, 0);
+    if (li < G) {
 #pragma unroll
-      for (int c = 0; c < kD / 8; ++c) {
-        const bf16x8 x = *reinterpret_cast<const bf16x8*>(kr + c * 8);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc += qv[c * 8 + e] * bf2f(x[e]);
+      for (int e = 0; e < 4; ++e) {
+        const int j = t * 16 + (lane >> 4) * 4 + e;
+        if (j < len) {
+          const float sj = acc[e] * scale + (bias_dist ? bias_dist[h * bias_stride + (len - 1 - j)] : 0.f);
+          p[li][j] = sj;
+          mxl = fmaxf(mxl, sj);
+        }
       }
-      if (bias_dist) acc += bias_dist[h * bias_stride + (len - 1 - j)];
-      s = acc;
-      p[j] = s;
     }
-    mx = fmaxf(mx, s);
   }
-  mx = wave_max(mx);
-  float sum = 0.f;
-  for (int j = lane; j < len; j += 64) {
-    const float e = __expf(p[j] - mx);
-    p[j] = e;
-    sum += e;
-  }
-  sum = wave_sum(sum);
+  mxl = fmaxf(mxl, __shfl_xor(mxl, 16));
+  mxl = fmaxf(mxl, __shfl_xor(mxl, 32));
+  if (lane < 16) red[w][lane] = mxl;
   __syncthreads();
-  const float inv = sum > 0.f ? 1.f / sum : 0.f;
-  // lane d accumulates output dim d
-  float o = 0.f;
-  const bf16* vcol = v + base * ldkv + h * kD + lane;
-  int j = 0;
-  for (; j + 4 <= len; j += 4) {
-    const float v0 = bf2f(vcol[(size_t)(j + 0) * ldkv]);
-    const float v1 = bf2f(vcol[(size_t)(j + 1) * ldkv]);
-    const float v2 = bf2f(vcol[(size_t)(j + 2) * ldkv]);
-    const float v3 = bf2f(vcol[(size_t)(j + 3) * ldkv]);
-    o += p[j] * v0 + p[j + 1] * v1 + p[j + 2] * v2 + p[j + 3] * v3;
+  float mx[GM];
+#pragma unroll
+  for (int g = 0; g < GM; ++g) {
+    float m = red[0][g];
+#pragma unroll
+    for (int x = 1; x < NW; ++x) m = fmaxf(m, red[x][g]);
+    mx[g] = m;
   }
-  for (; j < len; ++j) o += p[j] * bf2f(vcol[(size_t)j * ldkv]);
-  out[(size_t)row * ldo + h * kD + lane] = f2bf(o * inv);
+  __syncthreads();
+  float sm[GM];
+#pragma unroll
+  for (int g = 0; g < GM; ++g) sm[g] = 0.f;
+  for (int j = tid; j < len; j += NW * 64) {
+#pragma unroll
+    for (int g = 0; g < GM; ++g) {
+      if (g < G) {
+        const float e = __expf(p[g][j] - mx[g]);
+        p[g][j] = e;
+        sm[g] += e;
+      }
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < GM; ++g) {
+    const float s = wave_sum(sm[g]);
+    if (lane == 0) red[w][g] = s;
+  }
+  __syncthreads();
+  // ---- P·V: lane = (key sub 0..7, dims (lane&7)*8 .. +8) ----
+  const int ksub = lane >> 3, dc = (lane & 7) * 8;
+  float o[GM][8];
+#pragma unroll
+  for (int g = 0; g < GM; ++g)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[g][e] = 0.f;
+  for (int j0 = w * 8; j0 < len; j0 += NW * 8) {
+    const int j = j0 + ksub;
+    if (j < len) {
+      const bf16x8 vv = *reinterpret_cast<const bf16x8*>(v + phys(j) + dc);
+#pragma unroll
+      for (int g = 0; g < GM; ++g) {
+        if (g < G) {
+          const float pj = p[g][j];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[g][e] += pj * bf2f(vv[e]);
+        }
+      }
+    }
+  }
+  // reduce the 8 key-subgroups of the wave (lanes with equal lane&7)
+#pragma unroll
+  for (int g = 0; g < GM; ++g)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float x = o[g][e];
+      x += __shfl_xor(x, 8);
+      x += __shfl_xor(x, 16);
+      x += __shfl_xor(x, 32);
+      o[g][e] = x;
+    }
+  if (ksub == 0) {
+#pragma unroll
+    for (int g = 0; g < GM; ++g)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) po[w][g][dc + e] = o[g][e];
+  }
+  __syncthreads();
+  for (int i = tid; i < G * kD; i += NW * 64) {
+    const int g = i / kD, d = i % kD;
+    float s = 0.f, acc = 0.f;
+#pragma unroll
+    for (int x = 0; x < NW; ++x) {
+      s += red[x][g];
+      acc += po[x][g][d];
+    }
+    out[(size_t)(seq * group + g) * ldo + h * kD + d] = f2bf(s > 0.f ? acc / s : 0.f);
+  }
+}
+
+// hist'[r][j] = hist[parent[r]][j] for j < t; hist'[r][t] = parent[r]
+__global__ __launch_bounds__(256) void beam_reorder_hist_kernel(const int32_t* __restrict__ src,
+                                                                int32_t* __restrict__ dst,
+                                                                const int32_t* __restrict__ parent, int rows,
+                                                                int stride, const int32_t* __restrict__ step_dev) {
+  const int t = *step_dev;
+  const int n = rows * (t + 1);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int r = i / (t + 1), j = i % (t + 1);
+    const int pr = parent[r];
+    dst[(size_t)r * stride + j] = j < t ? src[(size_t)pr * stride + j] : pr;
+  }
 }
 
 // cache[row][t][0:ncols] = src[row][col0 : col0+ncols]
@@ -123,88 +215,153 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const bf16* __restrict
   }
 }
 
-constexpr int kTopkThreads = 256;
+constexpr int kTopkThreads = 1024;
+constexpr int kTopkWaves = kTopkThreads / 64;
 constexpr int kMaxBeamK = 16;
 
-// one block per beam row: log-softmax + beam score, then top-K (value desc,
-// index asc) via per-thread sorted lists and K rounds of block argmax
-__global__ __launch_bounds__(kTopkThreads) void beam_topk_kernel(const float* __restrict__ logits, int V,
-                                                                 const float* __restrict__ beam_scores, int eos,
-                                                                 int mask_eos, int K, float* __restrict__ out_score,
-                                                                 int32_t* __restrict__ out_token) {
-  __shared__ float red[kTopkThreads / 64];
-  __shared__ float cand_v[kTopkThreads];
-  __shared__ int cand_i[kTopkThreads];
-  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const float* x = logits + (size_t)row * V;
-  float mx = -FLT_MAX;
-  // normaliser over ALL tokens; the min-length EOS mask applies to selection
-  // only (HF applies MinLengthLogitsProcessor after log_softmax)
-  for (int i = tid; i < V; i += kTopkThreads) mx = fmaxf(mx, x[i]);
-  mx = wave_max(mx);
-  if (lane == 0) red[w] = mx;
-  __syncthreads();
-  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  __syncthreads();
-  float se = 0.f;
-  for (int i = tid; i < V; i += kTopkThreads) se += __expf(x[i] - mx);
-  se = wave_sum(se);
-  if (lane == 0) red[w] = se;
-  __syncthreads();
-  se = red[0] + red[1] + red[2] + red[3];
-  const float shift = beam_scores[row] - mx - __logf(se);
-  // per-thread sorted top-K
-  float tv[kMaxBeamK];
-  int ti[kMaxBeamK];
+// (value desc, index asc) ordering
+__device__ __forceinline__ bool better(float a, int ia, float b, int ib) { return a > b || (a == b && ia < ib); }
+
+// insert (val, id) into a sorted register list; compile-time indices only
+template <int KM>
+__device__ __forceinline__ void list_insert(float (&tv)[KM], int (&ti)[KM], float val, int id) {
 #pragma unroll
-  for (int r = 0; r < kMaxBeamK; ++r) { tv[r] = -FLT_MAX; ti[r] = 0x7fffffff; }
-  for (int i = tid; i < V; i += kTopkThreads) {
-    const float val = (mask_eos && i == eos) ? -FLT_MAX : x[i];
-    if (val > tv[K - 1]) {
-      int pos = K - 1;
-      while (pos > 0 && val > tv[pos - 1]) {
-        tv[pos] = tv[pos - 1];
-        ti[pos] = ti[pos - 1];
-        --pos;
-      }
-      tv[pos] = val;
-      ti[pos] = i;
+  for (int r = 0; r < KM; ++r) {
+    const bool sw = better(val, id, tv[r], ti[r]);
+    const float ov = tv[r];
+    const int oi = ti[r];
+    tv[r] = sw ? val : ov;
+    ti[r] = sw ? id : oi;
+    val = sw ? ov : val;
+    id = sw ? oi : id;
+  }
+}
+
+// K rounds of wave argmax over the lanes' list heads; results in lane r (< K)
+template <int KM>
+__device__ __forceinline__ void wave_topk(float (&tv)[KM], int (&ti)[KM], float& res_v, int& res_i) {
+  const int lane = threadIdx.x & 63;
+  res_v = -FLT_MAX;
+  res_i = 0x7fffffff;
+#pragma unroll
+  for (int r = 0; r < KM; ++r) {
+    float bv = tv[0];
+    int bi = ti[0];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const float ov = __shfl_xor(bv, off);
+      const int oi = __shfl_xor(bi, off);
+      if (better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+    }
+    if (lane == r) { res_v = bv; res_i = bi; }
+    if (ti[0] == bi && tv[0] == bv && bi != 0x7fffffff) {  // owner pops its head
+#pragma unroll
+      for (int x = 0; x + 1 < KM; ++x) { tv[x] = tv[x + 1]; ti[x] = ti[x + 1]; }
+      tv[KM - 1] = -FLT_MAX;
+      ti[KM - 1] = 0x7fffffff;
     }
   }
-  int head = 0;
-  for (int r = 0; r < K; ++r) {
-    cand_v[tid] = head < K ? tv[head] : -FLT_MAX;
-    cand_i[tid] = head < K ? ti[head] : 0x7fffffff;
-    __syncthreads();
-    for (int s = kTopkThreads / 2; s > 0; s >>= 1) {
-      if (tid < s) {
-        const float a = cand_v[tid], b = cand_v[tid + s];
-        const int ia = cand_i[tid], ib = cand_i[tid + s];
-        if (b > a || (b == a && ib < ia)) { cand_v[tid] = b; cand_i[tid] = ib; }
-      }
-      __syncthreads();
+}
+
+template <int K>
+__global__ __launch_bounds__(kTopkThreads) void beam_topk_kernel(const float* __restrict__ logits, int V,
+                                                                 const float* __restrict__ beam_scores, int eos,
+                                                                 int mask_eos, float* __restrict__ out_score,
+                                                                 int32_t* __restrict__ out_token) {
+  __shared__ float wm[kTopkWaves], ws[kTopkWaves];
+  constexpr int KM = K;
+  __shared__ float cv[kTopkWaves * KM];
+  __shared__ int ci[kTopkWaves * KM];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* x = logits + (size_t)row * V;
+  float tv[KM];
+  int ti[KM];
+#pragma unroll
+  for (int r = 0; r < KM; ++r) { tv[r] = -FLT_MAX; ti[r] = 0x7fffffff; }
+  // normaliser over ALL tokens; the min-length EOS mask applies to selection
+  // only (HF applies MinLengthLogitsProcessor after log_softmax)
+  float m = -FLT_MAX, s = 0.f;
+  for (int i = tid; i < V; i += kTopkThreads) {
+    const float val = x[i];
+    if (val > m) {
+      s = s * __expf(m - val) + 1.f;
+      m = val;
+    } else {
+      s += __expf(val - m);
     }
-    const int win = cand_i[0];
-    const float wv = cand_v[0];
-    if (tid == 0) {
-      out_score[(size_t)row * K + r] = wv == -FLT_MAX ? -FLT_MAX : wv + shift;
-      out_token[(size_t)row * K + r] = win;
+    const float sel = (mask_eos && i == eos) ? -FLT_MAX : val;
+    if (better(sel, i, tv[KM - 1], ti[KM - 1])) list_insert<KM>(tv, ti, sel, i);
+  }
+  // block log-sum-exp
+  const float wmax = wave_max(m);
+  float sa = (m == -FLT_MAX) ? 0.f : s * __expf(m - wmax);
+  sa = wave_sum(sa);
+  if (lane == 0) { wm[w] = wmax; ws[w] = sa; }
+  // wave-level top-K
+  float rv;
+  int ri;
+  wave_topk<KM>(tv, ti, rv, ri);
+  if (lane < K) { cv[w * KM + lane] = rv; ci[w * KM + lane] = ri; }
+  __syncthreads();
+  if (w == 0) {
+    float gm = -FLT_MAX;
+#pragma unroll
+    for (int x2 = 0; x2 < kTopkWaves; ++x2) gm = fmaxf(gm, wm[x2]);
+    float gs = 0.f;
+#pragma unroll
+    for (int x2 = 0; x2 < kTopkWaves; ++x2) gs += ws[x2] * __expf(wm[x2] - gm);
+    const float shift = beam_scores[row] - gm - __logf(gs);
+    // merge kTopkWaves sorted lists of K: lane l takes candidates l, l+64, ...
+#pragma unroll
+    for (int r = 0; r < KM; ++r) { tv[r] = -FLT_MAX; ti[r] = 0x7fffffff; }
+    for (int c = lane; c < kTopkWaves * K; c += 64) {
+      const int ww = c / K, rr = c % K;
+      list_insert<KM>(tv, ti, cv[ww * KM + rr], ci[ww * KM + rr]);
     }
-    if (head < K && ti[head] == win && tv[head] == wv) ++head;  // owner advances
-    __syncthreads();
+    wave_topk<KM>(tv, ti, rv, ri);
+    if (lane < K) {
+      out_score[(size_t)row * K + lane] = rv == -FLT_MAX ? -FLT_MAX : rv + shift;
+      out_token[(size_t)row * K + lane] = ri;
+    }
   }
 }
 
 }  // namespace
 
 void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int ldkv, int seq_stride, int group,
-                      const int32_t* lens, const int32_t* step_dev, const float* bias_dist, int bias_stride, bf16* out,
-                      int ldo, int rows, int H, float scale, hipStream_t stream) {
+                      const int32_t* lens, const int32_t* step_dev, const int32_t* hist, int hist_stride,
+                      const float* bias_dist, int bias_stride, bf16* out, int ldo, int rows, int H, float scale,
+                      hipStream_t stream) {
   ATPU_CHECK(rows > 0 && H > 0 && group >= 1, "decode_attention: bad shape");
   ATPU_CHECK(lens || step_dev, "decode_attention: need lens or a device step");
+  ATPU_CHECK(!hist || (step_dev && group == 1), "decode_attention: hist is for self attention (group 1)");
   ATPU_CHECK(ldq % 8 == 0 && ldkv % 8 == 0, "decode_attention: 16-B rows required");
-  hipLaunchKernelGGL(decode_attention_kernel, dim3(rows, H), dim3(64), 0, stream, q, ldq, k, v, ldkv, seq_stride, group,
-                     lens, step_dev, bias_dist, bias_stride, out, ldo, scale);
+  ATPU_CHECK((reinterpret_cast<uintptr_t>(k) & 15) == 0 && (reinterpret_cast<uintptr_t>(v) & 15) == 0,
+             "decode_attention: K/V must be 16-byte aligned");
+  const int nseq = (rows + group - 1) / group;
+  const dim3 grid(nseq, H);
+#define ATPU_DA(GM, NW)                                                                                          \
+  hipLaunchKernelGGL((decode_attention_kernel<GM, NW>), grid, dim3(NW * 64), 0, stream, q, ldq, k, v, ldkv,       \
+                     seq_stride, group, rows, lens, step_dev, hist, hist_stride, bias_dist, bias_stride, out, ldo, \
+                     scale)
+  if (group == 1)
+    ATPU_DA(1, 4);
+  else if (group <= 4)
+    ATPU_DA(4, 4);
+  else if (group <= 8)
+    ATPU_DA(8, 4);
+  else
+    ATPU_CHECK(false, "decode_attention: group (beams) must be <= 8");
+#undef ATPU_DA
+  ATPU_HIP_CHECK(hipGetLastError());
+}
+
+void beam_reorder_hist(const int32_t* src, int32_t* dst, const int32_t* parent, int rows, int stride,
+                       const int32_t* step_dev, hipStream_t stream) {
+  ATPU_CHECK(rows > 0 && stride > 0, "beam_reorder_hist: bad shape");
+  const int blocks = std::max(1, std::min(1024, (rows * stride + 255) / 256));
+  hipLaunchKernelGGL(beam_reorder_hist_kernel, dim3(blocks), dim3(256), 0, stream, src, dst, parent, rows, stride,
+                     step_dev);
   ATPU_HIP_CHECK(hipGetLastError());
 }
 
@@ -228,8 +385,17 @@ void gather_rows(const bf16* src, bf16* dst, const int32_t* parent, int nrows, i
 void beam_topk_rows(const float* logits, int rows, int V, const float* beam_scores, int eos, int mask_eos, int K,
                     float* out_score, int32_t* out_token, hipStream_t stream) {
   ATPU_CHECK(K >= 1 && K <= kMaxBeamK && K <= V, "beam_topk: 1 <= K <= 16");
-  hipLaunchKernelGGL(beam_topk_kernel, dim3(rows), dim3(kTopkThreads), 0, stream, logits, V, beam_scores, eos, mask_eos,
-                     K, out_score, out_token);
+#define ATPU_TK(KK)                                                                                               \
+  case KK:                                                                                                        \
+    hipLaunchKernelGGL(beam_topk_kernel<KK>, dim3(rows), dim3(kTopkThreads), 0, stream, logits, V, beam_scores,   \
+                       eos, mask_eos, out_score, out_token);                                                      \
+    break;
+  switch (K) {
+    ATPU_TK(1) ATPU_TK(2) ATPU_TK(3) ATPU_TK(4) ATPU_TK(5) ATPU_TK(6) ATPU_TK(7) ATPU_TK(8)
+    ATPU_TK(9) ATPU_TK(10) ATPU_TK(11) ATPU_TK(12) ATPU_TK(13) ATPU_TK(14) ATPU_TK(15) ATPU_TK(16)
+    default: break;
+  }
+#undef ATPU_TK
   ATPU_HIP_CHECK(hipGetLastError());
 }
 

@@ -38,10 +38,16 @@ constexpr int kRowBytes = kBK * 2;  // 128 B per staged row
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
-template <int BM, int BN, int WM, int WN, int EPI>
+// SPLIT: split-K. blockIdx.y = K slice (length K); the slice stores its fp32
+// partial tile in ws[slice][M][N] and splitk_reduce_kernel sums the slices in
+// order (deterministic) with the epilogue fused. (An in-kernel "last block
+// reduces" fixup was measured 10x slower: the device-scope fence it needs
+// writes back the XCD's whole L2 on gfx950.)
+template <int BM, int BN, int WM, int WN, int EPI, int SPLIT = 0>
 __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
     const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C, int ldc,
-    const float* __restrict__ bias, const bf16* __restrict__ R, int ldr, int M, int N, int K) {
+    const float* __restrict__ bias, const bf16* __restrict__ R, int ldr, int M, int N, int K,
+    float* __restrict__ ws = nullptr) {
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 16;
   constexpr int TN = BN / WN / 16;
@@ -56,6 +62,10 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ntn = (N + BN - 1) / BN;
   const int ntm = (M + BM - 1) / BM;
+  if constexpr (SPLIT) {
+    A += (size_t)blockIdx.y * K;
+    Bt += (size_t)blockIdx.y * K;
+  }
   const int tile = xcd_remap(blockIdx.x, ntm * ntn);
   const int m0 = (tile / ntn) * BM;
   const int n0 = (tile % ntn) * BN;
@@ -129,6 +139,21 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
     compute(cur);
     wait_vmcnt0();
     __syncthreads();
+  }
+
+  if constexpr (SPLIT) {
+    const size_t slab = (size_t)M * N;
+    float* mine = ws + blockIdx.y * slab;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + arow0 + i * 16 + frow;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + brow0 + j * 16 + fchunk * 4;
+        if (m < M && n < N) *reinterpret_cast<f32x4*>(mine + (size_t)m * N + n) = acc[i][j];
+      }
+    }
+    return;
   }
 
   // ---- epilogue: lane owns C[m][n..n+3] for each (i, j) fragment ----
@@ -394,6 +419,77 @@ void launch_256b(const GemmArgs& g, hipStream_t s) {
 
 
 
+// Sum the split-K fp32 partials [splits][M][N] in slice order and apply the epilogue.
+template <int EPI>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, bf16* __restrict__ C,
+                                                            int ldc, const float* __restrict__ bias,
+                                                            const bf16* __restrict__ R, int ldr, int M, int N) {
+  const int nq = N / 4;
+  const size_t slab = (size_t)M * N;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < M * nq; i += gridDim.x * blockDim.x) {
+    const int m = i / nq, n = (i % nq) * 4;
+    const float* src = ws + (size_t)m * N + n;
+    f32x4 v = *reinterpret_cast<const f32x4*>(src);
+    for (int z = 1; z < splits; ++z) v += *reinterpret_cast<const f32x4*>(src + z * slab);
+    if constexpr (EPI & kEpiBias) v += *reinterpret_cast<const f32x4*>(bias + n);
+    if constexpr (EPI & kEpiGelu) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = gelu_fast(v[e]);
+    }
+    if constexpr (EPI & kEpiTanh) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
+    }
+    if constexpr (EPI & kEpiRelu) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    if constexpr (EPI & kEpiResidual) {
+      const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + n);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += bf2f(r[e]);
+    }
+    if constexpr (EPI & kEpiOutF32) {
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + (size_t)m * ldc + n) = v;
+    } else {
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+      *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
+    }
+  }
+}
+
+void launch_splitk(const GemmArgs& g, int splits, hipStream_t s) {
+  constexpr int BM = 128, BN = 128;
+  const int nb = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+  const int kc = g.K / splits;
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, 2, 2, 0, 1>), dim3(nb, splits), dim3(256), 0, s, g.A, g.lda, g.Bt,
+                     g.ldb, nullptr, 0, nullptr, nullptr, 0, g.M, g.N, kc, g.ws);
+  const int work = g.M * (g.N / 4);
+  const dim3 rg(std::max(1, std::min(2048, (work + 255) / 256))), rb(256);
+#define ATPU_RED(E)                                                                                          \
+  case E:                                                                                                    \
+    hipLaunchKernelGGL((splitk_reduce_kernel<E>), rg, rb, 0, s, g.ws, splits, g.C, g.ldc, g.bias, g.R, g.ldr, \
+                       g.M, g.N);                                                                            \
+    break;
+  switch (g.epi) {
+    ATPU_RED(0)
+    ATPU_RED(kEpiBias)
+    ATPU_RED(kEpiBias | kEpiGelu)
+    ATPU_RED(kEpiBias | kEpiTanh)
+    ATPU_RED(kEpiBias | kEpiResidual)
+    ATPU_RED(kEpiResidual)
+    ATPU_RED(kEpiGelu)
+    ATPU_RED(kEpiRelu)
+    ATPU_RED(kEpiOutF32)
+    ATPU_RED(kEpiBias | kEpiOutF32)
+    default:
+      throw std::invalid_argument("atpu: unsupported GEMM epilogue " + std::to_string(g.epi));
+  }
+#undef ATPU_RED
+}
+
 template <int BM, int BN, int WM, int WN>
 void launch_tile(const GemmArgs& g, hipStream_t s) {
   const int nb = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
@@ -422,6 +518,22 @@ void launch_tile(const GemmArgs& g, hipStream_t s) {
 
 }  // namespace
 
+int gemm_splitk_splits(int M, int N, int K) {
+  // Skinny problems (decode: M = beams x docs) leave most of the 256 CUs idle
+  // with 128x128 tiles; split K so the grid reaches ~2 blocks per CU, keeping
+  // >= 2 K-tiles per split and an exact division of K.
+  static const int forced = [] {
+    const char* f = std::getenv("ATPU_GEMM_SPLITK");
+    return f ? std::atoi(f) : -1;
+  }();
+  const int nk = K / kBK;
+  const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  int want = forced >= 0 ? forced : (M > 1024 || tiles >= 256 ? 1 : (512 + tiles - 1) / tiles);
+  want = std::max(1, std::min({want, nk / 2, 16}));
+  while (want > 1 && nk % want) --want;
+  return want;
+}
+
 void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
   ATPU_CHECK(g.M > 0 && g.N > 0 && g.K > 0, "gemm: empty problem");
   ATPU_CHECK(g.K % kBK == 0, "gemm: K must be a multiple of 64");
@@ -441,6 +553,12 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
     const char* f = std::getenv("ATPU_GEMM_TILE");
     return f ? std::atoi(f) : 0;
   }();
+  if (g.splits > 1) {
+    ATPU_CHECK(g.ws && (g.K / kBK) % g.splits == 0, "gemm: split-K needs a workspace and K/64 % splits == 0");
+    launch_splitk(g, g.splits, stream);
+    ATPU_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const bool big_ok = g.N % 256 == 0;
   const bool use_big = !(g.epi & kEpiOutF32) && (forced ? (forced == 256 && big_ok) : (g.M >= 2048 && big_ok));
   if (use_big)

@@ -242,12 +242,14 @@ class T5Model:
         return torch.zeros((self.cfg.dec_layers, rows * T, 2 * self.cfg.d_model), dtype=dt, device=self.device)
 
     def step(self, tokens: torch.Tensor, step: torch.Tensor, cache: torch.Tensor, T: int, ckv: torch.Tensor,
-             src_lens: torch.Tensor, S: int, group: int) -> torch.Tensor:
+             src_lens: torch.Tensor, S: int, group: int, hist: Optional[torch.Tensor] = None) -> torch.Tensor:
         """One decoder position for ``rows`` sequences -> fp32 logits [rows, V].
 
         ``step`` is a 1-element int32 device tensor (position of ``tokens``);
         cache rows of sequence r are r*T .. r*T+T-1; encoder rows of batch item
-        r // group are (r//group)*S ...
+        r // group are (r//group)*S ... ``hist`` (int32 [rows, T]) are beam
+        backpointers: position j < step of row r was computed by row hist[r, j].
+        Every argument is a device tensor, so the step is hipGraph-capturable.
         """
         cfg, p = self.cfg, self.p
         d, H = cfg.d_model, cfg.heads
@@ -261,7 +263,7 @@ class T5Model:
             y = ops.rmsnorm(x, p[q + "ln1"], cfg.eps)
             qkv = ops.linear(y, p[q + "qkv"])
             ops.kv_append(qkv, d, 2 * d, c, T, step)
-            ctx = ops.decode_attention(qkv[:, :d], c[:, :d], c[:, d:], H, T, 1, step=step, bias_dist=dbias)
+            ctx = ops.decode_attention(qkv[:, :d], c[:, :d], c[:, d:], H, T, 1, step=step, bias_dist=dbias, hist=hist)
             x = ops.linear(ctx, p[q + "o"], residual=x)
             y = ops.rmsnorm(x, p[q + "ln2"], cfg.eps)
             cq = ops.linear(y, p[q + "cq"])

@@ -1,10 +1,13 @@
 """Seq2seq decode ops (K9-K11). Native kernels: ``csrc/kernels/decode.hip``.
 
 * :func:`decode_attention` — one query row per (row, head) vs a KV cache
-  (self: the row's own cache up to step t; cross: the encoder K/V of batch item
-  ``row // group`` masked by its source length), optional T5 distance bias.
+  (self: the row's cache up to step t, optionally through beam backpointers
+  ``hist``; cross: the encoder K/V of batch item ``row // group`` masked by its
+  source length, one workgroup per item so beams share the K/V stream),
+  optional T5 distance bias.
 * :func:`kv_append` — write step t's K/V into the cache (t on device).
-* :func:`gather_rows` — beam reorder of cache slabs.
+* :func:`beam_reorder_hist` — beam reorder of the backpointer table.
+* :func:`gather_rows` — explicit beam reorder of cache slabs.
 * :func:`beam_topk_rows` — log-softmax + beam score (+ EOS mask) + top-k per row.
 """
 from __future__ import annotations
@@ -23,33 +26,47 @@ HEAD_DIM = 64
 def decode_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, H: int, seq_stride: int, group: int = 1,
                      lens: Optional[torch.Tensor] = None, step: Optional[torch.Tensor] = None,
                      bias_dist: Optional[torch.Tensor] = None, scale: float = 1.0,
-                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """q [R, >=H*64]; k/v 2-D row views with ``seq_stride`` rows per sequence."""
+                     out: Optional[torch.Tensor] = None, hist: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """q [R, >=H*64]; k/v 2-D row views with ``seq_stride`` rows per sequence.
+
+    ``hist`` (int32 [R, T], self attention only): key j < t of row r lives in
+    the cache of row ``hist[r, j]``.
+    """
     R = q.shape[0]
     if not q.is_cuda:
-        return _decode_attention_ref(q, k, v, H, seq_stride, group, lens, step, bias_dist, scale, out)
+        return _decode_attention_ref(q, k, v, H, seq_stride, group, lens, step, bias_dist, scale, out, hist)
     check_bf16_dev(q, "q")
     check_bf16_dev(k, "k")
     check(lens is not None or step is not None, "need lens or step")
     if bias_dist is not None:
         check(bias_dist.dtype == torch.float32 and bias_dist.is_contiguous() and bias_dist.dim() == 2,
               "bias_dist must be fp32 [H, T]")
+    if hist is not None:
+        check(lens is None and group == 1, "hist is for self attention (group 1)")
+        check(hist.dtype == torch.int32 and hist.is_contiguous() and hist.shape[0] == R, "hist must be int32 [R, T]")
     out = torch.empty((R, H * HEAD_DIM), dtype=torch.bfloat16, device=q.device) if out is None else out
     native().decode_attention(ptr(q), row_stride(q, "q"), ptr(k), ptr(v), row_stride(k, "k"), seq_stride, group,
-                              ptr(lens), ptr(step), ptr(bias_dist), 0 if bias_dist is None else bias_dist.shape[1],
-                              ptr(out), row_stride(out, "out"), R, H, float(scale), stream_handle())
+                              ptr(lens), ptr(step), ptr(hist), 0 if hist is None else hist.shape[1], ptr(bias_dist),
+                              0 if bias_dist is None else bias_dist.shape[1], ptr(out), row_stride(out, "out"), R, H,
+                              float(scale), stream_handle())
     return out
 
 
-def _decode_attention_ref(q, k, v, H, seq_stride, group, lens, step, bias_dist, scale, out):
+def _decode_attention_ref(q, k, v, H, seq_stride, group, lens, step, bias_dist, scale, out, hist=None):
     R = q.shape[0]
     D = HEAD_DIM
     res = torch.zeros((R, H * D), dtype=torch.float32)
     for r in range(R):
         s = r // group
         n = int(lens[s]) if lens is not None else int(step.reshape(-1)[0]) + 1
-        kk = k[s * seq_stride:s * seq_stride + n, :H * D].float().view(n, H, D)
-        vv = v[s * seq_stride:s * seq_stride + n, :H * D].float().view(n, H, D)
+        if hist is not None:
+            src_rows = torch.cat([hist[r, :n - 1].long().cpu(), torch.tensor([r])])
+            rows_idx = src_rows * seq_stride + torch.arange(n)
+            kk = k[rows_idx, :H * D].float().view(n, H, D)
+            vv = v[rows_idx, :H * D].float().view(n, H, D)
+        else:
+            kk = k[s * seq_stride:s * seq_stride + n, :H * D].float().view(n, H, D)
+            vv = v[s * seq_stride:s * seq_stride + n, :H * D].float().view(n, H, D)
         qq = q[r, :H * D].float().view(H, D) * scale
         sc = torch.einsum("hd,nhd->hn", qq, kk)
         if bias_dist is not None:
@@ -71,6 +88,21 @@ def kv_append(src: torch.Tensor, col0: int, ncols: int, cache: torch.Tensor, seq
         return
     native().kv_append(ptr(src), row_stride(src, "src"), col0, ncols, ptr(cache), seq_stride,
                        row_stride(cache, "cache"), ptr(step), R, stream_handle())
+
+
+def beam_reorder_hist(src: torch.Tensor, dst: torch.Tensor, parent: torch.Tensor, step: torch.Tensor) -> None:
+    """dst[r, :t] = src[parent[r], :t]; dst[r, t] = parent[r] (t = step); [R, T] int32."""
+    R, T = src.shape
+    if not src.is_cuda:
+        t = int(step.reshape(-1)[0])
+        pl = parent.long().cpu()
+        dst[:, :t] = src[pl, :t]
+        dst[:, t] = parent.to(dst.dtype)
+        return
+    check(src.dtype == torch.int32 and dst.dtype == torch.int32 and parent.dtype == torch.int32,
+          "hist/parent must be int32")
+    check(src.is_contiguous() and dst.is_contiguous() and tuple(dst.shape) == (R, T), "hist must be contiguous [R, T]")
+    native().beam_reorder_hist(ptr(src), ptr(dst), ptr(parent), R, T, ptr(step), stream_handle())
 
 
 def gather_rows(src: torch.Tensor, dst: torch.Tensor, parent: torch.Tensor, nrows: int, seq_stride: int,

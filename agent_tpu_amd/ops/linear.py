@@ -1,10 +1,14 @@
 """Fused linear layer on the bf16 MFMA GEMM (K3/K5/K6).
 
 ``y = act(x @ w.T + bias) + residual`` with ``w`` in ``nn.Linear.weight``
-layout ``[N, K]``. Native kernel: ``csrc/kernels/gemm_bf16.hip``.
+layout ``[N, K]``. Native kernel: ``csrc/kernels/gemm_bf16.hip``. Skinny
+problems (decode steps, M = beams x docs) run split-K: fp32 partials in a
+caching-allocator workspace, summed in slice order by a reduce kernel that
+applies the epilogue.
 """
 from __future__ import annotations
 
+import functools
 from typing import Optional
 
 import torch
@@ -30,6 +34,11 @@ def linear_ref(x, w, bias=None, act=None, residual=None, out_f32=False):
     if residual is not None:
         y = y + residual.float()
     return y if out_f32 else y.to(x.dtype)
+
+
+@functools.lru_cache(maxsize=4096)
+def _splits(M: int, N: int, K: int) -> int:
+    return native().gemm_splitk_splits(M, N, K)
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: Optional[str] = None,
@@ -67,6 +76,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         out = torch.empty((M, N), dtype=odt, device=x.device)
     check(tuple(out.shape) == (M, N) and out.dtype == odt, "out must be [M, N] of the output dtype")
     ldc = row_stride(out, "out")
+    splits = _splits(M, N, K)
+    ws = torch.empty(splits * M * N, dtype=torch.float32, device=x.device) if splits > 1 else None
     native().gemm(ptr(x), lda, ptr(w), ldb, ptr(out), ldc, ptr(bias), ptr(residual), ldr, M, N, K, epi,
-                  stream_handle())
+                  stream_handle(), splits, ptr(ws))
     return out

@@ -7,8 +7,8 @@ descriptor (C4) and then runs the same registered ``@dp_task`` body as every
 worker. Bodies do their local (collective-free) work first; the per-rank
 errors are then exchanged, so a failure on ANY rank fails the job on rank 0
 with that rank's id in the message instead of hanging the others in a
-collective. ``MI355X_FAULT=rank:K`` injects a failure on rank
-K for tests.
+collective. ``MI355X_FAULT=rank:K[:stage[:times]]`` injects a
+failure on rank K for tests.
 
 Registered bodies: ``map_classify_csv`` (C2 all-gather of top-k) and
 ``risk_accumulate`` (C3 all-reduce of {count,sum,min,max}).
@@ -49,14 +49,26 @@ def init_from_env() -> None:
         dist.init_process_group("gloo")
 
 
+_FAULT_HITS: Dict[str, int] = {}
+
+
 def maybe_inject_fault(stage: str) -> None:
+    """``MI355X_FAULT=rank:K[:stage[:times]]`` raises on rank K (optionally only
+    at ``stage`` and only the first ``times`` times — later tasks succeed, which
+    lets tests check that the DP group survives a failed job)."""
     spec = os.getenv("MI355X_FAULT", "")
     if not spec.startswith("rank:"):
         return
     rank, _ = world()
     parts = spec.split(":")
-    if int(parts[1]) == rank and (len(parts) < 3 or parts[2] == stage):
-        raise RuntimeError(f"injected fault ({spec}) at {stage}")
+    if int(parts[1]) != rank or (len(parts) >= 3 and parts[2] not in ("", stage)):
+        return
+    if len(parts) >= 4:
+        n = _FAULT_HITS.get(stage, 0)
+        if n >= int(parts[3]):
+            return
+        _FAULT_HITS[stage] = n + 1
+    raise RuntimeError(f"injected fault ({spec}) at {stage}")
 
 
 def _check_errors(err: str) -> None:

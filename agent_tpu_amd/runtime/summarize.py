@@ -18,7 +18,9 @@ min_length=30, early_stopping=True)`` (``/root/reference/ops/map_summarize.py:53
 
 Device work per step: the decoder step (L layers of GEMMs, KV-cache appends,
 single-query attention), the LM-head GEMM and K10. Host work: bookkeeping on
-``[B, 2*num_beams]`` tensors and one gather of the KV caches by parent beam.
+``[B, 2*num_beams]`` tensors. Beam reorder never copies the KV cache: each
+row's history is a backpointer table ``hist[row, pos]`` (physical cache row of
+position ``pos``) and only that int table is gathered by parent beam (K11).
 """
 from __future__ import annotations
 
@@ -43,6 +45,7 @@ class GenConfig:
     min_length: int = 30
     length_penalty: float = 1.0
     early_stopping: bool = True
+    use_graph: bool = True  # replay the decoder step as one hipGraph (device runs only)
 
 
 @dataclass
@@ -68,7 +71,8 @@ def generate(model: T5Model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen:
     _, ckv = model.encode(src_ids, src_lens)
     t_enc = time.perf_counter()
     cache = model.new_cache(rows, T)
-    cache_alt = torch.empty_like(cache)
+    hist = torch.zeros((rows, T), dtype=torch.int32, device=dev)
+    hist_alt = torch.zeros_like(hist)
     step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
 
     run_seq = torch.full((B, nb, T), cfg.pad_id, dtype=torch.long)
@@ -83,12 +87,25 @@ def generate(model: T5Model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen:
     top_mask = torch.cat([torch.ones(nb, dtype=torch.bool), torch.zeros(K2 - nb, dtype=torch.bool)])
     tokens = torch.full((rows,), cfg.decoder_start_id, dtype=torch.int32, device=dev)
     lp = float(gen.length_penalty)
+    # Every step input is a static device buffer (tokens, step, cache, hist), so
+    # after one eager step the whole decoder step (~13 launches x L layers) is
+    # captured once and replayed: the host loop issues 1 launch per step.
+    use_graph = gen.use_graph and dev.type == "cuda"
+    graph, g_logits = None, None
 
     cur = 1  # sequence length so far (decoder start token included)
     steps = 0
     while cur < T:
         step_dev.fill_(cur - 1)
-        logits = model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb)
+        if graph is not None:
+            graph.replay()
+            logits = g_logits
+        else:
+            logits = model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist)
+            if use_graph:
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    g_logits = model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist)
         sc, tk = ops.beam_topk_rows(logits, run_scores.view(-1).to(dev), K2, cfg.eos_id, cur < gen.min_length)
         sc, tk = sc.cpu().view(B, nb * K2), tk.cpu().view(B, nb * K2).long()
         steps += 1
@@ -129,11 +146,11 @@ def generate(model: T5Model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen:
         fin_len = torch.gather(m_len, 1, keep)
 
         run_seq, run_scores = new_run_seq, new_run_scores
-        # KV caches follow their parent beams
+        # histories follow their parent beams (backpointers, no KV copy)
         par_rows = (torch.arange(B).view(-1, 1) * nb + parent).view(-1).to(torch.int32).to(dev)
-        ops.gather_rows(cache, cache_alt, par_rows, rows, T, step_dev, slabs=cfg.dec_layers)
-        cache, cache_alt = cache_alt, cache
-        tokens = run_seq[:, :, cur].reshape(-1).to(torch.int32).to(dev)
+        ops.beam_reorder_hist(hist, hist_alt, par_rows, step_dev)
+        hist.copy_(hist_alt)  # keep the captured buffer address
+        tokens.copy_(run_seq[:, :, cur].reshape(-1).to(torch.int32))
         cur += 1
         # early-stop heuristic (early_stopping=True: best running at current length)
         best_run = run_scores[:, :1] / float(cur - 1) ** lp

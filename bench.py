@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--words-per-row", type=int, default=150)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--csv", default="")
+    # rehearsal only: "gloo" lets >1 ranks share one GPU (RCCL refuses duplicate devices)
+    ap.add_argument("--dist-backend", default=os.environ.get("BENCH_DIST_BACKEND", "nccl"))
     return ap.parse_args()
 
 
@@ -57,14 +59,17 @@ def main() -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus and rank == 0:
         print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(a.dist_backend)
 
     from agent_tpu_amd._native import native
     from agent_tpu_amd.models.bert import config_for, init_random
-    from agent_tpu_amd.parallel.dp import broadcast_pack, all_gather_rows
+    from agent_tpu_amd.parallel.dp import all_gather_rows, broadcast_pack, comm_device
     from agent_tpu_amd.runtime.classify import ClassifyEngine
     from agent_tpu_amd.utils.synthetic import write_csv
 
@@ -106,7 +111,7 @@ def main() -> int:
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=comm_device(dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -133,6 +138,7 @@ def main() -> int:
                 "global_batch": B * world,
                 "seq_len": a.seq_len,
                 "parallelism": f"dp{world}",
+                "dist_backend": a.dist_backend if world > 1 else None,
                 "rows_per_gpu_per_step": B,
                 "num_labels": cfg.num_labels,
                 "topk": min(a.topk, cfg.num_labels),

@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""map_summarize throughput: T5-base batched beam search on one MI355X (BASELINE config 4).
+
+Decode settings are the reference's (``/root/reference/ops/map_summarize.py:53-59``):
+num_beams=4, max_length=130, min_length=30, early_stopping=True. Source docs are
+synthetic text hash-tokenized to ``--src-len`` tokens (the reference truncates at
+1024); weights are random-init T5-base. A step = one batch of ``--docs`` documents
+summarised end to end (tokenize -> encoder -> beam-search decode -> detokenize).
+
+Baseline: SURVEY.md §6 B12, T5-base-shaped proxy of the reference on CPU,
+3.72 s/doc = 0.269 docs/s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+
+BASELINE_DOCS_PER_SEC = 0.269
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="t5-base")
+    ap.add_argument("--docs", type=int, default=64, help="documents per step (batch)")
+    ap.add_argument("--src-len", type=int, default=512)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--num-beams", type=int, default=4)
+    ap.add_argument("--max-length", type=int, default=130)
+    ap.add_argument("--min-length", type=int, default=30)
+    a = ap.parse_args()
+
+    from agent_tpu_amd.models.t5 import config_for, init_random
+    from agent_tpu_amd.runtime.summarize import GenConfig, SummarizeEngine
+    from agent_tpu_amd.utils.synthetic import make_text_rows
+
+    dev = torch.device("cuda", 0)
+    cfg = config_for(a.model)
+    eng = SummarizeEngine(cfg, init_random(cfg, seed=0), dev, max_source_len=a.src_len)
+    gen = GenConfig(num_beams=a.num_beams, max_length=a.max_length, min_length=a.min_length)
+    docs = make_text_rows(a.docs * (a.warmup + a.steps), words_per_row=int(a.src_len * 0.8), seed=5)
+
+    for w in range(a.warmup):
+        eng.summarize(docs[w * a.docs:(w + 1) * a.docs], gen)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out_tokens, dec_steps, enc_ms, dec_ms, src_tokens = 0, 0, 0.0, 0.0, 0
+    for s in range(a.steps):
+        batch = docs[(a.warmup + s) * a.docs:(a.warmup + s + 1) * a.docs]
+        summaries, res = eng.summarize(batch, gen)
+        out_tokens += sum(len(x) - 1 for x in res.sequences)
+        dec_steps += res.steps
+        enc_ms += res.timing_ms["encode_ms"]
+        dec_ms += res.timing_ms["decode_ms"]
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    n = a.docs * a.steps
+    print(json.dumps({
+        "metric": "summarized docs/sec map_summarize T5-base (beams 4, max_len 130, min_len 30)",
+        "value": round(n / el, 3), "unit": "docs/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(el * 1000 / a.steps, 2), "higher_is_better": True,
+        "vs_baseline": round(n / el / BASELINE_DOCS_PER_SEC, 1), "dtype": "bf16",
+        "data": "synthetic text, random-init weights",
+        "config": {"model": a.model, "docs_per_step": a.docs, "src_len": a.src_len, "num_beams": a.num_beams,
+                   "max_length": a.max_length, "min_length": a.min_length,
+                   "decode_steps_per_batch": dec_steps / a.steps,
+                   "generated_tokens_per_sec": round(out_tokens / el, 1),
+                   "encode_ms_per_step": round(enc_ms / a.steps, 2),
+                   "decode_ms_per_step": round(dec_ms / a.steps, 2),
+                   "decode_ms_per_token_step": round(dec_ms / max(1, dec_steps), 3)},
+    }), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,119 @@
+"""Rank body for the multi-process DP tests (launched by torch.distributed.run).
+
+Each scenario exercises a collective of SURVEY.md §2.7 with the gloo backend
+(CPU) through the exact code the RCCL path runs. Rank 0 prints one
+``RESULT {json}`` line; any assertion failure exits non-zero.
+"""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from agent_tpu_amd.parallel import dp, dp_ops  # noqa: E402
+
+
+def scen_gather():
+    rank, ws = dp.world()
+    res = {}
+    for start, n in [(0, 0), (3, 1), (10, 5), (0, 7), (100, 1001)]:
+        s, k = dp.split_range(start, n, ws, rank)
+        ids = torch.arange(s, s + k, dtype=torch.int32).view(-1, 1).repeat(1, 3)
+        sc = torch.arange(s, s + k, dtype=torch.float32).view(-1, 1) * 0.5
+        gi, gs = dp.all_gather_rows(ids, sc)
+        assert gi.shape == (n, 3) and gs.shape == (n, 1), (gi.shape, n)
+        assert torch.equal(gi[:, 0], torch.arange(start, start + n, dtype=torch.int32))
+        assert torch.equal(gs[:, 0], torch.arange(start, start + n, dtype=torch.float32) * 0.5)
+        res[f"{start}+{n}"] = int(gi.shape[0])
+    return res
+
+
+def scen_pack():
+    from agent_tpu_amd.models.bert import config_for, init_random
+
+    rank, _ = dp.world()
+    cfg = config_for("bert-tiny")
+    pack = init_random(cfg, seed=7) if rank == 0 else None
+    out = dp.broadcast_pack(pack, cfg, torch.device("cpu"))
+    ref = init_random(cfg, seed=7)
+    assert torch.equal(out.buffer, ref.buffer)
+    desc = dp.broadcast_task({"op": "x", "n": 3} if rank == 0 else None)
+    assert desc == {"op": "x", "n": 3}
+    return {"bytes": int(out.buffer.numel() * out.buffer.element_size())}
+
+
+def scen_t5pack():
+    from agent_tpu_amd.models import t5
+
+    rank, _ = dp.world()
+    cfg = t5.config_for("t5-tiny")
+    pack = t5.init_random(cfg, seed=3) if rank == 0 else None
+    out = dp.broadcast_pack(pack, cfg, torch.device("cpu"), builder=t5.param_specs)
+    assert torch.equal(out.buffer, t5.init_random(cfg, seed=3).buffer)
+    return {"ok": True}
+
+
+def scen_risk():
+    """Rank 0 dispatches, the others serve in worker_loop (the app.py process model)."""
+    rank, ws = dp.world()
+    if rank != 0:
+        dp_ops.worker_loop()
+        return None
+    from ops.risk_accumulate import risk_accumulate
+
+    vals = [((i * 7919) % 1000) / 7.0 - 50.0 for i in range(1003)]
+    got = dp_ops.dispatch("risk_accumulate", {"values": vals})
+    ref = risk_accumulate({"values": vals})
+    out = {"got": got, "ref": ref}
+    items = [{"risk": "1.5"}, {"other": 2}, {"risk": 3}, {"risk": True}]
+    out["items"] = dp_ops.dispatch("risk_accumulate", {"items": items})
+    csv_path = os.environ["DP_TEST_CSV"]
+    out["csv"] = dp_ops.dispatch("risk_accumulate", {"source_uri": csv_path, "field": "risk", "start_row": 2,
+                                                     "shard_size": 40})
+    try:
+        dp_ops.dispatch("risk_accumulate", {"values": "nope"})
+        out["bad"] = None
+    except RuntimeError as exc:
+        out["bad"] = str(exc)
+    out["empty"] = dp_ops.dispatch("risk_accumulate", {"values": []})
+    dp_ops.shutdown_workers()
+    return out
+
+
+def scen_fault():
+    rank, _ = dp.world()
+    if rank != 0:
+        dp_ops.worker_loop()
+        return None
+    out = {}
+    try:
+        dp_ops.dispatch("risk_accumulate", {"values": [1.0, 2.0, 3.0, 4.0]})
+        out["err"] = None
+    except RuntimeError as exc:
+        out["err"] = str(exc)
+    # the job after a fault still works: workers kept serving (fault fires once)
+    out["after"] = dp_ops.dispatch("risk_accumulate", {"values": [1.0, 2.0]})
+    dp_ops.shutdown_workers()
+    return out
+
+
+def main():
+    scen = sys.argv[1]
+    dist.init_process_group("gloo")
+    try:
+        res = globals()[f"scen_{scen}"]()
+    finally:
+        if dist.is_initialized():
+            if scen not in ("risk", "fault"):  # worker_loop ranks already left the group
+                dist.barrier()
+            dist.destroy_process_group()
+    if int(os.environ.get("RANK", "0")) == 0:
+        print("RESULT " + json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

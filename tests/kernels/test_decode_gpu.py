@@ -51,7 +51,47 @@ def test_decode_self_with_bias_append_gather(gpu):
     assert torch.equal(d3[:, :7], c3[parent.long().cpu(), :7])
 
 
-@pytest.mark.parametrize("V,k,mask", [(4096, 8, False), (32128, 8, True), (50, 2, False)])
+def test_decode_self_hist_backpointers(gpu):
+    rows, H, T, t = 8, 4, 24, 13
+    d = H * 64
+    cache = _r((rows * T, 2 * d), gpu, seed=21)
+    q = _r((rows, d), gpu, seed=22)
+    g = torch.Generator().manual_seed(3)
+    hist = torch.randint(0, rows, (rows, T), generator=g, dtype=torch.int32)
+    step = torch.tensor([t], dtype=torch.int32)
+    bias = _r((H, T), gpu, 1.0, torch.float32, seed=23)
+    out = ops.decode_attention(q, cache[:, :d], cache[:, d:], H, T, 1, step=step.to(gpu), bias_dist=bias,
+                               hist=hist.to(gpu))
+    ref = _decode_attention_ref(q.cpu(), cache.cpu()[:, :d], cache.cpu()[:, d:], H, T, 1, None, step, bias.cpu(), 1.0,
+                                None, hist)
+    assert _rel(out, ref) < 2e-2
+    # reorder kernel vs CPU reference
+    parent = torch.tensor([3, 3, 0, 7, 1, 2, 2, 5], dtype=torch.int32)
+    dst = torch.zeros_like(hist)
+    ops.beam_reorder_hist(hist, dst, parent, step)
+    dgpu = torch.zeros_like(hist).to(gpu)
+    ops.beam_reorder_hist(hist.to(gpu), dgpu, parent.to(gpu), step.to(gpu))
+    assert torch.equal(dgpu.cpu()[:, :t + 1], dst[:, :t + 1])
+    assert torch.equal(dst[:, t], parent) and torch.equal(dst[:, :t], hist[parent.long(), :t])
+
+
+@pytest.mark.parametrize("rows,group,seqlen", [(256, 4, 512), (40, 4, 100), (24, 8, 7), (9, 3, 2048), (10, 4, 64),
+                                               (13, 5, 300)])
+def test_decode_cross_grouped_shapes(gpu, rows, group, seqlen):
+    H = 12
+    nseq = (rows + group - 1) // group
+    q = _r((rows, H * 64), gpu, seed=31)
+    kv = _r((nseq * seqlen, 2 * H * 64), gpu, seed=32)
+    g = torch.Generator().manual_seed(4)
+    lens = torch.randint(1, seqlen + 1, (nseq,), generator=g, dtype=torch.int32)
+    out = ops.decode_attention(q, kv[:, :H * 64], kv[:, H * 64:], H, seqlen, group, lens=lens.to(gpu))
+    ref = _decode_attention_ref(q.cpu(), kv.cpu()[:, :H * 64], kv.cpu()[:, H * 64:], H, seqlen, group, lens, None, None,
+                                1.0, None)
+    assert _rel(out, ref) < 2e-2
+
+
+@pytest.mark.parametrize("V,k,mask", [(4096, 8, False), (32128, 8, True), (50, 2, False), (32128, 16, False),
+                                      (1000, 1, True), (70000, 5, False)])
 def test_beam_topk_rows(gpu, V, k, mask):
     R = 12
     logits = _r((R, V), gpu, 3.0, torch.float32, seed=4)
@@ -62,6 +102,24 @@ def test_beam_topk_rows(gpu, V, k, mask):
     assert torch.equal(idx.cpu(), ridx)
     if mask:
         assert not (idx == 1).any()
+
+
+@pytest.mark.parametrize("M,N,K,act,res,bias", [(256, 768, 3072, None, True, False), (256, 3072, 768, "relu", False, False),
+                                                (256, 2304, 768, None, False, True), (96, 768, 768, "gelu", False, True),
+                                                (512, 768, 768, None, True, False)])
+def test_gemm_splitk_skinny(gpu, M, N, K, act, res, bias):
+    from agent_tpu_amd.ops.linear import _splits
+
+    x = _r((M, K), gpu, seed=41)
+    w = _r((N, K), gpu, 0.05, seed=42)
+    r = _r((M, N), gpu, seed=43) if res else None
+    b = _r((N,), gpu, 1.0, torch.float32, seed=44) if bias else None
+    y = ops.linear(x, w, bias=b, act=act, residual=r)
+    from agent_tpu_amd.ops.linear import linear_ref
+
+    ref = linear_ref(x.cpu(), w.cpu(), None if b is None else b.cpu(), act, None if r is None else r.cpu(), out_f32=True)
+    assert _splits(M, N, K) > 1
+    assert _rel(y, ref) < 2e-2
 
 
 def test_gemm_relu_and_f32_out(gpu):
@@ -100,7 +158,9 @@ def test_t5_step_and_generate_gpu(gpu):
     assert _rel(lg, lc) < 5e-2
     r1 = generate(gpu_m, ids.to(gpu), lens.to(gpu), GenConfig(num_beams=4, max_length=16, min_length=4))
     r2 = generate(gpu_m, ids.to(gpu), lens.to(gpu), GenConfig(num_beams=4, max_length=16, min_length=4))
-    assert r1.sequences == r2.sequences
+    r3 = generate(gpu_m, ids.to(gpu), lens.to(gpu), GenConfig(num_beams=4, max_length=16, min_length=4,
+                                                              use_graph=False))
+    assert r1.sequences == r2.sequences == r3.sequences
     assert all(2 <= len(s) <= 16 and s[0] == 0 for s in r1.sequences)
 
 
