@@ -1,0 +1,158 @@
+"""Agent loop against the mock controller: wire protocol, multi-task leases,
+bad tasks, result retry policy, signals and exit codes.
+
+The real ``app.py`` runs as a subprocess with env overrides (CPU only).
+"""
+import os
+import signal
+import subprocess
+import sys
+import time
+
+import pytest
+
+from .mock_controller import MockController
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+@pytest.fixture
+def ctl():
+    c = MockController().start()
+    yield c
+    c.stop()
+
+
+def start_agent(ctl, tasks="echo,risk_accumulate,read_csv_shard,map_tokenize", **env):
+    e = dict(os.environ)
+    e.update({"CONTROLLER_URL": ctl.url, "TASKS": tasks, "IDLE_SLEEP_SEC": "0.02", "ERROR_BACKOFF_SEC": "0.05",
+              "ERROR_LOG_EVERY_SEC": "0", "AGENT_NAME": "test-agent", "AGENT_LABELS": "zone=a,gpu,x=1=2",
+              "PYTHONUNBUFFERED": "1", "GPU_DISABLED": "1", "HIP_VISIBLE_DEVICES": ""})
+    e.update({k: str(v) for k, v in env.items()})
+    return subprocess.Popen([sys.executable, "app.py"], cwd=REPO, env=e, stdout=subprocess.PIPE,
+                            stderr=subprocess.STDOUT, text=True)
+
+
+def stop_agent(p, sig=signal.SIGTERM, timeout=30):
+    p.send_signal(sig)
+    out, _ = p.communicate(timeout=timeout)
+    return p.returncode, out
+
+
+def by_job(ctl):
+    return {r["job_id"]: r for r in ctl.results}
+
+
+def test_protocol_and_ops(ctl, tmp_path):
+    csv = tmp_path / "s.csv"
+    csv.write_text("id,text,risk\n1,a,0.5\n2,b,1.5\n3,c,2.5\n")
+    ctl.lease({"id": "j1", "op": "echo", "payload": {"x": 1}, "job_epoch": 7})
+    ctl.lease({"job_id": "j2", "op": "risk_accumulate", "payload": {"values": [1, "2", 3.5]}, "job_epoch": 1})
+    ctl.lease({"id": "j3", "op": "read_csv_shard", "payload": {"source_uri": str(csv), "start_row": 1,
+                                                              "shard_size": 5}})
+    ctl.lease({"id": "j4", "op": "map_tokenize", "payload": {"text": "abcdef", "chunk_size": 4}})
+    ctl.lease({"id": "j5", "op": "risk_accumulate", "payload": {"values": "bad"}})
+    ctl.lease({"id": "j6", "op": "nope", "payload": {}})
+    ctl.lease({"op": "echo", "payload": {}})  # no id: skipped, never resulted
+    ctl.lease({"id": "j8", "op": "echo", "payload": []})  # payload [] is falsy -> {} like the reference
+    p = start_agent(ctl)
+    try:
+        assert ctl.wait(lambda c: len(c.results) >= 7, 90), ctl.results
+        n = len(ctl.lease_requests)
+        assert ctl.wait(lambda c: len(c.lease_requests) > n, 30)  # next lease carries updated metrics
+    finally:
+        code, out = stop_agent(p)
+    assert code == 0, out
+    r = by_job(ctl)
+    assert r["j1"] == {"lease_id": "L1", "job_id": "j1", "job_epoch": 7, "status": "succeeded",
+                       "result": {"ok": True, "echo": {"x": 1}}, "error": None}
+    assert r["j2"]["status"] == "succeeded" and r["j2"]["job_epoch"] == 1
+    assert r["j2"]["result"]["count"] == 3 and r["j2"]["result"]["sum"] == 6.5
+    rows = r["j3"]["result"]["rows"]
+    assert r["j3"]["status"] == "succeeded" and [x["id"] for x in rows] == ["2", "3"]
+    assert r["j4"]["result"]["tokens"] == ["abcd", "ef"]
+    assert r["j5"]["status"] == "failed" and r["j5"]["result"] is None
+    assert r["j5"]["error"]["type"] == "ValueError" and r["j5"]["error"]["message"] == "payload.values must be a list"
+    assert "Traceback" in r["j5"]["error"]["trace"]
+    assert r["j6"]["status"] == "failed" and "Unknown op 'nope'" in r["j6"]["error"]["message"]
+    assert r["j8"]["result"] == {"ok": True, "echo": {}}
+    assert len(ctl.results) == 7  # the id-less task is never resulted
+    assert "bad task" in out
+    req = ctl.lease_requests[0]
+    assert set(req) == {"agent", "capabilities", "max_tasks", "timeout_ms", "labels", "worker_profile", "metrics"}
+    assert req["agent"] == "test-agent" and req["max_tasks"] == 1 and req["timeout_ms"] == 3000
+    assert req["capabilities"] == {"ops": ["echo", "risk_accumulate", "read_csv_shard", "map_tokenize"]}
+    assert req["labels"] == {"zone": "a", "gpu": True, "x": "1=2"}
+    prof = req["worker_profile"]
+    assert {"cpu", "gpu", "workers", "tier", "limits"} <= set(prof)
+    assert prof["limits"] == {"max_payload_bytes": 262144, "max_tokens": 2048}
+    assert {"jobs_completed", "jobs_failed", "rows_per_sec"} <= set(req["metrics"])
+    later = ctl.lease_requests[-1]["metrics"]
+    assert later["jobs_completed"] >= 5 and later["jobs_failed"] >= 2
+
+
+def test_multi_task_lease_runs_every_task(ctl):
+    ctl.lease(*[{"id": f"m{i}", "op": "echo", "payload": {"i": i}} for i in range(3)], lease_id="LM")
+    p = start_agent(ctl, MAX_TASKS=3)
+    try:
+        assert ctl.wait(lambda c: len(c.results) >= 3, 60)
+    finally:
+        code, _ = stop_agent(p)
+    assert code == 0
+    assert [r["job_id"] for r in ctl.results] == ["m0", "m1", "m2"]
+    assert all(r["lease_id"] == "LM" for r in ctl.results)
+    assert ctl.lease_requests[0]["max_tasks"] == 3
+
+
+def test_result_retry_policy(ctl):
+    ctl.result_codes = {"stale": [409], "flaky": [500, 503], "dead": [500, 500, 500, 500]}
+    for jid in ("stale", "flaky", "dead", "after"):
+        ctl.lease({"id": jid, "op": "echo", "payload": {}})
+    p = start_agent(ctl, RESULT_RETRIES=2)
+    try:
+        assert ctl.wait(lambda c: "after" in c.result_attempts, 60)
+    finally:
+        code, out = stop_agent(p)
+    assert code == 0
+    assert ctl.result_attempts["stale"] == 1  # 4xx is final (stale epoch)
+    assert ctl.result_attempts["flaky"] == 3 and "flaky" in by_job(ctl)
+    assert ctl.result_attempts["dead"] == 3 and "dead" not in by_job(ctl)
+    assert "post result error" in out
+
+
+def test_lease_errors_back_off_and_recover(ctl):
+    ctl.lease(status=500, body={"error": "boom"})
+    ctl.lease(status=200, body={"no_lease_id": True})
+    ctl.lease(status=200, body=["not", "a", "dict"])
+    ctl.lease({"id": "ok1", "op": "echo", "payload": {}})
+    p = start_agent(ctl)
+    try:
+        assert ctl.wait(lambda c: len(c.results) >= 1, 60)
+    finally:
+        code, out = stop_agent(p)
+    assert code == 0 and by_job(ctl)["ok1"]["status"] == "succeeded"
+    assert "lease error" in out
+
+
+def test_sigint_and_idle(ctl):
+    p = start_agent(ctl)
+    assert ctl.wait(lambda c: len(c.lease_requests) >= 3, 60)  # 204s -> idle polling
+    code, out = stop_agent(p, signal.SIGINT)
+    assert code == 0 and "stopped" in out
+
+
+def test_no_tasks_exits_2(ctl):
+    p = start_agent(ctl, tasks="")
+    out, _ = p.communicate(timeout=60)
+    assert p.returncode == 2 and "no TASKS" in out
+    assert not ctl.lease_requests
+
+
+def test_unavailable_op_not_advertised(ctl):
+    p = start_agent(ctl, tasks="echo,definitely_not_an_op")
+    try:
+        assert ctl.wait(lambda c: len(c.lease_requests) >= 1, 60)
+    finally:
+        code, out = stop_agent(p)
+    assert ctl.lease_requests[0]["capabilities"]["ops"] == ["echo"]
+    assert "op unavailable: definitely_not_an_op" in out
