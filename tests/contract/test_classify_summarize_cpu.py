@@ -1,0 +1,65 @@
+"""map_classify fallback stub and map_summarize on a CPU-only agent.
+
+map_classify: the reference's ``allow_fallback`` semantics
+(``/root/reference/ops/map_classify_tpu.py:22-28,84-89``, Appendix A probe:
+``fallback_reason`` overrides the real error). map_summarize: payload
+validation before model init (§2.4.16) and the fp32 CPU path
+(``SUMMARIZE_FORCE_CPU=1``) end to end on t5-tiny.
+"""
+import importlib
+
+import pytest
+import torch
+
+from ops import map_classify as mc
+
+pytestmark = pytest.mark.skipif(torch.cuda.is_available(), reason="CPU-only semantics")
+
+
+def test_classify_fallback_stub():
+    out = mc.map_classify_tpu({"input": [1, 2, 3], "topk": 3})
+    assert set(out) == {"op", "fallback", "reason", "topk", "elapsed_ms"}
+    assert out["op"] == "map_classify_tpu" and out["fallback"] == "cpu" and out["topk"] == []
+    assert "GPU" in out["reason"]
+    out = mc.map_classify({"input": [1], "fallback_reason": "forced"})
+    assert out["op"] == "map_classify" and out["reason"] == "forced"
+    assert mc.map_classify_tpu(None)["fallback"] == "cpu"
+    with pytest.raises(RuntimeError):
+        mc.map_classify({"input": [1], "allow_fallback": False})
+
+
+@pytest.fixture
+def summarize(monkeypatch):
+    monkeypatch.setenv("SUMMARIZE_MODEL", "t5-tiny")
+    monkeypatch.setenv("SUMMARIZE_FORCE_CPU", "1")
+    import ops.map_summarize as ms
+
+    ms = importlib.reload(ms)
+    yield ms
+    monkeypatch.undo()
+    importlib.reload(ms)
+
+
+def test_summarize_validation_before_init(summarize):
+    ms = summarize
+    assert ms.handle(None) == {"ok": False, "error": "empty payload"}
+    assert ms.handle({}) == {"ok": False, "error": "empty payload"}
+    assert ms.handle({"text": "   "}) == {"ok": False, "error": "no text provided"}
+    assert ms.handle({"text": 5}) == {"ok": False, "error": "no text provided"}
+    assert ms.handle({"texts": []})["error"] == "payload.texts must be a non-empty list of non-empty strings"
+    assert ms.handle({"texts": ["ok", ""]})["ok"] is False
+    assert ms.handle({"text": "x", "num_beams": "many"})["error"].startswith("bad generation parameter")
+    assert ms._engine is None  # nothing above initialised the model
+
+
+def test_summarize_cpu_end_to_end(summarize):
+    ms = summarize
+    doc = "alpha beta gamma delta epsilon zeta eta theta iota kappa lambda mu " * 4
+    out = ms.handle({"text": doc, "max_length": 12, "min_length": 4})
+    assert out["ok"] and out["device"] == "cpu" and out["model"] == "t5-tiny"
+    assert isinstance(out["summary"], str) and 2 <= out["decode_steps"] <= 11
+    outs = ms.handle({"texts": [doc, "short one"], "max_length": 10, "min_length": 3, "num_beams": 2})
+    assert outs["ok"] and len(outs["summaries"]) == 2
+    words = set(doc.split()) | {"short", "one"}
+    for s in outs["summaries"]:
+        assert all(w in words or w.startswith("<") for w in s.split())

@@ -77,3 +77,18 @@ def test_ops_loader(monkeypatch):
         ops_loader.load_ops(["echo", "nope"])
     ok, bad = ops_loader.load_ops_lenient(["echo", "nope"])
     assert list(ok) == ["echo"] and bad[0][0] == "nope"
+
+
+def test_every_op_has_a_contract():
+    """Reference contract format (ops/map_classify_tpu.CONTRACT.md:1-26): title + 4 sections."""
+    import os
+
+    here = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "ops")
+    modules = set(ops.OP_TO_MODULE.values())
+    for mod in modules:
+        path = os.path.join(here, f"{mod}.CONTRACT.md")
+        assert os.path.exists(path), f"missing {path}"
+        text = open(path).read()
+        assert text.startswith("# ") and "— Contract (v0)" in text.splitlines()[0], path
+        for sec in ("## Purpose", "## Inputs (payload)", "## Outputs", "## Notes"):
+            assert sec in text, (path, sec)

@@ -1,0 +1,118 @@
+"""worker_sizing: CPU formulas (reference worker_sizing.py:44-124 goldens),
+AMD GPU discovery from a fake KFD topology, visibility filters, HBM-derived
+batch sizing, TPU schema stability."""
+import os
+import types
+
+import pytest
+
+import worker_sizing as ws
+
+GIB = 1 << 30
+
+
+def _node(root, idx, props, banks=()):
+    d = os.path.join(root, str(idx))
+    os.makedirs(os.path.join(d, "mem_banks"))
+    with open(os.path.join(d, "properties"), "w") as f:
+        for k, v in props.items():
+            f.write(f"{k} {v}\n")
+    for b, (heap, size) in enumerate(banks):
+        bd = os.path.join(d, "mem_banks", str(b))
+        os.makedirs(bd)
+        with open(os.path.join(bd, "properties"), "w") as f:
+            f.write(f"heap_type {heap}\nsize_in_bytes {size}\n")
+
+
+@pytest.fixture
+def kfd(tmp_path, monkeypatch):
+    root = str(tmp_path / "nodes")
+    _node(root, 0, {"simd_count": 0, "cpu_cores_count": 64}, [(0, 512 * GIB)])
+    for i in (1, 2):
+        _node(root, i, {"simd_count": 1024, "simd_per_cu": 4, "gfx_target_version": 90500},
+              [(1, 288 * GIB), (0, 64 * GIB)])
+    monkeypatch.setenv("ATPU_KFD_TOPOLOGY", root)
+    for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DISABLED",
+              "CLASSIFY_BATCH_ROWS", "DP_WORLD_SIZE", "GPU_ONLY", "TPU_ONLY"):
+        monkeypatch.delenv(v, raising=False)
+    return root
+
+
+def test_kfd_discovery(kfd):
+    g = ws.detect_gpu()
+    assert g["gpu_present"] and g["gpu_count"] == 2 and g["vendor"] == "amd"
+    assert g["vram_gb"] == 288.0 and g["hbm_gb"] == [288.0, 288.0]
+    d = g["devices"][0]
+    assert d == {"index": 0, "name": "gfx950", "arch": "gfx950", "total_memory_bytes": 288 * GIB,
+                 "compute_units": 256}
+    assert g["max_gpu_workers"] == 2 and g["dp_world_size"] == 2
+    assert g["classify_batch_rows"] == 1024  # capped: GEMMs saturate near 128k tokens
+
+
+@pytest.mark.parametrize("var", ["HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"])
+def test_visibility_filters(kfd, monkeypatch, var):
+    monkeypatch.setenv(var, "1")
+    g = ws.detect_gpu()
+    assert g["gpu_count"] == 1 and g["devices"][0]["index"] == 0
+    for hidden in ("none", "-1", ""):
+        monkeypatch.setenv(var, hidden)
+        assert ws.detect_gpu()["gpu_present"] is False
+
+
+def test_gpu_disabled_and_batch_override(kfd, monkeypatch):
+    monkeypatch.setenv("CLASSIFY_BATCH_ROWS", "333")
+    monkeypatch.setenv("DP_WORLD_SIZE", "1")
+    g = ws.detect_gpu()
+    assert g["classify_batch_rows"] == 333 and g["dp_world_size"] == 1
+    monkeypatch.setenv("GPU_DISABLED", "yes")
+    assert ws.detect_gpu() == {"gpu_present": False, "gpu_count": 0, "vram_gb": None, "devices": [],
+                               "max_gpu_workers": 0}
+
+
+def test_batch_rows_from_small_hbm(monkeypatch):
+    monkeypatch.delenv("CLASSIFY_BATCH_ROWS", raising=False)
+    assert ws.classify_batch_rows(288 * GIB) == 1024
+    small = ws.classify_batch_rows(10 * GIB)
+    assert 64 <= small < 1024
+    assert ws.classify_batch_rows(1 * GIB) == 64
+
+
+def test_cpu_formulas_match_reference_probe(monkeypatch):
+    fake = types.SimpleNamespace(cpu_count=lambda logical=True: 8,
+                                 virtual_memory=lambda: types.SimpleNamespace(available=64 * GIB))
+    monkeypatch.setattr(ws, "psutil", fake)
+    for v in ("CPU_RESERVED_CORES_FLOOR", "CPU_RESERVED_CORES_CAP", "CPU_PIPELINE_FACTOR", "CPU_MIN_WORKERS",
+              "CPU_SOFT_CAP_MULTIPLIER", "CPU_PER_WORKER_BYTES"):
+        monkeypatch.delenv(v, raising=False)
+    c = ws.detect_cpu()
+    # [probe] in SURVEY.md §2.1 #30: 8 cores -> reserved 2, usable 6, target 24, cap 48
+    assert (c["total_cores"], c["reserved_cores"], c["usable_cores"]) == (8, 2, 6)
+    assert c["target_inflight_workers"] == 24 and c["cpu_soft_cap_workers"] == 48 == c["max_cpu_workers"]
+    monkeypatch.setenv("CPU_PER_WORKER_BYTES", str(8 * GIB))
+    assert ws.detect_cpu()["cpu_soft_cap_workers"] == 8  # RAM cap
+    monkeypatch.setenv("CPU_PIPELINE_FACTOR", "not-a-number")
+    assert ws.detect_cpu()["pipeline_factor"] == 4.0  # parse errors fall back to defaults
+
+
+def test_profile_schema_and_only_modes(kfd, monkeypatch):
+    p = ws.build_worker_profile()
+    assert set(p) == {"cpu", "gpu", "tpu", "workers"}
+    assert p["tpu"] == {"tpu_present": False, "tpu_kind": None, "devices": [], "max_tpu_workers": 0}
+    assert p["workers"]["max_total_workers"] == p["cpu"]["cpu_soft_cap_workers"] + 2
+    monkeypatch.setenv("GPU_ONLY", "1")
+    p = ws.build_worker_profile()
+    assert p["cpu"]["max_cpu_workers"] == 1 and p["workers"]["max_total_workers"] == 3
+    monkeypatch.setenv("TPU_NAME", "x")
+    assert ws.detect_tpu()["tpu_kind"] == "hinted" and ws.detect_tpu()["tpu_present"] is False
+    monkeypatch.setenv("TPU_DISABLED", "on")
+    assert ws.detect_tpu()["tpu_kind"] is None
+
+
+@pytest.mark.parametrize("raw,val", [("1", True), ("TRUE", True), ("y", True), ("on", True), ("0", False),
+                                     ("no", False), ("off", False), ("maybe", None), (None, None)])
+def test_env_bool(monkeypatch, raw, val):
+    if raw is None:
+        monkeypatch.delenv("X_BOOL", raising=False)
+    else:
+        monkeypatch.setenv("X_BOOL", raw)
+    assert ws.env_bool("X_BOOL", None) is val

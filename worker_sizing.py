@@ -171,8 +171,8 @@ def _visible_filter(devs: List[Dict[str, Any]]) -> Optional[List[Dict[str, Any]]
         if raw is None:
             continue
         raw = raw.strip().lower()
-        if raw in ("none", "-1", "void") or raw == "":
-            return [] if raw != "" else None
+        if raw in ("none", "-1", "void", ""):
+            return []  # set-but-empty hides every device, as in HIP/CUDA
         try:
             keep = [int(x) for x in raw.split(",") if x.strip()]
         except ValueError:
