@@ -74,6 +74,8 @@ PYBIND11_MODULE(_atpu, m) {
       py::arg("ldc"), py::arg("bias"), py::arg("R"), py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"),
       py::arg("epi"), py::arg("stream"), py::arg("splits") = 1, py::arg("ws") = 0);
   m.def("gemm_splitk_splits", &gemm_splitk_splits, "split-K factor chosen for an [M,N,K] GEMM");
+  m.def("gemm_256_variant", &gemm_256_variant, py::arg("set") = -1,
+        "256x256 GEMM schedule: 1 = ping-pong (default), 0 = full-line 2-stage; set >= 0 switches");
   m.attr("EPI_BIAS") = static_cast<int>(kEpiBias);
   m.attr("EPI_GELU") = static_cast<int>(kEpiGelu);
   m.attr("EPI_TANH") = static_cast<int>(kEpiTanh);

@@ -40,6 +40,8 @@ struct GemmArgs {
 void gemm_bf16(const GemmArgs& g, hipStream_t stream);
 // split count the library picks for an [M,N,K] problem (1 = no split-K)
 int gemm_splitk_splits(int M, int N, int K);
+// 256x256 schedule selector (benchmarks): set >= 0 switches; returns the current
+int gemm_256_variant(int set);
 
 // ------------------------------------------------------------ decode (K9-K11)
 // One query row per (row, head) against a KV cache. Cross attention (lens set):

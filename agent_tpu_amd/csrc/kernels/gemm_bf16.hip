@@ -379,6 +379,236 @@ __global__ __launch_bounds__(512, 2) void gemm256b_kernel(
 }
 
 
+// ============================================================================
+// 256x256 tile, 8 waves, PING-PONG schedule (kernel "256p").
+//
+// Two wave groups (wave row wm = 0 / 1; every SIMD hosts one wave of each) run
+// staggered by one barrier: between two consecutive s_barriers one group
+// issues its 16 MFMAs while the other issues its LDS fragment reads and LDS-DMA
+// staging, so the SIMD's matrix core never waits for the issue of memory ops
+// (the cost the 256b ablation exposed). Each K-tile is 4 phases (quadrants of
+// the wave's 128x64 output):
+//   p0: read A-top, B-left  -> MFMA (top, left)      stage quarter 0 of t+1
+//   p1: read B-right        -> MFMA (top, right)     stage quarter 1 of t+1
+//   p2: read A-bottom       -> MFMA (bottom, right)  stage quarter 2 of t+1
+//   p3: (registers only)    -> MFMA (bottom, left)   stage quarter 3 of t+1
+// Quarters are ROW sets of the 128-B-row images in the order they are first
+// read: Q0 = A-top rows {0-63,128-191}, Q1 = B-left rows {32-row blocks 0,2,4,6},
+// Q2 = B-right rows {blocks 1,3,5,7}, Q3 = A-bottom rows {64-127,192-255}.
+// Phase program: R (ds_read) ; G (2 DMA/wave) ; vmcnt(4) ; s_barrier ;
+// lgkmcnt(0) ; setprio(1) MFMA x16 setprio(0) ; s_barrier.
+// Hazards (checked for both stagger orders): with vmcnt(4) before the first
+// barrier a quarter issued at phase r is visible to every reader at phase
+// >= r+3 (each is issued >= 3 phases before its first read), and a restage at
+// phase r is safe after reads at phase <= r-2 (every restage is >= 2 phases
+// after the quarter's last read in the previous K-tile).
+// ============================================================================
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm256p_kernel(
+    const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C, int ldc,
+    const float* __restrict__ bias, const bf16* __restrict__ R, int ldr, int M, int N, int K) {
+  using namespace g2;
+  constexpr int kImg = 256 * 128;  // one operand image (256 rows x 128 B)
+  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kImg];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntn = N / 256, ntm = (M + 255) / 256;
+  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
+  const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 256;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // ---- staging: quarter q, instruction i of this wave covers quarter-local
+  // rows ql = (i*8 + wave)*8 + (lane>>3), 16-B chunk (lane&7) of each row ----
+  const int spos = lane & 7;
+  const bf16* src[4][2];
+  int dst[4][2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ql0 = (i * 8 + wave) * 8;  // first quarter-local row of this instruction
+      const int ql = ql0 + (lane >> 3);
+      int r, r0;  // image row of this lane / of the instruction's first row
+      if (q == 0 || q == 3) {
+        const int off = q == 3 ? 64 : 0;
+        r = (ql & 63) + (ql >> 6) * 128 + off;
+        r0 = (ql0 & 63) + (ql0 >> 6) * 128 + off;
+      } else {
+        const int off = q == 2 ? 32 : 0;
+        r = (ql & 31) + (ql >> 5) * 64 + off;
+        r0 = (ql0 & 31) + (ql0 >> 5) * 64 + off;
+      }
+      const bool is_a = (q == 0 || q == 3);
+      src[q][i] = is_a ? A + (size_t)min(m0 + r, M - 1) * lda + sw(r, spos) * 8
+                       : Bt + (size_t)(n0 + r) * ldb + sw(r, spos) * 8;
+      dst[q][i] = (is_a ? 0 : kImg) + r0 * 128;
+    }
+  auto stage = [&](int q, int kt) {
+    char* base = lds + (kt & 1) * 2 * kImg;
+    const int koff = kt * 64;
+    glds16(src[q][0] + koff, base + dst[q][0]);
+    glds16(src[q][1] + koff, base + dst[q][1]);
+  };
+
+  const int fr = lane & 15, fc = lane >> 4;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[2][4], bl[2][2], br[2][2];  // [kstep][frag]
+  auto read_a = [&](int buf, int qm) {
+    const char* img = lds + buf * 2 * kImg;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wm * 128 + qm * 64 + i * 16 + fr;
+        af[ks][i] = *reinterpret_cast<const bf16x8*>(img + r * 128 + sw(r, ks * 4 + fc) * 16);
+      }
+  };
+  auto read_b = [&](bf16x8 (&f)[2][2], int buf, int qn) {
+    const char* img = lds + buf * 2 * kImg + kImg;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wn * 64 + qn * 32 + j * 16 + fr;
+        f[ks][j] = *reinterpret_cast<const bf16x8*>(img + r * 128 + sw(r, ks * 4 + fc) * 16);
+      }
+  };
+  auto mma = [&](const bf16x8 (&bf)[2][2], int qm, int qn) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[qm * 4 + i][qn * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ks][j], af[ks][i], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+  };
+
+  const int nk = K / 64;
+  // prologue: K-tile 0 fully staged and visible
+#pragma unroll
+  for (int q = 0; q < 4; ++q) stage(q, 0);
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger: group 1 runs one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+#define ATPU_PP_SYNC_MMA(BF, QM, QN)                         \
+  __builtin_amdgcn_sched_barrier(0);                        \
+  __builtin_amdgcn_s_barrier();                             \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        \
+  __builtin_amdgcn_sched_barrier(0);                        \
+  __builtin_amdgcn_s_setprio(1);                            \
+  mma(BF, QM, QN);                                          \
+  __builtin_amdgcn_s_setprio(0);                            \
+  __builtin_amdgcn_sched_barrier(0);                        \
+  __builtin_amdgcn_s_barrier();                             \
+  __builtin_amdgcn_sched_barrier(0)
+
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    const bool more = t + 1 < nk;
+    // p0
+    read_a(buf, 0);
+    read_b(bl, buf, 0);
+    if (more) {
+      stage(0, t + 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    }
+    ATPU_PP_SYNC_MMA(bl, 0, 0);
+    // p1
+    read_b(br, buf, 1);
+    if (more) {
+      stage(1, t + 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    ATPU_PP_SYNC_MMA(br, 0, 1);
+    // p2
+    read_a(buf, 1);
+    if (more) {
+      stage(2, t + 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    ATPU_PP_SYNC_MMA(br, 1, 1);
+    // p3
+    if (more) {
+      stage(3, t + 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    ATPU_PP_SYNC_MMA(bl, 1, 0);
+  }
+#undef ATPU_PP_SYNC_MMA
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // close the stagger (equal barrier counts)
+
+  f32x4 bv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wn * 64 + j * 16 + fc * 4;
+    if constexpr (EPI & kEpiBias) bv[j] = *reinterpret_cast<const f32x4*>(bias + n);
+    else bv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + fr;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + fc * 4;
+      f32x4 v = acc[i][j] + bv[j];
+      if constexpr (EPI & kEpiGelu) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = gelu_fast(v[e]);
+      }
+      if constexpr (EPI & kEpiTanh) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
+      }
+      if constexpr (EPI & kEpiRelu) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if constexpr (EPI & kEpiResidual) {
+        const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += bf2f(r[e]);
+      }
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+      *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
+    }
+  }
+}
+
+void launch_256p(const GemmArgs& g, hipStream_t s) {
+  const int nb = ((g.M + 255) / 256) * (g.N / 256);
+#define ATPU_G256P(E)                                                                                     \
+  case E:                                                                                                 \
+    hipLaunchKernelGGL((gemm256p_kernel<E>), dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, \
+                       g.bias, g.R, g.ldr, g.M, g.N, g.K);                                                \
+    break;
+  switch (g.epi) {
+    ATPU_G256P(0)
+    ATPU_G256P(kEpiBias)
+    ATPU_G256P(kEpiBias | kEpiGelu)
+    ATPU_G256P(kEpiBias | kEpiTanh)
+    ATPU_G256P(kEpiBias | kEpiResidual)
+    ATPU_G256P(kEpiResidual)
+    ATPU_G256P(kEpiGelu)
+    ATPU_G256P(kEpiRelu)
+    default:
+      throw std::invalid_argument("atpu: unsupported GEMM epilogue " + std::to_string(g.epi));
+  }
+#undef ATPU_G256P
+}
+
 void launch_256b(const GemmArgs& g, hipStream_t s) {
   const int nb = ((g.M + 255) / 256) * (g.N / 256);
   static const int ablate = [] {
@@ -518,6 +748,16 @@ void launch_tile(const GemmArgs& g, hipStream_t s) {
 
 }  // namespace
 
+int gemm_256_variant(int set) {
+  // 256x256 schedule: 1 = ping-pong "256p" (default), 0 = "256b"; ATPU_GEMM_256=b|p
+  static int v = [] {
+    const char* f = std::getenv("ATPU_GEMM_256");
+    return (f && f[0] == 'b') ? 0 : 1;
+  }();
+  if (set >= 0) v = set;
+  return v;
+}
+
 int gemm_splitk_splits(int M, int N, int K) {
   // Skinny problems (decode: M = beams x docs) leave most of the 256 CUs idle
   // with 128x128 tiles; split K so the grid reaches ~2 blocks per CU, keeping
@@ -559,9 +799,12 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
     ATPU_HIP_CHECK(hipGetLastError());
     return;
   }
+  const int kernel256 = gemm_256_variant(-1);
   const bool big_ok = g.N % 256 == 0;
   const bool use_big = !(g.epi & kEpiOutF32) && (forced ? (forced == 256 && big_ok) : (g.M >= 2048 && big_ok));
-  if (use_big)
+  if (use_big && kernel256 == 1)
+    launch_256p(g, stream);
+  else if (use_big)
     launch_256b(g, stream);
   else
     launch_tile<128, 128, 2, 2>(g, stream);
