@@ -1,0 +1,246 @@
+"""BART encoder-decoder on the gfx950 kernels (map_summarize, family ``bart``).
+
+The reference summarizer is HF ``facebook/bart-large-cnn`` run through
+``BartForConditionalGeneration.generate`` on the CPU
+(``/root/reference/ops/map_summarize.py:9,46-59``). Same graph here, on the
+kernels the BERT path already uses (BART's post-LN layer has BERT's shape):
+
+  encoder : embed + learned positions (offset 2) + LayerNorm (K2)
+            -> L x [fused QKV GEMM + bias, attention (K4, 1/sqrt(64)),
+                    O-proj + bias + residual (GEMM epilogue), LayerNorm,
+                    FC1 + bias + GELU (epilogue), FC2 + bias + residual, LN]
+            -> ONE GEMM producing every decoder layer's cross K|V (+ bias).
+  decoder : per generated token: embed + position row of the device step + LN,
+            L x [QKV GEMM, KV-cache append, single-query self attention over
+                 the beam-backpointer history (K9), O-proj + residual, LN,
+                 cross Q GEMM, grouped cross attention over the item's encoder
+                 K/V, O-proj + residual, LN, FC1 GELU, FC2 + residual, LN]
+            -> tied LM head + final_logits_bias with fp32 logits (K10 input).
+
+Parameter layout follows HF ``BartForConditionalGeneration`` (Linear weights
+``[out, in]``), so :func:`from_hf_state_dict` is a rename + concat.
+"""
+from __future__ import annotations
+
+import dataclasses
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+
+from .. import ops
+from .params import ParamPack
+
+POS_OFFSET = 2  # BartLearnedPositionalEmbedding offset
+
+
+@dataclass(frozen=True)
+class BartConfig:
+    vocab_size: int = 50264
+    d_model: int = 1024
+    heads: int = 16
+    d_ff: int = 4096
+    enc_layers: int = 12
+    dec_layers: int = 12
+    max_positions: int = 1024
+    eps: float = 1e-5
+    pad_id: int = 1
+    bos_id: int = 0
+    eos_id: int = 2
+    decoder_start_id: int = 2
+    # generation defaults of facebook/bart-large-cnn's generation_config (the
+    # reference's generate() call overrides only beams/max/min/early_stopping)
+    forced_bos_id: Optional[int] = 0
+    forced_eos_id: Optional[int] = 2
+    no_repeat_ngram_size: int = 3
+    length_penalty: float = 2.0
+
+    def param_count(self) -> int:
+        d, f = self.d_model, self.d_ff
+        enc = self.enc_layers * (4 * d * d + 2 * d * f + 9 * d + f)
+        dec = self.dec_layers * (8 * d * d + 2 * d * f + 15 * d + f)
+        return self.vocab_size * (d + 1) + 2 * (self.max_positions + POS_OFFSET) * d + 4 * d + enc + dec
+
+
+PRESETS: Dict[str, BartConfig] = {
+    "bart-large-cnn": BartConfig(),
+    "bart-large": BartConfig(no_repeat_ngram_size=0, length_penalty=1.0, forced_bos_id=None),
+    "bart-base": BartConfig(d_model=768, heads=12, d_ff=3072, enc_layers=6, dec_layers=6),
+    "bart-tiny": BartConfig(vocab_size=4096, d_model=256, heads=4, d_ff=512, enc_layers=2, dec_layers=2,
+                            max_positions=256),
+}
+
+
+def config_for(name: str, **overrides) -> BartConfig:
+    key = name.split("/")[-1]  # accept "facebook/bart-large-cnn"
+    if key not in PRESETS:
+        raise ValueError(f"unknown BART preset {name!r}; known: {sorted(PRESETS)}")
+    return dataclasses.replace(PRESETS[key], **overrides)
+
+
+def param_specs(cfg: BartConfig):
+    d, f, bf, f32 = cfg.d_model, cfg.d_ff, torch.bfloat16, torch.float32
+    P = cfg.max_positions + POS_OFFSET
+    yield "shared", (cfg.vocab_size, d), bf
+    yield "final_logits_bias", (cfg.vocab_size,), f32
+    for side, L in (("enc", cfg.enc_layers), ("dec", cfg.dec_layers)):
+        yield f"{side}.pos", (P, d), bf
+        yield f"{side}.ln_emb_g", (d,), f32
+        yield f"{side}.ln_emb_b", (d,), f32
+        for i in range(L):
+            p = f"{side}.l{i}."
+            yield p + "qkv_w", (3 * d, d), bf
+            yield p + "qkv_b", (3 * d,), f32
+            yield p + "o_w", (d, d), bf
+            yield p + "o_b", (d,), f32
+            yield p + "ln1_g", (d,), f32
+            yield p + "ln1_b", (d,), f32
+            if side == "dec":
+                yield p + "cq_w", (d, d), bf
+                yield p + "cq_b", (d,), f32
+                yield p + "co_w", (d, d), bf
+                yield p + "co_b", (d,), f32
+                yield p + "lnc_g", (d,), f32
+                yield p + "lnc_b", (d,), f32
+            yield p + "f1_w", (f, d), bf
+            yield p + "f1_b", (f,), f32
+            yield p + "f2_w", (d, f), bf
+            yield p + "f2_b", (d,), f32
+            yield p + "ln2_g", (d,), f32
+            yield p + "ln2_b", (d,), f32
+    yield "dec.ckv_w", (cfg.dec_layers * 2 * d, d), bf  # every layer's cross K|V, one GEMM
+    yield "dec.ckv_b", (cfg.dec_layers * 2 * d,), f32
+
+
+def init_random(cfg: BartConfig, seed: int = 0, std: float = 0.02) -> ParamPack:
+    """Seeded random init (HF BART scheme: N(0, init_std) weights, zero biases, LN = 1/0)."""
+    pack = ParamPack(param_specs(cfg))
+    g = torch.Generator().manual_seed(int(seed))
+    for name in pack.names():
+        t = pack[name]
+        base = name.split(".")[-1]
+        if base.endswith("_g"):
+            t.fill_(1.0)
+        elif base.endswith("_b") or name == "final_logits_bias":
+            t.zero_()
+        else:
+            t.copy_((torch.randn(t.shape, generator=g) * std).to(t.dtype))
+    return pack
+
+
+def from_hf_state_dict(cfg: BartConfig, sd: Dict[str, torch.Tensor]) -> ParamPack:
+    pack = ParamPack(param_specs(cfg))
+
+    def put(name, t):
+        pack[name].copy_(t.to(pack[name].dtype).view(pack[name].shape))
+
+    put("shared", sd["model.shared.weight"])
+    put("final_logits_bias", sd["final_logits_bias"].reshape(-1))
+    ckv_w, ckv_b = [], []
+    for side, hf, L in (("enc", "model.encoder", cfg.enc_layers), ("dec", "model.decoder", cfg.dec_layers)):
+        put(f"{side}.pos", sd[f"{hf}.embed_positions.weight"])
+        put(f"{side}.ln_emb_g", sd[f"{hf}.layernorm_embedding.weight"])
+        put(f"{side}.ln_emb_b", sd[f"{hf}.layernorm_embedding.bias"])
+        for i in range(L):
+            b, p = f"{hf}.layers.{i}.", f"{side}.l{i}."
+            a = b + "self_attn."
+            put(p + "qkv_w", torch.cat([sd[a + f"{n}_proj.weight"] for n in "qkv"], 0))
+            put(p + "qkv_b", torch.cat([sd[a + f"{n}_proj.bias"] for n in "qkv"], 0))
+            put(p + "o_w", sd[a + "out_proj.weight"])
+            put(p + "o_b", sd[a + "out_proj.bias"])
+            put(p + "ln1_g", sd[b + "self_attn_layer_norm.weight"])
+            put(p + "ln1_b", sd[b + "self_attn_layer_norm.bias"])
+            if side == "dec":
+                c = b + "encoder_attn."
+                put(p + "cq_w", sd[c + "q_proj.weight"])
+                put(p + "cq_b", sd[c + "q_proj.bias"])
+                put(p + "co_w", sd[c + "out_proj.weight"])
+                put(p + "co_b", sd[c + "out_proj.bias"])
+                put(p + "lnc_g", sd[b + "encoder_attn_layer_norm.weight"])
+                put(p + "lnc_b", sd[b + "encoder_attn_layer_norm.bias"])
+                ckv_w += [sd[c + "k_proj.weight"], sd[c + "v_proj.weight"]]
+                ckv_b += [sd[c + "k_proj.bias"], sd[c + "v_proj.bias"]]
+            put(p + "f1_w", sd[b + "fc1.weight"])
+            put(p + "f1_b", sd[b + "fc1.bias"])
+            put(p + "f2_w", sd[b + "fc2.weight"])
+            put(p + "f2_b", sd[b + "fc2.bias"])
+            put(p + "ln2_g", sd[b + "final_layer_norm.weight"])
+            put(p + "ln2_b", sd[b + "final_layer_norm.bias"])
+    put("dec.ckv_w", torch.cat(ckv_w, 0))
+    put("dec.ckv_b", torch.cat(ckv_b, 0))
+    return pack
+
+
+class BartModel:
+    """Device-agnostic BART with the T5Model interface (encode / new_cache / step).
+
+    On a ROCm device every op is a HIP kernel; on CPU with ``fp32=True`` each
+    op's PyTorch reference runs (the oracle of the GPU tests and of the HF
+    parity test).
+    """
+
+    family = "bart"
+
+    def __init__(self, cfg: BartConfig, pack: ParamPack, fp32: bool = False):
+        self.cfg, self.pack = cfg, pack
+        self.p = pack.with_dtype(torch.float32) if fp32 else {n: pack[n] for n in pack.names()}
+        self.device = pack.buffer.device
+        dt = self.p["shared"].dtype
+        self._type0 = torch.zeros((2, cfg.d_model), dtype=dt, device=self.device)
+        self._pos_off = torch.tensor([POS_OFFSET], dtype=torch.int64, device=self.device)
+
+    def wrap_source(self, toks):
+        return [self.cfg.bos_id] + list(toks) + [self.cfg.eos_id]
+
+    # ------------------------------------------------------------- encoder
+    def encode(self, ids: torch.Tensor, lens: torch.Tensor):
+        """ids [B, S] int32, lens [B] -> (enc [B*S, d], cross K|V [B*S, L*2d])."""
+        cfg, p = self.cfg, self.p
+        B, S = ids.shape
+        H = cfg.heads
+        h = ops.embed_layernorm(ids, p["shared"], p["enc.pos"][POS_OFFSET:], self._type0, p["enc.ln_emb_g"],
+                                p["enc.ln_emb_b"], cfg.eps)
+        for i in range(cfg.enc_layers):
+            q = f"enc.l{i}."
+            qkv = ops.linear(h, p[q + "qkv_w"], p[q + "qkv_b"])
+            ctx = ops.attention_packed(qkv, lens, B, S, H)
+            h1 = ops.linear(ctx, p[q + "o_w"], p[q + "o_b"], residual=h)
+            h1 = ops.layernorm(h1, p[q + "ln1_g"], p[q + "ln1_b"], cfg.eps)
+            f = ops.linear(h1, p[q + "f1_w"], p[q + "f1_b"], act="gelu")
+            h2 = ops.linear(f, p[q + "f2_w"], p[q + "f2_b"], residual=h1)
+            h = ops.layernorm(h2, p[q + "ln2_g"], p[q + "ln2_b"], cfg.eps)
+        return h, ops.linear(h, p["dec.ckv_w"], p["dec.ckv_b"])
+
+    # ------------------------------------------------------------- decoder
+    def new_cache(self, rows: int, T: int) -> torch.Tensor:
+        """Self-attention K|V cache [L, rows*T, 2d]."""
+        dt = self.p["dec.l0.qkv_w"].dtype
+        return torch.zeros((self.cfg.dec_layers, rows * T, 2 * self.cfg.d_model), dtype=dt, device=self.device)
+
+    def step(self, tokens: torch.Tensor, step: torch.Tensor, cache: torch.Tensor, T: int, ckv: torch.Tensor,
+             src_lens: torch.Tensor, S: int, group: int, hist: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One decoder position for ``rows`` sequences -> fp32 logits [rows, V] (see T5Model.step)."""
+        cfg, p = self.cfg, self.p
+        d, H = cfg.d_model, cfg.heads
+        scale = (d // H) ** -0.5
+        x = ops.embed_gather(tokens, p["shared"])
+        pos = p["dec.pos"].index_select(0, step.reshape(1).long() + self._pos_off)
+        x = ops.layernorm(x, p["dec.ln_emb_g"], p["dec.ln_emb_b"], cfg.eps,
+                          residual=pos.expand(x.shape[0], d).contiguous())
+        for i in range(cfg.dec_layers):
+            q = f"dec.l{i}."
+            c = cache[i]
+            qkv = ops.linear(x, p[q + "qkv_w"], p[q + "qkv_b"])
+            ops.kv_append(qkv, d, 2 * d, c, T, step)
+            ctx = ops.decode_attention(qkv[:, :d], c[:, :d], c[:, d:], H, T, 1, step=step, scale=scale, hist=hist)
+            x = ops.layernorm(ops.linear(ctx, p[q + "o_w"], p[q + "o_b"], residual=x), p[q + "ln1_g"],
+                              p[q + "ln1_b"], cfg.eps)
+            cq = ops.linear(x, p[q + "cq_w"], p[q + "cq_b"])
+            kv = ckv[:, i * 2 * d:(i + 1) * 2 * d]
+            ctx = ops.decode_attention(cq, kv[:, :d], kv[:, d:], H, S, group, lens=src_lens, scale=scale)
+            x = ops.layernorm(ops.linear(ctx, p[q + "co_w"], p[q + "co_b"], residual=x), p[q + "lnc_g"],
+                              p[q + "lnc_b"], cfg.eps)
+            f = ops.linear(x, p[q + "f1_w"], p[q + "f1_b"], act="gelu")
+            x = ops.layernorm(ops.linear(f, p[q + "f2_w"], p[q + "f2_b"], residual=x), p[q + "ln2_g"],
+                              p[q + "ln2_b"], cfg.eps)
+        return ops.linear(x, p["shared"], p["final_logits_bias"], out_f32=True)

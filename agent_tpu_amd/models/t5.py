@@ -189,12 +189,17 @@ class T5Model:
     """Device-agnostic T5: ``pack`` on a ROCm device runs the HIP kernels; on CPU
     (with ``fp32=True``) every op's PyTorch reference, used as the oracle."""
 
+    family = "t5"
+
     def __init__(self, cfg: T5Config, pack: ParamPack, fp32: bool = False):
         self.cfg, self.pack = cfg, pack
         self.p = pack.with_dtype(torch.float32) if fp32 else {n: pack[n] for n in pack.names()}
         self.device = pack.buffer.device
         self._enc_bias: Dict[int, torch.Tensor] = {}
         self._dec_bias: Optional[torch.Tensor] = None
+
+    def wrap_source(self, toks):
+        return list(toks) + [self.cfg.eos_id]
 
     # ------------------------------------------------------------- biases
     def enc_bias(self, S: int) -> torch.Tensor:

@@ -14,7 +14,12 @@ min_length=30, early_stopping=True)`` (``/root/reference/ops/map_summarize.py:53
 * ``early_stopping=True`` freezes an item once ``num_beams`` hypotheses have
   finished; the loop ends when no item can improve;
 * EOS is masked (after log-softmax) while the sequence is shorter than
-  ``min_length``.
+  ``min_length``;
+* BART's generation defaults (facebook/bart-large-cnn generation_config, which
+  the reference's generate() call inherits): ``no_repeat_ngram_size`` bans (a
+  token that would repeat an n-gram of the hypothesis), ``forced_bos`` at
+  length 1 and ``forced_eos`` at ``max_length - 1`` (the only allowed token
+  gets log-prob 0), ``length_penalty`` 2.0.
 
 Device work per step: the decoder step (L layers of GEMMs, KV-cache appends,
 single-query attention), the LM-head GEMM and K10. Host work: bookkeeping on
@@ -32,7 +37,6 @@ import numpy as np
 import torch
 
 from .. import ops
-from ..models.t5 import T5Config, T5Model
 from ..tokenizer import pack_rows
 
 NEG = -1.0e9
@@ -43,9 +47,41 @@ class GenConfig:
     num_beams: int = 4
     max_length: int = 130
     min_length: int = 30
-    length_penalty: float = 1.0
+    length_penalty: Optional[float] = None  # None -> model default (T5 1.0, bart-large-cnn 2.0)
     early_stopping: bool = True
+    no_repeat_ngram_size: Optional[int] = None  # None -> model default (bart-large-cnn 3)
+    forced_bos_id: Optional[int] = None  # None -> model default (bart-large-cnn 0)
+    forced_eos_id: Optional[int] = None  # None -> model default (bart-large-cnn 2)
     use_graph: bool = True  # replay the decoder step as one hipGraph (device runs only)
+
+    def resolved(self, cfg) -> "GenConfig":
+        def pick(v, name, default):
+            return v if v is not None else getattr(cfg, name, default)
+
+        return GenConfig(self.num_beams, self.max_length, self.min_length,
+                         float(pick(self.length_penalty, "length_penalty", 1.0)), self.early_stopping,
+                         int(pick(self.no_repeat_ngram_size, "no_repeat_ngram_size", 0) or 0),
+                         pick(self.forced_bos_id, "forced_bos_id", None),
+                         pick(self.forced_eos_id, "forced_eos_id", None), self.use_graph)
+
+
+def ngram_bans(seq: torch.Tensor, n: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """HF NoRepeatNGramLogitsProcessor for every row of ``seq`` [R, cur] at once.
+
+    Returns ``(rows, tokens)``: token t is banned for row r when the row's last
+    n-1 tokens followed by t already occur in the row.
+    """
+    R, cur = seq.shape
+    if n <= 0 or cur + 1 < n or cur < n:
+        return torch.empty(0, dtype=torch.long), torch.empty(0, dtype=torch.long)
+    if n == 1:
+        rows = torch.arange(R).repeat_interleave(cur)
+        return rows, seq.reshape(-1)
+    ng = seq.unfold(1, n, 1)  # [R, cur-n+1, n]
+    prefix = seq[:, cur - n + 1:]  # [R, n-1]
+    match = (ng[:, :, :n - 1] == prefix.unsqueeze(1)).all(-1)
+    r, c = match.nonzero(as_tuple=True)
+    return r, ng[r, c, n - 1]
 
 
 @dataclass
@@ -56,9 +92,55 @@ class GenResult:
     timing_ms: Dict[str, float] = field(default_factory=dict)
 
 
-def generate(model: T5Model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfig) -> GenResult:
+def _select(logits: torch.Tensor, run_scores: torch.Tensor, K2: int, cfg, gen: GenConfig, cur: int, T: int,
+            run_seq: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per beam row: the top ``K2`` continuations ``(score [rows, K2], token [rows, K2])``
+    after log-softmax and the logits processors (min-length EOS mask, n-gram bans,
+    forced BOS/EOS), on the host."""
+    rows, V = logits.shape
+    forced = None
+    if gen.forced_bos_id is not None and cur == 1:
+        forced = int(gen.forced_bos_id)
+    elif gen.forced_eos_id is not None and cur == T - 1:
+        forced = int(gen.forced_eos_id)
+    if forced is not None:  # the only allowed token gets log-prob 0
+        sc = torch.full((rows, K2), float("-inf"))
+        sc[:, 0] = run_scores.view(-1)
+        tk = torch.arange(K2).view(1, -1).expand(rows, -1).clone()
+        tk[:, 1:] += (tk[:, 1:] >= forced).long()  # placeholders distinct from the forced token
+        tk[:, 0] = forced
+        return sc, tk
+    mask_eos = cur < gen.min_length
+    br, bt = ngram_bans(run_seq.view(rows, -1)[:, :cur], gen.no_repeat_ngram_size)
+    nban = int(torch.bincount(br, minlength=rows).max()) if br.numel() else 0
+    scores_dev = run_scores.view(-1).to(logits.device)
+    if K2 + nban <= 16:
+        sc, tk = ops.beam_topk_rows(logits, scores_dev, K2 + nban, cfg.eos_id, mask_eos)
+        sc, tk = sc.cpu(), tk.cpu().long()
+        if nban:
+            key = br * V + bt
+            flat = torch.arange(rows).view(-1, 1) * V + tk
+            banned = torch.isin(flat, key)
+            sc = sc.masked_fill(banned, float("-inf"))
+            # keep the K2 best per row, ties -> lower token id (stable sort over token order)
+            order = torch.argsort(tk, dim=1)
+            sc, tk = torch.gather(sc, 1, order), torch.gather(tk, 1, order)
+            top = torch.sort(sc, dim=1, descending=True, stable=True).indices[:, :K2]
+            sc, tk = torch.gather(sc, 1, top), torch.gather(tk, 1, top)
+        return sc, tk
+    # many bans in one row: exact torch path for this step
+    lp = torch.log_softmax(logits.float(), dim=-1)
+    if mask_eos:
+        lp[:, cfg.eos_id] = float("-inf")
+    lp[br.to(lp.device), bt.to(lp.device)] = float("-inf")
+    sc, tk = torch.topk(lp + scores_dev.view(-1, 1), K2, dim=-1)
+    return sc.cpu(), tk.cpu().long()
+
+
+def generate(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfig) -> GenResult:
     """Beam search for a batch. ``src_ids`` [B, S] int32 (on the model device)."""
-    cfg: T5Config = model.cfg
+    cfg = model.cfg
+    gen = gen.resolved(cfg)
     dev = model.device
     B, S = src_ids.shape
     nb = max(1, int(gen.num_beams))
@@ -106,8 +188,8 @@ def generate(model: T5Model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen:
                 graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(graph):
                     g_logits = model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist)
-        sc, tk = ops.beam_topk_rows(logits, run_scores.view(-1).to(dev), K2, cfg.eos_id, cur < gen.min_length)
-        sc, tk = sc.cpu().view(B, nb * K2), tk.cpu().view(B, nb * K2).long()
+        sc, tk = _select(logits, run_scores, K2, cfg, gen, cur, T, run_seq)
+        sc, tk = sc.view(B, nb * K2), tk.view(B, nb * K2)
         steps += 1
         # global top-K2 per item; ties -> lower flat index (beam * V + token) like torch.topk over [nb*V]
         beam_of = torch.arange(nb).repeat_interleave(K2).view(1, -1).expand(B, -1)
@@ -168,26 +250,50 @@ def generate(model: T5Model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen:
     return GenResult(seqs, scores, steps, {"encode_ms": (t_enc - t0) * 1e3, "decode_ms": (t_dec - t_enc) * 1e3})
 
 
-class SummarizeEngine:
-    """Texts -> summaries with a device-resident T5 (batched beam search)."""
+def build_model(name: str, pack=None, device: Optional[torch.device] = None, seed: int = 0, fp32: bool = False):
+    """``t5-*`` / ``bart-*`` preset name -> (model, pack); random init when no pack."""
+    from ..models import bart, t5
 
-    def __init__(self, cfg: T5Config, pack, device: torch.device, max_source_len: int = 512):
-        self.cfg = cfg
-        self.model = T5Model(cfg, pack if pack.buffer.device == device else pack.to(device))
-        self.device = device
+    fam = family_of(name)
+    mod = bart if fam == "bart" else t5
+    cfg = mod.config_for(name)
+    pack = pack if pack is not None else mod.init_random(cfg, seed=seed)
+    if device is not None and pack.buffer.device != device:
+        pack = pack.to(device)
+    cls = bart.BartModel if fam == "bart" else t5.T5Model
+    return cls(cfg, pack, fp32=fp32), pack
+
+
+def family_of(name: str) -> str:
+    key = name.split("/")[-1].lower()
+    if key.startswith("bart"):
+        return "bart"
+    if key.startswith("t5"):
+        return "t5"
+    raise ValueError(f"unknown summarization model {name!r} (t5-* or bart-*)")
+
+
+class SummarizeEngine:
+    """Texts -> summaries with a device-resident T5 or BART (batched beam search)."""
+
+    def __init__(self, model, max_source_len: int = 512):
+        self.model = model
+        self.cfg = model.cfg
+        self.device = model.device
         self.max_src = int(max_source_len)
 
     def encode_texts(self, texts: Sequence[str]) -> Tuple[torch.Tensor, torch.Tensor, List[Dict[int, str]]]:
-        """Hash-tokenize (same spec as K1, vocab = T5's), append EOS, pad to S % 8 == 0."""
-        from .. import tokenizer as T
+        """Hash-tokenize (same spec as K1, the model's vocab), wrap with the
+        model's specials (T5: ``toks </s>``; BART: ``<s> toks </s>``), pad to S % 8 == 0."""
         from .._native import native
 
         text, offs = pack_rows(texts)
         ids, lens = native().tokenize_host(text, offs, self.max_src + 1, self.cfg.vocab_size, 1 << 16)
+        n_special = len(self.model.wrap_source([]))
         rows = []
         for r in range(len(texts)):
             toks = [int(x) for x in ids[r, 1:lens[r] - 1]]  # strip [CLS]/[SEP]
-            rows.append(toks[: self.max_src - 1] + [self.cfg.eos_id])
+            rows.append(self.model.wrap_source(toks[: self.max_src - n_special]))
         S = max(8, (max(len(r) for r in rows) + 7) // 8 * 8)
         arr = np.full((len(rows), S), self.cfg.pad_id, dtype=np.int32)
         for r, toks in enumerate(rows):
@@ -206,7 +312,7 @@ class SummarizeEngine:
         return out
 
     def detokenize(self, seq: List[int], vmap: Dict[int, str]) -> str:
-        special = {self.cfg.pad_id, self.cfg.eos_id, self.cfg.decoder_start_id}
+        special = {self.cfg.pad_id, self.cfg.eos_id, self.cfg.decoder_start_id, getattr(self.cfg, "bos_id", -1)}
         return " ".join(vmap.get(t, f"<{t}>") for t in seq if t not in special)
 
     def summarize(self, texts: Sequence[str], gen: GenConfig) -> Tuple[List[str], GenResult]:

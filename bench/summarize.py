@@ -7,8 +7,8 @@ synthetic text hash-tokenized to ``--src-len`` tokens (the reference truncates a
 1024); weights are random-init T5-base. A step = one batch of ``--docs`` documents
 summarised end to end (tokenize -> encoder -> beam-search decode -> detokenize).
 
-Baseline: SURVEY.md §6 B12, T5-base-shaped proxy of the reference on CPU,
-3.72 s/doc = 0.269 docs/s.
+Baselines (reference-shaped proxies on CPU): B12 T5-base
+3.72 s/doc = 0.269 docs/s; B11 BART-large-CNN 6.47 s/doc = 0.155 docs/s.
 """
 from __future__ import annotations
 
@@ -23,7 +23,7 @@ sys.path.insert(0, REPO)
 
 import torch  # noqa: E402
 
-BASELINE_DOCS_PER_SEC = 0.269
+BASELINE_DOCS_PER_SEC = {"t5": 0.269, "bart": 0.155}
 
 
 def main() -> int:
@@ -38,13 +38,12 @@ def main() -> int:
     ap.add_argument("--min-length", type=int, default=30)
     a = ap.parse_args()
 
-    from agent_tpu_amd.models.t5 import config_for, init_random
-    from agent_tpu_amd.runtime.summarize import GenConfig, SummarizeEngine
+    from agent_tpu_amd.runtime.summarize import GenConfig, SummarizeEngine, build_model, family_of
     from agent_tpu_amd.utils.synthetic import make_text_rows
 
     dev = torch.device("cuda", 0)
-    cfg = config_for(a.model)
-    eng = SummarizeEngine(cfg, init_random(cfg, seed=0), dev, max_source_len=a.src_len)
+    model, _ = build_model(a.model, device=dev, seed=0)
+    eng = SummarizeEngine(model, max_source_len=a.src_len)
     gen = GenConfig(num_beams=a.num_beams, max_length=a.max_length, min_length=a.min_length)
     docs = make_text_rows(a.docs * (a.warmup + a.steps), words_per_row=int(a.src_len * 0.8), seed=5)
 
@@ -64,10 +63,10 @@ def main() -> int:
     el = time.perf_counter() - t0
     n = a.docs * a.steps
     print(json.dumps({
-        "metric": "summarized docs/sec map_summarize T5-base (beams 4, max_len 130, min_len 30)",
+        "metric": f"summarized docs/sec map_summarize {a.model} (beams 4, max_len 130, min_len 30)",
         "value": round(n / el, 3), "unit": "docs/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(el * 1000 / a.steps, 2), "higher_is_better": True,
-        "vs_baseline": round(n / el / BASELINE_DOCS_PER_SEC, 1), "dtype": "bf16",
+        "vs_baseline": round(n / el / BASELINE_DOCS_PER_SEC[family_of(a.model)], 1), "dtype": "bf16",
         "data": "synthetic text, random-init weights",
         "config": {"model": a.model, "docs_per_step": a.docs, "src_len": a.src_len, "num_beams": a.num_beams,
                    "max_length": a.max_length, "min_length": a.min_length,

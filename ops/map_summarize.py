@@ -1,12 +1,15 @@
-"""``map_summarize`` — abstractive summarisation on the T5 encoder-decoder HIP path.
+"""``map_summarize`` — abstractive summarisation on the encoder-decoder HIP path.
 
 Reference: ``/root/reference/ops/map_summarize.py`` (HF BART-large-CNN on CPU,
 one document per call, ``generate(num_beams=4, max_length=130, min_length=30,
-early_stopping=True)``). Here (BASELINE config 4): T5 with random-init weights
-on the hand-written kernels (agent_tpu_amd/models/t5.py), batched beam search
-with HF's semantics (agent_tpu_amd/runtime/summarize.py), documents tokenised
-with the same hash tokenizer as map_classify (no SentencePiece model is
-available offline; see map_summarize.CONTRACT.md).
+early_stopping=True)``). Here: T5 (BASELINE config 4, default) or BART
+(``SUMMARIZE_MODEL_FAMILY=bart``, model from the reference's ``BART_MODEL``
+env, default facebook/bart-large-cnn with its generation defaults) with
+random-init weights on the hand-written kernels (agent_tpu_amd/models/t5.py,
+bart.py), batched beam search with HF's semantics
+(agent_tpu_amd/runtime/summarize.py), documents tokenised with the same hash
+tokenizer as map_classify (no SentencePiece/BPE model is available offline;
+see map_summarize.CONTRACT.md).
 
 Output keys are the reference's ``{ok, summary, device, model}``; ``texts``
 (a list) returns ``summaries``. Fix: the payload is
@@ -23,7 +26,22 @@ from typing import Any, Dict, List, Optional
 
 from . import register_op
 
-MODEL_NAME = os.getenv("SUMMARIZE_MODEL", "t5-base")
+
+
+def _resolve_model() -> str:
+    fam = os.getenv("SUMMARIZE_MODEL_FAMILY", "").strip().lower()
+    name = os.getenv("SUMMARIZE_MODEL", "").strip()
+    if not fam:
+        fam = "bart" if name.split("/")[-1].lower().startswith("bart") else "t5"
+    if fam == "bart":
+        return name if name.split("/")[-1].lower().startswith("bart") else os.getenv("BART_MODEL",
+                                                                                      "facebook/bart-large-cnn")
+    if fam != "t5":
+        raise ValueError(f"SUMMARIZE_MODEL_FAMILY must be t5 or bart, got {fam!r}")
+    return name if name.split("/")[-1].lower().startswith("t5") else "t5-base"
+
+
+MODEL_NAME = _resolve_model()
 FORCE_CPU = os.getenv("SUMMARIZE_FORCE_CPU", "0").strip().lower() in ("1", "true", "yes")
 MAX_SOURCE_TOKENS = int(os.getenv("SUMMARIZE_MAX_SOURCE_TOKENS", "512"))
 
@@ -41,20 +59,15 @@ def _init_engine():
             return _engine
         import torch
 
-        from agent_tpu_amd.models.t5 import config_for, init_random
-        from agent_tpu_amd.runtime.summarize import SummarizeEngine
+        from agent_tpu_amd.runtime.summarize import SummarizeEngine, build_model
 
-        cfg = config_for(MODEL_NAME)
-        pack = init_random(cfg, seed=int(os.getenv("MODEL_SEED", "0")))
         if not FORCE_CPU and torch.cuda.is_available():
             dev = torch.device("cuda", int(os.getenv("LOCAL_RANK", "0")))
         else:
             dev = torch.device("cpu")
-        eng = SummarizeEngine(cfg, pack, dev, MAX_SOURCE_TOKENS)
-        if dev.type == "cpu":
-            from agent_tpu_amd.models.t5 import T5Model
-
-            eng.model = T5Model(cfg, pack, fp32=True)
+        model, _ = build_model(MODEL_NAME, device=dev, seed=int(os.getenv("MODEL_SEED", "0")),
+                               fp32=dev.type == "cpu")
+        eng = SummarizeEngine(model, MAX_SOURCE_TOKENS)
         _engine, _device = eng, ("cuda" if dev.type == "cuda" else "cpu")
         print(f"[map_summarize] {MODEL_NAME} ready on {_device}", flush=True)
         return _engine
@@ -65,7 +78,10 @@ def _gen_config(payload: Dict[str, Any]):
 
     return GenConfig(num_beams=int(payload.get("num_beams", 4)), max_length=int(payload.get("max_length", 130)),
                      min_length=int(payload.get("min_length", 30)),
-                     length_penalty=float(payload.get("length_penalty", 1.0)), early_stopping=True)
+                     length_penalty=(float(payload["length_penalty"]) if "length_penalty" in payload else None),
+                     no_repeat_ngram_size=(int(payload["no_repeat_ngram_size"])
+                                           if "no_repeat_ngram_size" in payload else None),
+                     early_stopping=True)
 
 
 @register_op("map_summarize")

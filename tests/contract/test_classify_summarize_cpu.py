@@ -63,3 +63,35 @@ def test_summarize_cpu_end_to_end(summarize):
     words = set(doc.split()) | {"short", "one"}
     for s in outs["summaries"]:
         assert all(w in words or w.startswith("<") for w in s.split())
+
+
+def test_summarize_bart_family_cpu(monkeypatch):
+    monkeypatch.delenv("SUMMARIZE_MODEL", raising=False)
+    monkeypatch.setenv("SUMMARIZE_MODEL_FAMILY", "bart")
+    monkeypatch.setenv("BART_MODEL", "bart-tiny")
+    monkeypatch.setenv("SUMMARIZE_FORCE_CPU", "1")
+    import ops.map_summarize as ms
+
+    try:
+        ms = importlib.reload(ms)
+        assert ms.MODEL_NAME == "bart-tiny"
+        doc = "one two three four five six seven eight nine ten " * 3
+        out = ms.handle({"text": doc, "max_length": 14, "min_length": 5})
+        assert out["ok"] and out["model"] == "bart-tiny" and isinstance(out["summary"], str)
+    finally:
+        monkeypatch.undo()
+        importlib.reload(ms)
+
+
+def test_model_resolution(monkeypatch):
+    import ops.map_summarize as ms
+
+    for env, want in [({}, "t5-base"), ({"SUMMARIZE_MODEL": "t5-small"}, "t5-small"),
+                      ({"SUMMARIZE_MODEL_FAMILY": "bart"}, "facebook/bart-large-cnn"),
+                      ({"SUMMARIZE_MODEL": "bart-base"}, "bart-base"),
+                      ({"SUMMARIZE_MODEL_FAMILY": "bart", "BART_MODEL": "bart-large"}, "bart-large")]:
+        for k in ("SUMMARIZE_MODEL", "SUMMARIZE_MODEL_FAMILY", "BART_MODEL"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        assert ms._resolve_model() == want, env

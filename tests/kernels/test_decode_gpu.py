@@ -175,3 +175,35 @@ def test_map_summarize_op_gpu(gpu, monkeypatch):
                      "max_length": 20, "min_length": 5})
     assert out["ok"] and out["device"] == "cuda" and len(out["summaries"]) == 2
     assert ms.handle({}) == {"ok": False, "error": "empty payload"}
+
+
+def test_bart_step_and_generate_gpu(gpu):
+    from agent_tpu_amd.models.bart import BartModel, config_for, init_random
+    from agent_tpu_amd.runtime.summarize import GenConfig, generate
+
+    cfg = config_for("bart-tiny")
+    pack = init_random(cfg, seed=2, std=0.1)
+    cpu_m, gpu_m = BartModel(cfg, pack, fp32=True), BartModel(cfg, pack.to(gpu))
+    B, S = 2, 24
+    g = torch.Generator().manual_seed(2)
+    ids = torch.randint(3, cfg.vocab_size, (B, S), generator=g, dtype=torch.int32)
+    lens = torch.tensor([24, 17], dtype=torch.int32)
+    ec, kc = cpu_m.encode(ids, lens)
+    eg, kg = gpu_m.encode(ids.to(gpu), lens.to(gpu))
+    assert _rel(eg[:S], ec[:S]) < 3e-2 and _rel(kg, kc) < 3e-2
+    T = 8
+    cc, cg = cpu_m.new_cache(B, T), gpu_m.new_cache(B, T)
+    step = torch.zeros(1, dtype=torch.int32)
+    tok = torch.full((B,), 2, dtype=torch.int32)
+    for t in range(3):
+        step.fill_(t)
+        lc = cpu_m.step(tok, step, cc, T, kc, lens, S, 1)
+        lg = gpu_m.step(tok.to(gpu), step.to(gpu), cg, T, kg, lens.to(gpu), S, 1)
+        assert _rel(lg, lc) < 5e-2, t
+        tok = lc.argmax(-1).to(torch.int32)
+    gen = GenConfig(num_beams=4, max_length=20, min_length=6)
+    r1 = generate(gpu_m, ids.to(gpu), lens.to(gpu), gen)
+    r2 = generate(gpu_m, ids.to(gpu), lens.to(gpu), GenConfig(num_beams=4, max_length=20, min_length=6,
+                                                              use_graph=False))
+    assert r1.sequences == r2.sequences
+    assert all(s[0] == 2 and s[1] == 0 and len(s) <= 20 for s in r1.sequences)
