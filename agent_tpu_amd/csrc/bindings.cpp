@@ -73,6 +73,10 @@ PYBIND11_MODULE(_atpu, m) {
       "bf16 MFMA GEMM C = epi(A @ Bt^T)", py::arg("A"), py::arg("lda"), py::arg("Bt"), py::arg("ldb"), py::arg("C"),
       py::arg("ldc"), py::arg("bias"), py::arg("R"), py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"),
       py::arg("epi"), py::arg("stream"), py::arg("splits") = 1, py::arg("ws") = 0);
+  m.def("trace_enabled", &trace_enabled, "roctx tracing active (MI355X_TRACE=1 and roctx loadable)");
+  m.def("trace_push", [](const std::string& n) { trace_push(n.c_str()); });
+  m.def("trace_pop", &trace_pop);
+  m.def("trace_mark", [](const std::string& n) { trace_mark(n.c_str()); });
   m.def("gemm_splitk_splits", &gemm_splitk_splits, "split-K factor chosen for an [M,N,K] GEMM");
   m.def("gemm_256_variant", &gemm_256_variant, py::arg("set") = -1,
         "256x256 GEMM schedule: 1 = ping-pong (default), 0 = full-line 2-stage; set >= 0 switches");

@@ -83,4 +83,10 @@ class HostStager {
   std::thread thread_;
 };
 
+// roctx ranges (MI355X_TRACE=1; no-ops otherwise), see runtime/trace.cpp
+bool trace_enabled();
+void trace_push(const char* name);
+void trace_pop();
+void trace_mark(const char* name);
+
 }  // namespace atpu

@@ -23,6 +23,7 @@ from typing import Any, Callable, Dict, Tuple
 import torch
 import torch.distributed as dist
 
+from ..utils.trace import span
 from .dp import all_gather_rows, broadcast_task, comm_device, is_dist, split_range, world
 
 _TASKS: Dict[str, Callable[[Dict[str, Any]], Any]] = {}
@@ -129,11 +130,11 @@ def _open_table(path: str):
 def classify_csv_task(payload: Dict[str, Any]) -> Any:
     from ops._gpu_runtime import get_gpu_handle, get_model_path  # agent-level registry
 
-    t0 = time.perf_counter()
     rank, ws = world()
+    timing: Dict[str, float] = {}
     # model load is itself collective (C1 broadcast), so it happens on every rank
-    h = get_gpu_handle(get_model_path(payload.get("model_path")))
-    timing: Dict[str, float] = {"load_ms": (time.perf_counter() - t0) * 1000.0}
+    with span("load_ms", timing):
+        h = get_gpu_handle(get_model_path(payload.get("model_path")))
     err, idx, sc, meta = "", None, None, {}
     try:
         start = int(payload.get("start_row", 0))
@@ -147,18 +148,17 @@ def classify_csv_task(payload: Dict[str, Any]) -> Any:
         total = max(0, min(size, table.num_rows - start))
         s_r, n_r = split_range(start, total, ws, rank)
         maybe_inject_fault("classify")
-        t1 = time.perf_counter()
-        idx, sc, st = h.engine.classify_table(table.native, s_r, n_r, col)
-        timing["classify_ms"] = (time.perf_counter() - t1) * 1000.0
+        with span("classify_ms", timing):
+            idx, sc, st = h.engine.classify_table(table.native, s_r, n_r, col)
+        timing.update({f"{k}_ms": round(v, 3) for k, v in st.timing_ms.items()})
         meta = {"start_row": start, "end_row": start + total, "world": ws}
     except Exception as exc:
         err = f"{type(exc).__name__}: {exc}"
         if os.getenv("ATPU_DEBUG"):
             traceback.print_exc()
     _check_errors(err)
-    t2 = time.perf_counter()
-    idx, sc = all_gather_rows(idx, sc)
-    timing["allgather_ms"] = (time.perf_counter() - t2) * 1000.0
+    with span("allgather_ms", timing):
+        idx, sc = all_gather_rows(idx, sc)
     if rank != 0:
         return None
     meta["timing_ms"] = timing

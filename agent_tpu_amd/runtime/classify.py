@@ -30,6 +30,7 @@ from .._native import native
 from ..models.bert import BertClassifier, BertConfig
 from ..models.params import ParamPack
 from ..tokenizer import DEFAULT_MAX_ROW_BYTES, pack_rows
+from ..utils.trace import span
 
 
 @dataclass
@@ -151,22 +152,28 @@ class ClassifyEngine:
         cs, ks = int(self.copy_stream.cuda_stream), int(compute.cuda_stream)
         nb = (n + self.B - 1) // self.B
         t0 = time.perf_counter()
-        st.submit(0, table, start, min(self.B, n), col, self.max_row_bytes, host_threads)
+        tm = stats.timing_ms  # host-side enqueue time per stage (+ roctx ranges under MI355X_TRACE=1)
+        with span("csv_stage", tm):
+            st.submit(0, table, start, min(self.B, n), col, self.max_row_bytes, host_threads)
         for i in range(nb):
             slot = i % self.n_slots
             if i + 1 < nb:
                 b1 = start + (i + 1) * self.B
-                st.submit((i + 1) % self.n_slots, table, b1, min(self.B, start + n - b1), col,
-                          self.max_row_bytes, host_threads)
-            rows, _ = st.upload(slot, self.text[slot].data_ptr(), self.text[slot].numel(),
-                                self.offs[slot].data_ptr(), cs, ks)
-            _, idx, sc = self.run_slot(slot, int(rows))
+                with span("csv_stage", tm):
+                    st.submit((i + 1) % self.n_slots, table, b1, min(self.B, start + n - b1), col,
+                              self.max_row_bytes, host_threads)
+            with span("h2d_upload", tm):
+                rows, _ = st.upload(slot, self.text[slot].data_ptr(), self.text[slot].numel(),
+                                    self.offs[slot].data_ptr(), cs, ks)
+            with span("encoder_launch", tm):
+                _, idx, sc = self.run_slot(slot, int(rows))
             st.release(slot, ks)
             r0 = i * self.B
             out_idx[r0:r0 + rows].copy_(idx[:rows], non_blocking=True)
             out_score[r0:r0 + rows].copy_(sc[:rows], non_blocking=True)
             stats.batches += 1
-        torch.cuda.synchronize(dev)
+        with span("device_drain", tm):
+            torch.cuda.synchronize(dev)
         stats.rows = n
         stats.wall_s = time.perf_counter() - t0
         return out_idx, out_score, stats

@@ -38,6 +38,7 @@ import torch
 
 from .. import ops
 from ..tokenizer import pack_rows
+from ..utils.trace import span
 
 NEG = -1.0e9
 
@@ -150,7 +151,8 @@ def generate(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfi
     rows = B * nb
     t0 = time.perf_counter()
 
-    _, ckv = model.encode(src_ids, src_lens)
+    with span("encode"):
+        _, ckv = model.encode(src_ids, src_lens)
     t_enc = time.perf_counter()
     cache = model.new_cache(rows, T)
     hist = torch.zeros((rows, T), dtype=torch.int32, device=dev)
@@ -188,7 +190,8 @@ def generate(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfi
                 graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(graph):
                     g_logits = model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist)
-        sc, tk = _select(logits, run_scores, K2, cfg, gen, cur, T, run_seq)
+        with span("beam_select"):
+            sc, tk = _select(logits, run_scores, K2, cfg, gen, cur, T, run_seq)
         sc, tk = sc.view(B, nb * K2), tk.view(B, nb * K2)
         steps += 1
         # global top-K2 per item; ties -> lower flat index (beam * V + token) like torch.topk over [nb*V]

@@ -167,10 +167,38 @@ METRICS = Metrics()
 
 
 # --------------------------------------------------------------- profile
-def worker_profile() -> Dict[str, Any]:
+GPU_OPS = {"map_classify", "map_classify_tpu", "map_summarize", "risk_accumulate"}
+
+
+def gpu_health(caps: List[str]) -> Optional[Dict[str, Any]]:
+    """Start-up device check (arch, HBM, MFMA probe) when a GPU op is enabled."""
+    if not (set(caps) & GPU_OPS) or os.getenv("GPU_DISABLED", "").strip().lower() in ("1", "true", "yes", "on"):
+        return None
+    if os.getenv("GPU_HEALTH_CHECK", "1").strip().lower() in ("0", "false", "no", "off"):
+        return None
+    try:
+        import torch
+
+        if not torch.cuda.is_available():
+            return {"ok": False, "error": "no ROCm device visible"}
+        from agent_tpu_amd.runtime import health
+
+        return health.check()
+    except Exception as exc:
+        return {"ok": False, "error": f"{type(exc).__name__}: {exc}"}
+
+
+def worker_profile(health: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
     from worker_sizing import build_worker_profile
 
     prof = build_worker_profile()
+    if health is not None and prof.get("gpu", {}).get("gpu_present"):
+        prof["gpu"]["health"] = {"ok": health.get("ok", False), "healthy": health.get("healthy", []),
+                                 "unhealthy": {str(k): v for k, v in health.get("unhealthy", {}).items()}}
+        if "healthy" in health:
+            # advertise only devices that passed (reduced capacity after a fault)
+            prof["gpu"]["gpu_count"] = len(health["healthy"])
+            prof["gpu"]["max_gpu_workers"] = len(health["healthy"])
     prof["tier"] = "mi355x" if prof.get("gpu", {}).get("gpu_present") else "cpu"
     prof["limits"] = {"max_payload_bytes": int(os.getenv("MAX_PAYLOAD_BYTES", "262144")),
                       "max_tokens": int(os.getenv("MAX_TOKENS", "2048"))}
@@ -232,6 +260,17 @@ class Controller:
             time.sleep(min(2.0, 0.1 * 2**attempt))
 
 
+def _op_span(op: str):
+    """roctx range around a job under MI355X_TRACE=1 (no import cost otherwise)."""
+    if os.getenv("MI355X_TRACE", "0").strip().lower() not in ("1", "true"):
+        import contextlib
+
+        return contextlib.nullcontext()
+    from agent_tpu_amd.utils.trace import span
+
+    return span(f"job:{op}")
+
+
 def extract_task(task: Any) -> Tuple[str, str, Dict[str, Any], Any]:
     """-> (job_id, op, payload, job_epoch) with the reference's checks (app.py:221-234)."""
     if not isinstance(task, dict):
@@ -259,7 +298,11 @@ class Agent:
         # advertise only what can run: a leased-but-unloadable op would fail every job
         self.caps = [c for c in CAPS_LIST if c in self.handlers] if errors and self.handlers else list(CAPS_LIST)
         self.ctl = Controller(CONTROLLER_URL, HTTP_TIMEOUT_SEC)
-        self.profile = worker_profile()
+        self.health = gpu_health(self.caps)
+        if self.health is not None:
+            print(f"{LOG} gpu health ok={self.health.get('ok')} healthy={self.health.get('healthy')} "
+                  f"unhealthy={self.health.get('unhealthy', {})} {self.health.get('error', '')}", flush=True)
+        self.profile = worker_profile(self.health)
 
     def run_task(self, lease_id: str, task: Any) -> None:
         try:
@@ -273,11 +316,13 @@ class Agent:
             fn = self.handlers.get(op)
             if fn is None:
                 raise RuntimeError(f"Unknown op '{op}'")
-            out = fn(payload)  # inline: one job at a time per agent (ref app.py:286-287)
+            with _op_span(op):
+                out = fn(payload)  # inline: one job at a time per agent (ref app.py:286-287)
             if FAIL_ON_NOT_OK and isinstance(out, dict) and out.get("ok") is False:
                 raise RuntimeError(str(out.get("error", "op returned ok=false")))
         except Exception as exc:
             err = {"type": type(exc).__name__, "message": str(exc), "trace": traceback.format_exc(limit=12)}
+            self._note_device_fault(str(exc))
         ok = err is None
         ms = (time.time() - t0) * 1000.0
         METRICS.job_done(ok, out)
@@ -290,6 +335,21 @@ class Agent:
             print(f"{LOG} ok job={job_id} op={op} ms={ms:.1f}", flush=True)
         else:
             log_every("exec", f"{LOG} FAIL job={job_id} op={op} ms={ms:.1f} err={err}")
+
+    _FAULT_MARKERS = ("hipError", "HIP error", "HSA_STATUS_ERROR", "illegal memory access",
+                      "device-side assert", "GPU Hang", "Memory access fault")
+
+    def _note_device_fault(self, msg: str) -> None:
+        """A HIP fault marks this agent's device unhealthy and re-advertises the profile."""
+        if self.health is None or not any(m in msg for m in self._FAULT_MARKERS):
+            return
+        from agent_tpu_amd.runtime import health
+
+        dev = int(os.getenv("LOCAL_RANK", "0"))
+        health.mark_unhealthy(dev, msg[:200])
+        self.health = health.last()
+        self.profile = worker_profile(self.health)
+        print(f"{LOG} device {dev} marked unhealthy: {msg[:200]}", flush=True)
 
     def loop(self) -> None:
         while _running:

@@ -1,0 +1,66 @@
+"""Runtime services on a real MI355X: health check, roctx tracing switch,
+map_classify op forms (reference ids form, texts, CSV shard) and the risk GPU path."""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_health_check(gpu):
+    from agent_tpu_amd.runtime import health
+
+    h = health.check()
+    assert h["ok"] and 0 in h["healthy"] and not h["unhealthy"], h
+    d = h["devices"][0]
+    assert d["arch"].startswith("gfx950") and d["hbm_total_gb"] > 200 and d["compute_units"] >= 256
+    health.mark_unhealthy(0, "test")
+    assert health.last()["ok"] is False and "0" not in map(str, health.last()["healthy"])
+    health._unhealthy.clear()
+
+
+def test_map_classify_op_forms(gpu, tmp_path, monkeypatch):
+    monkeypatch.setenv("GPU_MODEL_PATH", "bert-tiny?labels=5&batch=64")
+    from agent_tpu_amd.utils.synthetic import write_csv
+    from ops import map_classify as mc
+
+    out = mc.map_classify_tpu({"input": [101] + [2000 + i for i in range(30)] + [102] + [0] * 96, "topk": 3,
+                               "allow_fallback": False})
+    assert set(out) == {"op", "model_path", "topk", "elapsed_ms"} and out["op"] == "map_classify_tpu"
+    assert len(out["topk"]) == 3 and abs(sum(t["score"] for t in out["topk"]) - 1.0) < 1.0
+    assert out["topk"][0]["score"] >= out["topk"][1]["score"] >= out["topk"][2]["score"]
+    bad = mc.map_classify({"input": [1, 2, 3]})
+    assert bad["fallback"] == "cpu" and "Input size mismatch" in bad["reason"]
+    texts = mc.map_classify({"texts": ["hello world", "", "another row of text"], "topk": 2})
+    assert texts["ok"] and texts["row_count"] == 3 and len(texts["rows"][2]["topk"]) == 2
+    path = str(tmp_path / "rows.csv")
+    write_csv(path, 300, 40)
+    csv = mc.map_classify({"source_uri": path, "start_row": 10, "shard_size": 150, "topk": 2})
+    assert csv["ok"] and csv["row_count"] == 150 and csv["start_row"] == 10 and csv["end_row"] == 160
+    assert csv["rows"][0]["row"] == 10 and csv["dp_world_size"] == 1
+    # CSV path == texts path on the same rows (same tokenizer, same weights)
+    import csv as pycsv
+
+    with open(path, newline="") as f:
+        rows = [r["text"] for r in pycsv.DictReader(f)][10:20]
+    ref = mc.map_classify({"texts": rows, "topk": 2})
+    for a, b in zip(csv["rows"][:10], ref["rows"]):
+        assert [t["index"] for t in a["topk"]] == [t["index"] for t in b["topk"]]
+        assert abs(a["topk"][0]["score"] - b["topk"][0]["score"]) < 1e-3
+    summ = mc.map_classify({"source_uri": path, "start_row": 0, "shard_size": 300, "output": "summary"})
+    assert sum(summ["top1_histogram"].values()) == 300 and "rows" not in summ
+    assert "classify_ms" in csv["timing_ms"] and "h2d_upload_ms" in csv["timing_ms"]
+
+
+def test_risk_gpu_path_matches_cpu(gpu, monkeypatch):
+    from ops.risk_accumulate import risk_accumulate
+
+    vals = [((i * 7919) % 100003) / 97.0 - 400.0 for i in range(200_003)]
+    monkeypatch.setenv("RISK_DEVICE", "cpu")
+    ref = risk_accumulate({"values": vals})
+    monkeypatch.setenv("RISK_DEVICE", "gpu")
+    got = risk_accumulate({"values": vals})
+    assert got["device"] == "gpu" and got["count"] == ref["count"]
+    assert got["min"] == ref["min"] and got["max"] == ref["max"]
+    assert abs(got["sum"] - ref["sum"]) <= 1e-9 * max(1.0, abs(ref["sum"]))

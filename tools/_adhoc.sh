@@ -1,9 +1,8 @@
 set -o pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests/kernels/test_decode_gpu.py -x -q > gpurun_out/pytest_dec.log 2>&1 || { tail -40 gpurun_out/pytest_dec.log; exit 1; }
-tail -2 gpurun_out/pytest_dec.log
-timeout -k 10 500 python bench/summarize.py --model bart-large-cnn --docs 64 --steps 2 --warmup 1 > gpurun_out/summ_bart64.log 2>&1 || { tail -30 gpurun_out/summ_bart64.log; exit 1; }
-tail -1 gpurun_out/summ_bart64.log
-timeout -k 10 500 python bench/summarize.py --model bart-large-cnn --docs 256 --steps 1 --warmup 1 > gpurun_out/summ_bart256.log 2>&1 || { tail -30 gpurun_out/summ_bart256.log; exit 1; }
-tail -1 gpurun_out/summ_bart256.log
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { tail -60 gpurun_out/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu.log
+cd /tmp && export TMPDIR=/tmp
+MI355X_TRACE=1 timeout -k 10 400 rocprofv3 --kernel-trace --marker-trace -d $GRAFT_REPO_ROOT/gpurun_out/trace -o tr -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 > $GRAFT_REPO_ROOT/gpurun_out/trace.log 2>&1 || { tail -30 $GRAFT_REPO_ROOT/gpurun_out/trace.log; exit 1; }
+tail -1 $GRAFT_REPO_ROOT/gpurun_out/trace.log
