@@ -403,7 +403,8 @@ __global__ __launch_bounds__(512, 2) void gemm256b_kernel(
 // phase r is safe after reads at phase <= r-2 (every restage is >= 2 phases
 // after the quarter's last read in the previous K-tile).
 // ============================================================================
-template <int EPI>
+// DBG (timing-only ablation, results WRONG): 1 = skip the epilogue (acc kept live)
+template <int EPI, int DBG = 0>
 __global__ __launch_bounds__(512, 1) void gemm256p_kernel(
     const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C, int ldc,
     const float* __restrict__ bias, const bf16* __restrict__ R, int ldr, int M, int N, int K) {
@@ -546,49 +547,105 @@ __global__ __launch_bounds__(512, 1) void gemm256p_kernel(
   }
 #undef ATPU_PP_SYNC_MMA
   if (wm == 0) __builtin_amdgcn_s_barrier();  // close the stagger (equal barrier counts)
+  if constexpr (DBG & 1) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
+  // the last MFMAs' results are read by inline-asm v_permlane below, which the
+  // hazard recognizer cannot see: pad the MFMA-write -> VALU-read window
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
 
-  f32x4 bv[4];
+  // ---- epilogue, widened (guide T21 for the 16x16 layout): v_permlane16_swap
+  // of fragments (2p, j) and (2p+1, j) leaves every lane with 8 consecutive
+  // fp32 columns of ONE row -> 16-B residual loads and 16-B stores (half the
+  // VMEM instructions of the 8-B row-per-lane tail) ----
+  const int hi = fc & 1, cq = (fc >> 1) * 8;  // row parity within the pair, column half
+  bf16x8 res[4][4];
+  if constexpr (EPI & kEpiResidual) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int pp = 0; pp < 4; ++pp) {
+        const int m = min(m0 + wm * 128 + (2 * pp + hi) * 16 + fr, M - 1);
+        res[j][pp] = *reinterpret_cast<const bf16x8*>(R + (size_t)m * ldr + n0 + wn * 64 + j * 16 + cq);
+      }
+  }
+  f32x4 bias8[4][2];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int n = n0 + wn * 64 + j * 16 + fc * 4;
-    if constexpr (EPI & kEpiBias) bv[j] = *reinterpret_cast<const f32x4*>(bias + n);
-    else bv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int n = n0 + wn * 64 + j * 16 + cq;
+    if constexpr (EPI & kEpiBias) {
+      bias8[j][0] = *reinterpret_cast<const f32x4*>(bias + n);
+      bias8[j][1] = *reinterpret_cast<const f32x4*>(bias + n + 4);
+    } else {
+      bias8[j][0] = bias8[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   }
+  // row pair outer, column fragment inner: the 4 consecutive 16-B stores of a
+  // lane cover its row's whole 128-B line segment (write combining in L2)
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wm * 128 + i * 16 + fr;
-    if (m >= M) continue;
+  for (int pp = 0; pp < 4; ++pp) {
+    const int m = m0 + wm * 128 + (2 * pp + hi) * 16 + fr;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + fc * 4;
-      f32x4 v = acc[i][j] + bv[j];
+      const int n = n0 + wn * 64 + j * 16 + cq;
+      const f32x4 lo4 = acc[2 * pp][j], hi4 = acc[2 * pp + 1][j];
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        // v_permlane16_swap (odd 16-lane rows of x <-> even rows of y): the
+        // even lane keeps row 2p (own cols 0-3 + partner's 4-7), the odd lane
+        // row 2p+1 (semantics probed: tools/probes/permlane_probe.hip).
+        // Operands are laundered through v_mov into fresh early-clobber
+        // registers: handing element extracts of the accumulator tuples to
+        // the swap directly got both operands allocated to one register.
+        unsigned x, y;
+        asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %3\n\ts_nop 1\n\tv_permlane16_swap_b32 %0, %1"
+                     : "=&v"(x), "=&v"(y)
+                     : "v"(lo4[e]), "v"(hi4[e]));
+        v[e] = __builtin_bit_cast(float, x) + bias8[j][0][e];
+        v[4 + e] = __builtin_bit_cast(float, y) + bias8[j][1][e];
+      }
       if constexpr (EPI & kEpiGelu) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = gelu_fast(v[e]);
+        for (int e = 0; e < 8; ++e) v[e] = gelu_fast(v[e]);
       }
       if constexpr (EPI & kEpiTanh) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
+        for (int e = 0; e < 8; ++e) v[e] = tanhf(v[e]);
       }
       if constexpr (EPI & kEpiRelu) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
       }
       if constexpr (EPI & kEpiResidual) {
-        const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + n);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += bf2f(r[e]);
+        for (int e = 0; e < 8; ++e) v[e] += bf2f(res[j][pp][e]);
       }
-      bf16x4 o;
+      bf16x8 o;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
-      *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e]);
+      if (m < M) *reinterpret_cast<bf16x8*>(C + (size_t)m * ldc + n) = o;
     }
   }
 }
 
 void launch_256p(const GemmArgs& g, hipStream_t s) {
   const int nb = ((g.M + 255) / 256) * (g.N / 256);
+  static const int ablate = [] {
+    const char* f = std::getenv("ATPU_GEMM_ABLATE");
+    return f ? std::atoi(f) : 0;
+  }();
+  if (ablate == 4) {  // no epilogue (timing only)
+    hipLaunchKernelGGL((gemm256p_kernel<kEpiBias, 1>), dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C,
+                       g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K);
+    return;
+  }
 #define ATPU_G256P(E)                                                                                     \
   case E:                                                                                                 \
     hipLaunchKernelGGL((gemm256p_kernel<E>), dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, \
@@ -800,7 +857,8 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
     return;
   }
   const int kernel256 = gemm_256_variant(-1);
-  const bool big_ok = g.N % 256 == 0;
+  const bool big_ok = g.N % 256 == 0 && g.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(g.C) & 15) == 0 &&
+                      (!(g.epi & kEpiResidual) || (g.ldr % 8 == 0 && (reinterpret_cast<uintptr_t>(g.R) & 15) == 0));
   const bool use_big = !(g.epi & kEpiOutF32) && (forced ? (forced == 256 && big_ok) : (g.M >= 2048 && big_ok));
   if (use_big && kernel256 == 1)
     launch_256p(g, stream);
