@@ -63,6 +63,37 @@ __device__ __forceinline__ float gelu_fast(float x) {
   return 0.5f * x * (1.0f + erf_x);
 }
 
+// gelu_fast over 8 independent values, written stage by stage so the
+// transcendental results (v_rcp, v_exp) are consumed several instructions
+// after they are produced: the per-element form left hipcc padding every
+// trans->use pair with s_nop. Same A&S 7.1.26 erf, exp folded into exp2.
+__device__ __forceinline__ void gelu_fast8(float (&v)[8]) {
+  float t[8], ex[8], p[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t[e] = fmaf(0.3275911f * 0.70710678118654752f, fabsf(v[e]), 1.0f);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ex[e] = v[e] * v[e];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t[e] = __builtin_amdgcn_rcpf(t[e]);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ex[e] = __builtin_amdgcn_exp2f(ex[e] * (-0.5f * 1.4426950408889634f));
+#pragma unroll
+  for (int e = 0; e < 8; ++e) p[e] = fmaf(1.061405429f, t[e], -1.453152027f);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) p[e] = fmaf(p[e], t[e], 1.421413741f);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) p[e] = fmaf(p[e], t[e], -0.284496736f);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) p[e] = fmaf(p[e], t[e], 0.254829592f);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) p[e] = fmaf(-p[e] * t[e], ex[e], 1.0f);  // |erf(x/sqrt2)|
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float half_x = 0.5f * v[e];
+    v[e] = fmaf(half_x, copysignf(p[e], v[e]), half_x);
+  }
+}
+
 __device__ __forceinline__ float bf2f(bf16 x) { return static_cast<float>(x); }
 __device__ __forceinline__ bf16 f2bf(float x) { return static_cast<bf16>(x); }
 

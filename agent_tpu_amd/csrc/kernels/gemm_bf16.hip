@@ -586,6 +586,7 @@ __global__ __launch_bounds__(512, 1) void gemm256p_kernel(
       bias8[j][0] = bias8[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
+  const bool full_tile = m0 + 256 <= M;  // uniform: no per-store bounds branch
   // row pair outer, column fragment inner: the 4 consecutive 16-B stores of a
   // lane cover its row's whole 128-B line segment (write combining in L2)
 #pragma unroll
@@ -611,10 +612,7 @@ __global__ __launch_bounds__(512, 1) void gemm256p_kernel(
         v[e] = __builtin_bit_cast(float, x) + bias8[j][0][e];
         v[4 + e] = __builtin_bit_cast(float, y) + bias8[j][1][e];
       }
-      if constexpr (EPI & kEpiGelu) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = gelu_fast(v[e]);
-      }
+      if constexpr (EPI & kEpiGelu) gelu_fast8(v);
       if constexpr (EPI & kEpiTanh) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = tanhf(v[e]);
@@ -630,7 +628,7 @@ __global__ __launch_bounds__(512, 1) void gemm256p_kernel(
       bf16x8 o;
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e]);
-      if (m < M) *reinterpret_cast<bf16x8*>(C + (size_t)m * ldc + n) = o;
+      if (full_tile || m < M) *reinterpret_cast<bf16x8*>(C + (size_t)m * ldc + n) = o;
     }
   }
 }

@@ -18,6 +18,8 @@ parity test against transformers with identical random weights.
 from __future__ import annotations
 
 import dataclasses
+import math
+import os
 from dataclasses import dataclass
 from typing import Dict, Optional, Tuple
 
@@ -49,6 +51,15 @@ class BertConfig:
         layer = 4 * H * H + 4 * H + 2 * H * I + I + H + 4 * H
         head = H * H + H + self.num_labels * H + self.num_labels
         return emb + L * layer + head
+
+    def flops_per_row_executed(self, seq_len: int, cls_only_last: bool = True) -> float:
+        """FLOPs actually executed per row when the last layer runs on [CLS] only."""
+        if not cls_only_last:
+            return self.flops_per_row(seq_len)
+        H, I, S = self.hidden, self.intermediate, seq_len
+        full_layer = 2 * S * (4 * H * H + 2 * H * I) + 4 * S * S * H
+        last = 2 * S * 2 * H * H + 2 * (2 * H * H + 2 * H * I) + 4 * S * H
+        return self.flops_per_row(seq_len) - full_layer + last
 
     def flops_per_row(self, seq_len: int) -> float:
         """Forward FLOPs for one row of ``seq_len`` tokens (GEMMs + attention)."""
@@ -165,18 +176,29 @@ class BertClassifier:
     PyTorch reference path of every op; pass ``fp32=True`` for an fp32 oracle).
     """
 
-    def __init__(self, cfg: BertConfig, pack: ParamPack, fp32: bool = False):
+    def __init__(self, cfg: BertConfig, pack: ParamPack, fp32: bool = False, cls_only_last: Optional[bool] = None):
         self.cfg = cfg
         self.pack = pack
         self.p = pack.with_dtype(torch.float32) if fp32 else {n: pack[n] for n in pack.names()}
         self.device = pack.buffer.device
+        # The classifier reads only the [CLS] row of the last layer (pooler on
+        # h[:, 0]). So in that layer only K/V need every token; Q, attention
+        # output, O-proj, LN and the FFN run on the B [CLS] rows. The logits are
+        # those of the full computation; only dead rows are skipped.
+        if cls_only_last is None:
+            cls_only_last = os.getenv("ATPU_CLS_ONLY_LAST", "1") not in ("0", "false", "no")
+        self.cls_only_last = bool(cls_only_last)
 
-    def encode(self, ids: torch.Tensor, lens: torch.Tensor, type_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def encode(self, ids: torch.Tensor, lens: torch.Tensor, type_ids: Optional[torch.Tensor] = None,
+               cls_only_last: bool = False) -> torch.Tensor:
+        """Hidden states ``[B*S, H]``, or ``[B, H]`` [CLS] states with ``cls_only_last``."""
         cfg, p = self.cfg, self.p
         B, S = ids.shape
+        H = cfg.hidden
         h = ops.embed_layernorm(ids, p["emb.word"], p["emb.pos"], p["emb.type"], p["emb.ln_g"], p["emb.ln_b"],
                                 cfg.eps, type_ids=type_ids)
-        for i in range(cfg.layers):
+        last_full = cfg.layers - 1 if cls_only_last else cfg.layers
+        for i in range(last_full):
             q = f"l{i}."
             qkv = ops.linear(h, p[q + "qkv_w"], p[q + "qkv_b"])
             ctx = ops.attention_packed(qkv, lens, B, S, cfg.heads)
@@ -185,16 +207,31 @@ class BertClassifier:
             f = ops.linear(h1, p[q + "f1_w"], p[q + "f1_b"], act="gelu")
             h2 = ops.linear(f, p[q + "f2_w"], p[q + "f2_b"], residual=h1)
             h = ops.layernorm(h2, p[q + "ln2_g"], p[q + "ln2_b"], cfg.eps)
-        return h
+        if not cls_only_last:
+            return h
+        # last layer on the [CLS] rows: K/V GEMM over every token (rows H..3H of
+        # the fused weight), Q GEMM over the B [CLS] rows, single-query attention
+        q = f"l{cfg.layers - 1}."
+        w, b = p[q + "qkv_w"], p[q + "qkv_b"]
+        kv = ops.linear(h, w[H:], b[H:])
+        h_cls = h.view(B, S, H)[:, 0, :]  # strided view: row stride S*H
+        qc = ops.linear(h_cls, w[:H], b[:H])
+        ctx = ops.decode_attention(qc, kv[:, :H], kv[:, H:], cfg.heads, S, 1, lens=lens,
+                                   scale=1.0 / math.sqrt(cfg.head_dim))
+        h1 = ops.linear(ctx, p[q + "o_w"], p[q + "o_b"], residual=h_cls.contiguous())
+        h1 = ops.layernorm(h1, p[q + "ln1_g"], p[q + "ln1_b"], cfg.eps)
+        f = ops.linear(h1, p[q + "f1_w"], p[q + "f1_b"], act="gelu")
+        h2 = ops.linear(f, p[q + "f2_w"], p[q + "f2_b"], residual=h1)
+        return ops.layernorm(h2, p[q + "ln2_g"], p[q + "ln2_b"], cfg.eps)
 
     def pooled(self, h: torch.Tensor, B: int, S: int) -> torch.Tensor:
-        cls_rows = h.view(B, S, self.cfg.hidden)[:, 0, :]  # strided view: row stride S*H
+        cls_rows = h if h.shape[0] == B else h.view(B, S, self.cfg.hidden)[:, 0, :]  # strided: row stride S*H
         return ops.linear(cls_rows, self.p["pool_w"], self.p["pool_b"], act="tanh")
 
     def forward(self, ids: torch.Tensor, lens: torch.Tensor, k: int = 5,
                 type_ids: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
         """Returns ``(logits[B,C] fp32, topk_idx[B,k] int32, topk_prob[B,k] fp32)``."""
         B, S = ids.shape
-        h = self.encode(ids, lens, type_ids)
+        h = self.encode(ids, lens, type_ids, cls_only_last=self.cls_only_last and S > 1)
         pooled = self.pooled(h, B, S)
         return ops.classify_head_topk(pooled, self.p["cls_w"], self.p["cls_b"], k)

@@ -119,7 +119,8 @@ def main() -> int:
     assert idx.shape[0] == total_rows, (idx.shape, total_rows)
     value = total_rows / elapsed
     if rank == 0:
-        flops = cfg.flops_per_row(a.seq_len) * total_rows / elapsed
+        cls_only = eng.model.cls_only_last
+        flops = cfg.flops_per_row_executed(a.seq_len, cls_only) * total_rows / elapsed
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -144,7 +145,10 @@ def main() -> int:
                 "topk": min(a.topk, cfg.num_labels),
                 "hipgraph": not a.no_graph,
                 "weight_broadcast_ms": round(bcast_ms, 2),
+                "last_layer_cls_only": cls_only,
                 "achieved_tflops_per_gpu": round(flops / world / 1e12, 1),
+                "model_equivalent_tflops_per_gpu": round(cfg.flops_per_row(a.seq_len) * total_rows / elapsed
+                                                         / world / 1e12, 1),
             },
         }
         print(json.dumps(out), flush=True)

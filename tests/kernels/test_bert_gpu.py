@@ -49,3 +49,27 @@ def test_engine_table_graph_vs_eager_vs_texts(gpu, tmp_path, nat):
         rows = [r["text"] for r in csv.DictReader(f)][10:260]
     res = eng_e.classify_texts(rows)
     assert torch.equal(res.idx, ie.cpu())
+
+
+def test_cls_only_last_layer_matches_full(gpu):
+    """Pruned last layer ([CLS] rows only) == full last layer, on the GPU and vs the CPU oracle."""
+    import torch
+
+    from agent_tpu_amd.models.bert import BertClassifier, config_for, init_random
+
+    cfg = config_for("bert-base", num_labels=4)
+    pack = init_random(cfg, seed=3, bias_std=0.02)
+    B, S = 16, 128
+    g = torch.Generator().manual_seed(0)
+    ids = torch.randint(1000, cfg.vocab_size, (B, S), generator=g, dtype=torch.int32)
+    lens = torch.randint(8, S + 1, (B,), generator=g, dtype=torch.int32)
+    ids[torch.arange(S).view(1, S) >= lens.view(B, 1)] = 0
+    dev = pack.to(gpu)
+    pruned = BertClassifier(cfg, dev, cls_only_last=True)
+    full = BertClassifier(cfg, dev, cls_only_last=False)
+    lp, ip, pp = pruned.forward(ids.to(gpu), lens.to(gpu), 4)
+    lf, if_, pf = full.forward(ids.to(gpu), lens.to(gpu), 4)
+    assert (lp - lf).abs().max().item() < 3e-2 * max(1.0, lf.abs().max().item())
+    oracle = BertClassifier(cfg, pack, fp32=True, cls_only_last=False)
+    lo, _, _ = oracle.forward(ids, lens, 4)
+    assert (lp.cpu() - lo).abs().max().item() < 5e-2 * max(1.0, lo.abs().max().item())
