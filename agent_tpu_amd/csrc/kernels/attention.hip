@@ -4,8 +4,10 @@
 //   O[b,q,h,:] = softmax_k( scale * Q[b,q,h]·K[b,k,h] + bias[h,q,k] ) · V[b,k,h,:]
 //   keys k >= lens[b] are masked; causal=1 additionally masks k > q.
 //
-// D = 64 (BERT-base/large, T5-base). Workgroup = 4 waves = 128 queries of one
-// (batch, head); each wave owns 32 queries. Keys are processed in chunks of
+// D = 64 (BERT-base/large, T5-base). Workgroup = 8 waves = 128 queries of one
+// (batch, head); each wave owns 16 queries (one MFMA column tile), which keeps
+// a wave at <= 128 VGPRs: 2 workgroups = 4 waves/SIMD per CU to hide the
+// staging latency (the 4-wave/32-query layout needed 251 VGPRs, 2 waves/SIMD). Keys are processed in chunks of
 // 128 with an fp32 online softmax, so any Skv works; BERT (S=128) is one chunk.
 //
 // CDNA4 mapping (cdna_hip_programming.md §3, App. B "Fused attention"):
@@ -16,9 +18,12 @@
 //    inside a 32-key step is permuted identically on both operands).
 //  * K chunk staged by global_load_lds (16 B/lane) into a row-swizzled image
 //    (chunk ^ ((row>>1)&7)) read conflict-free with ds_read_b128.
-//  * V chunk staged transposed, V^T[d][key], with 8-byte slots swizzled by
-//    (key>>2) ^ ((d&15)<<1): the PV A-operand reads (ds_read_b64, 16 d-rows x
-//    2 key groups per half-wave) hit 32 distinct slots -> conflict-free.
+//  * V chunk staged ROW-major by global_load_lds like K (no VGPR round trip),
+//    16-B chunks swizzled chunk ^ (((row>>1)&3)<<1); the PV A operand (8 keys
+//    of one d column per lane) is gathered with ds_read_b64_tr_b16 (guide
+//    T10): a 16-lane group reads a 4-key x 16-d block and lane i receives
+//    column i. The chunk-pair swizzle puts the 8 rows a 32-lane half reads in
+//    8 distinct 32-B bank groups -> conflict-free.
 //  * Q fragments go global -> VGPR directly (read once per wave).
 #include "atpu/common.h"
 #include "atpu/kernels.h"
@@ -30,20 +35,29 @@ constexpr int kD = 64;
 constexpr int kKC = 128;  // keys per chunk
 constexpr int kQB = 128;  // queries per workgroup
 constexpr int kKRowB = kD * 2;     // 128 B per K row
-constexpr int kVtRowB = kKC * 2;   // 256 B per V^T row
+constexpr int kVRowB = kD * 2;     // 128 B per V row
 constexpr int kLdsK = kKC * kKRowB;  // 16 KiB
-constexpr int kLdsV = kD * kVtRowB;  // 16 KiB
+constexpr int kLdsV = kKC * kVRowB;  // 16 KiB
 
 __device__ __forceinline__ int kswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
-// byte offset of V^T[d][key] (key in [0,128))
-__device__ __forceinline__ int vt_off(int d, int key) {
-  return d * kVtRowB + ((((key >> 2) ^ ((d & 15) << 1))) << 3) + ((key & 3) << 1);
+__device__ __forceinline__ int vswz(int row, int chunk) { return chunk ^ (((row >> 1) & 3) << 1); }
+
+typedef short v4s __attribute__((vector_size(8)));
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses row q, elements
+// 4p..4p+3 of a 4x16 block; lane i gets column i of the 4 rows (row q -> elem q)
+__device__ __forceinline__ bf16x4 lds_read_tr16(const char* p) {
+  const v4s r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
+  return __builtin_bit_cast(bf16x4, r);
 }
 
-__global__ __launch_bounds__(256, 2) void attention_fwd_kernel(
+constexpr int kWaves = 8;
+constexpr int kThreads = kWaves * 64;
+
+template <bool HAS_BIAS, bool CAUSAL>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(HAS_BIAS ? 2 : 4))) void attention_fwd_kernel(
     const bf16* __restrict__ Q, int ldq, const bf16* __restrict__ Kp, int ldk, const bf16* __restrict__ V, int ldv,
     bf16* __restrict__ O, int ldo, const int32_t* __restrict__ lens, const float* __restrict__ bias, int Sq, int Skv,
-    int H, float scale, int causal) {
+    int H, float scale) {
   __shared__ __attribute__((aligned(16))) char lds[kLdsK + kLdsV];
   char* ldsK = lds;
   char* ldsV = lds + kLdsK;
@@ -58,154 +72,144 @@ __global__ __launch_bounds__(256, 2) void attention_fwd_kernel(
   const bf16* Kb = Kp + (size_t)b * Skv * ldk + h * kD;
   const bf16* Vb = V + (size_t)b * Skv * ldv + h * kD;
 
-  // ---- this wave's Q fragments: 2 query tiles x 2 d-steps, 16 B each ----
-  const int qw = qblk * kQB + wave * 32;
-  bf16x8 qf[2][2];
+  // ---- this wave's Q fragments: 16 queries x 2 d-steps, 16 B each ----
+  const int qw = qblk * kQB + wave * 16;
+  bf16x8 qf[2];
+  {
+    const int q = min(qw + fr, Sq - 1);
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int q = min(qw + qt * 16 + fr, Sq - 1);
-#pragma unroll
-    for (int ds = 0; ds < 2; ++ds) qf[qt][ds] = *reinterpret_cast<const bf16x8*>(Qb + (size_t)q * ldq + ds * 32 + fg * 8);
+    for (int ds = 0; ds < 2; ++ds) qf[ds] = *reinterpret_cast<const bf16x8*>(Qb + (size_t)q * ldq + ds * 32 + fg * 8);
   }
 
-  float m_run[2], l_run[2];
-  f32x4 o[4][2];  // O^T tiles [d-tile][q-tile]
+  float m_run = -1e30f, l_run = 0.f;
+  f32x4 o[4];  // O^T tiles [d-tile] for the wave's 16 queries
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    m_run[qt] = -1e30f;
-    l_run[qt] = 0.f;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o[dt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int kv_end = causal ? min(len, qblk * kQB + kQB) : len;
+  const int kv_end = CAUSAL ? min(len, qblk * kQB + kQB) : len;
   for (int kc = 0; kc < kv_end; kc += kKC) {
     __syncthreads();  // previous chunk fully consumed
     // ---- stage K chunk: 16 wave-instructions of 8 rows (4 per wave) ----
     {
       const int srow = lane >> 3, spos = lane & 7;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = (i * 4 + wave) * 8 + srow;
+      for (int i = 0; i < 16 / kWaves; ++i) {
+        const int r = (i * kWaves + wave) * 8 + srow;
         const int key = min(kc + r, Skv - 1);
-        glds16(Kb + (size_t)key * ldk + kswz(r, spos) * 8, ldsK + (i * 4 + wave) * 8 * kKRowB);
+        glds16(Kb + (size_t)key * ldk + kswz(r, spos) * 8, ldsK + (i * kWaves + wave) * 8 * kKRowB);
       }
     }
-    // ---- stage V chunk transposed: thread -> (key, 8 d) pieces ----
+    // ---- stage V chunk row-major (same DMA pattern as K, V swizzle) ----
+    {
+      const int srow = lane >> 3, spos = lane & 7;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int piece = i * 256 + tid;  // 1024 pieces = 128 keys x 8 d-groups
-      const int key = piece >> 3, dg = (piece & 7) * 8;
-      const int gk = min(kc + key, Skv - 1);
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(Vb + (size_t)gk * ldv + dg);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) *reinterpret_cast<bf16*>(ldsV + vt_off(dg + e, key)) = v[e];
+      for (int i = 0; i < 16 / kWaves; ++i) {
+        const int r = (i * kWaves + wave) * 8 + srow;
+        const int key = min(kc + r, Skv - 1);
+        glds16(Vb + (size_t)key * ldv + vswz(r, spos) * 8, ldsV + (i * kWaves + wave) * 8 * kVRowB);
+      }
     }
     wait_vmcnt0();
     __syncthreads();
 
-    // ---- S^T = K·Q^T : s[kt][qt] holds keys kt*16 + fg*4 + r, query fr ----
-    f32x4 s[8][2];
+    // ---- S^T = K·Q^T : s[kt] holds keys kt*16 + fg*4 + r, query fr ----
+    f32x4 s[8];
 #pragma unroll
     for (int kt = 0; kt < 8; ++kt) {
-      s[kt][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-      s[kt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ds = 0; ds < 2; ++ds) {
         const int r = kt * 16 + fr;
         const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ldsK + r * kKRowB + kswz(r, ds * 4 + fg) * 16);
-        s[kt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][ds], s[kt][0], 0, 0, 0);
-        s[kt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][ds], s[kt][1], 0, 0, 0);
+        s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ds], s[kt], 0, 0, 0);
       }
     }
 
     // ---- scale, bias, mask, online softmax (per query column) ----
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const int q = qw + qt * 16 + fr;
+    {
+      const int q = qw + fr;
       const int qc = min(q, Sq - 1);
       float cmax = -1e30f;
 #pragma unroll
       for (int kt = 0; kt < 8; ++kt) {
         const int key0 = kc + kt * 16 + fg * 4;
         f32x4 bv = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (bias && key0 < Skv) {
+        if constexpr (HAS_BIAS) {
           // Skv % 4 == 0 is enforced on the host for the bias path
-          bv = *reinterpret_cast<const f32x4*>(bias + ((size_t)h * Sq + qc) * Skv + key0);
+          if (key0 < Skv) bv = *reinterpret_cast<const f32x4*>(bias + ((size_t)h * Sq + qc) * Skv + key0);
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = key0 + r;
-          float x = s[kt][qt][r] * scale + bv[r];
-          const bool dead = key >= len || (causal && key > q);
+          float x = s[kt][r] * scale + bv[r];
+          const bool dead = key >= len || (CAUSAL && key > q);
           x = dead ? -1e30f : x;
-          s[kt][qt][r] = x;
+          s[kt][r] = x;
           cmax = fmaxf(cmax, x);
         }
       }
       cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
       cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
-      const float m_new = fmaxf(m_run[qt], cmax);
-      const float alpha = __expf(m_run[qt] - m_new);
+      const float m_new = fmaxf(m_run, cmax);
+      const float alpha = __expf(m_run - m_new);
       float psum = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float x = s[kt][qt][r];
+          const float x = s[kt][r];
           const float p = x <= -1e29f ? 0.f : __expf(x - m_new);
-          s[kt][qt][r] = p;
+          s[kt][r] = p;
           psum += p;
         }
       psum += __shfl_xor(psum, 16, 64);
       psum += __shfl_xor(psum, 32, 64);
-      l_run[qt] = l_run[qt] * alpha + psum;
-      m_run[qt] = m_new;
+      l_run = l_run * alpha + psum;
+      m_run = m_new;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[dt][qt] *= alpha;
+      for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
     }
 
     // ---- O^T += V^T · P^T over 4 key-steps of 32 ----
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      bf16x8 pf[2];
+      bf16x8 pf;
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          pf[qt][e] = f2bf(s[2 * ks][qt][e]);
-          pf[qt][4 + e] = f2bf(s[2 * ks + 1][qt][e]);
-        }
+      for (int e = 0; e < 4; ++e) {
+        pf[e] = f2bf(s[2 * ks][e]);
+        pf[4 + e] = f2bf(s[2 * ks + 1][e]);
+      }
+      const int tq = fr >> 2, tp = fr & 3;  // transposed-read lane roles
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const int d = dt * 16 + fr;
-        const bf16x4 lo = *reinterpret_cast<const bf16x4*>(ldsV + vt_off(d, ks * 32 + fg * 4));
-        const bf16x4 hi = *reinterpret_cast<const bf16x4*>(ldsV + vt_off(d, ks * 32 + 16 + fg * 4));
+        const int klo = ks * 32 + fg * 4 + tq, khi = klo + 16;
+        const int c = dt * 2 + (tp >> 1);
+        const bf16x4 lo = lds_read_tr16(ldsV + klo * kVRowB + vswz(klo, c) * 16 + (tp & 1) * 8);
+        const bf16x4 hi = lds_read_tr16(ldsV + khi * kVRowB + vswz(khi, c) * 16 + (tp & 1) * 8);
         bf16x8 vf;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           vf[e] = lo[e];
           vf[4 + e] = hi[e];
         }
-        o[dt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[0], o[dt][0], 0, 0, 0);
-        o[dt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[1], o[dt][1], 0, 0, 0);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[dt], 0, 0, 0);
       }
     }
   }
 
   // ---- normalise and store: lane holds O[q][dt*16 + fg*4 + 0..3] ----
+  {
+    const int q = qw + fr;
+    if (q < Sq) {
+      const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+      bf16* orow = O + ((size_t)b * Sq + q) * ldo + h * kD;
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int q = qw + qt * 16 + fr;
-    if (q >= Sq) continue;
-    const float inv = l_run[qt] > 0.f ? 1.f / l_run[qt] : 0.f;
-    bf16* orow = O + ((size_t)b * Sq + q) * ldo + h * kD;
+      for (int dt = 0; dt < 4; ++dt) {
+        bf16x4 v;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      bf16x4 v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = f2bf(o[dt][qt][e] * inv);
-      *reinterpret_cast<bf16x4*>(orow + dt * 16 + fg * 4) = v;
+        for (int e = 0; e < 4; ++e) v[e] = f2bf(o[dt][e] * inv);
+        *reinterpret_cast<bf16x4*>(orow + dt * 16 + fg * 4) = v;
+      }
     }
   }
 }
@@ -220,8 +224,18 @@ void attention_fwd_strided(const bf16* q, int ldq, const bf16* k, int ldk, const
   ATPU_CHECK(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0, "attention: row strides must be 16-B");
   ATPU_CHECK(!bias || Skv % 4 == 0, "attention: bias path needs Skv % 4 == 0");
   const dim3 grid((Sq + kQB - 1) / kQB, H, B);
-  hipLaunchKernelGGL(attention_fwd_kernel, grid, dim3(256), 0, stream, q, ldq, k, ldk, v, ldv, out, ldo, lens, bias,
-                     Sq, Skv, H, scale, causal);
+#define ATPU_ATTN(HB, CA)                                                                                   \
+  hipLaunchKernelGGL((attention_fwd_kernel<HB, CA>), grid, dim3(kThreads), 0, stream, q, ldq, k, ldk, v, ldv, out, \
+                     ldo, lens, bias, Sq, Skv, H, scale)
+  if (bias && causal)
+    ATPU_ATTN(true, true);
+  else if (bias)
+    ATPU_ATTN(true, false);
+  else if (causal)
+    ATPU_ATTN(false, true);
+  else
+    ATPU_ATTN(false, false);
+#undef ATPU_ATTN
   ATPU_HIP_CHECK(hipGetLastError());
 }
 
