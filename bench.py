@@ -30,8 +30,9 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = "classified rows/sec (whole node) map_classify BERT-base at 1/2/4/8 MI355X"
-# reference-compute proxy, BERT-base S=128 batch 32 = 35.2 rows/s
-BASELINE_ROWS_PER_SEC = 35.2
+# BASELINE.md / SURVEY.md §6 reference-compute proxies at S=128, batch 32:
+# B9 BERT-base 35.2 rows/s, B10 BERT-large 8.2 rows/s
+BASELINE_ROWS_PER_SEC = {"bert-base": 35.2, "bert-large": 8.2}
 
 
 def parse():
@@ -122,7 +123,7 @@ def main() -> int:
         cls_only = eng.model.cls_only_last
         flops = cfg.flops_per_row_executed(a.seq_len, cls_only) * total_rows / elapsed
         out = {
-            "metric": METRIC,
+            "metric": METRIC if a.model == "bert-base" else METRIC.replace("BERT-base", a.model),
             "value": round(value, 2),
             "unit": "rows/s",
             "n_gpus": world,
@@ -131,7 +132,8 @@ def main() -> int:
             "ms_per_step": round(elapsed * 1000.0 / a.steps, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / BASELINE_ROWS_PER_SEC, 2),
+            "vs_baseline": (round(value / BASELINE_ROWS_PER_SEC[a.model], 2)
+                            if a.model in BASELINE_ROWS_PER_SEC else None),
             "dtype": "bf16",
             "data": "synthetic CSV rows (random words), random-init weights",
             "config": {
