@@ -209,6 +209,7 @@ PYBIND11_MODULE(_atpu, m) {
                                for (const auto& s : t.header()) h.append(decode(s));
                                return h;
                              })
+      .def_property_readonly("index_from_cache", &CsvTable::index_from_cache)
       .def("column_index", &CsvTable::column_index)
       .def("row",
            [](const CsvTable& t, size_t i) {

@@ -27,21 +27,23 @@ class CsvTable {
   int64_t mtime_ns() const { return mtime_ns_; }
   // number of non-blank data records after the header
   size_t num_rows() const { return starts_.size(); }
+  // true when the row index came from the on-disk cache (ATPU_CSV_INDEX_DIR)
+  bool index_from_cache() const { return index_from_cache_; }
   const std::vector<std::string>& header() const { return header_; }
   int column_index(const std::string& name) const;
 
   // Parse data record `row` into its fields.
   void parse_row(size_t row, std::vector<std::string>& fields) const;
 
-  // Pack field `col` of rows [start, start+n) into `out` (capacity `cap`
-  // bytes) with int32 offsets[n+1]; each value truncated to `max_bytes`.
-  // Work is split over `threads` host threads. Returns bytes written, or -1
-  // if `cap` is too small.
   // Parse field `col` of rows [start, start+n) as doubles (Python float()
   // syntax minus '_' separators; surrounding whitespace ignored). Throws
   // std::invalid_argument naming the first bad value.
   void extract_doubles(size_t start, size_t n, int col, double* out, int threads) const;
 
+  // Pack field `col` of rows [start, start+n) into `out` (capacity `cap`
+  // bytes) with int32 offsets[n+1]; each value truncated to `max_bytes`.
+  // Work is split over `threads` host threads. Returns bytes written, or -1
+  // if `cap` is too small.
   int64_t extract_column(size_t start, size_t n, int col, uint8_t* out, size_t cap,
                          int32_t* offsets, size_t max_bytes, int threads) const;
 
@@ -52,6 +54,11 @@ class CsvTable {
   // Extract only field `col` of the record starting at `pos` into `out`.
   void parse_field(size_t pos, int col, std::string& out, size_t max_bytes) const;
   void build_index();
+  // persisted row index: <ATPU_CSV_INDEX_DIR>/<hash>.rowidx,
+  // valid for the same (path, size, mtime)
+  bool load_index_cache(const std::string& file);
+  void save_index_cache(const std::string& file) const;
+  bool index_from_cache_ = false;
 
   std::string path_;
   const char* data_ = nullptr;

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cctype>
+#include <cstdio>
 #include <cstdlib>
 #include <cerrno>
 #include <cstring>
@@ -47,7 +48,19 @@ CsvTable::CsvTable(const std::string& path) : path_(path) {
     ::madvise(p, size_, MADV_SEQUENTIAL);
     data_ = static_cast<const char*>(p);
   }
-  build_index();
+  const char* dir = std::getenv("ATPU_CSV_INDEX_DIR");
+  std::string cache;
+  if (dir && *dir) {
+    uint64_t h = 1469598103934665603ULL;  // FNV-1a of the path
+    for (unsigned char c : path_) h = (h ^ c) * 1099511628211ULL;
+    char name[40];
+    std::snprintf(name, sizeof(name), "/%016llx.rowidx", static_cast<unsigned long long>(h));
+    cache = std::string(dir) + name;
+  }
+  if (cache.empty() || !load_index_cache(cache)) {
+    build_index();
+    if (!cache.empty()) save_index_cache(cache);
+  }
   if (data_) ::madvise(const_cast<char*>(data_), size_, MADV_RANDOM);
 }
 
@@ -138,6 +151,56 @@ void CsvTable::parse_field(size_t pos, int col, std::string& out, size_t max_byt
         break;
     }
   }
+}
+
+namespace {
+constexpr char kIdxMagic[8] = {'A', 'T', 'P', 'U', 'I', 'D', 'X', '1'};
+}
+
+bool CsvTable::load_index_cache(const std::string& file) {
+  FILE* f = std::fopen(file.c_str(), "rb");
+  if (!f) return false;
+  char magic[8];
+  uint64_t size = 0, plen = 0, n = 0;
+  int64_t mtime = 0;
+  bool ok = std::fread(magic, 1, 8, f) == 8 && std::memcmp(magic, kIdxMagic, 8) == 0 &&
+            std::fread(&size, 8, 1, f) == 1 && std::fread(&mtime, 8, 1, f) == 1 && std::fread(&plen, 8, 1, f) == 1 &&
+            size == size_ && mtime == mtime_ns_ && plen == path_.size() && plen < (1u << 20);
+  if (ok) {
+    std::string p(plen, '\0');
+    ok = std::fread(&p[0], 1, plen, f) == plen && p == path_ && std::fread(&n, 8, 1, f) == 1 && n <= size_;
+    if (ok) {
+      starts_.resize(n);
+      ok = n == 0 || std::fread(starts_.data(), 8, n, f) == n;
+      for (size_t i = 0; ok && i < n; ++i) ok = starts_[i] < size_ && (i == 0 || starts_[i] > starts_[i - 1]);
+    }
+  }
+  std::fclose(f);
+  if (!ok) {
+    starts_.clear();
+    return false;
+  }
+  header_.clear();
+  if (size_ > 0) parse_record(0, &header_);
+  index_from_cache_ = true;
+  return true;
+}
+
+void CsvTable::save_index_cache(const std::string& file) const {
+  const std::string tmp = file + ".tmp" + std::to_string(::getpid());
+  FILE* f = std::fopen(tmp.c_str(), "wb");
+  if (!f) return;  // best effort: an unwritable cache dir only costs the rebuild
+  const uint64_t size = size_, plen = path_.size(), n = starts_.size();
+  const int64_t mtime = mtime_ns_;
+  bool ok = std::fwrite(kIdxMagic, 1, 8, f) == 8 && std::fwrite(&size, 8, 1, f) == 1 &&
+            std::fwrite(&mtime, 8, 1, f) == 1 && std::fwrite(&plen, 8, 1, f) == 1 &&
+            std::fwrite(path_.data(), 1, plen, f) == plen && std::fwrite(&n, 8, 1, f) == 1 &&
+            (n == 0 || std::fwrite(starts_.data(), 8, n, f) == n);
+  ok = (std::fclose(f) == 0) && ok;
+  if (ok)
+    std::rename(tmp.c_str(), file.c_str());
+  else
+    std::remove(tmp.c_str());
 }
 
 void CsvTable::build_index() {

@@ -119,6 +119,21 @@ def lru_capacity() -> int:
     return max(1, int(os.getenv("MODEL_LRU_SIZE", "4")))
 
 
+def lru_budget_bytes(device) -> int:
+    """HBM budget for resident models: ``MODEL_LRU_GB`` or
+    25 % of the device's memory. Eviction is LRU and deterministic, so every DP
+    rank (same request sequence, same configs) evicts the same models."""
+    gb = os.getenv("MODEL_LRU_GB", "").strip()
+    if gb:
+        return int(float(gb) * 2**30)
+    try:
+        import torch
+
+        return int(torch.cuda.get_device_properties(device).total_memory * 0.25)
+    except Exception:
+        return 64 * 2**30
+
+
 def device_for_rank():
     import torch
 
@@ -139,11 +154,22 @@ def get_gpu_handle(model_path: str, device=None) -> GpuHandle:
             return h
         h = GpuHandle(parse_spec(model_path), device)
         _cache[key] = h
-        while len(_cache) > lru_capacity():
+        budget = lru_budget_bytes(device)
+        evicted = False
+        while len(_cache) > 1 and (len(_cache) > lru_capacity() or _resident_bytes() > budget):
             _cache.popitem(last=False)
+            evicted = True
+        if evicted:
+            import torch
+
+            torch.cuda.empty_cache()  # hand the evicted packs/graph pools back to the device
         return h
+
+
+def _resident_bytes() -> int:
+    return sum(h.engine.memory_bytes() for h in _cache.values())
 
 
 def cache_info() -> Dict[str, Any]:
     with _lock:
-        return {"entries": [k[0] for k in _cache], "capacity": lru_capacity()}
+        return {"entries": [k[0] for k in _cache], "capacity": lru_capacity(), "resident_bytes": _resident_bytes()}

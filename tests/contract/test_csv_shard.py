@@ -100,3 +100,30 @@ def test_native_column_extract_and_floats(tmp_path, nat):
     assert list(vals) == [float(r["risk"]) for r in ref]
     with pytest.raises(ValueError, match="could not convert string to float"):
         t.float_column(0, 5, t.column_index("text"), 1)
+
+
+def test_persisted_row_index(tmp_path, monkeypatch):
+    """ATPU_CSV_INDEX_DIR persists the row index; a changed file invalidates it."""
+    import os
+    import subprocess
+    import sys
+
+    from agent_tpu_amd.utils.synthetic import write_csv
+
+    path = str(tmp_path / "big.csv")
+    write_csv(path, 2000, 20)
+    idx_dir = tmp_path / "idx"
+    idx_dir.mkdir()
+    code = ("import sys; sys.path.insert(0, %r); import torch; from agent_tpu_amd._native import native; "
+            "t = native().CsvTable(%r); print(t.index_from_cache, t.num_rows, t.row(1234)[0])") % (
+        os.getcwd(), path)
+    env = dict(os.environ, ATPU_CSV_INDEX_DIR=str(idx_dir))
+    run = lambda: subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,  # noqa: E731
+                                 timeout=120).stdout.split()
+    first, second = run(), run()
+    assert first[0] == "False" and second[0] == "True" and first[1:] == second[1:] == ["2000", "1234"]
+    assert len(list(idx_dir.iterdir())) == 1
+    with open(path, "a") as f:
+        f.write("2000,new row,0.5\n")
+    third = run()
+    assert third[0] == "False" and third[1] == "2001"

@@ -24,6 +24,8 @@ def test_host_code_is_sanitizer_clean(tmp_path):
            "-fsanitize=address,undefined", "-lpthread", "-o", exe]
     b = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert b.returncode == 0, b.stderr[-4000:]
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1")
+    (tmp_path / "idx").mkdir()
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1",
+               ATPU_CSV_INDEX_DIR=str(tmp_path / "idx"))
     r = subprocess.run([exe], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0 and "clean" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])

@@ -64,3 +64,21 @@ def test_risk_gpu_path_matches_cpu(gpu, monkeypatch):
     assert got["device"] == "gpu" and got["count"] == ref["count"]
     assert got["min"] == ref["min"] and got["max"] == ref["max"]
     assert abs(got["sum"] - ref["sum"]) <= 1e-9 * max(1.0, abs(ref["sum"]))
+
+
+def test_model_lru_hbm_budget(gpu, monkeypatch):
+    import ops._gpu_runtime as rt
+
+    monkeypatch.setenv("MODEL_LRU_SIZE", "8")
+    with rt._lock:
+        rt._cache.clear()
+    one = rt.get_gpu_handle("bert-tiny?seed=1&batch=32")
+    per = rt.cache_info()["resident_bytes"]
+    monkeypatch.setenv("MODEL_LRU_GB", str(2.5 * per / 2**30))  # room for two
+    rt.get_gpu_handle("bert-tiny?seed=2&batch=32")
+    assert rt.cache_info()["entries"] == ["bert-tiny?seed=1&batch=32", "bert-tiny?seed=2&batch=32"]
+    assert rt.get_gpu_handle("bert-tiny?seed=1&batch=32") is one  # hit refreshes recency
+    rt.get_gpu_handle("bert-tiny?seed=3&batch=32")  # evicts seed=2 (least recent)
+    assert rt.cache_info()["entries"] == ["bert-tiny?seed=1&batch=32", "bert-tiny?seed=3&batch=32"]
+    with rt._lock:
+        rt._cache.clear()

@@ -79,6 +79,7 @@ int main() {
   for (const auto& body : fixed) {
     const std::string p = write_tmp(body, idx++);
     exercise(p);
+    exercise(p);  // second open reads the persisted row index when ATPU_CSV_INDEX_DIR is set
     std::remove(p.c_str());
   }
   for (int it = 0; it < 300; ++it) {
