@@ -47,6 +47,8 @@ def init_from_env() -> None:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
+        if torch.cuda.is_available():  # gloo rehearsal: ranks may share a GPU
+            torch.cuda.set_device(local % torch.cuda.device_count())
         dist.init_process_group("gloo")
 
 
@@ -72,7 +74,16 @@ def maybe_inject_fault(stage: str) -> None:
     raise RuntimeError(f"injected fault ({spec}) at {stage}")
 
 
+_ERR_TYPES = {"ValueError": ValueError, "TypeError": TypeError, "KeyError": KeyError}
+
+
 def _check_errors(err: str) -> None:
+    """Exchange per-rank errors (``"Type: message"``) so every rank fails together.
+
+    If EVERY rank failed with the same input-validation error (a bad payload is
+    bad everywhere) it is re-raised with its own type and message, keeping the
+    single-process op's contract; otherwise a RuntimeError names each rank.
+    """
     if not is_dist():
         if err:
             raise RuntimeError(err)
@@ -81,8 +92,13 @@ def _check_errors(err: str) -> None:
     errs = [None] * ws
     dist.all_gather_object(errs, err)
     bad = [(r, e) for r, e in enumerate(errs) if e]
-    if bad:
-        raise RuntimeError("; ".join(f"rank {r}: {e}" for r, e in bad))
+    if not bad:
+        return
+    if len(bad) == ws and len(set(e for _, e in bad)) == 1:
+        typ, _, msg = bad[0][1].partition(": ")
+        if typ in _ERR_TYPES:
+            raise _ERR_TYPES[typ](msg)
+    raise RuntimeError("; ".join(f"rank {r}: {e}" for r, e in bad))
 
 
 def run_collective(name: str, payload: Dict[str, Any]) -> Any:

@@ -139,7 +139,8 @@ def device_for_rank():
 
     if not torch.cuda.is_available():
         raise RuntimeError("No ROCm GPU available (torch.cuda.is_available() is False)")
-    local = int(os.getenv("LOCAL_RANK", "0"))
+    # modulo: ranks may share a device in single-GPU rehearsals (gloo backend)
+    local = int(os.getenv("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     return torch.device("cuda", local)
 

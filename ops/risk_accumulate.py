@@ -3,8 +3,11 @@
 Parity with ``/root/reference/ops/risk_accumulate.py:10-77`` (same output keys,
 same raised ``ValueError`` messages, float64 accumulation, ``bool`` accepted as
 numeric). Large ``values`` lists go through the GPU reduction kernel (K12) when
-a device is present (``RISK_DEVICE=auto|gpu|cpu``); the DP-over-8-GPU variant
-with an RCCL all-reduce lives in :mod:`agent_tpu_amd.parallel.risk`.
+a device is present (``RISK_DEVICE=auto|gpu|cpu``). ``source_uri`` + ``field``
+reduces a CSV column (native column parse). Under ``torchrun`` (DP world > 1)
+the op runs on every GPU of the node: each rank reduces its shard and the
+partials are combined with RCCL all-reduces
+(:func:`agent_tpu_amd.parallel.dp_ops.risk_task`).
 
 Sums are taken with ``math.fsum``-free sequential float64 addition on the CPU
 path so that results are bit-identical to the reference's ``sum()``; the GPU
@@ -81,10 +84,40 @@ def _gpu_available() -> bool:
         return False
 
 
+def _dp_world() -> int:
+    try:
+        from agent_tpu_amd.parallel.dp import world
+
+        return world()[1]
+    except Exception:
+        return 1
+
+
 @register_op("risk_accumulate")
 def risk_accumulate(payload: Dict[str, Any]) -> Dict[str, Any]:
     t0 = time.time()
     payload = payload if payload is not None else {}
+    if _dp_world() > 1:
+        # node-wide DP reduce (BASELINE config 5): every rank reduces its shard
+        # with K12, then two RCCL all-reduces (SUM {count,sum}, MAX {max,-min})
+        from agent_tpu_amd.parallel.dp_ops import dispatch
+
+        return dispatch("risk_accumulate", payload)
+    if "source_uri" in payload:
+        from agent_tpu_amd.ops.reduce import reduce_stats_tensor, stats_dict
+        from agent_tpu_amd.parallel.dp_ops import _local_values
+
+        x, _ = _local_values(payload, 0, 1)
+        if _use_gpu(x.numel()):
+            import torch
+
+            x = x.to(torch.device("cuda", torch.cuda.current_device()))
+        stats = stats_dict(reduce_stats_tensor(x.contiguous()).tolist()) if x.numel() else \
+            {"count": 0, "sum": 0.0, "mean": 0.0, "min": None, "max": None}
+        if x.is_cuda:
+            stats["device"] = "gpu"
+        stats["compute_time_ms"] = (time.time() - t0) * 1000.0
+        return stats
     values = _gather(payload)
     if not values:
         return {"count": 0, "sum": 0.0, "mean": 0.0, "min": None, "max": None,

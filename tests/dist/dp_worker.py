@@ -77,8 +77,8 @@ def scen_risk():
     try:
         dp_ops.dispatch("risk_accumulate", {"values": "nope"})
         out["bad"] = None
-    except RuntimeError as exc:
-        out["bad"] = str(exc)
+    except Exception as exc:
+        out["bad"] = f"{type(exc).__name__}: {exc}"
     out["empty"] = dp_ops.dispatch("risk_accumulate", {"values": []})
     dp_ops.shutdown_workers()
     return out

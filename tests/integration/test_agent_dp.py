@@ -1,0 +1,74 @@
+"""The agent's data-parallel process model end to end (CPU, gloo, 2 ranks):
+``torchrun --nproc-per-node 2 app.py`` — rank 0 leases from the mock
+controller and dispatches, rank 1 serves in ``dp_ops.worker_loop`` — for the
+node-wide risk reduce (BASELINE config 5's collective path), with clean
+SIGTERM shutdown of both ranks."""
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+
+import psutil
+import pytest
+
+from .mock_controller import MockController
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture
+def ctl():
+    c = MockController().start()
+    yield c
+    c.stop()
+
+
+def test_dp_agent_risk_reduce_and_shutdown(ctl, tmp_path):
+    csv = tmp_path / "risk.csv"
+    csv.write_text("id,risk\n" + "".join(f"{i},{(i * 13 % 97) / 4.0}\n" for i in range(500)))
+    vals = [1.0, 2.5, "3", True, -7.25]
+    ctl.lease({"id": "v", "op": "risk_accumulate", "payload": {"values": vals}})
+    ctl.lease({"id": "c", "op": "risk_accumulate", "payload": {"source_uri": str(csv), "field": "risk",
+                                                               "start_row": 10, "shard_size": 300}})
+    ctl.lease({"id": "bad", "op": "risk_accumulate", "payload": {"values": "nope"}})
+    ctl.lease({"id": "e", "op": "echo", "payload": {"k": 1}})
+    ctl.lease({"id": "after", "op": "risk_accumulate", "payload": {"values": [4.0, 6.0]}})
+    env = dict(os.environ, CONTROLLER_URL=ctl.url, TASKS="echo,risk_accumulate", IDLE_SLEEP_SEC="0.02",
+               ERROR_LOG_EVERY_SEC="0", ATPU_DP_BACKEND="gloo", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="",
+               GPU_DISABLED="1", OMP_NUM_THREADS="1", PYTHONUNBUFFERED="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", "app.py"]
+    p = subprocess.Popen(cmd, cwd=REPO, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    try:
+        assert ctl.wait(lambda c: "after" in {r["job_id"] for r in c.results}, 180), ctl.results
+    finally:
+        ranks = psutil.Process(p.pid).children(recursive=True)
+        for r in ranks:  # the exact rank PIDs of this launcher
+            try:
+                r.send_signal(signal.SIGTERM)
+            except psutil.NoSuchProcess:
+                pass
+        out, _ = p.communicate(timeout=120)
+    res = {r["job_id"]: r for r in ctl.results}
+    v = res["v"]["result"]
+    assert res["v"]["status"] == "succeeded" and v["dp_world_size"] == 2
+    assert v["count"] == 5 and v["sum"] == sum([1.0, 2.5, 3.0, 1.0, -7.25]) and v["min"] == -7.25 and v["max"] == 3.0
+    c = res["c"]["result"]
+    ref = [(i * 13 % 97) / 4.0 for i in range(10, 310)]
+    assert c["count"] == 300 and abs(c["sum"] - sum(ref)) < 1e-9 and c["min"] == min(ref) and c["max"] == max(ref)
+    assert res["bad"]["status"] == "failed" and res["bad"]["error"]["type"] == "ValueError"
+    assert res["bad"]["error"]["message"] == "payload.values must be a list"
+    assert res["e"]["result"] == {"ok": True, "echo": {"k": 1}}
+    assert res["after"]["result"]["sum"] == 10.0  # the DP group survived the failed job
+    assert p.returncode == 0, out[-3000:]
+    assert "dp worker rank=1 ready" in out and "stopped" in out
