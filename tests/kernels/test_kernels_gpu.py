@@ -209,3 +209,19 @@ def test_reduce_stats(gpu, n):
     assert out[2].item() == x.min().item() and out[3].item() == x.max().item()
     out32 = ops.reduce_stats_tensor(x.float().to(gpu)).cpu()
     assert math.isclose(out32[1].item(), x.float().double().sum().item(), rel_tol=1e-10, abs_tol=1e-6)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("off,n", [(0, 1), (1, 5), (3, 1000), (1, 4099), (2, 1 << 20), (0, (1 << 21) + 3)])
+def test_reduce_stats_vector_paths(gpu, dtype, off, n):
+    """16-B vector body + misaligned head + tail of the K12 kernel vs fp64 torch."""
+    from agent_tpu_amd.ops.reduce import reduce_stats_tensor
+
+    g = torch.Generator().manual_seed(n)
+    base = (torch.rand(off + n, generator=g, dtype=torch.float64) * 200 - 100).to(dtype)
+    x = base.to(gpu)[off:]
+    got = reduce_stats_tensor(x).cpu().tolist()
+    ref = base[off:].double()
+    assert got[0] == n
+    assert abs(got[1] - float(ref.sum())) <= 1e-9 * max(1.0, float(ref.abs().sum()))
+    assert got[2] == float(ref.min()) and got[3] == float(ref.max())

@@ -1,7 +1,9 @@
 set -o pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out
-timeout -k 10 300 python -m pytest tests/kernels/test_rccl_gpu.py -x -q > gpurun_out/pytest_rccl.log 2>&1 || { tail -40 gpurun_out/pytest_rccl.log; exit 1; }
-tail -2 gpurun_out/pytest_rccl.log
-timeout -k 10 300 python bench.py --model bert-large --steps 10 --warmup 2 > gpurun_out/bench_large.log 2>&1 || { tail -30 gpurun_out/bench_large.log; exit 1; }
-tail -1 gpurun_out/bench_large.log | cut -c1-700
+timeout -k 10 300 python -m pytest tests/kernels/test_kernels_gpu.py -x -q -k "reduce" > gpurun_out/pytest_red.log 2>&1 || { tail -40 gpurun_out/pytest_red.log; exit 1; }
+tail -2 gpurun_out/pytest_red.log
+timeout -k 10 300 python bench/risk_scaling.py > gpurun_out/risk.log 2>&1 || { tail -30 gpurun_out/risk.log; exit 1; }
+tail -1 gpurun_out/risk.log | cut -c1-500
+timeout -k 10 300 python bench/risk_scaling.py --dtype f32 > gpurun_out/risk32.log 2>&1 || { tail -30 gpurun_out/risk32.log; exit 1; }
+tail -1 gpurun_out/risk32.log | cut -c1-500
