@@ -117,7 +117,11 @@ def _select(logits: torch.Tensor, run_scores: torch.Tensor, K2: int, cfg, gen: G
     scores_dev = run_scores.view(-1).to(logits.device)
     if K2 + nban <= 16:
         sc, tk = ops.beam_topk_rows(logits, scores_dev, K2 + nban, cfg.eos_id, mask_eos)
-        sc, tk = sc.cpu(), tk.cpu().long()
+        if sc.is_cuda:  # one D2H copy (one sync) for scores and token ids
+            both = torch.cat([sc, tk.view(torch.float32)], 1).cpu()
+            sc, tk = both[:, :K2 + nban].contiguous(), both[:, K2 + nban:].contiguous().view(torch.int32).long()
+        else:
+            sc, tk = sc.cpu(), tk.cpu().long()
         if nban:
             key = br * V + bt
             flat = torch.arange(rows).view(-1, 1) * V + tk
@@ -177,19 +181,24 @@ def generate(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfi
     use_graph = gen.use_graph and dev.type == "cuda"
     graph, g_logits = None, None
 
-    cur = 1  # sequence length so far (decoder start token included)
-    steps = 0
-    while cur < T:
-        step_dev.fill_(cur - 1)
+    def launch(length: int) -> torch.Tensor:
+        """Enqueue the decoder step for sequence length ``length`` -> logits."""
+        nonlocal graph, g_logits
+        step_dev.fill_(length - 1)
         if graph is not None:
             graph.replay()
-            logits = g_logits
-        else:
-            logits = model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist)
-            if use_graph:
-                graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(graph):
-                    g_logits = model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist)
+            return g_logits
+        out = model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist)
+        if use_graph:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                g_logits = model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist)
+        return out
+
+    cur = 1  # sequence length so far (decoder start token included)
+    steps = 0
+    logits = launch(cur)
+    while True:
         with span("beam_select"):
             sc, tk = _select(logits, run_scores, K2, cfg, gen, cur, T, run_seq)
         sc, tk = sc.view(B, nb * K2), tk.view(B, nb * K2)
@@ -211,9 +220,20 @@ def generate(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfi
         # running beams for the next step: best nb non-hit continuations
         run_cand = top_sc + hits.float() * NEG
         nxt = torch.topk(run_cand, nb, dim=1).indices
-        new_run_seq = torch.gather(cand_seq, 1, nxt.unsqueeze(-1).expand(-1, -1, T))
-        new_run_scores = torch.gather(run_cand, 1, nxt)
+        run_seq = torch.gather(cand_seq, 1, nxt.unsqueeze(-1).expand(-1, -1, T))
+        run_scores = torch.gather(run_cand, 1, nxt)
         parent = torch.gather(top_beam, 1, nxt)  # beam index within the item
+
+        if cur + 1 < T:
+            # enqueue step cur+1 NOW: histories follow their parent beams
+            # (backpointers, no KV copy), new tokens, decoder-step graph. The
+            # finished-hypothesis bookkeeping below runs on the host while the
+            # GPU computes it (a step launched past an early stop is dropped).
+            par_rows = (torch.arange(B).view(-1, 1) * nb + parent).view(-1).to(torch.int32).to(dev)
+            ops.beam_reorder_hist(hist, hist_alt, par_rows, step_dev)
+            hist.copy_(hist_alt)  # keep the captured buffer address
+            tokens.copy_(run_seq[:, :, cur].reshape(-1).to(torch.int32))
+            logits = launch(cur + 1)
 
         # finished hypotheses: hits among the top nb candidates
         did = hits & top_mask.view(1, -1)
@@ -230,13 +250,9 @@ def generate(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfi
         fin_done = torch.gather(m_done, 1, keep)
         fin_len = torch.gather(m_len, 1, keep)
 
-        run_seq, run_scores = new_run_seq, new_run_scores
-        # histories follow their parent beams (backpointers, no KV copy)
-        par_rows = (torch.arange(B).view(-1, 1) * nb + parent).view(-1).to(torch.int32).to(dev)
-        ops.beam_reorder_hist(hist, hist_alt, par_rows, step_dev)
-        hist.copy_(hist_alt)  # keep the captured buffer address
-        tokens.copy_(run_seq[:, :, cur].reshape(-1).to(torch.int32))
         cur += 1
+        if cur >= T:
+            break
         # early-stop heuristic (early_stopping=True: best running at current length)
         best_run = run_scores[:, :1] / float(cur - 1) ** lp
         worst_fin = torch.where(fin_done, fin_scores.min(dim=1, keepdim=True).values, torch.full_like(fin_scores, NEG))
