@@ -10,8 +10,9 @@ with that rank's id in the message instead of hanging the others in a
 collective. ``MI355X_FAULT=rank:K[:stage[:times]]`` injects a
 failure on rank K for tests.
 
-Registered bodies: ``map_classify_csv`` (C2 all-gather of top-k) and
-``risk_accumulate`` (C3 all-reduce of {count,sum,min,max}).
+Registered bodies: ``map_classify_csv`` (C2 all-gather of top-k),
+``risk_accumulate`` (C3 all-reduce of {count,sum,min,max}) and
+``map_summarize`` (C5 all-gather of generated token ids).
 """
 from __future__ import annotations
 
@@ -236,3 +237,45 @@ def risk_task(payload: Dict[str, Any]) -> Any:
     out["compute_time_ms"] = (time.perf_counter() - t0) * 1000.0
     out["dp_world_size"] = ws
     return out
+
+
+# ------------------------------------------------------------ map_summarize
+@dp_task("map_summarize")
+def summarize_task(payload: Dict[str, Any]) -> Any:
+    """Each rank beam-searches its contiguous shard of the documents; the
+    int32 token ids ``[docs_r, max_length]`` (-1 padded) are all-gathered to
+    rank 0 (C5), which detokenizes. Reference: ``ops/map_summarize.py:46-68``
+    (one document per call, CPU)."""
+    import ops.map_summarize as ms
+
+    rank, ws = world()
+    timing: Dict[str, float] = {}
+    with span("load_ms", timing):
+        eng = ms._init_engine()  # first call: C1 broadcast of the weights
+    texts = payload["texts"]
+    gen = ms._gen_config(payload)
+    err, steps = "", 0
+    seqs = torch.full((0, gen.max_length), -1, dtype=torch.int32)
+    try:
+        s_r, n_r = split_range(0, len(texts), ws, rank)
+        maybe_inject_fault("summarize")
+        if n_r:
+            with span("generate_ms", timing):
+                res = eng.generate_ids(texts[s_r:s_r + n_r], gen)
+            steps = res.steps
+            seqs = torch.full((n_r, gen.max_length), -1, dtype=torch.int32)
+            for i, sq in enumerate(res.sequences):
+                seqs[i, :len(sq)] = torch.tensor(sq[:gen.max_length], dtype=torch.int32)
+    except Exception as exc:
+        err = f"{type(exc).__name__}: {exc}"
+        if os.getenv("ATPU_DEBUG"):
+            traceback.print_exc()
+    _check_errors(err)
+    with span("allgather_ms", timing):
+        (seqs,) = all_gather_rows(seqs)
+    if rank != 0:
+        return None
+    rows = [[int(t) for t in r if t >= 0] for r in seqs.cpu().tolist()]
+    summaries = eng.detokenize_all(texts, rows)
+    return ms.result(bool(payload.get("texts_mode", True)), summaries, steps, timing,
+                     float(payload.get("t0", time.time())), dp_world_size=ws)

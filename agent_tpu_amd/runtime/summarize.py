@@ -269,13 +269,24 @@ def generate(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfi
     return GenResult(seqs, scores, steps, {"encode_ms": (t_enc - t0) * 1e3, "decode_ms": (t_dec - t_enc) * 1e3})
 
 
-def build_model(name: str, pack=None, device: Optional[torch.device] = None, seed: int = 0, fp32: bool = False):
-    """``t5-*`` / ``bart-*`` preset name -> (model, pack); random init when no pack."""
+def build_model(name: str, pack=None, device: Optional[torch.device] = None, seed: int = 0, fp32: bool = False,
+                broadcast: bool = False):
+    """``t5-*`` / ``bart-*`` preset name -> (model, pack); random init when no pack.
+
+    ``broadcast``: inside a DP group, rank 0 initialises the weights and every
+    rank receives them in ONE RCCL broadcast of the flat ParamPack (C1)."""
     from ..models import bart, t5
 
     fam = family_of(name)
     mod = bart if fam == "bart" else t5
     cfg = mod.config_for(name)
+    if broadcast:
+        from ..parallel.dp import broadcast_pack, world
+
+        if world()[0] == 0 and pack is None:
+            pack = mod.init_random(cfg, seed=seed)
+        pack = broadcast_pack(pack, cfg, device if device is not None else torch.device("cpu"),
+                              builder=mod.param_specs)
     pack = pack if pack is not None else mod.init_random(cfg, seed=seed)
     if device is not None and pack.buffer.device != device:
         pack = pack.to(device)
@@ -301,7 +312,8 @@ class SummarizeEngine:
         self.device = model.device
         self.max_src = int(max_source_len)
 
-    def encode_texts(self, texts: Sequence[str]) -> Tuple[torch.Tensor, torch.Tensor, List[Dict[int, str]]]:
+    def encode_texts(self, texts: Sequence[str], with_maps: bool = True
+                     ) -> Tuple[torch.Tensor, torch.Tensor, List[Dict[int, str]]]:
         """Hash-tokenize (same spec as K1, the model's vocab), wrap with the
         model's specials (T5: ``toks </s>``; BART: ``<s> toks </s>``), pad to S % 8 == 0."""
         from .._native import native
@@ -318,7 +330,7 @@ class SummarizeEngine:
         for r, toks in enumerate(rows):
             arr[r, :len(toks)] = toks
         lens_t = torch.tensor([len(r) for r in rows], dtype=torch.int32)
-        vocab_maps = [self._reverse_map(t) for t in texts]
+        vocab_maps = [self._reverse_map(t) for t in texts] if with_maps else []
         return torch.from_numpy(arr).to(self.device), lens_t.to(self.device), vocab_maps
 
     def _reverse_map(self, text: str) -> Dict[int, str]:
@@ -333,6 +345,14 @@ class SummarizeEngine:
     def detokenize(self, seq: List[int], vmap: Dict[int, str]) -> str:
         special = {self.cfg.pad_id, self.cfg.eos_id, self.cfg.decoder_start_id, getattr(self.cfg, "bos_id", -1)}
         return " ".join(vmap.get(t, f"<{t}>") for t in seq if t not in special)
+
+    def generate_ids(self, texts: Sequence[str], gen: GenConfig) -> GenResult:
+        """Token sequences only (a DP rank's shard; rank 0 detokenizes)."""
+        ids, lens, _ = self.encode_texts(texts, with_maps=False)
+        return generate(self.model, ids, lens, gen)
+
+    def detokenize_all(self, texts: Sequence[str], seqs: List[List[int]]) -> List[str]:
+        return [self.detokenize(s, self._reverse_map(t)) for t, s in zip(texts, seqs)]
 
     def summarize(self, texts: Sequence[str], gen: GenConfig) -> Tuple[List[str], GenResult]:
         ids, lens, maps = self.encode_texts(texts)

@@ -11,6 +11,11 @@ bart.py), batched beam search with HF's semantics
 tokenizer as map_classify (no SentencePiece/BPE model is available offline;
 see map_summarize.CONTRACT.md).
 
+Under ``torchrun`` (DP world > 1) the documents are split over the ranks
+(contiguous shards), every rank decodes its shard with its own GPU, and the
+token ids come back to rank 0 in one all-gather; the
+weights reach the ranks in one RCCL broadcast of the flat pack (C1).
+
 Output keys are the reference's ``{ok, summary, device, model}``; ``texts``
 (a list) returns ``summaries``. Fix: the payload is
 validated BEFORE the model is built. ``SUMMARIZE_FORCE_CPU=1`` runs the fp32
@@ -62,15 +67,39 @@ def _init_engine():
         from agent_tpu_amd.runtime.summarize import SummarizeEngine, build_model
 
         if not FORCE_CPU and torch.cuda.is_available():
-            dev = torch.device("cuda", int(os.getenv("LOCAL_RANK", "0")))
+            dev = torch.device("cuda", int(os.getenv("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
         else:
             dev = torch.device("cpu")
         model, _ = build_model(MODEL_NAME, device=dev, seed=int(os.getenv("MODEL_SEED", "0")),
-                               fp32=dev.type == "cpu")
+                               fp32=dev.type == "cpu", broadcast=_dp_world() > 1)
         eng = SummarizeEngine(model, MAX_SOURCE_TOKENS)
         _engine, _device = eng, ("cuda" if dev.type == "cuda" else "cpu")
         print(f"[map_summarize] {MODEL_NAME} ready on {_device}", flush=True)
         return _engine
+
+
+def _dp_world() -> int:
+    try:
+        from agent_tpu_amd.parallel.dp import world
+
+        return world()[1]
+    except Exception:
+        return 1
+
+
+_GEN_KEYS = ("num_beams", "max_length", "min_length", "length_penalty", "no_repeat_ngram_size")
+
+
+def result(texts_mode: bool, summaries: List[str], steps: int, timing_ms: Dict[str, float], t0: float,
+           **extra: Any) -> Dict[str, Any]:
+    out: Dict[str, Any] = {"ok": True, "device": _device, "model": MODEL_NAME,
+                           "elapsed_ms": (time.time() - t0) * 1000.0, "decode_steps": steps,
+                           "timing_ms": timing_ms, **extra}
+    if texts_mode:
+        out["summaries"] = summaries
+    else:
+        out["summary"] = summaries[0]
+    return out
 
 
 def _gen_config(payload: Dict[str, Any]):
@@ -105,13 +134,12 @@ def handle(payload: Optional[Dict[str, Any]]) -> Dict[str, Any]:
     except (TypeError, ValueError) as exc:
         return {"ok": False, "error": f"bad generation parameter: {exc}"}
     t0 = time.time()
+    if _dp_world() > 1:
+        from agent_tpu_amd.parallel.dp_ops import dispatch
+
+        desc = {k: payload[k] for k in _GEN_KEYS if k in payload}
+        desc.update(texts=texts, texts_mode="texts" in payload, t0=t0)
+        return dispatch("map_summarize", desc)
     eng = _init_engine()
     summaries, res = eng.summarize(texts, gen)
-    out: Dict[str, Any] = {"ok": True, "device": _device, "model": MODEL_NAME,
-                           "elapsed_ms": (time.time() - t0) * 1000.0, "decode_steps": res.steps,
-                           "timing_ms": res.timing_ms}
-    if "texts" in payload:
-        out["summaries"] = summaries
-    else:
-        out["summary"] = summaries[0]
-    return out
+    return result("texts" in payload, summaries, res.steps, res.timing_ms, t0)

@@ -101,6 +101,28 @@ def scen_fault():
     return out
 
 
+def scen_summarize():
+    """C5: documents split over the ranks, token ids all-gathered to rank 0;
+    equals the single-process batch on the same (broadcast) weights."""
+    rank, ws = dp.world()
+    if rank != 0:
+        import ops.map_summarize  # noqa: F401  registers nothing new; same module on every rank
+        dp_ops.worker_loop()
+        return None
+    import ops.map_summarize as ms
+
+    words = "alpha beta gamma delta epsilon zeta eta theta iota kappa lambda mu".split()
+    texts = [" ".join(words[(i + j) % len(words)] for j in range(9)) for i in range(5)]
+    gen = {"num_beams": 3, "max_length": 10, "min_length": 3}
+    out = {"dp": ms.handle({"texts": texts, **gen})}
+    out["single_dp"] = ms.handle({"text": texts[0], **gen})  # rank 1 gets an empty shard
+    eng = ms._init_engine()
+    ref, _ = eng.summarize(texts, ms._gen_config(gen))
+    out["ref"] = ref
+    dp_ops.shutdown_workers()
+    return out
+
+
 def main():
     scen = sys.argv[1]
     dist.init_process_group("gloo")
@@ -108,7 +130,7 @@ def main():
         res = globals()[f"scen_{scen}"]()
     finally:
         if dist.is_initialized():
-            if scen not in ("risk", "fault"):  # worker_loop ranks already left the group
+            if scen not in ("risk", "fault", "summarize"):  # worker_loop ranks already left the group
                 dist.barrier()
             dist.destroy_process_group()
     if int(os.environ.get("RANK", "0")) == 0:

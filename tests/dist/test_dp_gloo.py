@@ -1,7 +1,8 @@
 """Multi-process DP tests on CPU (gloo, world_size 2 and 4, 127.0.0.1).
 
 SURVEY.md §4.4(4a): the collective shapes of the RCCL path (C1 weight
-broadcast, C2 ragged all-gather, C3 risk all-reduce, C4 task descriptor) and
+broadcast, C2 ragged all-gather, C3 risk all-reduce, C4 task descriptor,
+C5 summarize token-id all-gather) and
 the rank-0-leases / others-serve process model, including fault propagation
 (``MI355X_FAULT``), run through ``torch.distributed.run`` like the driver's
 multi-GPU bench.
@@ -74,3 +75,12 @@ def test_fault_on_one_rank_fails_job_and_workers_survive():
     assert res["err"] is not None and "rank 1" in res["err"] and "injected fault" in res["err"]
     assert "rank 0" not in res["err"]
     assert res["after"]["count"] == 2 and res["after"]["sum"] == 3.0
+
+
+def test_summarize_dp_matches_single_process():
+    res = run_ranks("summarize", 2, {"SUMMARIZE_MODEL": "t5-tiny", "SUMMARIZE_FORCE_CPU": "1"})
+    dp, ref = res["dp"], res["ref"]
+    assert dp["ok"] and dp["dp_world_size"] == 2 and len(dp["summaries"]) == 5
+    assert dp["summaries"] == ref
+    assert "allgather_ms" in dp["timing_ms"] and dp["model"] == "t5-tiny"
+    assert res["single_dp"]["summary"] == ref[0] and "summaries" not in res["single_dp"]
