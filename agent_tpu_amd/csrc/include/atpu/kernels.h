@@ -40,6 +40,8 @@ struct GemmArgs {
 void gemm_bf16(const GemmArgs& g, hipStream_t stream);
 // split count the library picks for an [M,N,K] problem (1 = no split-K)
 int gemm_splitk_splits(int M, int N, int K);
+// skinny-M selector (benchmarks): 1 = 64x64 multi-stage dec kernel, 0 = 128x128 split-K
+int gemm_dec_mode(int set);
 // 256x256 schedule selector (benchmarks): set >= 0 switches; returns the current
 int gemm_256_variant(int set);
 

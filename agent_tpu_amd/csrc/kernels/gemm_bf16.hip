@@ -704,6 +704,197 @@ void launch_256b(const GemmArgs& g, hipStream_t s) {
 
 
 
+
+// ============================================================================
+// Skinny-M GEMM ("dec"): decode steps (M = docs x beams, ~256-2048 rows) and
+// the CLS-only last encoder layer. The 128x128 kernel underfills the chip at
+// these M (48 tiles for [1024 x 768]) and its two-buffer loop waits one full
+// L2/HBM round trip per K-tile, so even split 6 ways it ran ~12 us + a 5 us
+// reduce for a 1.2 GFLOP problem. Here:
+//  * 64x64 tiles, 4 waves (2x2, 32x32 each): 4x the blocks of 128x128;
+//  * an NST-deep LDS ring fed by LDS-DMA keeps NST-1 K-tiles in flight
+//    (counted vmcnt, one barrier per K-tile), so the loop runs at L2->LDS
+//    bandwidth instead of latency;
+//  * M-fastest tile order under the XCD remap: the blocks of one XCD share
+//    weight panels, so each XCD's L2 pulls a distinct slice of the weights.
+// Same swizzle, fragment layout and epilogue as the 128x128 kernel.
+// ============================================================================
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int EPI, int NST, int SPLIT>
+__global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict__ A, int lda,
+                                                          const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C,
+                                                          int ldc, const float* __restrict__ bias,
+                                                          const bf16* __restrict__ R, int ldr, int M, int N, int K,
+                                                          float* __restrict__ ws) {
+  constexpr int BM = 64, BN = 64;
+  constexpr int STAGE = (BM + BN) * kRowBytes;  // 16 KiB: A rows 0-63, B rows 64-127
+  constexpr int LPS = (BM + BN) / 8 / 4;        // DMA instructions per wave per stage (4)
+  __shared__ __attribute__((aligned(16))) char lds[NST * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntm = (M + BM - 1) / BM;
+  const int ntn = (N + BN - 1) / BN;
+  if constexpr (SPLIT) {
+    A += (size_t)blockIdx.y * K;
+    Bt += (size_t)blockIdx.y * K;
+  }
+  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
+  const int m0 = (tile % ntm) * BM;
+  const int n0 = (tile / ntm) * BN;
+
+  const int srow = lane >> 3, spos = lane & 7;
+  const bf16* src[LPS];
+#pragma unroll
+  for (int i = 0; i < LPS; ++i) {
+    const int r = (i * 4 + wave) * 8 + srow;  // staged row 0..127 (wave-uniform half)
+    if (r < BM) {
+      src[i] = A + (size_t)min(m0 + r, M - 1) * lda + swz(r, spos) * 8;
+    } else {
+      src[i] = Bt + (size_t)min(n0 + r - BM, N - 1) * ldb + swz(r, spos) * 8;
+    }
+  }
+  auto stage = [&](int kt, int slot) {
+    char* base = lds + slot * STAGE;
+#pragma unroll
+    for (int i = 0; i < LPS; ++i) glds16(src[i] + kt * kBK, base + (i * 4 + wave) * 8 * kRowBytes);
+  };
+
+  const int wm = wave >> 1, wn = wave & 1;
+  const int frow = lane & 15, fchunk = lane >> 4;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int slot) {
+    const char* base = lds + slot * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[2], bfg[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = wm * 32 + i * 16 + frow;
+        af[i] = *reinterpret_cast<const bf16x8*>(base + r * kRowBytes + swz(r, ks * 4 + fchunk) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = BM + wn * 32 + j * 16 + frow;
+        bfg[j] = *reinterpret_cast<const bf16x8*>(base + r * kRowBytes + swz(r, ks * 4 + fchunk) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  const int nk = K / kBK;
+#pragma unroll
+  for (int t = 0; t < NST - 1; ++t)
+    if (t < nk) stage(t, t);
+  for (int kt = 0; kt < nk; ++kt) {
+    // stages issued so far: min(nk, kt + NST - 1); stage kt must have landed
+    if (kt + NST - 1 <= nk)
+      wait_vmcnt<(NST - 2) * LPS>();
+    else
+      wait_vmcnt0();
+    // raw s_barrier: __syncthreads() would add a vmcnt(0) fence and drain the ring.
+    // After the counted wait every wave's DMA for stage kt has landed; the
+    // barrier publishes that and frees slot (kt-1)%NST (its ds_reads retired
+    // before the MFMAs that consumed them).
+    asm volatile("s_barrier" ::: "memory");
+    if (kt + NST - 1 < nk) stage(kt + NST - 1, (kt + NST - 1) % NST);
+    compute(kt % NST);
+  }
+
+  if constexpr (SPLIT) {
+    float* mine = ws + blockIdx.y * (size_t)M * N;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = m0 + wm * 32 + i * 16 + frow;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + wn * 32 + j * 16 + fchunk * 4;
+        if (m < M && n < N) *reinterpret_cast<f32x4*>(mine + (size_t)m * N + n) = acc[i][j];
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = m0 + wm * 32 + i * 16 + frow;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn * 32 + j * 16 + fchunk * 4;
+      if (n >= N) continue;
+      f32x4 v = acc[i][j];
+      if constexpr (EPI & kEpiBias) v += *reinterpret_cast<const f32x4*>(bias + n);
+      if constexpr (EPI & kEpiGelu) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = gelu_fast(v[e]);
+      }
+      if constexpr (EPI & kEpiTanh) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
+      }
+      if constexpr (EPI & kEpiRelu) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if constexpr (EPI & kEpiResidual) {
+        const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += bf2f(r[e]);
+      }
+      if constexpr (EPI & kEpiOutF32) {
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + (size_t)m * ldc + n) = v;
+      } else {
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+        *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
+      }
+    }
+  }
+}
+
+// Ring depth 4 (64 KiB LDS, 2 blocks/CU). 8 stages measured the same on the
+// decode shapes (tools/bench_decode_gemm.py), so the loop is not bound by
+// bytes in flight per CU.
+constexpr int kDecStages = 4;
+
+void launch_dec(const GemmArgs& g, hipStream_t s) {
+  const dim3 grid(((g.M + 63) / 64) * ((g.N + 63) / 64)), block(256);
+#define ATPU_DEC_CASE(E)                                                                                       \
+  case E:                                                                                                      \
+    hipLaunchKernelGGL((gemm_dec_kernel<E, kDecStages, 0>), grid, block, 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, \
+                       g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, nullptr);                                    \
+    break;
+  switch (g.epi) {
+    ATPU_DEC_CASE(0)
+    ATPU_DEC_CASE(kEpiBias)
+    ATPU_DEC_CASE(kEpiBias | kEpiGelu)
+    ATPU_DEC_CASE(kEpiBias | kEpiTanh)
+    ATPU_DEC_CASE(kEpiBias | kEpiResidual)
+    ATPU_DEC_CASE(kEpiResidual)
+    ATPU_DEC_CASE(kEpiGelu)
+    ATPU_DEC_CASE(kEpiRelu)
+    ATPU_DEC_CASE(kEpiOutF32)
+    ATPU_DEC_CASE(kEpiBias | kEpiOutF32)
+    default:
+      throw std::invalid_argument("atpu: unsupported GEMM epilogue " + std::to_string(g.epi));
+  }
+#undef ATPU_DEC_CASE
+}
+
 // Sum the split-K fp32 partials [splits][M][N] in slice order and apply the epilogue.
 template <int EPI>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, bf16* __restrict__ C,
@@ -745,12 +936,18 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-void launch_splitk(const GemmArgs& g, int splits, hipStream_t s) {
-  constexpr int BM = 128, BN = 128;
-  const int nb = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+void launch_splitk(const GemmArgs& g, int splits, bool dec, hipStream_t s) {
   const int kc = g.K / splits;
-  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, 2, 2, 0, 1>), dim3(nb, splits), dim3(256), 0, s, g.A, g.lda, g.Bt,
-                     g.ldb, nullptr, 0, nullptr, nullptr, 0, g.M, g.N, kc, g.ws);
+  if (dec) {
+    const int nb = ((g.M + 63) / 64) * ((g.N + 63) / 64);
+    hipLaunchKernelGGL((gemm_dec_kernel<0, kDecStages, 1>), dim3(nb, splits), dim3(256), 0, s, g.A, g.lda, g.Bt,
+                       g.ldb, nullptr, 0, nullptr, nullptr, 0, g.M, g.N, kc, g.ws);
+  } else {
+    constexpr int BM = 128, BN = 128;
+    const int nb = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, 2, 2, 0, 1>), dim3(nb, splits), dim3(256), 0, s, g.A, g.lda, g.Bt,
+                       g.ldb, nullptr, 0, nullptr, nullptr, 0, g.M, g.N, kc, g.ws);
+  }
   const int work = g.M * (g.N / 4);
   const dim3 rg(std::max(1, std::min(2048, (work + 255) / 256))), rb(256);
 #define ATPU_RED(E)                                                                                          \
@@ -813,18 +1010,42 @@ int gemm_256_variant(int set) {
   return v;
 }
 
+int gemm_dec_mode(int set) {
+  // skinny-M path: 1 = 64x64 multi-stage "dec" kernel (default), 0 = 128x128 split-K; ATPU_GEMM_DEC=0|1
+  static int v = [] {
+    const char* f = std::getenv("ATPU_GEMM_DEC");
+    return (f && f[0] == '0') ? 0 : 1;
+  }();
+  if (set >= 0) v = set;
+  return v;
+}
+
+namespace {
+// problems the 128x128 grid would leave under two blocks per CU
+bool skinny(int M, int N) { return M <= 2048 && ((M + 127) / 128) * ((N + 127) / 128) < 512; }
+}  // namespace
+
 int gemm_splitk_splits(int M, int N, int K) {
-  // Skinny problems (decode: M = beams x docs) leave most of the 256 CUs idle
-  // with 128x128 tiles; split K so the grid reaches ~2 blocks per CU, keeping
-  // >= 2 K-tiles per split and an exact division of K.
+  // Skinny problems (decode: M = beams x docs) leave most of the 256 CUs idle.
+  // dec kernel: split K only when even 64x64 tiles give < 128 blocks AND the
+  // K loop is long (>= 32 K-tiles): the reduce launch costs ~4 us, which a
+  // 12-16 K-tile loop does not win back (measured, tools/bench_decode_gemm.py).
+  // 128x128 kernel: split so the grid reaches ~2 blocks per CU, >= 2 K-tiles per split.
   static const int forced = [] {
     const char* f = std::getenv("ATPU_GEMM_SPLITK");
     return f ? std::atoi(f) : -1;
   }();
   const int nk = K / kBK;
-  const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
-  int want = forced >= 0 ? forced : (M > 1024 || tiles >= 256 ? 1 : (512 + tiles - 1) / tiles);
-  want = std::max(1, std::min({want, nk / 2, 16}));
+  int want;
+  if (gemm_dec_mode(-1) == 1 && skinny(M, N)) {
+    const int tiles = ((M + 63) / 64) * ((N + 63) / 64);
+    want = forced >= 0 ? forced : (tiles >= 128 || nk < 32 ? 1 : (256 + tiles - 1) / tiles);
+    want = std::max(1, std::min({want, nk / 8, 16}));
+  } else {
+    const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
+    want = forced >= 0 ? forced : (M > 1024 || tiles >= 256 ? 1 : (512 + tiles - 1) / tiles);
+    want = std::max(1, std::min({want, nk / 2, 16}));
+  }
   while (want > 1 && nk % want) --want;
   return want;
 }
@@ -850,7 +1071,7 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
   }();
   if (g.splits > 1) {
     ATPU_CHECK(g.ws && (g.K / kBK) % g.splits == 0, "gemm: split-K needs a workspace and K/64 % splits == 0");
-    launch_splitk(g, g.splits, stream);
+    launch_splitk(g, g.splits, gemm_dec_mode(-1) == 1 && skinny(g.M, g.N), stream);
     ATPU_HIP_CHECK(hipGetLastError());
     return;
   }
@@ -862,6 +1083,8 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
     launch_256p(g, stream);
   else if (use_big)
     launch_256b(g, stream);
+  else if (!forced && gemm_dec_mode(-1) == 1 && skinny(g.M, g.N))
+    launch_dec(g, stream);
   else
     launch_tile<128, 128, 2, 2>(g, stream);
   ATPU_HIP_CHECK(hipGetLastError());

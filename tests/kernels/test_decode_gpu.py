@@ -107,19 +107,47 @@ def test_beam_topk_rows(gpu, V, k, mask):
 @pytest.mark.parametrize("M,N,K,act,res,bias", [(256, 768, 3072, None, True, False), (256, 3072, 768, "relu", False, False),
                                                 (256, 2304, 768, None, False, True), (96, 768, 768, "gelu", False, True),
                                                 (512, 768, 768, None, True, False)])
-def test_gemm_splitk_skinny(gpu, M, N, K, act, res, bias):
+@pytest.mark.parametrize("mode", [0, 1])
+def test_gemm_splitk_skinny(gpu, M, N, K, act, res, bias, mode):
+    """mode 0: 128x128 split-K partials + reduce; mode 1: the 64x64 multi-stage
+    dec kernel (split-K only when even its grid is small)."""
+    from agent_tpu_amd._native import native
+    from agent_tpu_amd.ops.linear import _splits, linear_ref
+
+    prev = native().gemm_dec_mode(mode)
+    _splits.cache_clear()
+    try:
+        x = _r((M, K), gpu, seed=41)
+        w = _r((N, K), gpu, 0.05, seed=42)
+        r = _r((M, N), gpu, seed=43) if res else None
+        b = _r((N,), gpu, 1.0, torch.float32, seed=44) if bias else None
+        y = ops.linear(x, w, bias=b, act=act, residual=r)
+        ref = linear_ref(x.cpu(), w.cpu(), None if b is None else b.cpu(), act, None if r is None else r.cpu(),
+                         out_f32=True)
+        if mode == 0:
+            assert _splits(M, N, K) > 1
+        assert _rel(y, ref) < 2e-2
+    finally:
+        native().gemm_dec_mode(1)
+        _splits.cache_clear()
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 200, 64 * 13), (1024, 768, 768), (64, 64, 64), (70, 132, 128),
+                                   (2000, 1000, 3072), (256, 768, 3072), (96, 256, 64 * 40)])
+def test_gemm_dec_exact_integers(gpu, M, N, K):
+    """{-1,0,1} operands: exact in fp32 and bf16, so the dec kernel (ragged
+    M/N edges, ring tails for K-tile counts around the stage depth, split-K
+    for the small grids) must match bit for bit."""
     from agent_tpu_amd.ops.linear import _splits
 
-    x = _r((M, K), gpu, seed=41)
-    w = _r((N, K), gpu, 0.05, seed=42)
-    r = _r((M, N), gpu, seed=43) if res else None
-    b = _r((N,), gpu, 1.0, torch.float32, seed=44) if bias else None
-    y = ops.linear(x, w, bias=b, act=act, residual=r)
-    from agent_tpu_amd.ops.linear import linear_ref
-
-    ref = linear_ref(x.cpu(), w.cpu(), None if b is None else b.cpu(), act, None if r is None else r.cpu(), out_f32=True)
-    assert _splits(M, N, K) > 1
-    assert _rel(y, ref) < 2e-2
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randint(-1, 2, (M, K), generator=g).to(torch.bfloat16)
+    w = torch.randint(-1, 2, (N, K), generator=g).to(torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    y = ops.linear(x.to(gpu), w.to(gpu), out_f32=True)
+    assert torch.equal(y.cpu(), ref), (M, N, K, _splits(M, N, K))
+    yb = ops.linear(x.to(gpu), w.to(gpu))
+    assert torch.equal(yb.cpu().float(), ref.to(torch.bfloat16).float())
 
 
 def test_gemm_relu_and_f32_out(gpu):
