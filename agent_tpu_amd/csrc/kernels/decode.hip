@@ -33,6 +33,13 @@ namespace {
 constexpr int kD = 64;
 constexpr int kMaxKeys = 2048;
 
+// Memory-level parallelism: a decode step is a latency-bound stream of short
+// K/V rows, so both loops issue U independent tiles' loads before consuming
+// any (one round trip per U tiles instead of per tile), and the self-attention
+// backpointer rows are resolved once into LDS (phase 1) and reused by P.V.
+constexpr int kUnrollS = 4;  // 16-key score tiles in flight per wave
+constexpr int kUnrollV = 4;  // 8-key V slabs in flight per wave
+
 template <int GM, int NW>
 __global__ __launch_bounds__(NW * 64) void decode_attention_kernel(
     const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k, const bf16* __restrict__ v, int ldkv,
@@ -42,14 +49,16 @@ __global__ __launch_bounds__(NW * 64) void decode_attention_kernel(
   __shared__ float p[GM][kMaxKeys];
   __shared__ float po[NW][GM][kD];
   __shared__ float red[NW][16];
+  __shared__ int prow[GM == 1 ? kMaxKeys : 1];  // self attention: physical cache row of key j
   const int seq = blockIdx.x, h = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int G = min(group, nrows - seq * group);
   int len = lens ? lens[seq] : (*step_dev + 1);
   len = min(len, kMaxKeys);
-  auto phys = [&](int j) -> size_t {
-    const int r = (hist && j < len - 1) ? hist[(size_t)seq * hist_stride + j] : seq;
-    return ((size_t)r * seq_stride + j) * ldkv + h * kD;
+  const bool use_hist = GM == 1 && hist != nullptr;
+  auto row_of = [&](int j) -> int {
+    return (use_hist && j < len - 1) ? hist[(size_t)seq * hist_stride + j] : seq;
   };
+  auto at = [&](int r, int j) -> size_t { return ((size_t)r * seq_stride + j) * ldkv + h * kD; };
   // ---- scores on MFMA: S^T[16 keys x 16 queries] = K[16 x 64] . Q^T[64 x 16] ----
   // A operand = K rows (lane&15 = key, (lane>>4)*8 = dims), B operand = the
   // group's queries zero-padded to 16 (loop invariant, 8 VGPRs). Lane l gets
@@ -65,21 +74,34 @@ __global__ __launch_bounds__(NW * 64) void decode_attention_kernel(
     for (int e = 0; e < 8; ++e) { qb0[e] = f2bf(0.f); qb1[e] = f2bf(0.f); }
   }
   float mxl = -FLT_MAX;
-  for (int t = w; t * 16 < len; t += NW) {
-    const bf16* kr = k + phys(min(t * 16 + li, len - 1));
-    const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(kr + kq);
-    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(kr + 32 + kq);
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, qb0, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, qb1, acc, 0, 0, 0);
-    if (li < G) {
+  for (int t0 = w; t0 * 16 < len; t0 += NW * kUnrollS) {
+    bf16x8 a0[kUnrollS], a1[kUnrollS];
+    int rr[kUnrollS];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int j = t * 16 + (lane >> 4) * 4 + e;
-        if (j < len) {
-          const float sj = acc[e] * scale + (bias_dist ? bias_dist[h * bias_stride + (len - 1 - j)] : 0.f);
-          p[li][j] = sj;
-          mxl = fmaxf(mxl, sj);
+    for (int u = 0; u < kUnrollS; ++u) rr[u] = row_of(min((t0 + u * NW) * 16 + li, len - 1));
+#pragma unroll
+    for (int u = 0; u < kUnrollS; ++u) {
+      const bf16* kr = k + at(rr[u], min((t0 + u * NW) * 16 + li, len - 1));
+      a0[u] = *reinterpret_cast<const bf16x8*>(kr + kq);
+      a1[u] = *reinterpret_cast<const bf16x8*>(kr + 32 + kq);
+    }
+#pragma unroll
+    for (int u = 0; u < kUnrollS; ++u) {
+      const int t = t0 + u * NW;
+      if (t * 16 >= len) break;
+      if (GM == 1 && lane < 16 && t * 16 + lane < len) prow[t * 16 + lane] = rr[u];
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], qb0, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], qb1, acc, 0, 0, 0);
+      if (li < G) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int j = t * 16 + (lane >> 4) * 4 + e;
+          if (j < len) {
+            const float sj = acc[e] * scale + (bias_dist ? bias_dist[h * bias_stride + (len - 1 - j)] : 0.f);
+            p[li][j] = sj;
+            mxl = fmaxf(mxl, sj);
+          }
         }
       }
     }
@@ -123,16 +145,25 @@ __global__ __launch_bounds__(NW * 64) void decode_attention_kernel(
   for (int g = 0; g < GM; ++g)
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[g][e] = 0.f;
-  for (int j0 = w * 8; j0 < len; j0 += NW * 8) {
-    const int j = j0 + ksub;
-    if (j < len) {
-      const bf16x8 vv = *reinterpret_cast<const bf16x8*>(v + phys(j) + dc);
+  for (int j0 = w * 8; j0 < len; j0 += NW * 8 * kUnrollV) {
+    bf16x8 vv[kUnrollV];
 #pragma unroll
-      for (int g = 0; g < GM; ++g) {
-        if (g < G) {
-          const float pj = p[g][j];
+    for (int u = 0; u < kUnrollV; ++u) {
+      const int j = min(j0 + u * NW * 8 + ksub, len - 1);
+      const int r = use_hist ? prow[j] : seq;
+      vv[u] = *reinterpret_cast<const bf16x8*>(v + at(r, j) + dc);
+    }
 #pragma unroll
-          for (int e = 0; e < 8; ++e) o[g][e] += pj * bf2f(vv[e]);
+    for (int u = 0; u < kUnrollV; ++u) {
+      const int j = j0 + u * NW * 8 + ksub;
+      if (j < len) {
+#pragma unroll
+        for (int g = 0; g < GM; ++g) {
+          if (g < G) {
+            const float pj = p[g][j];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[g][e] += pj * bf2f(vv[u][e]);
+          }
         }
       }
     }

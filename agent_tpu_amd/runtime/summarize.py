@@ -163,17 +163,28 @@ def generate(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfi
     hist_alt = torch.zeros_like(hist)
     step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
 
-    run_seq = torch.full((B, nb, T), cfg.pad_id, dtype=torch.long)
+    # Host beam state lives in numpy: the per-step bookkeeping is ~40 tiny
+    # array ops, ~4x cheaper than torch CPU ops, and everything that is not
+    # needed to launch the next step (sequence copies, finished-hypothesis
+    # merge, early-stop test) runs after that launch, under the GPU step.
+    run_seq = np.full((B, nb, T), cfg.pad_id, dtype=np.int64)
     run_seq[:, :, 0] = cfg.decoder_start_id
-    run_scores = torch.zeros((B, nb), dtype=torch.float32)
+    run_scores = np.zeros((B, nb), dtype=np.float32)
     run_scores[:, 1:] = NEG
-    fin_seq = run_seq.clone()
-    fin_scores = torch.full((B, nb), NEG, dtype=torch.float32)
-    fin_done = torch.zeros((B, nb), dtype=torch.bool)
-    fin_len = torch.ones((B, nb), dtype=torch.long)
-    unsat = torch.ones((B, 1), dtype=torch.bool)
-    top_mask = torch.cat([torch.ones(nb, dtype=torch.bool), torch.zeros(K2 - nb, dtype=torch.bool)])
+    fin_seq = run_seq.copy()
+    fin_scores = np.full((B, nb), NEG, dtype=np.float32)
+    fin_done = np.zeros((B, nb), dtype=bool)
+    fin_len = np.ones((B, nb), dtype=np.int64)
+    unsat = np.ones((B, 1), dtype=bool)
+    top_mask = np.arange(K2) < nb
+    rowsB = np.arange(B)[:, None]
+    beam_of0 = np.broadcast_to(np.repeat(np.arange(nb, dtype=np.int64), K2)[None, :], (B, nb * K2))
+    neg = np.float32(NEG)
     tokens = torch.full((rows,), cfg.decoder_start_id, dtype=torch.int32, device=dev)
+    pin = dev.type == "cuda"
+    par_host = torch.empty(rows, dtype=torch.int32, pin_memory=pin)
+    tok_host = torch.empty(rows, dtype=torch.int32, pin_memory=pin)
+    par_dev = torch.empty(rows, dtype=torch.int32, device=dev)
     lp = float(gen.length_penalty)
     # Every step input is a static device buffer (tokens, step, cache, hist), so
     # after one eager step the whole decoder step (~13 launches x L layers) is
@@ -200,72 +211,67 @@ def generate(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfi
     logits = launch(cur)
     while True:
         with span("beam_select"):
-            sc, tk = _select(logits, run_scores, K2, cfg, gen, cur, T, run_seq)
-        sc, tk = sc.view(B, nb * K2), tk.view(B, nb * K2)
+            sc_t, tk_t = _select(logits, torch.from_numpy(run_scores), K2, cfg, gen, cur, T,
+                                 torch.from_numpy(run_seq))
+        sc = sc_t.numpy().reshape(B, nb * K2)
+        tk = tk_t.numpy().astype(np.int64, copy=False).reshape(B, nb * K2)
         steps += 1
-        # global top-K2 per item; ties -> lower flat index (beam * V + token) like torch.topk over [nb*V]
-        beam_of = torch.arange(nb).repeat_interleave(K2).view(1, -1).expand(B, -1)
-        flat = beam_of * V + tk
-        order = torch.argsort(flat, dim=1)
-        sc, tk, beam_of, flat = (torch.gather(x, 1, order) for x in (sc, tk, beam_of, flat))
-        top_sc, pos = torch.sort(sc, dim=1, descending=True, stable=True)
-        pos = pos[:, :K2]
-        top_sc = top_sc[:, :K2]
-        top_tok = torch.gather(tk, 1, pos)
-        top_beam = torch.gather(beam_of, 1, pos)
-        cand_seq = torch.gather(run_seq, 1, top_beam.unsqueeze(-1).expand(-1, -1, T)).clone()
-        cand_seq[:, :, cur] = top_tok
+        # global top-K2 per item, ties -> lower flat index (beam * V + token),
+        # like torch.topk over the item's [nb * V] scores: score desc, flat asc
+        order = np.lexsort((beam_of0 * V + tk, -sc), axis=1)[:, :K2]
+        top_sc, top_tok, top_beam = sc[rowsB, order], tk[rowsB, order], beam_of0[rowsB, order]
         hits = (top_tok == cfg.eos_id) | (cur + 1 >= T)
 
         # running beams for the next step: best nb non-hit continuations
-        run_cand = top_sc + hits.float() * NEG
-        nxt = torch.topk(run_cand, nb, dim=1).indices
-        run_seq = torch.gather(cand_seq, 1, nxt.unsqueeze(-1).expand(-1, -1, T))
-        run_scores = torch.gather(run_cand, 1, nxt)
-        parent = torch.gather(top_beam, 1, nxt)  # beam index within the item
+        run_cand = np.where(hits, top_sc + neg, top_sc)
+        nxt = np.argsort(-run_cand, axis=1, kind="stable")[:, :nb]
+        parent = top_beam[rowsB, nxt]  # beam index within the item
+        new_tok = top_tok[rowsB, nxt]
+        run_scores = run_cand[rowsB, nxt]
 
         if cur + 1 < T:
             # enqueue step cur+1 NOW: histories follow their parent beams
-            # (backpointers, no KV copy), new tokens, decoder-step graph. The
-            # finished-hypothesis bookkeeping below runs on the host while the
-            # GPU computes it (a step launched past an early stop is dropped).
-            par_rows = (torch.arange(B).view(-1, 1) * nb + parent).view(-1).to(torch.int32).to(dev)
-            ops.beam_reorder_hist(hist, hist_alt, par_rows, step_dev)
+            # (backpointers, no KV copy), new tokens, decoder-step graph
+            par_host.numpy()[:] = (rowsB * nb + parent).reshape(-1)
+            tok_host.numpy()[:] = new_tok.reshape(-1)
+            par_dev.copy_(par_host, non_blocking=True)
+            tokens.copy_(tok_host, non_blocking=True)
+            ops.beam_reorder_hist(hist, hist_alt, par_dev, step_dev)
             hist.copy_(hist_alt)  # keep the captured buffer address
-            tokens.copy_(run_seq[:, :, cur].reshape(-1).to(torch.int32))
             logits = launch(cur + 1)
 
-        # finished hypotheses: hits among the top nb candidates
-        did = hits & top_mask.view(1, -1)
-        fin_cand = top_sc / float(cur) ** lp  # generated length = cur + 1 - prompt(1)
-        full = fin_done.all(dim=1, keepdim=True) & gen.early_stopping
-        fin_cand = fin_cand + full.float() * NEG + (~unsat).float() * NEG + (~did).float() * NEG
-        m_seq = torch.cat([fin_seq, cand_seq], 1)
-        m_sc = torch.cat([fin_scores, fin_cand], 1)
-        m_done = torch.cat([fin_done, did], 1)
-        m_len = torch.cat([fin_len, torch.full((B, K2), cur + 1, dtype=torch.long)], 1)
-        keep = torch.topk(m_sc, nb, dim=1).indices
-        fin_seq = torch.gather(m_seq, 1, keep.unsqueeze(-1).expand(-1, -1, T))
-        fin_scores = torch.gather(m_sc, 1, keep)
-        fin_done = torch.gather(m_done, 1, keep)
-        fin_len = torch.gather(m_len, 1, keep)
+        # ---- under the GPU step: sequences, finished hypotheses, early stop ----
+        prev_seq = run_seq
+        run_seq = prev_seq[rowsB, parent]
+        run_seq[:, :, cur] = new_tok
+        did = hits & top_mask[None, :]
+        fin_cand = top_sc / np.float32(float(cur) ** lp)  # generated length = cur + 1 - prompt(1)
+        full = fin_done.all(axis=1, keepdims=True) & bool(gen.early_stopping)
+        fin_cand = fin_cand + full * neg + (~unsat) * neg + (~did) * neg
+        m_sc = np.concatenate([fin_scores, fin_cand.astype(np.float32)], 1)
+        keep = np.argsort(-m_sc, axis=1, kind="stable")[:, :nb]
+        from_fin = keep < nb
+        kc = np.maximum(keep - nb, 0)
+        cand_rows = prev_seq[rowsB, top_beam[rowsB, kc]]
+        cand_rows[:, :, cur] = top_tok[rowsB, kc]
+        fin_seq = np.where(from_fin[:, :, None], fin_seq[rowsB, np.minimum(keep, nb - 1)], cand_rows)
+        fin_scores = m_sc[rowsB, keep]
+        fin_done = np.where(from_fin, fin_done[rowsB, np.minimum(keep, nb - 1)], did[rowsB, kc])
+        fin_len = np.where(from_fin, fin_len[rowsB, np.minimum(keep, nb - 1)], cur + 1)
 
         cur += 1
         if cur >= T:
             break
         # early-stop heuristic (early_stopping=True: best running at current length)
-        best_run = run_scores[:, :1] / float(cur - 1) ** lp
-        worst_fin = torch.where(fin_done, fin_scores.min(dim=1, keepdim=True).values, torch.full_like(fin_scores, NEG))
-        unsat = unsat & (best_run > worst_fin).any(dim=1, keepdim=True)
-        open_beam = ~(fin_done.all() & gen.early_stopping)
-        if not (bool(unsat.any()) and bool(open_beam) and not bool(hits.all())):
+        best_run = run_scores[:, :1] / np.float32(float(cur - 1) ** lp)
+        worst_fin = np.where(fin_done, fin_scores.min(axis=1, keepdims=True), neg)
+        unsat = unsat & (best_run > worst_fin).any(axis=1, keepdims=True)
+        open_beam = not (bool(fin_done.all()) and bool(gen.early_stopping))
+        if not (bool(unsat.any()) and open_beam and not bool(hits.all())):
             break
     t_dec = time.perf_counter()
-    seqs, scores = [], []
-    for b in range(B):
-        n = int(fin_len[b, 0])
-        seqs.append(fin_seq[b, 0, :n].tolist())
-        scores.append(float(fin_scores[b, 0]))
+    seqs = [fin_seq[b, 0, :int(fin_len[b, 0])].tolist() for b in range(B)]
+    scores = [float(fin_scores[b, 0]) for b in range(B)]
     return GenResult(seqs, scores, steps, {"encode_ms": (t_enc - t0) * 1e3, "decode_ms": (t_dec - t_enc) * 1e3})
 
 
@@ -303,6 +309,14 @@ def family_of(name: str) -> str:
     raise ValueError(f"unknown summarization model {name!r} (t5-* or bart-*)")
 
 
+@dataclass
+class WordMap:
+    """Sorted token ids, index of the first word producing each, the words."""
+    ids: np.ndarray
+    word_of: np.ndarray
+    words: List[str]
+
+
 class SummarizeEngine:
     """Texts -> summaries with a device-resident T5 or BART (batched beam search)."""
 
@@ -330,10 +344,11 @@ class SummarizeEngine:
         for r, toks in enumerate(rows):
             arr[r, :len(toks)] = toks
         lens_t = torch.tensor([len(r) for r in rows], dtype=torch.int32)
-        vocab_maps = [self._reverse_map(t) for t in texts] if with_maps else []
+        vocab_maps = self.word_maps(texts) if with_maps else []
         return torch.from_numpy(arr).to(self.device), lens_t.to(self.device), vocab_maps
 
     def _reverse_map(self, text: str) -> Dict[int, str]:
+        """Python oracle of :meth:`word_maps` (first source word producing each id)."""
         from .. import tokenizer as T
 
         out: Dict[int, str] = {}
@@ -342,9 +357,43 @@ class SummarizeEngine:
                 out.setdefault(tok_id, word)
         return out
 
-    def detokenize(self, seq: List[int], vmap: Dict[int, str]) -> str:
+    def word_maps(self, texts: Sequence[str]) -> List["WordMap"]:
+        """Per text: sorted token ids -> the first whitespace word producing each.
+
+        Every word of every text is one row of ONE native tokenizer call (the
+        per-word Python hashing of :meth:`_reverse_map` cost ~1 ms per document,
+        more than the GPU decode of a 256-document batch per document)."""
+        from .._native import native
+
+        words = [t.split() for t in texts]
+        flat = [w for ws in words for w in ws]
+        if not flat:
+            return [WordMap(np.zeros(0, np.int32), np.zeros(0, np.int64), ws) for ws in words]
+        text, offs = pack_rows(flat)
+        ids, lens = native().tokenize_host(text, offs, 66, self.cfg.vocab_size, 1 << 30)
+        ntok = lens.astype(np.int64) - 2  # tokens of word i at ids[i, 1 : 1 + ntok]
+        cols = np.arange(64)[None, :]
+        out, pos = [], 0
+        for ws in words:
+            n = len(ws)
+            blk, nt = ids[pos:pos + n, 1:65], ntok[pos:pos + n]
+            mask = cols < nt[:, None]
+            tok = blk[mask]  # word-major order
+            widx = np.broadcast_to(np.arange(n)[:, None], blk.shape)[mask]
+            uniq, first = np.unique(tok, return_index=True)
+            out.append(WordMap(uniq, widx[first], ws))
+            pos += n
+        return out
+
+    def detokenize(self, seq: List[int], vmap: "WordMap") -> str:
         special = {self.cfg.pad_id, self.cfg.eos_id, self.cfg.decoder_start_id, getattr(self.cfg, "bos_id", -1)}
-        return " ".join(vmap.get(t, f"<{t}>") for t in seq if t not in special)
+        keep = [t for t in seq if t not in special]
+        if not keep:
+            return ""
+        q = np.asarray(keep, dtype=np.int64)
+        i = np.minimum(np.searchsorted(vmap.ids, q), max(len(vmap.ids) - 1, 0))
+        hit = (vmap.ids[i] == q) if len(vmap.ids) else np.zeros(len(q), bool)
+        return " ".join(vmap.words[vmap.word_of[j]] if h else f"<{t}>" for t, j, h in zip(keep, i, hit))
 
     def generate_ids(self, texts: Sequence[str], gen: GenConfig) -> GenResult:
         """Token sequences only (a DP rank's shard; rank 0 detokenizes)."""
@@ -352,9 +401,10 @@ class SummarizeEngine:
         return generate(self.model, ids, lens, gen)
 
     def detokenize_all(self, texts: Sequence[str], seqs: List[List[int]]) -> List[str]:
-        return [self.detokenize(s, self._reverse_map(t)) for t, s in zip(texts, seqs)]
+        return [self.detokenize(s, m) for s, m in zip(seqs, self.word_maps(texts))]
 
     def summarize(self, texts: Sequence[str], gen: GenConfig) -> Tuple[List[str], GenResult]:
-        ids, lens, maps = self.encode_texts(texts)
+        ids, lens, _ = self.encode_texts(texts, with_maps=False)
         res = generate(self.model, ids, lens, gen)
+        maps = self.word_maps(texts)
         return [self.detokenize(s, m) for s, m in zip(res.sequences, maps)], res

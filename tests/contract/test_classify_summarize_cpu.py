@@ -95,3 +95,36 @@ def test_model_resolution(monkeypatch):
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         assert ms._resolve_model() == want, env
+
+
+def test_word_maps_match_python_oracle():
+    """The native batched reverse map equals the per-word Python oracle:
+    first word producing each id, punctuation splits, >24-byte pieces, the
+    64-token cap, unicode and control characters."""
+    import numpy as np
+    import torch
+
+    from agent_tpu_amd.models import t5
+    from agent_tpu_amd.runtime.summarize import SummarizeEngine
+
+    cfg = t5.config_for("t5-tiny")
+
+    class Stub:
+        def __init__(self):
+            self.cfg, self.device = cfg, torch.device("cpu")
+
+        def wrap_source(self, toks):
+            return list(toks) + [cfg.eos_id]
+
+    eng = SummarizeEngine(Stub(), 64)
+    long_word = "x" * 70 + "-" + "y" * 30
+    texts = ["The quick, brown fox; jumps over the lazy dog's back.", "naïve café déjà-vu   tab\there",
+             long_word + " " + "z" * 2000, "a\x01b c\x1fd e", "", "   ", "repeat repeat REPEAT Repeat."]
+    for text, wm in zip(texts, eng.word_maps(texts)):
+        oracle = eng._reverse_map(text)
+        got = {int(t): wm.words[int(w)] for t, w in zip(wm.ids, wm.word_of)}
+        assert got == oracle, text
+        seq = sorted(oracle)[:5] + [12345 % cfg.vocab_size, cfg.eos_id]
+        want = " ".join(oracle.get(t, f"<{t}>") for t in seq if t != cfg.eos_id and t != cfg.pad_id)
+        assert eng.detokenize(seq, wm) == want
+    assert np.asarray(eng.word_maps([""])[0].ids).size == 0
