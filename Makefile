@@ -2,7 +2,7 @@
 PY ?= python
 NPROC ?= 8
 
-.PHONY: build build-debug test test-gpu test-dist sanitize bench bench-dp bench-summarize bench-risk bench-agent profile clean
+.PHONY: build build-debug test test-gpu test-gpu-serial test-dist sanitize bench bench-dp bench-summarize bench-risk bench-agent profile clean
 
 build:            ## compile every HIP/C++ source for gfx950 in-tree
 	$(PY) agent_tpu_amd/csrc/build.py
@@ -15,6 +15,9 @@ test: build       ## CPU suite: contracts, HF parity, integration, gloo DP, host
 
 test-gpu: build   ## kernel numerics + model/op tests on the GPU
 	$(PY) -m pytest tests -m gpu -q
+
+test-gpu-serial: build  ## same, every launch synchronous + serialized (localises a faulting kernel)
+	HIP_LAUNCH_BLOCKING=1 AMD_SERIALIZE_KERNEL=3 AMD_SERIALIZE_COPY=3 $(PY) -m pytest tests -m gpu -q -x
 
 test-dist:
 	$(PY) -m pytest tests/dist -q

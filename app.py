@@ -147,20 +147,31 @@ class Metrics:
 
 
 def gpu_metrics() -> Dict[str, Any]:
-    """HBM use per device, only if this process already initialised the GPU."""
+    """``gpu_util[]`` from amdgpu sysfs; HBM use per device only if this process
+    already initialised the GPU."""
+    out: Dict[str, Any] = {}
+    try:
+        from worker_sizing import probe_gpu_busy
+
+        util = probe_gpu_busy()
+        if util:
+            out["gpu_util"] = util
+    except Exception:
+        pass
     try:
         import torch
 
         if not torch.cuda.is_available() or not torch.cuda.is_initialized():
-            return {}
+            return out
         used, total = [], []
         for i in range(torch.cuda.device_count()):
             free_b, tot_b = torch.cuda.mem_get_info(i)
             used.append(round((tot_b - free_b) / 2**30, 2))
             total.append(round(tot_b / 2**30, 2))
-        return {"hbm_used_gb": used, "hbm_total_gb": total}
+        out.update({"hbm_used_gb": used, "hbm_total_gb": total})
     except Exception:
-        return {}
+        pass
+    return out
 
 
 METRICS = Metrics()

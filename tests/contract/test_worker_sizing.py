@@ -116,3 +116,27 @@ def test_env_bool(monkeypatch, raw, val):
     else:
         monkeypatch.setenv("X_BOOL", raw)
     assert ws.env_bool("X_BOOL", None) is val
+
+
+def test_gpu_busy_from_fake_drm(tmp_path, monkeypatch):
+    """gpu_util[]: amdgpu cards only (vendor 0x1002), card order, connectors skipped."""
+    def card(name, vendor, busy=None):
+        d = tmp_path / name / "device"
+        d.mkdir(parents=True)
+        (d / "vendor").write_text(vendor + "\n")
+        if busy is not None:
+            (d / "gpu_busy_percent").write_text(f"{busy}\n")
+
+    card("card1", "0x1002", 37)
+    card("card10", "0x1002", 100)
+    card("card2", "0x1002", 0)
+    card("card3", "0x8086", 50)  # not AMD
+    (tmp_path / "card1-DP-1").mkdir()  # connector
+    (tmp_path / "renderD128").mkdir()
+    monkeypatch.setenv("ATPU_DRM_ROOT", str(tmp_path))
+    assert ws.probe_gpu_busy() == [0.37, 0.0, 1.0]
+    import app
+
+    assert app.gpu_metrics()["gpu_util"] == [0.37, 0.0, 1.0]
+    monkeypatch.setenv("ATPU_DRM_ROOT", str(tmp_path / "missing"))
+    assert ws.probe_gpu_busy() == []

@@ -142,6 +142,31 @@ def probe_kfd(root: Optional[str] = None) -> List[Dict[str, Any]]:
     return devs
 
 
+DRM_ROOT = "/sys/class/drm"
+
+
+def probe_gpu_busy(root: Optional[str] = None) -> List[float]:
+    """Utilisation (0..1) of every AMD GPU from amdgpu's sysfs ``gpu_busy_percent``,
+    in card order (no HIP context, no subprocess; the lease metric ``gpu_util``)."""
+    root = root or os.getenv("ATPU_DRM_ROOT", DRM_ROOT)
+    try:
+        cards = [c for c in os.listdir(root) if c.startswith("card") and c[4:].isdigit()]
+    except OSError:
+        return []
+    out: List[float] = []
+    for c in sorted(cards, key=lambda c: int(c[4:])):
+        dev = os.path.join(root, c, "device")
+        try:
+            with open(os.path.join(dev, "vendor")) as f:
+                if f.read().strip().lower() != "0x1002":
+                    continue
+            with open(os.path.join(dev, "gpu_busy_percent")) as f:
+                out.append(round(int(f.read().strip()) / 100.0, 3))
+        except (OSError, ValueError):
+            continue
+    return out
+
+
 def probe_amd_smi() -> List[Dict[str, Any]]:
     try:
         out = subprocess.run(["amd-smi", "static", "--asic", "--vram", "--json"], capture_output=True, text=True,
