@@ -16,10 +16,16 @@ tests. Collectives issued by a DP classify task:
 
 Shard planning is contiguous and balanced (:func:`split_range`), so results
 concatenate in rank order into the original row order.
+
+Elastic recovery: :func:`shrink` drops ranks whose device
+faulted. The survivors build a new process group over the healthy ranks (a
+new RCCL communicator, ``use_local_synchronization`` so the lost ranks take no
+part), and every collective here runs on that group. Global rank 0 (the agent)
+is never dropped.
 """
 from __future__ import annotations
 
-from typing import Any, List, Optional, Tuple
+from typing import Any, Iterable, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -29,8 +35,51 @@ def is_dist() -> bool:
     return dist.is_available() and dist.is_initialized()
 
 
+_GROUP = None  # active DP group after a shrink (None = the default group)
+_MEMBERS: Optional[List[int]] = None  # its global ranks, ascending
+_LOST: List[int] = []
+
+
+def group():
+    return _GROUP
+
+
+def members() -> List[int]:
+    """Global ranks of the active DP group."""
+    if not is_dist():
+        return [0]
+    return list(_MEMBERS) if _MEMBERS is not None else list(range(dist.get_world_size()))
+
+
 def world() -> Tuple[int, int]:
-    return (dist.get_rank(), dist.get_world_size()) if is_dist() else (0, 1)
+    """(rank within the active DP group, its size); rank -1 once this rank was dropped."""
+    if not is_dist():
+        return (0, 1)
+    if _MEMBERS is None:
+        return (dist.get_rank(), dist.get_world_size())
+    me = dist.get_rank()
+    return (_MEMBERS.index(me) if me in _MEMBERS else -1, len(_MEMBERS))
+
+
+def lost_ranks() -> List[int]:
+    return list(_LOST)
+
+
+def shrink(lost: Iterable[int]) -> bool:
+    """Drop global ranks ``lost`` from the DP group; every member calls this with
+    the same set (the exchanged per-rank errors). Returns False when nothing
+    changes or rank 0 would be dropped (the agent process cannot leave)."""
+    global _GROUP, _MEMBERS
+    cur = members()
+    gone = set(lost) & set(cur)
+    if not gone or 0 in gone:
+        return False
+    keep = [r for r in cur if r not in gone]
+    _LOST.extend(sorted(gone))
+    _MEMBERS = keep
+    if dist.get_rank() in keep:
+        _GROUP = dist.new_group(ranks=keep, use_local_synchronization=True)
+    return True
 
 
 def split_range(start: int, n: int, world_size: int, rank: int) -> Tuple[int, int]:
@@ -63,7 +112,7 @@ def broadcast_pack(pack, cfg, device: torch.device, src: int = 0, builder=None):
     if is_dist():
         cdev = comm_device(device)
         buf = out.buffer if out.buffer.device == cdev else out.buffer.to(cdev)
-        dist.broadcast(buf, src=src)
+        dist.broadcast(buf, src=src, group=_GROUP)
         if buf is not out.buffer:
             out.buffer.copy_(buf)
     return out
@@ -74,7 +123,7 @@ def broadcast_task(obj: Any, src: int = 0) -> Any:
     if not is_dist():
         return obj
     box = [obj]
-    dist.broadcast_object_list(box, src=src)
+    dist.broadcast_object_list(box, src=src, group=_GROUP)
     return box[0]
 
 
@@ -91,7 +140,7 @@ def all_gather_rows(*tensors: torch.Tensor) -> Tuple[torch.Tensor, ...]:
     cdev = comm_device(dev)
     cnt = torch.tensor([tensors[0].shape[0]], dtype=torch.int64, device=cdev)
     counts = torch.empty(ws, dtype=torch.int64, device=cdev)
-    dist.all_gather_into_tensor(counts, cnt)
+    dist.all_gather_into_tensor(counts, cnt, group=_GROUP)
     counts_l: List[int] = counts.tolist()
     mx = max(counts_l) if counts_l else 0
     outs = []
@@ -102,7 +151,7 @@ def all_gather_rows(*tensors: torch.Tensor) -> Tuple[torch.Tensor, ...]:
             t = torch.cat([t, pad], 0)
         t = t.contiguous()
         g = torch.empty((ws * mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=cdev)
-        dist.all_gather_into_tensor(g, t)
+        dist.all_gather_into_tensor(g, t, group=_GROUP)
         if all(c == mx for c in counts_l):
             outs.append(g.to(dev))
         else:

@@ -8,7 +8,9 @@ worker. Bodies do their local (collective-free) work first; the per-rank
 errors are then exchanged, so a failure on ANY rank fails the job on rank 0
 with that rank's id in the message instead of hanging the others in a
 collective. ``MI355X_FAULT=rank:K[:stage[:times]]`` injects a
-failure on rank K for tests.
+failure on rank K for tests; a ``:device`` kind raises a HIP-style device
+fault, which drops that rank from the DP group (elastic shrink, SURVEY.md
+§5.3) while the job that hit it fails and names the rank.
 
 Registered bodies: ``map_classify_csv`` (C2 all-gather of top-k),
 ``risk_accumulate`` (C3 all-reduce of {count,sum,min,max}) and
@@ -25,7 +27,8 @@ import torch
 import torch.distributed as dist
 
 from ..utils.trace import span
-from .dp import all_gather_rows, broadcast_task, comm_device, is_dist, split_range, world
+from . import dp
+from .dp import all_gather_rows, broadcast_task, comm_device, is_dist, members, split_range, world
 
 _TASKS: Dict[str, Callable[[Dict[str, Any]], Any]] = {}
 _SHUTDOWN = "__shutdown__"
@@ -56,22 +59,38 @@ def init_from_env() -> None:
 _FAULT_HITS: Dict[str, int] = {}
 
 
+# substrings of a HIP/HSA device fault (vs. an ordinary Python error of the op)
+FAULT_MARKERS = ("hipError", "HIP error", "HSA_STATUS_ERROR", "illegal memory access", "device-side assert",
+                 "GPU Hang", "Memory access fault")
+
+
+def is_device_fault(msg: str) -> bool:
+    return any(m in msg for m in FAULT_MARKERS)
+
+
+class LeftGroup(Exception):
+    """This rank's device faulted and it was dropped from the DP group."""
+
+
 def maybe_inject_fault(stage: str) -> None:
-    """``MI355X_FAULT=rank:K[:stage[:times]]`` raises on rank K (optionally only
-    at ``stage`` and only the first ``times`` times — later tasks succeed, which
-    lets tests check that the DP group survives a failed job)."""
+    """``MI355X_FAULT=rank:K[:stage[:times[:device]]]`` raises on global rank K
+    (optionally only at ``stage``, only the first ``times`` times — later tasks
+    succeed, so tests can check that the DP group survives — and as a device
+    fault with ``:device``)."""
     spec = os.getenv("MI355X_FAULT", "")
     if not spec.startswith("rank:"):
         return
-    rank, _ = world()
+    rank = dist.get_rank() if is_dist() else 0
     parts = spec.split(":")
     if int(parts[1]) != rank or (len(parts) >= 3 and parts[2] not in ("", stage)):
         return
-    if len(parts) >= 4:
+    if len(parts) >= 4 and parts[3]:
         n = _FAULT_HITS.get(stage, 0)
         if n >= int(parts[3]):
             return
         _FAULT_HITS[stage] = n + 1
+    if len(parts) >= 5 and parts[4] == "device":
+        raise RuntimeError(f"hipErrorLaunchFailure: injected device fault ({spec}) at {stage}")
     raise RuntimeError(f"injected fault ({spec}) at {stage}")
 
 
@@ -91,15 +110,22 @@ def _check_errors(err: str) -> None:
         return
     rank, ws = world()
     errs = [None] * ws
-    dist.all_gather_object(errs, err)
-    bad = [(r, e) for r, e in enumerate(errs) if e]
+    dist.all_gather_object(errs, err, group=dp.group())
+    glob = members()  # group index -> global rank (errors name global ranks)
+    bad = [(glob[r], e) for r, e in enumerate(errs) if e]
     if not bad:
         return
     if len(bad) == ws and len(set(e for _, e in bad)) == 1:
         typ, _, msg = bad[0][1].partition(": ")
         if typ in _ERR_TYPES:
             raise _ERR_TYPES[typ](msg)
-    raise RuntimeError("; ".join(f"rank {r}: {e}" for r, e in bad))
+    msg = "; ".join(f"rank {r}: {e}" for r, e in bad)
+    faulted = [r for r, e in bad if is_device_fault(e)]
+    if faulted and os.getenv("ATPU_ELASTIC", "1") != "0" and dp.shrink(faulted):
+        if dist.get_rank() in faulted:
+            raise LeftGroup(msg)
+        msg += f" (dropped from the DP group: ranks {faulted}; DP world now {len(members())})"
+    raise RuntimeError(msg)
 
 
 def run_collective(name: str, payload: Dict[str, Any]) -> Any:
@@ -124,6 +150,9 @@ def worker_loop() -> int:
             break
         try:
             run_collective(desc["op"], desc["payload"])
+        except LeftGroup as exc:
+            print(f"[agent-mi355x] dp worker rank={rank} left the DP group after a device fault: {exc}", flush=True)
+            break
         except Exception as exc:  # rank 0 reports; keep serving
             print(f"[agent-mi355x] dp worker rank={rank} task {desc.get('op')} failed: {exc}", flush=True)
     if is_dist():
@@ -226,8 +255,8 @@ def risk_task(payload: Dict[str, Any]) -> Any:
         s = stats.to(cdev)
         sums = s[:2].clone()
         ext = torch.stack([s[3], -s[2]])  # max, -min -> one MAX all-reduce
-        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
-        dist.all_reduce(ext, op=dist.ReduceOp.MAX)
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=dp.group())
+        dist.all_reduce(ext, op=dist.ReduceOp.MAX, group=dp.group())
         stats = torch.stack([sums[0], sums[1], -ext[1], ext[0]]).cpu()
     else:
         stats = stats.cpu()

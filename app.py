@@ -347,20 +347,31 @@ class Agent:
         else:
             log_every("exec", f"{LOG} FAIL job={job_id} op={op} ms={ms:.1f} err={err}")
 
-    _FAULT_MARKERS = ("hipError", "HIP error", "HSA_STATUS_ERROR", "illegal memory access",
-                      "device-side assert", "GPU Hang", "Memory access fault")
-
     def _note_device_fault(self, msg: str) -> None:
-        """A HIP fault marks this agent's device unhealthy and re-advertises the profile."""
-        if self.health is None or not any(m in msg for m in self._FAULT_MARKERS):
+        """A HIP fault marks the device unhealthy and re-advertises the profile.
+
+        DP errors name global ranks (``rank K: ...``, one process per GPU, so
+        rank K drives device K); a fault without a rank prefix is this
+        process's own device."""
+        if self.health is None:
             return
+        import re
+
+        from agent_tpu_amd.parallel.dp_ops import is_device_fault
         from agent_tpu_amd.runtime import health
 
-        dev = int(os.getenv("LOCAL_RANK", "0"))
-        health.mark_unhealthy(dev, msg[:200])
-        self.health = health.last()
-        self.profile = worker_profile(self.health)
-        print(f"{LOG} device {dev} marked unhealthy: {msg[:200]}", flush=True)
+        parts = re.split(r"(?:^|; )rank (\d+): ", msg)
+        if len(parts) > 1:
+            found = [(int(parts[i]), parts[i + 1]) for i in range(1, len(parts) - 1, 2)]
+        else:
+            found = [(int(os.getenv("LOCAL_RANK", "0")), msg)]
+        hit = [(dev, m) for dev, m in found if is_device_fault(m)]
+        for dev, m in hit:
+            health.mark_unhealthy(dev, m[:200])
+            print(f"{LOG} device {dev} marked unhealthy: {m[:200]}", flush=True)
+        if hit:
+            self.health = health.last()
+            self.profile = worker_profile(self.health)
 
     def loop(self) -> None:
         while _running:

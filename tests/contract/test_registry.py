@@ -92,3 +92,26 @@ def test_every_op_has_a_contract():
         assert text.startswith("# ") and "— Contract (v0)" in text.splitlines()[0], path
         for sec in ("## Purpose", "## Inputs (payload)", "## Outputs", "## Notes"):
             assert sec in text, (path, sec)
+
+
+def test_device_fault_marks_the_faulting_ranks_device(monkeypatch):
+    """DP errors name global ranks ("rank K: ..."; rank K drives device K): a
+    HIP fault on rank 2 marks device 2, an ordinary error on rank 1 marks
+    nothing, and an un-prefixed fault marks this process's own device."""
+    import types
+
+    import app
+    from agent_tpu_amd.runtime import health
+
+    monkeypatch.setattr(health, "_unhealthy", {})
+    monkeypatch.setattr(health, "_last", {"ok": True, "devices": [], "healthy": [0, 1, 2, 3], "unhealthy": {}})
+    monkeypatch.setattr(app, "worker_profile", lambda h: {"health": h})
+    me = types.SimpleNamespace(health=health.last(), profile=None)
+    app.Agent._note_device_fault(me, "rank 1: ValueError: bad; rank 2: RuntimeError: hipErrorLaunchFailure: boom")
+    assert sorted(health._unhealthy) == [2] and health.last()["healthy"] == [0, 1, 3]
+    assert me.profile == {"health": health.last()}
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    app.Agent._note_device_fault(me, "RuntimeError: HIP error: illegal memory access")
+    assert sorted(health._unhealthy) == [2, 3]
+    app.Agent._note_device_fault(me, "ValueError: payload.values must be a list")
+    assert sorted(health._unhealthy) == [2, 3]

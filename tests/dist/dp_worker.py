@@ -123,6 +123,38 @@ def scen_summarize():
     return out
 
 
+def scen_shrink():
+    """Elastic recovery: a device fault on rank 2 fails that job (naming rank 2),
+    drops rank 2 from the DP group, and the next jobs run on ranks {0, 1}."""
+    rank, ws = dp.world()
+    if rank != 0:
+        dp_ops.worker_loop()
+        return None
+    from ops.risk_accumulate import risk_accumulate
+
+    vals = [((i * 7919) % 1000) / 7.0 - 50.0 for i in range(1003)]
+    out = {}
+    try:
+        dp_ops.dispatch("risk_accumulate", {"values": vals})
+        out["err"] = None
+    except RuntimeError as exc:
+        out["err"] = str(exc)
+    out["members"] = dp.members()
+    out["lost"] = dp.lost_ranks()
+    got = dp_ops.dispatch("risk_accumulate", {"values": vals})
+    ref = risk_accumulate({"values": vals})
+    out["after_ok"] = got["count"] == ref["count"] and abs(got["sum"] - ref["sum"]) < 1e-9
+    out["after_world"] = got["dp_world_size"]
+    # a plain (non-device) failure on a survivor does not shrink the group
+    try:
+        dp_ops.dispatch("risk_accumulate", {"values": "bad"})
+    except ValueError as exc:
+        out["bad"] = str(exc)
+    out["members_after_bad"] = dp.members()
+    dp_ops.shutdown_workers()
+    return out
+
+
 def main():
     scen = sys.argv[1]
     dist.init_process_group("gloo")
@@ -130,7 +162,7 @@ def main():
         res = globals()[f"scen_{scen}"]()
     finally:
         if dist.is_initialized():
-            if scen not in ("risk", "fault", "summarize"):  # worker_loop ranks already left the group
+            if scen not in ("risk", "fault", "summarize", "shrink"):  # worker_loop ranks already left the group
                 dist.barrier()
             dist.destroy_process_group()
     if int(os.environ.get("RANK", "0")) == 0:

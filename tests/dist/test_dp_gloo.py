@@ -84,3 +84,16 @@ def test_summarize_dp_matches_single_process():
     assert dp["summaries"] == ref
     assert "allgather_ms" in dp["timing_ms"] and dp["model"] == "t5-tiny"
     assert res["single_dp"]["summary"] == ref[0] and "summaries" not in res["single_dp"]
+
+
+def test_device_fault_shrinks_dp_world():
+    """SURVEY.md §5.3 elastic recovery: rank 2's device fault fails the job that
+    hit it, rank 2 leaves the DP group, and later jobs run (and shard) over the
+    two healthy ranks; an ordinary op error does not shrink the group."""
+    res = run_ranks("shrink", 3, {"MI355X_FAULT": "rank:2:risk:1:device"})
+    assert res["err"] is not None and "rank 2" in res["err"] and "hipError" in res["err"]
+    assert "dropped from the DP group" in res["err"]
+    assert res["members"] == [0, 1] and res["lost"] == [2]
+    assert res["after_ok"] and res["after_world"] == 2
+    assert res["bad"] == "payload.values must be a list"
+    assert res["members_after_bad"] == [0, 1]
