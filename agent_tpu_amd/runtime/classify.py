@@ -18,6 +18,7 @@ batch instead of ~100.
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -55,7 +56,7 @@ class RunStats:
 class ClassifyEngine:
     def __init__(self, cfg: BertConfig, pack: ParamPack, device: torch.device, batch_rows: int = 512,
                  seq_len: int = 128, topk: int = 5, max_row_bytes: int = DEFAULT_MAX_ROW_BYTES,
-                 use_graph: bool = True, slots: int = 2):
+                 use_graph: bool = True, slots: int = 2, concurrent: Optional[bool] = None):
         if pack.buffer.device != device:
             pack = pack.to(device)
         self.cfg, self.pack, self.device = cfg, pack, device
@@ -68,17 +69,30 @@ class ClassifyEngine:
         cap = self.B * self.max_row_bytes
         self.text = [torch.empty(cap, dtype=torch.uint8, device=device) for _ in range(slots)]
         self.offs = [torch.zeros(self.B + 1, dtype=torch.int32, device=device) for _ in range(slots)]
-        self.ids = torch.zeros((self.B, self.S), dtype=torch.int32, device=device)
-        self.lens = torch.zeros(self.B, dtype=torch.int32, device=device)
+        # per-slot token buffers: with concurrent slots two batches are in flight at once
+        self.ids_s = [torch.zeros((self.B, self.S), dtype=torch.int32, device=device) for _ in range(slots)]
+        self.lens_s = [torch.zeros(self.B, dtype=torch.int32, device=device) for _ in range(slots)]
+        self.ids, self.lens = self.ids_s[0], self.lens_s[0]
         self.copy_stream = torch.cuda.Stream(device) if device.type == "cuda" else None
+        # Concurrent slots: batch i runs on compute stream i % slots, so the
+        # encoders of two consecutive batches overlap on the GPU. A GEMM block
+        # fills a CU (128 KiB LDS, full register file), so overlap happens at CU
+        # granularity: the memory-bound kernels (attention, LayerNorm, GEMM store
+        # tails) of one batch run on some CUs while the other batch's GEMM main
+        # loops run on the rest, instead of every CU alternating between regimes.
+        if concurrent is None:
+            concurrent = os.getenv("ATPU_CONCURRENT_SLOTS", "1") not in ("0", "false", "no")
+        self.concurrent = bool(concurrent) and device.type == "cuda" and slots > 1
+        self.compute_streams = [torch.cuda.Stream(device) for _ in range(slots)] if self.concurrent else None
         self._graphs: Dict[int, Tuple["torch.cuda.CUDAGraph", Tuple[torch.Tensor, ...]]] = {}
         self._stager = None
 
     # ------------------------------------------------------------ device step
     def _step(self, slot: int, rows: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        ids, lens = self.ids_s[slot], self.lens_s[slot]
         ops.tokenize(self.text[slot], self.offs[slot], self.S, self.cfg.vocab_size, self.max_row_bytes,
-                     ids=self.ids, lens=self.lens, rows=rows)
-        return self.model.forward(self.ids[:rows], self.lens[:rows], self.k)
+                     ids=ids, lens=lens, rows=rows)
+        return self.model.forward(ids[:rows], lens[:rows], self.k)
 
     def _graph_step(self, slot: int):
         if slot not in self._graphs:
@@ -148,8 +162,12 @@ class ClassifyEngine:
         if n == 0:
             return out_idx, out_score, stats
         st = self._get_stager()
-        compute = torch.cuda.current_stream(dev)
-        cs, ks = int(self.copy_stream.cuda_stream), int(compute.cuda_stream)
+        caller = torch.cuda.current_stream(dev)
+        streams = self.compute_streams or [caller] * self.n_slots
+        for s in streams:
+            if s is not caller:
+                s.wait_stream(caller)  # out_* and earlier work were enqueued on the caller's stream
+        cs = int(self.copy_stream.cuda_stream)
         nb = (n + self.B - 1) // self.B
         t0 = time.perf_counter()
         tm = stats.timing_ms  # host-side enqueue time per stage (+ roctx ranges under MI355X_TRACE=1)
@@ -162,16 +180,22 @@ class ClassifyEngine:
                 with span("csv_stage", tm):
                     st.submit((i + 1) % self.n_slots, table, b1, min(self.B, start + n - b1), col,
                               self.max_row_bytes, host_threads)
-            with span("h2d_upload", tm):
-                rows, _ = st.upload(slot, self.text[slot].data_ptr(), self.text[slot].numel(),
-                                    self.offs[slot].data_ptr(), cs, ks)
-            with span("encoder_launch", tm):
-                _, idx, sc = self.run_slot(slot, int(rows))
-            st.release(slot, ks)
-            r0 = i * self.B
-            out_idx[r0:r0 + rows].copy_(idx[:rows], non_blocking=True)
-            out_score[r0:r0 + rows].copy_(sc[:rows], non_blocking=True)
+            stream = streams[slot]
+            ks = int(stream.cuda_stream)
+            with torch.cuda.stream(stream):
+                with span("h2d_upload", tm):
+                    rows, _ = st.upload(slot, self.text[slot].data_ptr(), self.text[slot].numel(),
+                                        self.offs[slot].data_ptr(), cs, ks)
+                with span("encoder_launch", tm):
+                    _, idx, sc = self.run_slot(slot, int(rows))
+                st.release(slot, ks)
+                r0 = i * self.B
+                out_idx[r0:r0 + rows].copy_(idx[:rows], non_blocking=True)
+                out_score[r0:r0 + rows].copy_(sc[:rows], non_blocking=True)
             stats.batches += 1
+        for s in streams:
+            if s is not caller:
+                caller.wait_stream(s)
         with span("device_drain", tm):
             torch.cuda.synchronize(dev)
         stats.rows = n

@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--num-labels", type=int, default=2)
     ap.add_argument("--words-per-row", type=int, default=150)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--slots", type=int, default=int(os.environ.get("BENCH_SLOTS", "2")),
+                    help="staging slots = batches in flight (each on its own compute stream)")
     ap.add_argument("--csv", default="")
     # rehearsal only: "gloo" lets >1 ranks share one GPU (RCCL refuses duplicate devices)
     ap.add_argument("--dist-backend", default=os.environ.get("BENCH_DIST_BACKEND", "nccl"))
@@ -91,7 +93,8 @@ def main() -> int:
     torch.cuda.synchronize(dev)
     bcast_ms = (time.perf_counter() - t_b) * 1000.0
 
-    eng = ClassifyEngine(cfg, pack, dev, batch_rows=B, seq_len=a.seq_len, topk=a.topk, use_graph=not a.no_graph)
+    eng = ClassifyEngine(cfg, pack, dev, batch_rows=B, seq_len=a.seq_len, topk=a.topk, use_graph=not a.no_graph,
+                          slots=a.slots)
 
     def run(start_batch: int, nbatches: int):
         idx, score, _ = eng.classify_table(table, start_batch * B, nbatches * B, col)
@@ -146,6 +149,7 @@ def main() -> int:
                 "num_labels": cfg.num_labels,
                 "topk": min(a.topk, cfg.num_labels),
                 "hipgraph": not a.no_graph,
+                "concurrent_batches": a.slots if eng.concurrent else 1,
                 "weight_broadcast_ms": round(bcast_ms, 2),
                 "last_layer_cls_only": cls_only,
                 "achieved_tflops_per_gpu": round(flops / world / 1e12, 1),

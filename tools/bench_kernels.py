@@ -38,7 +38,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
-    ap.add_argument("--variants", action="store_true", help="also time the 256b GEMM schedule (vs 256p)")
+    ap.add_argument("--variants", default="",
+                    help="comma list of extra 256x256 GEMM variants to time (0=256b, 2=256p+nt stores)")
     a = ap.parse_args()
     from agent_tpu_amd._native import native
 
@@ -79,16 +80,18 @@ def main():
                           lambda: torch.nn.functional.layer_norm(x768, (H,), gam.bfloat16(), bet.bfloat16(), 1e-12),
                           0)
     sel = [k for k in cases if not a.only or k in a.only.split(",")]
-    times = {k: {"ours": [], "lib": [], "ours_256b": []} for k in sel}
+    variants = [int(v) for v in a.variants.split(",") if v]
+    times = {k: {"ours": [], "lib": [], **{f"v{v}": [] for v in variants}} for k in sel}
     for rd in range(a.rounds):
         for k in (sel if rd % 2 == 0 else list(reversed(sel))):
             ours, lib, _ = cases[k]
             times[k]["ours"].append(timeit(ours, a.iters))
             times[k]["lib"].append(timeit(lib, a.iters))
-            if a.variants and k.startswith("gemm"):
-                nat.gemm_256_variant(0)
-                times[k]["ours_256b"].append(timeit(ours, a.iters))
-                nat.gemm_256_variant(1)
+            if k.startswith("gemm"):
+                for v in variants:
+                    nat.gemm_256_variant(v)
+                    times[k][f"v{v}"].append(timeit(ours, a.iters))
+                    nat.gemm_256_variant(1)
     for k in sel:
         fl = cases[k][2]
         o, l = statistics.median(times[k]["ours"]), statistics.median(times[k]["lib"])
@@ -96,8 +99,9 @@ def main():
         if fl:
             out[k]["ours_tflops"] = round(fl / o / 1e9, 1)
             out[k]["lib_tflops"] = round(fl / l / 1e9, 1)
-        if times[k]["ours_256b"]:
-            out[k]["ours_256b_tflops"] = round(fl / statistics.median(times[k]["ours_256b"]) / 1e9, 1)
+        for v in variants:
+            if times[k][f"v{v}"]:
+                out[k][f"v{v}_tflops"] = round(fl / statistics.median(times[k][f"v{v}"]) / 1e9, 1)
         print(k, json.dumps(out[k]), flush=True)
     print("JSON", json.dumps(out))
 
