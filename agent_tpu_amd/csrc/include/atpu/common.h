@@ -97,6 +97,14 @@ __device__ __forceinline__ void gelu_fast8(float (&v)[8]) {
 __device__ __forceinline__ float bf2f(bf16 x) { return static_cast<float>(x); }
 __device__ __forceinline__ bf16 f2bf(float x) { return static_cast<bf16>(x); }
 
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// two fp32 -> one dword of bf16 (RNE; one v_cvt_pk_bf16_f32), lo in bits 0-15
+__device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
+  return __builtin_bit_cast(unsigned, bf16x2{f2bf(lo), f2bf(hi)});
+}
+
 // Bijective XCD-aware block remap (guide §5 "XCD swizzle must be bijective"):
 // blocks that the dispatcher places on one XCD (b % 8 equal) get a contiguous
 // range of logical tile ids, so neighbouring tiles share that XCD's L2.

@@ -26,6 +26,7 @@
 #include "atpu/common.h"
 #include "atpu/kernels.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <string>
 #include <type_traits>
@@ -403,6 +404,110 @@ __global__ __launch_bounds__(512, 2) void gemm256b_kernel(
 // phase r is safe after reads at phase <= r-2 (every restage is >= 2 phases
 // after the quarter's last read in the previous K-tile).
 // ============================================================================
+// Epilogue of the 256x256 kernels: wave (wm, wn) owns C rows m0+wm*128 .. +128,
+// columns n0+wn*64 .. +64; acc[i][j] = the 16x16 fragment (row block i, col block j).
+// FULL: every row of the tile is < M (no per-store bounds test; the persistent
+// kernel also relies on every wave issuing exactly 16 stores).
+// ABL (timing-only ablations, results WRONG): 1 = all VALU work, no stores;
+// 2 = stores of the raw accumulator bits, no VALU work.
+// lds_bias: when non-null, the tile's 256 bias values staged in LDS (read
+// there instead of global memory: no exposed load round trip in the tail).
+template <int EPI, bool FULL = false, int ABL = 0, bool NT = false>
+__device__ __forceinline__ void epilogue_256(const f32x4 (&acc)[8][4], int m0, int n0, int wm, int wn, int lane,
+                                             bf16* __restrict__ C, int ldc, const float* __restrict__ bias,
+                                             const bf16* __restrict__ R, int ldr, int M,
+                                             const float* lds_bias = nullptr) {
+  const int fr = lane & 15, fc = lane >> 4;
+  // ---- epilogue, widened (guide T21 for the 16x16 layout). Lane (fr, fc) owns
+  // rows (2p)*16+fr and (2p+1)*16+fr, columns j*16+fc*4..+3 of fragments
+  // (2p, j), (2p+1, j). Bias, activation and residual are applied there in
+  // fp32, both fragments are packed to bf16 pairs, and ONE v_permlane16_swap
+  // per dword pair leaves every lane 8 consecutive bf16 columns of one row
+  // (even fc: row 2p, odd fc: row 2p+1; probed: tools/probes/permlane_probe.hip)
+  // -> one 16-B store. Swapping packed bf16 pairs instead of fp32 values halves
+  // the swaps and needs no operand laundering (distinct scalars, "+v").
+  const int hi = fc & 1, cq = (fc >> 1) * 8;  // stored row parity, stored column half
+  // residual: loaded as 16-B rows in the STORED layout (one row pair ahead of
+  // its use: 2 x 16 VGPRs live, the persistent kernel keeps its staging state
+  // through the epilogue), then taken to the fragment layout by the same
+  // (involutive) dword swap the outputs go through
+  u32x4 res[4][4];
+  auto load_res = [&](int pp) {
+    if constexpr (EPI & kEpiResidual) {
+      const int m = min(m0 + wm * 128 + (2 * pp + hi) * 16 + fr, M - 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        res[pp][j] = *reinterpret_cast<const u32x4*>(R + (size_t)m * ldr + n0 + wn * 64 + j * 16 + cq);
+    }
+  };
+  load_res(0);
+  f32x4 b4[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = wn * 64 + j * 16 + fc * 4;
+    if constexpr (EPI & kEpiBias) {
+      b4[j] = lds_bias ? *reinterpret_cast<const f32x4*>(lds_bias + c) : *reinterpret_cast<const f32x4*>(bias + n0 + c);
+    } else {
+      b4[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  const bool full_tile = m0 + 256 <= M;  // uniform: no per-store bounds branch
+  // row pair outer, column fragment inner: the 4 consecutive 16-B stores of a
+  // lane cover its row's whole 128-B line segment (write combining in L2)
+#pragma unroll
+  for (int pp = 0; pp < 4; ++pp) {
+    const int m = m0 + wm * 128 + (2 * pp + hi) * 16 + fr;
+    if (pp + 1 < 4) load_res(pp + 1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + cq;
+      if constexpr (ABL == 2) {
+        // both fragments feed the store (else half the MFMAs are dead code)
+        const u32x4 a = __builtin_bit_cast(u32x4, acc[2 * pp][j]) ^ __builtin_bit_cast(u32x4, acc[2 * pp + 1][j]);
+        *reinterpret_cast<u32x4*>(C + (size_t)m * ldc + n) = a;
+        continue;
+      }
+      float v[8];  // [0..3] row 2p, [4..7] row 2p+1, columns fc*4..+3
+      const f32x4 lo4 = acc[2 * pp][j] + b4[j], hi4 = acc[2 * pp + 1][j] + b4[j];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = lo4[e], v[4 + e] = hi4[e];
+      if constexpr (EPI & kEpiGelu) gelu_fast8(v);
+      if constexpr (EPI & kEpiTanh) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = tanhf(v[e]);
+      }
+      if constexpr (EPI & kEpiRelu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if constexpr (EPI & kEpiResidual) {
+        unsigned r0 = res[pp][j][0], r1 = res[pp][j][1], r2 = res[pp][j][2], r3 = res[pp][j][3];
+        asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %2\n\tv_permlane16_swap_b32 %1, %3"
+                     : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3));
+        const unsigned rr[4] = {r0, r1, r2, r3};  // row 2p cols 0-3 | row 2p+1 cols 0-3
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[2 * e] += __builtin_bit_cast(float, rr[e] << 16);
+          v[2 * e + 1] += __builtin_bit_cast(float, rr[e] & 0xffff0000u);
+        }
+      }
+      unsigned l0 = pack_bf16x2(v[0], v[1]), l1 = pack_bf16x2(v[2], v[3]);
+      unsigned h0 = pack_bf16x2(v[4], v[5]), h1 = pack_bf16x2(v[6], v[7]);
+      asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %2\n\tv_permlane16_swap_b32 %1, %3"
+                   : "+v"(l0), "+v"(l1), "+v"(h0), "+v"(h1));
+      if constexpr (ABL == 1) {
+        asm volatile("" ::"v"(l0), "v"(l1), "v"(h0), "v"(h1));
+        continue;
+      }
+      if (FULL || full_tile || m < M) {
+        u32x4* cp = reinterpret_cast<u32x4*>(C + (size_t)m * ldc + n);
+        if constexpr (NT) __builtin_nontemporal_store(u32x4{l0, l1, h0, h1}, cp);
+        else *cp = u32x4{l0, l1, h0, h1};
+      }
+    }
+  }
+}
+
 // DBG (timing-only ablation, results WRONG): 1 = skip the epilogue (acc kept live)
 template <int EPI, int DBG = 0>
 __global__ __launch_bounds__(512, 1) void gemm256p_kernel(
@@ -554,83 +659,7 @@ __global__ __launch_bounds__(512, 1) void gemm256p_kernel(
       for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
     return;
   }
-  // the last MFMAs' results are read by inline-asm v_permlane below, which the
-  // hazard recognizer cannot see: pad the MFMA-write -> VALU-read window
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-
-  // ---- epilogue, widened (guide T21 for the 16x16 layout): v_permlane16_swap
-  // of fragments (2p, j) and (2p+1, j) leaves every lane with 8 consecutive
-  // fp32 columns of ONE row -> 16-B residual loads and 16-B stores (half the
-  // VMEM instructions of the 8-B row-per-lane tail) ----
-  const int hi = fc & 1, cq = (fc >> 1) * 8;  // row parity within the pair, column half
-  bf16x8 res[4][4];
-  if constexpr (EPI & kEpiResidual) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int pp = 0; pp < 4; ++pp) {
-        const int m = min(m0 + wm * 128 + (2 * pp + hi) * 16 + fr, M - 1);
-        res[j][pp] = *reinterpret_cast<const bf16x8*>(R + (size_t)m * ldr + n0 + wn * 64 + j * 16 + cq);
-      }
-  }
-  f32x4 bias8[4][2];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = n0 + wn * 64 + j * 16 + cq;
-    if constexpr (EPI & kEpiBias) {
-      bias8[j][0] = *reinterpret_cast<const f32x4*>(bias + n);
-      bias8[j][1] = *reinterpret_cast<const f32x4*>(bias + n + 4);
-    } else {
-      bias8[j][0] = bias8[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-  const bool full_tile = m0 + 256 <= M;  // uniform: no per-store bounds branch
-  // row pair outer, column fragment inner: the 4 consecutive 16-B stores of a
-  // lane cover its row's whole 128-B line segment (write combining in L2)
-#pragma unroll
-  for (int pp = 0; pp < 4; ++pp) {
-    const int m = m0 + wm * 128 + (2 * pp + hi) * 16 + fr;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + cq;
-      const f32x4 lo4 = acc[2 * pp][j], hi4 = acc[2 * pp + 1][j];
-      float v[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        // v_permlane16_swap (odd 16-lane rows of x <-> even rows of y): the
-        // even lane keeps row 2p (own cols 0-3 + partner's 4-7), the odd lane
-        // row 2p+1 (semantics probed: tools/probes/permlane_probe.hip).
-        // Operands are laundered through v_mov into fresh early-clobber
-        // registers: handing element extracts of the accumulator tuples to
-        // the swap directly got both operands allocated to one register.
-        unsigned x, y;
-        asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %3\n\ts_nop 1\n\tv_permlane16_swap_b32 %0, %1"
-                     : "=&v"(x), "=&v"(y)
-                     : "v"(lo4[e]), "v"(hi4[e]));
-        v[e] = __builtin_bit_cast(float, x) + bias8[j][0][e];
-        v[4 + e] = __builtin_bit_cast(float, y) + bias8[j][1][e];
-      }
-      if constexpr (EPI & kEpiGelu) gelu_fast8(v);
-      if constexpr (EPI & kEpiTanh) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = tanhf(v[e]);
-      }
-      if constexpr (EPI & kEpiRelu) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-      }
-      if constexpr (EPI & kEpiResidual) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += bf2f(res[j][pp][e]);
-      }
-      bf16x8 o;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e]);
-      if (full_tile || m < M) *reinterpret_cast<bf16x8*>(C + (size_t)m * ldc + n) = o;
-    }
-  }
+  epilogue_256<EPI>(acc, m0, n0, wm, wn, lane, C, ldc, bias, R, ldr, M);
 }
 
 void launch_256p(const GemmArgs& g, hipStream_t s) {
@@ -662,6 +691,365 @@ void launch_256p(const GemmArgs& g, hipStream_t s) {
       throw std::invalid_argument("atpu: unsupported GEMM epilogue " + std::to_string(g.epi));
   }
 #undef ATPU_G256P
+}
+
+
+
+// Full-line epilogue of the persistent kernel ("line"): the wave's 128 x 64
+// output (one 128-B line per row) goes out as 16 stores of 8 rows x 128 B
+// FULL lines, after an LDS transpose through a private 2 KiB scratch per wave
+// (16 rows x 128 B, 16-B chunks XOR-swizzled by row & 7). Per 16-row block i:
+//   residual: 2 x 16-B full-line loads (issued one block ahead) -> LDS ->
+//             8-B reads in the fragment layout -> added in fp32
+//   output:   acc + bias (+act) (+res) -> bf16 -> 4 x ds_write_b64 in the
+//             fragment layout -> 2 x ds_read_b128 in line layout -> 2 stores
+// The fragment-layout 8-B accesses are 2-way bank conflicted (rows r, r+8
+// share a swizzle), the line-layout ones conflict-free. DS ops of one wave
+// execute in order, so the scratch needs no barrier, only lgkmcnt waits.
+template <int EPI, bool NT>
+__device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int m0, int n0, int wm, int wn, int lane,
+                                                  bf16* __restrict__ C, int ldc, const bf16* __restrict__ R, int ldr,
+                                                  const float* lds_bias, char* scratch) {
+  const int fr = lane & 15, fc = lane >> 4;
+  f32x4 b4[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if constexpr (EPI & kEpiBias) b4[j] = *reinterpret_cast<const f32x4*>(lds_bias + wn * 64 + j * 16 + fc * 4);
+    else b4[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  // line layout: lane -> row lr (+8 for the second half), 16-B chunk lc
+  const int lr = lane >> 3, lc = lane & 7;
+  const int line_off0 = lr * 128 + ((lc ^ (lr & 7)) << 4);
+  const int line_off1 = (lr + 8) * 128 + ((lc ^ ((lr + 8) & 7)) << 4);
+  // fragment layout: row fr, bytes j*32 + fc*8 (16-B chunk j*2 + fc/2, half fc&1)
+  auto frag_off = [&](int j) { return fr * 128 + (((j * 2 + (fc >> 1)) ^ (fr & 7)) << 4) + (fc & 1) * 8; };
+  const size_t row0 = (size_t)(m0 + wm * 128);
+  const int col = n0 + wn * 64 + lc * 8;
+  u32x4 res[2][2];
+  auto load_res = [&](int i) {
+    if constexpr (EPI & kEpiResidual) {
+      const bf16* rp = R + (row0 + i * 16 + lr) * ldr + col;
+      res[i & 1][0] = *reinterpret_cast<const u32x4*>(rp);
+      res[i & 1][1] = *reinterpret_cast<const u32x4*>(rp + 8 * (size_t)ldr);
+    }
+  };
+  load_res(0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i + 1 < 8) load_res(i + 1);
+    float v[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 t = acc[i][j] + b4[j];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[j][e] = t[e];
+    }
+    if constexpr (EPI & kEpiGelu) {
+      gelu_fast8(*reinterpret_cast<float(*)[8]>(&v[0][0]));
+      gelu_fast8(*reinterpret_cast<float(*)[8]>(&v[2][0]));
+    }
+    if constexpr (EPI & kEpiTanh) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[j][e] = tanhf(v[j][e]);
+    }
+    if constexpr (EPI & kEpiRelu) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[j][e] = fmaxf(v[j][e], 0.f);
+    }
+    if constexpr (EPI & kEpiResidual) {
+      *reinterpret_cast<u32x4*>(scratch + line_off0) = res[i & 1][0];
+      *reinterpret_cast<u32x4*>(scratch + line_off1) = res[i & 1][1];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bf16x4 r = *reinterpret_cast<const bf16x4*>(scratch + frag_off(j));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[j][e] += bf2f(r[e]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const unsigned p0 = pack_bf16x2(v[j][0], v[j][1]), p1 = pack_bf16x2(v[j][2], v[j][3]);
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<u32x2*>(scratch + frag_off(j)) = u32x2{p0, p1};
+    }
+    const u32x4 o0 = *reinterpret_cast<const u32x4*>(scratch + line_off0);
+    const u32x4 o1 = *reinterpret_cast<const u32x4*>(scratch + line_off1);
+    u32x4* cp = reinterpret_cast<u32x4*>(C + (row0 + i * 16 + lr) * ldc + col);
+    u32x4* cp1 = reinterpret_cast<u32x4*>(C + (row0 + i * 16 + lr + 8) * ldc + col);
+    if constexpr (NT) {
+      __builtin_nontemporal_store(o0, cp);
+      __builtin_nontemporal_store(o1, cp1);
+    } else {
+      *cp = o0;
+      *cp1 = o1;
+    }
+  }
+}
+
+// ============================================================================
+// 256x256 PERSISTENT ping-pong kernel ("256s"): the 256p schedule with one
+// workgroup per CU walking its tiles, and the LDS-DMA stream running on from
+// the last K-tile of a tile into K-tile 0 of the next. What that buys over one
+// launch per tile (hipBLASLt's stream-K kernels do the same at these shapes):
+//  * K-tile 0 of tile i+1 is staged during the last K-tile of tile i and lands
+//    while tile i's epilogue runs: no exposed prologue per tile;
+//  * the epilogue's 16 stores per wave stay in flight into the first phases
+//    of tile i+1: the waits of its phases 0-1 allow them (vmcnt counts every
+//    VMEM op of the wave in issue order, and K-tile 0 was issued before them);
+//  * no workgroup launch / drain per tile.
+// Tile walk: virtual block v = blockIdx.x + it * gridDim.x (gridDim.x % 8 == 0
+// keeps v % 8 = the XCD), tile = xcd_remap(v, tiles): each XCD walks a
+// contiguous tile range, N-fastest, exactly as the one-launch-per-tile grid.
+// The phase/quarter program and its hazard argument are those of 256p; the
+// epilogue has no barrier, so the two wave groups stay staggered across tiles.
+// ============================================================================
+// DBG (timing-only ablation, results WRONG): 1 = skip the epilogue (acc kept live)
+template <int EPI, int DBG = 0, bool NT = false, bool LINE = false>
+__global__ __launch_bounds__(512, 1) void gemm256s_kernel(
+    const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C, int ldc,
+    const float* __restrict__ bias, const bf16* __restrict__ R, int ldr, int M, int N, int K) {
+  using namespace g2;
+  constexpr int kImg = 256 * 128;
+  constexpr int kEpiOps = 16;  // VMEM ops per wave the epilogue leaves in flight (16-B stores)
+  constexpr int kBiasOff = 2 * 2 * kImg;  // [2 tiles][256] fp32 bias after the operand buffers
+  // ONE __shared__ array: a second LDS object makes hipcc drain vmcnt before ds_reads
+  constexpr int kEpiOff = kBiasOff + 2 * 256 * 4;  // LINE epilogue: 2 KiB scratch per wave
+  __shared__ __attribute__((aligned(16))) char lds[kEpiOff + (LINE ? 8 * 2048 : 0)];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntn = N / 256, ntm = (M + 255) / 256, ntiles = ntm * ntn;
+  const int G = gridDim.x;
+  const int wm = wave >> 2, wn = wave & 3;
+  int v = blockIdx.x;
+  if (v >= ntiles) return;
+
+  // staging rows of quarter q / instruction i (same map as 256p); the lane's
+  // row is recomputed per tile (registers are the budget here), the LDS
+  // destination is wave-uniform (scalar)
+  const int spos = lane & 7;
+  auto qrow = [&](int q, int ql) {
+    return (q == 0 || q == 3) ? (ql & 63) + (ql >> 6) * 128 + (q == 3 ? 64 : 0)
+                              : (ql & 31) + (ql >> 5) * 64 + (q == 2 ? 32 : 0);
+  };
+  int dst[4][2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) dst[q][i] = (q == 0 || q == 3 ? 0 : kImg) + qrow(q, (i * 8 + wave) * 8) * 128;
+  const bf16* src[4][2];
+  auto set_src = [&](int tm0, int tn0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = qrow(q, (i * 8 + wave) * 8 + (lane >> 3));
+        src[q][i] = (q == 0 || q == 3) ? A + (size_t)min(tm0 + r, M - 1) * lda + sw(r, spos) * 8
+                                       : Bt + (size_t)(tn0 + r) * ldb + sw(r, spos) * 8;
+      }
+  };
+  auto stage = [&](int q, int kt, int buf) {
+    char* base = lds + buf * 2 * kImg;
+    const int koff = kt * 64;
+    glds16(src[q][0] + koff, base + dst[q][0]);
+    glds16(src[q][1] + koff, base + dst[q][1]);
+  };
+
+  const int fr = lane & 15, fc = lane >> 4;
+  f32x4 acc[8][4];
+  bf16x8 af[2][4], bl[2][2], br[2][2];
+  auto read_a = [&](int buf, int qm) {
+    const char* img = lds + buf * 2 * kImg;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wm * 128 + qm * 64 + i * 16 + fr;
+        af[ks][i] = *reinterpret_cast<const bf16x8*>(img + r * 128 + sw(r, ks * 4 + fc) * 16);
+      }
+  };
+  auto read_b = [&](bf16x8 (&f)[2][2], int buf, int qn) {
+    const char* img = lds + buf * 2 * kImg + kImg;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wn * 64 + qn * 32 + j * 16 + fr;
+        f[ks][j] = *reinterpret_cast<const bf16x8*>(img + r * 128 + sw(r, ks * 4 + fc) * 16);
+      }
+  };
+  auto mma = [&](const bf16x8 (&bf)[2][2], int qm, int qn) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[qm * 4 + i][qn * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ks][j], af[ks][i], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+  };
+
+  const int nk = K / 64;
+  int tile = xcd_remap(v, ntiles);
+  int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 256;
+  set_src(m0, n0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) stage(q, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger: group 1 runs one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+#define ATPU_PS_SYNC_MMA(BF, QM, QN)                         \
+  __builtin_amdgcn_sched_barrier(0);                        \
+  __builtin_amdgcn_s_barrier();                             \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        \
+  __builtin_amdgcn_sched_barrier(0);                        \
+  __builtin_amdgcn_s_setprio(1);                            \
+  mma(BF, QM, QN);                                          \
+  __builtin_amdgcn_s_setprio(0);                            \
+  __builtin_amdgcn_sched_barrier(0);                        \
+  __builtin_amdgcn_s_barrier();                             \
+  __builtin_amdgcn_sched_barrier(0)
+
+  int buf = 0;        // LDS buffer of the current K-tile (global K-tile parity)
+  int tile_par = 0;   // bias buffer of the current tile
+  bool first = true;  // no epilogue stores in flight before the first tile
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int vn = v + G;
+    const bool has_next = vn < ntiles;
+    const int cm0 = m0, cn0 = n0;
+    for (int t = 0; t < nk; ++t) {
+      const bool last = t + 1 == nk;
+      const bool more = !last || has_next;
+      int kn = t + 1;  // K-tile staged during this one
+      if (last && has_next) {
+        // the stream runs on into K-tile 0 of the next tile
+        tile = xcd_remap(vn, ntiles);
+        m0 = (tile / ntn) * 256;
+        n0 = (tile % ntn) * 256;
+        set_src(m0, n0);
+        kn = 0;
+      }
+      const bool relax = t == 0 && !first;  // epilogue stores of the previous tile may be in flight
+      // p0
+      read_a(buf, 0);
+      read_b(bl, buf, 0);
+      if ((EPI & kEpiBias) && t == 0) {
+        // this tile's bias -> LDS (waves w, w+4 write the same 256 B: every wave
+        // issues the same op count). Only makes the waits below stricter.
+        __builtin_amdgcn_global_load_lds((const ATPU_GLOBAL_AS void*)(bias + cn0 + (wave & 3) * 64 + lane),
+                                         (ATPU_LDS_AS void*)(lds + kBiasOff + (tile_par * 256 + (wave & 3) * 64) * 4),
+                                         4, 0, 0);
+      }
+      if (more) {
+        stage(0, kn, buf ^ 1);
+        if (relax) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + kEpiOps) : "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
+      ATPU_PS_SYNC_MMA(bl, 0, 0);
+      // p1
+      read_b(br, buf, 1);
+      if (more) {
+        stage(1, kn, buf ^ 1);
+        if (relax) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + kEpiOps) : "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      ATPU_PS_SYNC_MMA(br, 0, 1);
+      // p2
+      read_a(buf, 1);
+      if (more) {
+        stage(2, kn, buf ^ 1);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      }
+      ATPU_PS_SYNC_MMA(br, 1, 1);
+      // p3
+      if (more) {
+        stage(3, kn, buf ^ 1);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      }
+      ATPU_PS_SYNC_MMA(bl, 1, 0);
+      buf ^= 1;
+    }
+    if constexpr (DBG & 1) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+    } else {
+      if constexpr (LINE)
+        epilogue_256_line<EPI, NT>(acc, cm0, cn0, wm, wn, lane, C, ldc, R, ldr,
+                                   reinterpret_cast<const float*>(lds + kBiasOff) + tile_par * 256,
+                                   lds + kEpiOff + wave * 2048);
+      else
+        epilogue_256<EPI, true, (DBG >> 1), NT>(acc, cm0, cn0, wm, wn, lane, C, ldc, bias, R, ldr, M,
+                                            reinterpret_cast<const float*>(lds + kBiasOff) + tile_par * 256);
+    }
+    if (!has_next) break;
+    v = vn;
+    first = false;
+    tile_par ^= 1;
+  }
+#undef ATPU_PS_SYNC_MMA
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // close the stagger (equal barrier counts)
+}
+
+int num_cus() {
+  static const int n = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess)
+      cus = 256;
+    return cus > 0 ? cus : 256;
+  }();
+  return n;
+}
+
+template <bool NT, bool LINE = false>
+void launch_256s(const GemmArgs& g, hipStream_t s) {
+  const int tiles = ((g.M + 255) / 256) * (g.N / 256);
+  // one workgroup per CU; a multiple of 8 so v % 8 keeps naming the XCD
+  int nb = std::min(tiles, num_cus());
+  if (nb >= 8) nb &= ~7;
+  static const int ablate = [] {
+    const char* f = std::getenv("ATPU_GEMM_ABLATE");
+    return f ? std::atoi(f) : 0;
+  }();
+  if (ablate == 4 || ablate == 5 || ablate == 6) {  // timing only: no epilogue / no stores / no VALU
+    auto k = ablate == 4 ? gemm256s_kernel<kEpiBias, 1> : ablate == 5 ? gemm256s_kernel<kEpiBias, 2>
+                                                                       : gemm256s_kernel<kEpiBias, 4>;
+    hipLaunchKernelGGL(k, dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M,
+                       g.N, g.K);
+    return;
+  }
+#define ATPU_G256S(E)                                                                                          \
+  case E:                                                                                                      \
+    hipLaunchKernelGGL((gemm256s_kernel<E, 0, NT, LINE>), dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, \
+                       g.bias, g.R, g.ldr, g.M, g.N, g.K);                                                     \
+    break;
+  switch (g.epi) {
+    ATPU_G256S(0)
+    ATPU_G256S(kEpiBias)
+    ATPU_G256S(kEpiBias | kEpiGelu)
+    ATPU_G256S(kEpiBias | kEpiTanh)
+    ATPU_G256S(kEpiBias | kEpiResidual)
+    ATPU_G256S(kEpiResidual)
+    ATPU_G256S(kEpiGelu)
+    ATPU_G256S(kEpiRelu)
+    default:
+      throw std::invalid_argument("atpu: unsupported GEMM epilogue " + std::to_string(g.epi));
+  }
+#undef ATPU_G256S
 }
 
 void launch_256b(const GemmArgs& g, hipStream_t s) {
@@ -1001,10 +1389,21 @@ void launch_tile(const GemmArgs& g, hipStream_t s) {
 }  // namespace
 
 int gemm_256_variant(int set) {
-  // 256x256 schedule: 1 = ping-pong "256p" (default), 0 = "256b"; ATPU_GEMM_256=b|p
+  // 256x256 schedule (ATPU_GEMM_256=b|p|s|l|n):
+  //   0 "256b" one K-tile per barrier pair   1 "256p" ping-pong, one launch per tile
+  //   2 "256s" persistent ping-pong, permlane epilogue
+  //   3 "256l" persistent, full-line LDS-transposed epilogue
+  //   4 "256n" = 256l with non-temporal stores (default; docs/PERF_NOTES.md)
   static int v = [] {
     const char* f = std::getenv("ATPU_GEMM_256");
-    return (f && f[0] == 'b') ? 0 : 1;
+    if (!f) return 4;
+    switch (f[0]) {
+      case 'b': return 0;
+      case 'p': return 1;
+      case 's': return 2;
+      case 'l': return 3;
+      default: return 4;
+    }
   }();
   if (set >= 0) v = set;
   return v;
@@ -1079,7 +1478,13 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
   const bool big_ok = g.N % 256 == 0 && g.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(g.C) & 15) == 0 &&
                       (!(g.epi & kEpiResidual) || (g.ldr % 8 == 0 && (reinterpret_cast<uintptr_t>(g.R) & 15) == 0));
   const bool use_big = !(g.epi & kEpiOutF32) && (forced ? (forced == 256 && big_ok) : (g.M >= 2048 && big_ok));
-  if (use_big && kernel256 == 1)
+  // 256s counts its epilogue's stores in the next tile's waits: whole row tiles only
+  const bool persistent_ok = g.M % 256 == 0;
+  if (use_big && persistent_ok && kernel256 >= 2) {
+    if (kernel256 == 2) launch_256s<false, false>(g, stream);
+    else if (kernel256 == 3) launch_256s<false, true>(g, stream);
+    else launch_256s<true, true>(g, stream);
+  } else if (use_big && kernel256 >= 1)
     launch_256p(g, stream);
   else if (use_big)
     launch_256b(g, stream);

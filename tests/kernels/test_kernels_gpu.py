@@ -70,6 +70,34 @@ def test_gemm256_exact_integers(gpu):
     assert torch.equal(y, ref)
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])  # 256b, 256p, 256s, 256l, 256n
+@pytest.mark.parametrize("M,N,K", [(8192, 2304, 768), (65536, 768, 768), (16384, 768, 3072), (4096, 3072, 64)])
+def test_gemm256_variants_exact(gpu, nat, variant, M, N, K):
+    # every 256x256 schedule on exact data; the persistent kernel walks several
+    # tiles per workgroup here (tiles > CUs), so a mis-counted wait across the
+    # tile boundary shows up as wrong tiles
+    g = torch.Generator().manual_seed(9)
+    x = torch.randint(-1, 2, (M, K), generator=g).to(torch.bfloat16)
+    w = torch.randint(-1, 2, (N, K), generator=g).to(torch.bfloat16)
+    b = torch.randint(-4, 5, (N,), generator=g).float()
+    r = torch.randint(-3, 4, (M, N), generator=g).to(torch.bfloat16)
+    xg, wg, bg, rg = x.to(gpu), w.to(gpu), b.to(gpu), r.to(gpu)
+    exact = (x.float() @ w.float().t() + b)
+    prev = nat.gemm_256_variant(-1)
+    try:
+        nat.gemm_256_variant(variant)
+        for _ in range(3):  # repeated launches: races are intermittent
+            y = ops.linear(xg, wg, bg, residual=rg).cpu().float()
+            assert torch.equal(y, (exact + r.float()).to(torch.bfloat16).float())
+            y = ops.linear(xg, wg, bg).cpu().float()
+            assert torch.equal(y, exact.to(torch.bfloat16).float())
+        yg = ops.linear(xg, wg, bg, act="gelu").cpu().float()
+        ref = torch.nn.functional.gelu(exact).to(torch.bfloat16).float()
+        assert (yg - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
+    finally:
+        nat.gemm_256_variant(prev)
+
+
 def test_gemm_strided_rows(gpu):
     # pooler case: A rows taken every S rows (CLS tokens) of a [B*S, H] tensor
     B, S, H = 37, 128, 768
