@@ -744,10 +744,7 @@ __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int 
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[j][e] = t[e];
     }
-    if constexpr (EPI & kEpiGelu) {
-      gelu_fast8(*reinterpret_cast<float(*)[8]>(&v[0][0]));
-      gelu_fast8(*reinterpret_cast<float(*)[8]>(&v[2][0]));
-    }
+    if constexpr (EPI & kEpiGelu) gelu_poly16(*reinterpret_cast<float(*)[16]>(&v[0][0]));
     if constexpr (EPI & kEpiTanh) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
