@@ -81,7 +81,10 @@ PYBIND11_MODULE(_atpu, m) {
   m.def("gemm_dec_mode", &gemm_dec_mode, py::arg("set") = -1,
         "skinny-M GEMM path: 1 = 64x64 multi-stage dec kernel, 0 = 128x128 split-K; returns the current");
   m.def("gemm_256_variant", &gemm_256_variant, py::arg("set") = -1,
-        "256x256 GEMM schedule: 1 = ping-pong (default), 0 = full-line 2-stage; set >= 0 switches");
+        "256x256 GEMM schedule: 0 = 256b, 1 = 256p ping-pong, 2 = 256s persistent, 3 = 256l full-line "
+        "epilogue, 4 = 256n full-line + nt stores (default); set >= 0 switches, returns the current");
+  m.def("attention_persist_mode", &attention_persist_mode, py::arg("set") = -1,
+        "packed BERT attention: 1 = persistent prefetching kernel (default), 0 = one item per workgroup");
   m.attr("EPI_BIAS") = static_cast<int>(kEpiBias);
   m.attr("EPI_GELU") = static_cast<int>(kEpiGelu);
   m.attr("EPI_TANH") = static_cast<int>(kEpiTanh);

@@ -44,6 +44,7 @@ int gemm_splitk_splits(int M, int N, int K);
 int gemm_dec_mode(int set);
 // 256x256 schedule selector (benchmarks): set >= 0 switches; returns the current
 int gemm_256_variant(int set);
+int attention_persist_mode(int set);  // packed BERT attention: 1 persistent (default), 0 per-item
 
 // ------------------------------------------------------------ decode (K9-K11)
 // One query row per (row, head) against a KV cache. Cross attention (lens set):

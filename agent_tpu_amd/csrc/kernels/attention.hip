@@ -28,6 +28,9 @@
 #include "atpu/common.h"
 #include "atpu/kernels.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace atpu {
 namespace {
 
@@ -214,7 +217,202 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(HAS_BI
   }
 }
 
+
+// ============================================================================
+// Persistent packed-QKV attention (BERT encoder: no bias, not causal, S <= 128,
+// so one key chunk per (batch, head) item). The one-item-per-workgroup kernel
+// above waits a full HBM round trip for K/V/Q before every item and only
+// 2 workgroups per CU (98 VGPRs) overlap those waits. Here each workgroup walks
+// items b*H + h = blockIdx.x + i * gridDim.x and prefetches item i+1 while it
+// computes item i, everything by LDS-DMA (no VGPR loads the compiler would
+// drain with vmcnt(0)):
+//   top:   s_waitcnt vmcnt(4) -> K/V(i), Q(i) landed; only the previous item's
+//          4 output stores may still be in flight. barrier.
+//   Q(i) fragments LDS -> VGPR (the wave's private 2 KiB Q image), lgkmcnt(0)
+//   issue: K/V(i+1) -> the other 32 KiB buffer, Q(i+1) -> the wave's Q image
+//   compute item i (same MFMA / softmax / transposed-V code as above), store O
+// A K/V buffer is restaged one barrier after the compute that read it; the Q
+// image is private to its wave and restaged after that wave's reads retired.
+// LDS 80 KiB -> two workgroups per CU.
+// ============================================================================
+constexpr int kQImg = 16 * kKRowB;  // one wave's 16 query rows
+
+__device__ __forceinline__ bf16x4 lds_read_tr16_asm(const char* p) {
+  v4s r;
+  const unsigned a = (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return __builtin_bit_cast(bf16x4, r);
+}
+
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void attention_packed_persist_kernel(
+    const bf16* __restrict__ QKV, int ldq, bf16* __restrict__ O, int ldo, const int32_t* __restrict__ lens, int S,
+    int H, int items, float scale) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * (kLdsK + kLdsV) + kWaves * kQImg];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+  const int srow = lane >> 3, spos = lane & 7;
+  const int hd = H * kD;
+  char* qimg = lds + 2 * (kLdsK + kLdsV) + wave * kQImg;
+  int item = blockIdx.x;
+  if (item >= items) return;
+
+  auto stage = [&](int it, int buf) {
+    const int b = __builtin_amdgcn_readfirstlane(it / H), h = __builtin_amdgcn_readfirstlane(it % H);
+    // buffer resource over this item's rows (scalar base + 32-bit lane offsets,
+    // guide T8): one VGPR per DMA. The lane offsets are recomputed per item from
+    // the lane id (v_mbcnt, rematerialisable): kept live across the loop they were
+    // spilled (the compute phase needs ~120 VGPRs under the 128 cap of 2 groups/CU).
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16*>(QKV + (size_t)b * S * ldq + h * kD), 0, S * ldq * 2, 0x00020000);
+    const int l = __lane_id();
+    const int sr = l >> 3, sp = l & 7;
+    char* ldsK = lds + buf * (kLdsK + kLdsV);
+    char* ldsV = ldsK + kLdsK;
+    auto dma = [&](uint32_t off, char* dst) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (ATPU_LDS_AS void*)dst, 16, off, 0, 0, 0);
+    };
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = (i * kWaves + wave) * 8 + sr;
+      const uint32_t row = (uint32_t)min(r, S - 1) * (uint32_t)ldq;
+      dma((row + hd + kswz(r, sp) * 8) * 2, ldsK + (i * kWaves + wave) * 8 * kKRowB);
+      dma((row + 2 * hd + vswz(r, sp) * 8) * 2, ldsV + (i * kWaves + wave) * 8 * kVRowB);
+    }
+    // this wave's 16 query rows (swizzled like K: conflict-free fragment reads)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = i * 8 + sr;
+      dma(((uint32_t)min(wave * 16 + r, S - 1) * (uint32_t)ldq + kswz(r, sp) * 8) * 2, qimg + i * 8 * kKRowB);
+    }
+  };
+
+  stage(item, 0);
+  int buf = 0;
+  for (;;) {
+    const int next = item + gridDim.x;
+    const bool has_next = next < items;
+    // K/V/Q(item) are older than the previous item's 4 output stores
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8 qf[2];
+#pragma unroll
+    for (int ds = 0; ds < 2; ++ds) qf[ds] = *reinterpret_cast<const bf16x8*>(qimg + fr * kKRowB + kswz(fr, ds * 4 + fg) * 16);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // Q image read before it is restaged
+    __builtin_amdgcn_sched_barrier(0);
+    if (has_next) stage(next, buf ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+    const char* ldsK = lds + buf * (kLdsK + kLdsV);
+    const char* ldsV = ldsK + kLdsK;
+    const int len = min(lens[item / H], S);
+
+    f32x4 s[8];
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ds = 0; ds < 2; ++ds) {
+        const int r = kt * 16 + fr;
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ldsK + r * kKRowB + kswz(r, ds * 4 + fg) * 16);
+        s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ds], s[kt], 0, 0, 0);
+      }
+    }
+    float mx = -1e30f;
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kt * 16 + fg * 4 + r;
+        const float x = key < len ? s[kt][r] * scale : -1e30f;
+        s[kt][r] = x;
+        mx = fmaxf(mx, x);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float psum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float x = s[kt][r];
+        const float p = x <= -1e29f ? 0.f : __expf(x - mx);
+        s[kt][r] = p;
+        psum += p;
+      }
+    psum += __shfl_xor(psum, 16, 64);
+    psum += __shfl_xor(psum, 32, 64);
+
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      bf16x8 pf;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        pf[e] = f2bf(s[2 * ks][e]);
+        pf[4 + e] = f2bf(s[2 * ks + 1][e]);
+      }
+      const int tq = fr >> 2, tp = fr & 3;
+      // transposed V reads by inline asm: the builtin form makes hipcc's waitcnt
+      // pass assume it may alias the LDS-DMA in flight to the other buffer and
+      // drain it (vmcnt(0)) right here, which serialises the prefetch
+#pragma unroll
+      for (int dh = 0; dh < 4; dh += 2) {  // two d-tiles per wait: 8 VGPRs of V fragments live
+        bf16x4 lo[2], hi[2];
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const int klo = ks * 32 + fg * 4 + tq, khi = klo + 16;
+          const int c = (dh + d) * 2 + (tp >> 1);
+          lo[d] = lds_read_tr16_asm(ldsV + klo * kVRowB + vswz(klo, c) * 16 + (tp & 1) * 8);
+          hi[d] = lds_read_tr16_asm(ldsV + khi * kVRowB + vswz(khi, c) * 16 + (tp & 1) * 8);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);  // keep the reads' consumers below the wait (guide §5.4 rule 18)
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          bf16x8 vf;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            vf[e] = lo[d][e];
+            vf[4 + e] = hi[d][e];
+          }
+          o[dh + d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[dh + d], 0, 0, 0);
+        }
+      }
+    }
+    {
+      const int q = wave * 16 + fr;
+      const float inv = psum > 0.f ? 1.f / psum : 0.f;
+      bf16* orow = O + ((size_t)(item / H) * S + min(q, S - 1)) * ldo + (item % H) * kD;
+      // S % 16 == 0 (host check): every lane stores, so each wave issues
+      // exactly 4 stores per item (the count the vmcnt(4) above relies on)
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        bf16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = f2bf(o[dt][e] * inv);
+        *reinterpret_cast<bf16x4*>(orow + dt * 16 + fg * 4) = v;
+      }
+    }
+    if (!has_next) break;
+    buf ^= 1;
+    item = next;
+  }
+}
+
 }  // namespace
+
+int attention_persist_mode(int set) {
+  // 1 = persistent prefetching kernel for the packed BERT case (default), 0 = one item per workgroup
+  static int v = [] {
+    const char* f = std::getenv("ATPU_ATTN_PERSIST");
+    return (f && f[0] == '0') ? 0 : 1;
+  }();
+  if (set >= 0) v = set;
+  return v;
+}
 
 void attention_fwd_strided(const bf16* q, int ldq, const bf16* k, int ldk, const bf16* v, int ldv, bf16* out,
                            int ldo, const int32_t* lens, const float* bias, int B, int Sq, int Skv, int H, int D,
@@ -242,6 +440,20 @@ void attention_fwd_strided(const bf16* q, int ldq, const bf16* k, int ldk, const
 void attention_fwd(const bf16* qkv, const int32_t* lens, const float* bias, bf16* out, int B, int S, int H, int D,
                    float scale, hipStream_t stream) {
   const int hd = H * D;
+  if (!bias && lens && D == kD && S <= kKC && S % 16 == 0 && attention_persist_mode(-1) == 1) {
+    static const int nb = [] {
+      int dev = 0, cus = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+      return 2 * cus;  // two workgroups per CU (<= 128 VGPRs, 80 KiB LDS each)
+    }();
+    const int items = B * H;
+    hipLaunchKernelGGL(attention_packed_persist_kernel, dim3(std::min(items, nb)), dim3(kThreads), 0, stream, qkv,
+                       3 * hd, out, hd, lens, S, H, items, scale);
+    ATPU_HIP_CHECK(hipGetLastError());
+    return;
+  }
   attention_fwd_strided(qkv, 3 * hd, qkv + hd, 3 * hd, qkv + 2 * hd, 3 * hd, out, hd, lens, bias, B, S, S, H, D,
                         scale, 0, stream);
 }

@@ -122,6 +122,29 @@ def test_attention_packed(gpu, B, S, H):
     assert _rel_err(out, ref) < 2e-2
 
 
+@pytest.mark.parametrize("S", [128, 64])
+def test_attention_persistent_matches_per_item(gpu, nat, S):
+    # the persistent prefetching kernel walks several (batch, head) items per
+    # workgroup here (B*H > 2 workgroups per CU), with ragged key lengths
+    B, H = 96, 12
+    qkv = _rand((B * S, 3 * H * 64), gpu, seed=16)
+    lens = torch.randint(2, S + 1, (B,), generator=torch.Generator().manual_seed(3), dtype=torch.int32).to(gpu)
+    prev = nat.attention_persist_mode(-1)
+    try:
+        nat.attention_persist_mode(0)
+        ref = ops.attention_packed(qkv, lens, B, S, H)
+        nat.attention_persist_mode(1)
+        for _ in range(3):
+            out = ops.attention_packed(qkv, lens, B, S, H)
+            assert _rel_err(out, ref) < 1e-3
+    finally:
+        nat.attention_persist_mode(prev)
+    hd = H * 64
+    qc = qkv[: 4 * S].cpu()
+    r32 = attention_ref(qc[:, :hd], qc[:, hd:2 * hd], qc[:, 2 * hd:], lens[:4].cpu(), 4, S, S, H, 1 / math.sqrt(64))
+    assert _rel_err(out[: 4 * S], r32) < 2e-2
+
+
 def test_attention_spike_forces_rescale(gpu):
     # one huge key late in the sequence forces the online-softmax rescale branch
     B, S, H = 1, 256, 1
