@@ -227,7 +227,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(HAS_BI
 // computes item i, everything by LDS-DMA (no VGPR loads the compiler would
 // drain with vmcnt(0)):
 //   top:   s_waitcnt vmcnt(4) -> K/V(i), Q(i) landed; only the previous item's
-//          4 output stores may still be in flight. barrier.
+//          4 output stores may still be in flight (vmcnt(0) for the first item).
+//          barrier.
 //   Q(i) fragments LDS -> VGPR (the wave's private 2 KiB Q image), lgkmcnt(0)
 //   issue: K/V(i+1) -> the other 32 KiB buffer, Q(i+1) -> the wave's Q image
 //   compute item i (same MFMA / softmax / transposed-V code as above), store O
@@ -289,11 +290,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 
   stage(item, 0);
   int buf = 0;
+  bool first = true;
   for (;;) {
     const int next = item + gridDim.x;
     const bool has_next = next < items;
-    // K/V/Q(item) are older than the previous item's 4 output stores
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    // K/V/Q(item) are older than the previous item's 4 output stores (none
+    // before the first item: its 6 DMAs are the newest ops)
+    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    first = false;
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     bf16x8 qf[2];
@@ -421,6 +426,24 @@ void attention_fwd_strided(const bf16* q, int ldq, const bf16* k, int ldk, const
   ATPU_CHECK(B > 0 && Sq > 0 && Skv > 0 && H > 0, "attention: empty problem");
   ATPU_CHECK(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0, "attention: row strides must be 16-B");
   ATPU_CHECK(!bias || Skv % 4 == 0, "attention: bias path needs Skv % 4 == 0");
+  // packed BERT layout (q | k | v column blocks of one [rows, 3*H*64] tensor),
+  // one key chunk, whole 16-query tiles: the persistent prefetching kernel
+  const bool packed = k == q + H * kD && v == k + H * kD && ldk == ldq && ldv == ldq;
+  if (packed && !bias && !causal && lens && Sq == Skv && Sq <= kKC && Sq % 16 == 0 &&
+      attention_persist_mode(-1) == 1) {
+    static const int nb = [] {
+      int dev = 0, cus = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+      return 2 * cus;  // two workgroups per CU (<= 128 VGPRs, 80 KiB LDS each)
+    }();
+    const int items = B * H;
+    hipLaunchKernelGGL(attention_packed_persist_kernel, dim3(std::min(items, nb)), dim3(kThreads), 0, stream, q, ldq,
+                       out, ldo, lens, Sq, H, items, scale);
+    ATPU_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const dim3 grid((Sq + kQB - 1) / kQB, H, B);
 #define ATPU_ATTN(HB, CA)                                                                                   \
   hipLaunchKernelGGL((attention_fwd_kernel<HB, CA>), grid, dim3(kThreads), 0, stream, q, ldq, k, ldk, v, ldv, out, \
@@ -440,20 +463,6 @@ void attention_fwd_strided(const bf16* q, int ldq, const bf16* k, int ldk, const
 void attention_fwd(const bf16* qkv, const int32_t* lens, const float* bias, bf16* out, int B, int S, int H, int D,
                    float scale, hipStream_t stream) {
   const int hd = H * D;
-  if (!bias && lens && D == kD && S <= kKC && S % 16 == 0 && attention_persist_mode(-1) == 1) {
-    static const int nb = [] {
-      int dev = 0, cus = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-        cus = 256;
-      return 2 * cus;  // two workgroups per CU (<= 128 VGPRs, 80 KiB LDS each)
-    }();
-    const int items = B * H;
-    hipLaunchKernelGGL(attention_packed_persist_kernel, dim3(std::min(items, nb)), dim3(kThreads), 0, stream, qkv,
-                       3 * hd, out, hd, lens, S, H, items, scale);
-    ATPU_HIP_CHECK(hipGetLastError());
-    return;
-  }
   attention_fwd_strided(qkv, 3 * hd, qkv + hd, 3 * hd, qkv + 2 * hd, 3 * hd, out, hd, lens, bias, B, S, S, H, D,
                         scale, 0, stream);
 }
