@@ -699,7 +699,7 @@ void launch_256p(const GemmArgs& g, hipStream_t s) {
 // output (one 128-B line per row) goes out as 16 stores of 8 rows x 128 B
 // FULL lines, after an LDS transpose through a private 2 KiB scratch per wave
 // (16 rows x 128 B, 16-B chunks XOR-swizzled by row & 7). Per 16-row block i:
-//   residual: 2 x 16-B full-line loads (issued one block ahead) -> LDS ->
+//   residual: 2 x 16-B full-line loads (all 8 blocks issued up front) -> LDS ->
 //             8-B reads in the fragment layout -> added in fp32
 //   output:   acc + bias (+act) (+res) -> bf16 -> 4 x ds_write_b64 in the
 //             fragment layout -> 2 x ds_read_b128 in line layout -> 2 stores
@@ -725,18 +725,21 @@ __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int 
   auto frag_off = [&](int j) { return fr * 128 + (((j * 2 + (fc >> 1)) ^ (fr & 7)) << 4) + (fc & 1) * 8; };
   const size_t row0 = (size_t)(m0 + wm * 128);
   const int col = n0 + wn * 64 + lc * 8;
-  u32x4 res[2][2];
-  auto load_res = [&](int i) {
-    if constexpr (EPI & kEpiResidual) {
+  // all 16 residual loads go out at once (64 VGPRs: the operand fragments are
+  // dead here). Loading one 16-row block ahead left every other block waiting
+  // a full memory latency (~4 latencies per tile: o-proj ran 38 % over its main
+  // loop); now only the first block waits.
+  u32x4 res[8][2];
+  if constexpr (EPI & kEpiResidual) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
       const bf16* rp = R + (row0 + i * 16 + lr) * ldr + col;
-      res[i & 1][0] = *reinterpret_cast<const u32x4*>(rp);
-      res[i & 1][1] = *reinterpret_cast<const u32x4*>(rp + 8 * (size_t)ldr);
+      res[i][0] = *reinterpret_cast<const u32x4*>(rp);
+      res[i][1] = *reinterpret_cast<const u32x4*>(rp + 8 * (size_t)ldr);
     }
-  };
-  load_res(0);
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    if (i + 1 < 8) load_res(i + 1);
     float v[4][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -758,8 +761,8 @@ __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int 
         for (int e = 0; e < 4; ++e) v[j][e] = fmaxf(v[j][e], 0.f);
     }
     if constexpr (EPI & kEpiResidual) {
-      *reinterpret_cast<u32x4*>(scratch + line_off0) = res[i & 1][0];
-      *reinterpret_cast<u32x4*>(scratch + line_off1) = res[i & 1][1];
+      *reinterpret_cast<u32x4*>(scratch + line_off0) = res[i][0];
+      *reinterpret_cast<u32x4*>(scratch + line_off1) = res[i][1];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const bf16x4 r = *reinterpret_cast<const bf16x4*>(scratch + frag_off(j));
