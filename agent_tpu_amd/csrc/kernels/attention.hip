@@ -226,12 +226,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(HAS_BI
 // items b*H + h = blockIdx.x + i * gridDim.x and prefetches item i+1 while it
 // computes item i, everything by LDS-DMA (no VGPR loads the compiler would
 // drain with vmcnt(0)):
-//   top:   s_waitcnt vmcnt(4) -> K/V(i), Q(i) landed; only the previous item's
-//          4 output stores may still be in flight (vmcnt(0) for the first item).
+//   top:   s_waitcnt vmcnt(2) -> K/V(i), Q(i) landed; only the previous item's
+//          2 output stores may still be in flight (vmcnt(0) for the first item).
 //          barrier.
 //   Q(i) fragments LDS -> VGPR (the wave's private 2 KiB Q image), lgkmcnt(0)
 //   issue: K/V(i+1) -> the other 32 KiB buffer, Q(i+1) -> the wave's Q image
-//   compute item i (same MFMA / softmax / transposed-V code as above), store O
+//   compute item i (same MFMA / softmax / transposed-V code as above); O is
+//   staged through the K half of the buffer (free after a barrier following
+//   QK^T) and stored as whole 128-B rows
 // A K/V buffer is restaged one barrier after the compute that read it; the Q
 // image is private to its wave and restaged after that wave's reads retired.
 // LDS 80 KiB -> two workgroups per CU.
@@ -266,7 +268,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     // spilled (the compute phase needs ~120 VGPRs under the 128 cap of 2 groups/CU).
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<bf16*>(QKV + (size_t)b * S * ldq + h * kD), 0, S * ldq * 2, 0x00020000);
-    const int l = __lane_id();
+    int l = __lane_id();
+    asm volatile("" : "+v"(l));  // opaque per call: no loop-invariant offsets to keep live (or spill)
     const int sr = l >> 3, sp = l & 7;
     char* ldsK = lds + buf * (kLdsK + kLdsV);
     char* ldsV = ldsK + kLdsK;
@@ -294,10 +297,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   for (;;) {
     const int next = item + gridDim.x;
     const bool has_next = next < items;
-    // K/V/Q(item) are older than the previous item's 4 output stores (none
+    // K/V/Q(item) are older than the previous item's 2 output stores (none
     // before the first item: its 6 DMAs are the newest ops)
     if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     first = false;
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -323,6 +326,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ds], s[kt], 0, 0, 0);
       }
     }
+    // every wave's K reads have retired (its MFMAs consumed them): the K half
+    // of this buffer becomes the O staging area below
+    __builtin_amdgcn_s_barrier();
     float mx = -1e30f;
 #pragma unroll
     for (int kt = 0; kt < 8; ++kt)
@@ -388,17 +394,34 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       }
     }
     {
-      const int q = wave * 16 + fr;
+      // O goes out through LDS (this wave's 2 KiB of the K half of the buffer,
+      // free since the barrier after QK^T; 16-B chunks XOR-swizzled by row) so
+      // each store writes whole 128-B head rows: 8 rows x 128 B per
+      // wave-instruction instead of 16 rows x 32 B (partial-line stores were
+      // most of the GEMM tail's cost, docs/PERF_NOTES.md).
       const float inv = psum > 0.f ? 1.f / psum : 0.f;
-      bf16* orow = O + ((size_t)(item / H) * S + min(q, S - 1)) * ldo + (item % H) * kD;
-      // S % 16 == 0 (host check): every lane stores, so each wave issues
-      // exactly 4 stores per item (the count the vmcnt(4) above relies on)
+      char* ost = const_cast<char*>(ldsK) + wave * 16 * kKRowB;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         bf16x4 v;
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = f2bf(o[dt][e] * inv);
-        *reinterpret_cast<bf16x4*>(orow + dt * 16 + fg * 4) = v;
+        const int ch = dt * 2 + (fg >> 1);
+        *reinterpret_cast<bf16x4*>(ost + fr * kKRowB + ((ch ^ (fr & 7)) << 4) + (fg & 1) * 8) = v;
+      }
+      // rows past S (S = 64: waves 4-7) computed query S-1 (clamped Q rows)
+      // and rewrite its identical values; S % 16 == 0 (host check): every lane
+      // stores, so each wave issues exactly 2 stores per item (the count the
+      // top-of-loop vmcnt(2) relies on)
+      int l2 = __lane_id();
+      asm volatile("" : "+v"(l2));
+      const int lr = l2 >> 3, lc = l2 & 7;
+      const bf16* obase0 = O + (size_t)(item / H) * S * ldo + (item % H) * kD + lc * 8;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int r = lr + hh * 8;
+        const u32x4 val = *reinterpret_cast<const u32x4*>(ost + r * kKRowB + ((lc ^ (r & 7)) << 4));
+        *reinterpret_cast<u32x4*>(const_cast<bf16*>(obase0) + (size_t)min(wave * 16 + r, S - 1) * ldo) = val;
       }
     }
     if (!has_next) break;

@@ -73,3 +73,34 @@ def test_cls_only_last_layer_matches_full(gpu):
     oracle = BertClassifier(cfg, pack, fp32=True, cls_only_last=False)
     lo, _, _ = oracle.forward(ids, lens, 4)
     assert (lp.cpu() - lo).abs().max().item() < 5e-2 * max(1.0, lo.abs().max().item())
+
+
+def test_bert_base_production_batch(gpu, nat):
+    """The bench shape (B=64, S=128: M=8192 rows) runs the persistent GEMM and
+    persistent attention kernels; compare against the per-tile GEMM + per-item
+    attention kernels on the same batch, and against the fp32 oracle."""
+    cfg = config_for("bert-base", num_labels=5)
+    pack = init_random(cfg, seed=11, bias_std=0.02)
+    B, S = 64, 128
+    g = torch.Generator().manual_seed(4)
+    ids = torch.randint(1000, cfg.vocab_size, (B, S), generator=g, dtype=torch.int32)
+    ids[:, 0] = 101
+    lens = torch.randint(16, S + 1, (B,), generator=g, dtype=torch.int32)
+    ids[torch.arange(S).view(1, S) >= lens.view(B, 1)] = 0
+    dev = BertClassifier(cfg, pack.to(gpu))
+    gl, gi, gs = dev.forward(ids.to(gpu), lens.to(gpu), k=3)
+    pv, pa = nat.gemm_256_variant(-1), nat.attention_persist_mode(-1)
+    try:
+        nat.gemm_256_variant(1)
+        nat.attention_persist_mode(0)
+        bl, bi, bs = dev.forward(ids.to(gpu), lens.to(gpu), k=3)
+    finally:
+        nat.gemm_256_variant(pv)
+        nat.attention_persist_mode(pa)
+    assert (gl - bl).abs().max().item() < 2e-2 * max(1.0, bl.abs().max().item())
+    margin = bs[:, 0] - bs[:, 1]
+    ok = margin > 0.02
+    assert torch.equal(gi[ok, 0], bi[ok, 0])
+    oracle = BertClassifier(cfg, pack, fp32=True)
+    rl, _, _ = oracle.forward(ids[:4], lens[:4], k=3)
+    assert (gl[:4].cpu() - rl).abs().max().item() < 5e-2 * max(1.0, rl.abs().max().item())
