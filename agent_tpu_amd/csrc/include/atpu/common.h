@@ -96,38 +96,38 @@ __device__ __forceinline__ void gelu_fast8(float (&v)[8]) {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-// erf-GELU on 16 values with NO transcendental: erf(z) = z * P(t) on the
-// clamped z = clamp(x/sqrt2, -3.5, 3.5), t = 2 z^2 / 3.5^2 - 1 in [-1, 1], P a
-// degree-12 least-squares Chebyshev fit (monomial in t; tools/gelu_fit.py).
-// Evaluated here in x-space (clamp x to +-3.5*sqrt2, 1/sqrt2 folded into the
-// coefficients). Max |gelu error| <= 3.4e-6 over all x (<= 8.7e-7 for
-// |x| < 4) in fp32. The Horner chain runs on float2 -> v_pk_fma_f32, two values
-// per instruction; the A&S form (gelu_fast8) spends a v_rcp and a v_exp per
-// value, each a quarter-rate transcendental. In the FFN1 epilogue, whose VALU
-// issue is not hidden behind MFMAs, this is ~40 % fewer VALU cycles.
+// erf-GELU on 16 values with NO transcendental:
+//   xc = clamp(x, -A, A),  w = xc^2 - A^2/2,  gelu(x) = x * (0.5 + xc * Q(w))
+// Q ~= erf(xc/sqrt2) / (2 xc), a degree-10 least-squares Chebyshev fit on
+// |xc| <= A = 3.25*sqrt2, rescaled to monomials in the CENTRED w: as well
+// conditioned as the Chebyshev interval, and w is one FMA (tools/gelu_fit.py).
+// fp32 max |gelu error| 1.7e-5 over all x, 3.6e-6 for |x| < 4 (bf16 output
+// resolution at 1.0 is 3.9e-3). Per pair of values: 2 v_med3 + 13 packed ops
+// (v_pk_fma_f32 / v_pk_mul_f32); the A&S form (gelu_fast8) spends a v_rcp and a
+// v_exp per value, each a quarter-rate transcendental. The FFN1 epilogue's VALU
+// issue is not hidden behind MFMAs, so this count is its tail cost.
 __device__ __forceinline__ void gelu_poly16(float (&v)[16]) {
-  constexpr float kC[13] = {2.855813205e-01f,  -1.419170350e-01f, 1.037684307e-01f,  -8.104421943e-02f,
-                            6.250595301e-02f,  -4.579368234e-02f, 3.184378892e-02f,  -2.125407569e-02f,
-                            1.203811448e-02f,  -5.087599624e-03f, 3.172110533e-03f,  -2.829871373e-03f,
-                            1.047181780e-03f};
-  constexpr float kClamp = 4.949747562e+00f;  // 3.5 * sqrt(2)
-  constexpr float kT = 8.16326513886e-02f;    // 1 / 3.5^2
-  f32x2 xc[8], t[8], p[8];
+  constexpr int kDeg = 10;
+  constexpr float kQ[kDeg + 1] = {1.536687613e-01f,  -7.178471889e-03f, 4.856055602e-04f, -3.426085095e-05f,
+                                  2.347781901e-06f,  -1.526724844e-07f, 8.713541888e-09f, -4.079194205e-10f,
+                                  2.366933385e-11f,  -1.725522828e-12f, 5.926992431e-14f};
+  constexpr float kClamp = 4.596194267e+00f;  // A = 3.25 * sqrt(2)
+  constexpr float kH = 1.056250000e+01f;      // A^2 / 2
+  f32x2 xc[8], w[8], p[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     xc[e] = f32x2{__builtin_amdgcn_fmed3f(v[2 * e], -kClamp, kClamp),
                   __builtin_amdgcn_fmed3f(v[2 * e + 1], -kClamp, kClamp)};
-    t[e] = __builtin_elementwise_fma(xc[e] * xc[e], f32x2{kT, kT}, f32x2{-1.f, -1.f});
-    p[e] = f32x2{kC[12], kC[12]};
+    w[e] = __builtin_elementwise_fma(xc[e], xc[e], f32x2{-kH, -kH});
+    p[e] = f32x2{kQ[kDeg], kQ[kDeg]};
   }
 #pragma unroll
-  for (int k = 11; k >= 0; --k)
+  for (int k = kDeg - 1; k >= 0; --k)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) p[e] = __builtin_elementwise_fma(p[e], t[e], f32x2{kC[k], kC[k]});
+    for (int e = 0; e < 8; ++e) p[e] = __builtin_elementwise_fma(p[e], w[e], f32x2{kQ[k], kQ[k]});
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const f32x2 hx = f32x2{v[2 * e], v[2 * e + 1]} * 0.5f;
-    const f32x2 g = __builtin_elementwise_fma(hx, xc[e] * p[e], hx);  // 0.5x (1 + erf)
+    const f32x2 g = f32x2{v[2 * e], v[2 * e + 1]} * __builtin_elementwise_fma(xc[e], p[e], f32x2{0.5f, 0.5f});
     v[2 * e] = g[0];
     v[2 * e + 1] = g[1];
   }

@@ -98,6 +98,30 @@ def test_gemm256_variants_exact(gpu, nat, variant, M, N, K):
         nat.gemm_256_variant(prev)
 
 
+@pytest.mark.parametrize("variant", [1, 4])  # 256p (per tile, A&S erf), 256n (persistent, polynomial)
+def test_gemm_gelu_accuracy(gpu, nat, variant):
+    # W = I: the accumulator is x exactly, so the output is bf16(gelu_epilogue(x)).
+    # 3M bf16 inputs in [-8, 8]: within one bf16 ulp (+3e-5 absolute) of the exact
+    # erf-GELU everywhere, and equal to bf16(exact) for nearly all |x| < 4
+    M, N = 4096, 768
+    x = torch.linspace(-8, 8, M * N).to(torch.bfloat16).view(M, N)
+    eye = torch.eye(N).to(torch.bfloat16)
+    b = torch.zeros(N)
+    exact = 0.5 * x.double() * (1 + torch.erf(x.double() / math.sqrt(2)))
+    prev = nat.gemm_256_variant(-1)
+    try:
+        nat.gemm_256_variant(variant)
+        y = ops.linear(x.to(gpu), eye.to(gpu), b.to(gpu), act="gelu").cpu()
+    finally:
+        nat.gemm_256_variant(prev)
+    ref = exact.to(torch.bfloat16)
+    diff = (y.double() - exact).abs()
+    ulp = ref.double().abs() * 2.0 ** -7
+    assert (diff <= ulp + 3e-5).all(), diff.max().item()
+    inner = x.abs() < 4
+    assert (y[inner] != ref[inner]).double().mean().item() < 0.08
+
+
 def test_gemm_strided_rows(gpu):
     # pooler case: A rows taken every S rows (CLS tokens) of a [B*S, H] tensor
     B, S, H = 37, 128, 768
