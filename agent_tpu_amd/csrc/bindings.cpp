@@ -83,6 +83,13 @@ PYBIND11_MODULE(_atpu, m) {
   m.def("gemm_256_variant", &gemm_256_variant, py::arg("set") = -1,
         "256x256 GEMM schedule: 0 = 256b, 1 = 256p ping-pong, 2 = 256s persistent, 3 = 256l full-line "
         "epilogue, 4 = 256n full-line + nt stores (default); set >= 0 switches, returns the current");
+  m.def("cu_budget", &cu_budget, py::arg("set") = -1,
+        "get/set the CU count persistent grids are sized for (0 = the device's; set it to the CU share of "
+        "CU-masked streams)");
+  m.def("num_cus", &num_cus, "CUs persistent grids are sized for");
+  m.def("make_cu_mask_stream", &make_cu_mask_stream, py::arg("first_bit"), py::arg("nbits"),
+        "create a HIP stream restricted to CU-mask bits [first_bit, first_bit+nbits) (bit i -> XCD i % 8); "
+        "returns the hipStream_t as an int (wrap with torch.cuda.ExternalStream)");
   m.def("attention_persist_mode", &attention_persist_mode, py::arg("set") = -1,
         "packed BERT attention: 1 = persistent prefetching kernel (default), 0 = one item per workgroup");
   m.attr("EPI_BIAS") = static_cast<int>(kEpiBias);

@@ -45,6 +45,9 @@ int gemm_dec_mode(int set);
 // 256x256 schedule selector (benchmarks): set >= 0 switches; returns the current
 int gemm_256_variant(int set);
 int attention_persist_mode(int set);  // packed BERT attention: 1 persistent (default), 0 per-item
+int num_cus();                        // CUs a persistent grid is sized for (device count, or the budget below)
+int cu_budget(int set);               // >0: size persistent grids for this many CUs (CU-masked streams)
+int64_t make_cu_mask_stream(int first_bit, int nbits);  // hipStream_t over CU-mask bits [first, first+n)
 
 // ------------------------------------------------------------ decode (K9-K11)
 // One query row per (row, head) against a KV cache. Cross attention (lens set):

@@ -454,13 +454,8 @@ void attention_fwd_strided(const bf16* q, int ldq, const bf16* k, int ldk, const
   const bool packed = k == q + H * kD && v == k + H * kD && ldk == ldq && ldv == ldq;
   if (packed && !bias && !causal && lens && Sq == Skv && Sq <= kKC && Sq % 16 == 0 &&
       attention_persist_mode(-1) == 1) {
-    static const int nb = [] {
-      int dev = 0, cus = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-        cus = 256;
-      return 2 * cus;  // two workgroups per CU (<= 128 VGPRs, 80 KiB LDS each)
-    }();
+    const int nb = 2 * num_cus();  // two workgroups per CU (<= 128 VGPRs, 80 KiB LDS each)
+
     const int items = B * H;
     hipLaunchKernelGGL(attention_packed_persist_kernel, dim3(std::min(items, nb)), dim3(kThreads), 0, stream, q, ldq,
                        out, ldo, lens, Sq, H, items, scale);

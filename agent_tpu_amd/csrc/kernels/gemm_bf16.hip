@@ -26,6 +26,8 @@
 #include "atpu/common.h"
 #include "atpu/kernels.h"
 
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 #include <cstdlib>
 #include <string>
@@ -1004,6 +1006,15 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
   if (wm == 0) __builtin_amdgcn_s_barrier();  // close the stagger (equal barrier counts)
 }
 
+}  // namespace
+
+static int g_cu_budget = 0;
+
+int cu_budget(int set) {
+  if (set >= 0) g_cu_budget = set;
+  return g_cu_budget;
+}
+
 int num_cus() {
   static const int n = [] {
     int dev = 0, cus = 0;
@@ -1012,8 +1023,22 @@ int num_cus() {
       cus = 256;
     return cus > 0 ? cus : 256;
   }();
-  return n;
+  // persistent grids are sized for the CUs a launch can use: a CU-masked stream
+  // (ClassifyEngine's split mode) sees only its share of the chip
+  return g_cu_budget > 0 ? std::min(g_cu_budget, n) : n;
 }
+
+int64_t make_cu_mask_stream(int first_bit, int nbits) {
+  // CU mask bits are dealt round-robin over the XCDs (bit i -> XCD i % 8), so a
+  // contiguous bit range is an even share of every XCD (and of its L2)
+  uint32_t mask[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int b = first_bit; b < first_bit + nbits && b < 256; ++b) mask[b / 32] |= 1u << (b % 32);
+  hipStream_t s = nullptr;
+  ATPU_HIP_CHECK(hipExtStreamCreateWithCUMask(&s, 8, mask));
+  return reinterpret_cast<int64_t>(s);
+}
+
+namespace {
 
 template <bool NT, bool LINE = false>
 void launch_256s(const GemmArgs& g, hipStream_t s) {

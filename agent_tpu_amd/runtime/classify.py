@@ -84,6 +84,18 @@ class ClassifyEngine:
             concurrent = os.getenv("ATPU_CONCURRENT_SLOTS", "1") not in ("0", "false", "no")
         self.concurrent = bool(concurrent) and device.type == "cuda" and slots > 1
         self.compute_streams = [torch.cuda.Stream(device) for _ in range(slots)] if self.concurrent else None
+        # CU split (ATPU_CU_SPLIT=1): slot i's stream is CU-masked to an even 1/slots share of every
+        # XCD, and persistent grids are sized for that share (process-wide cu_budget). Without it a
+        # persistent GEMM holds every CU (146 KiB LDS per workgroup) and the other batch's kernels
+        # only slot in at kernel boundaries.
+        self.cu_split = self.concurrent and os.getenv("ATPU_CU_SPLIT", "0") not in ("0", "false", "no")
+        if self.cu_split:
+            nat = native()
+            nat.cu_budget(0)
+            share = (nat.num_cus() // slots) // 8 * 8
+            self.compute_streams = [torch.cuda.ExternalStream(nat.make_cu_mask_stream(i * share, share), device=device)
+                                    for i in range(slots)]
+            nat.cu_budget(share)
         self._graphs: Dict[int, Tuple["torch.cuda.CUDAGraph", Tuple[torch.Tensor, ...]]] = {}
         self._stager = None
 

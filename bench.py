@@ -149,7 +149,7 @@ def main() -> int:
                 "num_labels": cfg.num_labels,
                 "topk": min(a.topk, cfg.num_labels),
                 "hipgraph": not a.no_graph,
-                "concurrent_batches": a.slots if eng.concurrent else 1,
+                "concurrent_batches": a.slots if eng.concurrent else 1, "cu_split": bool(eng.cu_split),
                 "weight_broadcast_ms": round(bcast_ms, 2),
                 "last_layer_cls_only": cls_only,
                 "achieved_tflops_per_gpu": round(flops / world / 1e12, 1),
