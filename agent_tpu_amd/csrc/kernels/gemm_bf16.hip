@@ -697,6 +697,15 @@ void launch_256p(const GemmArgs& g, hipStream_t s) {
 
 
 
+// 16-B global load the compiler does not track: its waitcnt pass treats the
+// counter as out of order once loads, stores and LDS-DMA are all pending and
+// waits vmcnt(0) at the first use; the line epilogue counts its own waits
+__device__ __forceinline__ u32x4 load16_untracked(const void* p) {
+  u32x4 r;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+
 // Full-line epilogue of the persistent kernel ("line"): the wave's 128 x 64
 // output (one 128-B line per row) goes out as 16 stores of 8 rows x 128 B
 // FULL lines, after an LDS transpose through a private 2 KiB scratch per wave
@@ -711,7 +720,8 @@ void launch_256p(const GemmArgs& g, hipStream_t s) {
 template <int EPI, bool NT>
 __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int m0, int n0, int wm, int wn, int lane,
                                                   bf16* __restrict__ C, int ldc, const bf16* __restrict__ R, int ldr,
-                                                  const float* lds_bias, char* scratch) {
+                                                  const float* lds_bias, char* scratch,
+                                                  const u32x4 (&pre)[2][2]) {
   const int fr = lane & 15, fc = lane >> 4;
   f32x4 b4[4];
 #pragma unroll
@@ -731,13 +741,19 @@ __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int 
   // dead here). Loading one 16-row block ahead left every other block waiting
   // a full memory latency (~4 latencies per tile: o-proj ran 38 % over its main
   // loop); now only the first block waits.
+  // blocks 0-1 were issued by the caller during the last MMA phase (pre)
   u32x4 res[8][2];
   if constexpr (EPI & kEpiResidual) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 2; ++i) {
+      res[i][0] = pre[i][0];
+      res[i][1] = pre[i][1];
+    }
+#pragma unroll
+    for (int i = 2; i < 8; ++i) {
       const bf16* rp = R + (row0 + i * 16 + lr) * ldr + col;
-      res[i][0] = *reinterpret_cast<const u32x4*>(rp);
-      res[i][1] = *reinterpret_cast<const u32x4*>(rp + 8 * (size_t)ldr);
+      res[i][0] = load16_untracked(rp);
+      res[i][1] = load16_untracked(rp + 8 * (size_t)ldr);
     }
   }
 #pragma unroll
@@ -763,6 +779,12 @@ __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int 
         for (int e = 0; e < 4; ++e) v[j][e] = fmaxf(v[j][e], 0.f);
     }
     if constexpr (EPI & kEpiResidual) {
+      // block i's two loads have landed once at most 14 younger VMEM ops are
+      // pending: blocks 0-1 (issued in the last MMA phase) are followed by the
+      // other pre load pair and 12 loads; block i >= 2 by 2 (7 - i) loads; and
+      // every earlier block added its 2 stores -> 14 for every i
+      asm volatile("s_waitcnt vmcnt(14)" : "+v"(res[i][0]), "+v"(res[i][1]) :: "memory");
+      __builtin_amdgcn_sched_barrier(0);
       *reinterpret_cast<u32x4*>(scratch + line_off0) = res[i][0];
       *reinterpret_cast<u32x4*>(scratch + line_off1) = res[i][1];
 #pragma unroll
@@ -927,8 +949,12 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
     const int vn = v + G;
     const bool has_next = vn < ntiles;
     const int cm0 = m0, cn0 = n0;
-    for (int t = 0; t < nk; ++t) {
-      const bool last = t + 1 == nk;
+    u32x4 pre[2][2];  // LINE + residual: epilogue residual blocks 0-1, issued in the last phase
+    // one K-tile; the last one is a separate instantiation so that pre[] is
+    // live only from its p3 to the epilogue (assigned in a loop iteration it
+    // would be live around the whole K loop and spill)
+    auto kstep = [&](int t, auto last_c) {
+      constexpr bool last = decltype(last_c)::value;
       const bool more = !last || has_next;
       int kn = t + 1;  // K-tile staged during this one
       if (last && has_next) {
@@ -980,9 +1006,34 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
         stage(3, kn, buf ^ 1);
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       }
+      if constexpr (LINE && (EPI & kEpiResidual)) {
+        // the first two 16-row residual blocks of the line epilogue go out now
+        // (into br's registers, dead after p2) and land under this phase's MMAs:
+        // the tail then starts without a full memory latency
+        if constexpr (last) {
+          // buffer loads: scalar base, one 32-bit lane offset (recomputed from
+          // the lane id, opaque so it is not hoisted and kept live), row steps
+          // as scalar offsets - the 64-bit address math spilled
+          const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+              const_cast<bf16*>(R + (size_t)(cm0 + wm * 128) * ldr + cn0 + wn * 64), 0, 0x7fffffff, 0x00020000);
+          int l2 = __lane_id();
+          asm volatile("" : "+v"(l2));
+          const int vo = ((l2 >> 3) * ldr + (l2 & 7) * 8) * 2;
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int so = (i * 16 + h * 8) * ldr * 2;
+              // untracked (see load16_untracked); the epilogue waits for it
+              asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(pre[i][h]) : "v"(vo), "s"(rs), "s"(so) : "memory");
+            }
+        }
+      }
       ATPU_PS_SYNC_MMA(bl, 1, 0);
       buf ^= 1;
-    }
+    };
+    for (int t = 0; t + 1 < nk; ++t) kstep(t, std::false_type{});
+    kstep(nk - 1, std::true_type{});
     if constexpr (DBG & 1) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -992,7 +1043,7 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
       if constexpr (LINE)
         epilogue_256_line<EPI, NT>(acc, cm0, cn0, wm, wn, lane, C, ldc, R, ldr,
                                    reinterpret_cast<const float*>(lds + kBiasOff) + tile_par * 256,
-                                   lds + kEpiOff + wave * 2048);
+                                   lds + kEpiOff + wave * 2048, pre);
       else
         epilogue_256<EPI, true, (DBG >> 1), NT>(acc, cm0, cn0, wm, wn, lane, C, ldc, bias, R, ldr, M,
                                             reinterpret_cast<const float*>(lds + kBiasOff) + tile_par * 256);
