@@ -4,6 +4,9 @@
 // (NG groups of 4 per lane, 8-byte vector loads/stores), so statistics are a
 // register pass plus one wave butterfly — a single HBM read and write per row.
 // fp32 statistics, two-pass (mean, then centred variance) for accuracy.
+#include <cstdlib>
+#include <string>
+
 #include "atpu/common.h"
 #include "atpu/kernels.h"
 
@@ -69,6 +72,77 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const bf16* __restrict__
   load_row<NG>(x + (size_t)row * N, v, lane);
   if (res) add_row<NG>(res + (size_t)row * N, v, lane);
   ln_store<NG>(v, gamma, beta, out + (size_t)row * N, N, eps, lane);
+}
+
+__device__ __forceinline__ float half_sum(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Half-wave-per-row LayerNorm: 32 lanes own one row, each lane NG chunks of 8
+// contiguous bf16 (16-byte loads/stores), so one wave instruction moves two
+// 512-byte row segments instead of one 512-byte segment with 8-byte accesses.
+// Half the memory instructions of layernorm_kernel for the same bytes; the
+// statistics stay fp32 two-pass, reduced over the half wave.
+template <int NG>
+__global__ __launch_bounds__(256) void layernorm_hw_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, bf16* __restrict__ out,
+                                                           int rows, float eps) {
+  const int hl = threadIdx.x & 31;
+  const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
+  const bool live = row < rows;
+  const int r = live ? row : rows - 1;  // dead half-waves read a valid row, never store
+  constexpr int N = NG * 256;
+  const bf16* xr = x + (size_t)r * N + hl * 8;
+  float v[NG * 8];
+  bf16x8 xv[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) xv[g] = *reinterpret_cast<const bf16x8*>(xr + g * 256);
+  if (res) {
+    const bf16* rr = res + (size_t)r * N + hl * 8;
+    bf16x8 rv[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) rv[g] = *reinterpret_cast<const bf16x8*>(rr + g * 256);
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[g * 8 + e] = bf2f(xv[g][e]) + bf2f(rv[g][e]);
+  } else {
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[g * 8 + e] = bf2f(xv[g][e]);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NG * 8; ++i) s += v[i];
+  const float mean = half_sum(s) * (1.0f / N);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NG * 8; ++i) {
+    const float d = v[i] - mean;
+    q += d * d;
+  }
+  const float rstd = rsqrtf(half_sum(q) * (1.0f / N) + eps);
+  if (!live) return;
+  bf16* orow = out + (size_t)row * N + hl * 8;
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int c = g * 256 + hl * 8;
+    const f32x4 g0 = *reinterpret_cast<const f32x4*>(gamma + c);
+    const f32x4 g1 = *reinterpret_cast<const f32x4*>(gamma + c + 4);
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(beta + c);
+    const f32x4 b1 = *reinterpret_cast<const f32x4*>(beta + c + 4);
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o[e] = f2bf((v[g * 8 + e] - mean) * rstd * g0[e] + b0[e]);
+      o[e + 4] = f2bf((v[g * 8 + e + 4] - mean) * rstd * g1[e] + b1[e]);
+    }
+    *reinterpret_cast<bf16x8*>(orow + g * 256) = o;
+  }
 }
 
 template <int NG>
@@ -152,9 +226,20 @@ void layernorm_bf16(const bf16* x, const bf16* res, const float* gamma, const fl
                     float eps, hipStream_t stream) {
   check_width(N);
   if (rows <= 0) return;
-  const dim3 grid((rows + 3) / 4);
-  ATPU_NG_DISPATCH(N, hipLaunchKernelGGL(layernorm_kernel<NG>, grid, dim3(256), 0, stream, x, res, gamma, beta, out,
-                                         rows, eps));
+  // ATPU_LN_KERNEL=wave selects the wave-per-row kernel (A/B against the default half-wave kernel).
+  static const bool wave_per_row = [] {
+    const char* e = std::getenv("ATPU_LN_KERNEL");
+    return e && std::string(e) == "wave";
+  }();
+  if (wave_per_row) {
+    const dim3 grid((rows + 3) / 4);
+    ATPU_NG_DISPATCH(N, hipLaunchKernelGGL(layernorm_kernel<NG>, grid, dim3(256), 0, stream, x, res, gamma, beta, out,
+                                           rows, eps));
+  } else {
+    const dim3 grid((rows + 7) / 8);
+    ATPU_NG_DISPATCH(N, hipLaunchKernelGGL(layernorm_hw_kernel<NG>, grid, dim3(256), 0, stream, x, res, gamma, beta,
+                                           out, rows, eps));
+  }
   ATPU_HIP_CHECK(hipGetLastError());
 }
 

@@ -197,10 +197,11 @@ def test_attention_strided_bias_causal(gpu, causal):
 
 
 # ------------------------------------------------------------ norms/embed
-@pytest.mark.parametrize("N", [256, 768, 1024])
-def test_layernorm_residual(gpu, N):
-    x = _rand((1000, N), gpu, 2.0, seed=21)
-    r = _rand((1000, N), gpu, seed=22)
+@pytest.mark.parametrize("N,rows", [(256, 1000), (768, 1000), (768, 1003), (1024, 1000), (2048, 77)])
+def test_layernorm_residual(gpu, N, rows):
+    # rows=1003/77: the last 8-row block of the half-wave kernel is partial
+    x = _rand((rows, N), gpu, 2.0, seed=21)
+    r = _rand((rows, N), gpu, seed=22)
     g = _rand((N,), gpu, 1.0, torch.float32, seed=23)
     b = _rand((N,), gpu, 1.0, torch.float32, seed=24)
     y = ops.layernorm(x, g, b, 1e-12, residual=r)
