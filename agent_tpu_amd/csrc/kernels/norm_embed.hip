@@ -85,7 +85,7 @@ __device__ __forceinline__ float half_sum(float v) {
 // 512-byte row segments instead of one 512-byte segment with 8-byte accesses.
 // Half the memory instructions of layernorm_kernel for the same bytes; the
 // statistics stay fp32 two-pass, reduced over the half wave.
-template <int NG>
+template <int NG, bool NTL>
 __global__ __launch_bounds__(256) void layernorm_hw_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, bf16* __restrict__ out,
@@ -99,7 +99,11 @@ __global__ __launch_bounds__(256) void layernorm_hw_kernel(const bf16* __restric
   float v[NG * 8];
   bf16x8 xv[NG];
 #pragma unroll
-  for (int g = 0; g < NG; ++g) xv[g] = *reinterpret_cast<const bf16x8*>(xr + g * 256);
+  for (int g = 0; g < NG; ++g) {
+    // NTL: the pre-norm input is dead after this pass; stream it past the caches
+    if constexpr (NTL) xv[g] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(xr + g * 256));
+    else xv[g] = *reinterpret_cast<const bf16x8*>(xr + g * 256);
+  }
   if (res) {
     const bf16* rr = res + (size_t)r * N + hl * 8;
     bf16x8 rv[NG];
@@ -227,18 +231,25 @@ void layernorm_bf16(const bf16* x, const bf16* res, const float* gamma, const fl
   check_width(N);
   if (rows <= 0) return;
   // ATPU_LN_KERNEL=wave selects the wave-per-row kernel (A/B against the default half-wave kernel).
-  static const bool wave_per_row = [] {
+  static const int mode = [] {
     const char* e = std::getenv("ATPU_LN_KERNEL");
-    return e && std::string(e) == "wave";
+    const std::string m = e ? e : "";
+    return m == "wave" ? 1 : (m == "hw" ? 2 : 0);
   }();
+  const bool wave_per_row = mode == 1;
   if (wave_per_row) {
     const dim3 grid((rows + 3) / 4);
     ATPU_NG_DISPATCH(N, hipLaunchKernelGGL(layernorm_kernel<NG>, grid, dim3(256), 0, stream, x, res, gamma, beta, out,
                                            rows, eps));
   } else {
     const dim3 grid((rows + 7) / 8);
-    ATPU_NG_DISPATCH(N, hipLaunchKernelGGL(layernorm_hw_kernel<NG>, grid, dim3(256), 0, stream, x, res, gamma, beta,
-                                           out, rows, eps));
+    if (mode == 2) {
+      ATPU_NG_DISPATCH(N, hipLaunchKernelGGL((layernorm_hw_kernel<NG, false>), grid, dim3(256), 0, stream, x, res,
+                                             gamma, beta, out, rows, eps));
+    } else {
+      ATPU_NG_DISPATCH(N, hipLaunchKernelGGL((layernorm_hw_kernel<NG, true>), grid, dim3(256), 0, stream, x, res,
+                                             gamma, beta, out, rows, eps));
+    }
   }
   ATPU_HIP_CHECK(hipGetLastError());
 }
