@@ -247,6 +247,7 @@ __device__ __forceinline__ bf16x4 lds_read_tr16_asm(const char* p) {
   return __builtin_bit_cast(bf16x4, r);
 }
 
+template <int CPOL>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void attention_packed_persist_kernel(
     const bf16* __restrict__ QKV, int ldq, bf16* __restrict__ O, int ldo, const int32_t* __restrict__ lens, int S,
     int H, int items, float scale) {
@@ -274,7 +275,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     char* ldsK = lds + buf * (kLdsK + kLdsV);
     char* ldsV = ldsK + kLdsK;
     auto dma = [&](uint32_t off, char* dst) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (ATPU_LDS_AS void*)dst, 16, off, 0, 0, 0);
+      // CPOL 2 = nt: Q/K/V are read exactly once, stream them past L2/MALL so the
+      // residual and the next GEMM's operands stay resident
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (ATPU_LDS_AS void*)dst, 16, off, 0, 0, CPOL);
     };
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -457,8 +460,16 @@ void attention_fwd_strided(const bf16* q, int ldq, const bf16* k, int ldk, const
     const int nb = 2 * num_cus();  // two workgroups per CU (<= 128 VGPRs, 80 KiB LDS each)
 
     const int items = B * H;
-    hipLaunchKernelGGL(attention_packed_persist_kernel, dim3(std::min(items, nb)), dim3(kThreads), 0, stream, q, ldq,
-                       out, ldo, lens, Sq, H, items, scale);
+    static const bool nt = [] {
+      const char* f = std::getenv("ATPU_ATTN_NT");
+      return !(f && f[0] == '0');
+    }();
+    if (nt)
+      hipLaunchKernelGGL(attention_packed_persist_kernel<2>, dim3(std::min(items, nb)), dim3(kThreads), 0, stream, q,
+                         ldq, out, ldo, lens, Sq, H, items, scale);
+    else
+      hipLaunchKernelGGL(attention_packed_persist_kernel<0>, dim3(std::min(items, nb)), dim3(kThreads), 0, stream, q,
+                         ldq, out, ldo, lens, Sq, H, items, scale);
     ATPU_HIP_CHECK(hipGetLastError());
     return;
   }
