@@ -146,10 +146,11 @@ PYBIND11_MODULE(_atpu, m) {
     rmsnorm_bf16(P<const bf16>(x), P<const float>(g), P<bf16>(out), rows, N, eps, S(stream));
   });
   m.def("embed_layernorm", [](uintptr_t ids, uintptr_t tt, uintptr_t word, uintptr_t pos, uintptr_t type, uintptr_t g,
-                              uintptr_t b, uintptr_t out, int B, int Sq, int N, int vocab, float eps, uintptr_t stream) {
+                              uintptr_t b, uintptr_t out, int B, int Sq, int N, int vocab, int type_vocab, float eps,
+                              uintptr_t stream) {
     embed_layernorm(P<const int32_t>(ids), P<const int32_t>(tt), P<const bf16>(word), P<const bf16>(pos),
-                    P<const bf16>(type), P<const float>(g), P<const float>(b), P<bf16>(out), B, Sq, N, vocab, eps,
-                    S(stream));
+                    P<const bf16>(type), P<const float>(g), P<const float>(b), P<bf16>(out), B, Sq, N, vocab,
+                    type_vocab, eps, S(stream));
   });
   m.def("embed_gather", [](uintptr_t ids, uintptr_t table, uintptr_t out, int tokens, int N, int vocab,
                            uintptr_t stream) {

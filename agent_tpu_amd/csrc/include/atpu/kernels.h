@@ -86,10 +86,11 @@ void layernorm_bf16(const bf16* x, const bf16* res, const float* gamma, const fl
 // out = x * rsqrt(mean(x^2) + eps) * gamma (T5 RMSNorm, no mean subtraction)
 void rmsnorm_bf16(const bf16* x, const float* gamma, bf16* out, int rows, int N, float eps,
                   hipStream_t stream);
-// Fused BERT embedding: out[t] = LN(word[ids[t]] + pos[t % S] + type[tt[t]]).
+// Fused BERT embedding: out[t] = LN(word[ids[t]] + pos[t % S] + type[tt[t]]); ids clamped to
+// [0, vocab), type ids to [0, type_vocab).
 void embed_layernorm(const int32_t* ids, const int32_t* type_ids, const bf16* word, const bf16* pos,
                      const bf16* type, const float* gamma, const float* beta, bf16* out, int B, int S, int N,
-                     int vocab, float eps, hipStream_t stream);
+                     int vocab, int type_vocab, float eps, hipStream_t stream);
 // Plain embedding gather (T5 encoder/decoder input): out[t] = table[ids[t]] * scale
 void embed_gather(const int32_t* ids, const bf16* table, bf16* out, int tokens, int N, int vocab,
                   hipStream_t stream);

@@ -717,6 +717,25 @@ __device__ __forceinline__ u32x4 load16_untracked(const void* p) {
 // The fragment-layout 8-B accesses are 2-way bank conflicted (rows r, r+8
 // share a swizzle), the line-layout ones conflict-free. DS ops of one wave
 // execute in order, so the scratch needs no barrier, only lgkmcnt waits.
+// VMEM accounting of the line epilogue (per wave). s_waitcnt vmcnt(N) waits
+// until all but the wave's N youngest vector-memory ops are done; on gfx950
+// loads, stores and LDS-DMA of the global/buffer kinds all count on vmcnt and
+// retire IN ISSUE ORDER (MI355X_MICROARCH.md, s_waitcnt paragraph; CDNA4 ISA
+// "Data dependency resolution": only flat_* returns out of order, and the
+// epilogue issues none). Each 16-row block i has kLineLoadsPerBlock residual
+// loads and kLineStoresPerBlock output stores (distinct rows: never merged).
+// Younger than block i's loads when it waits: the loads of blocks i+1..7 and
+// the stores of blocks 0..i-1, i.e. L*(7-i) + S*i, which is the same for
+// every i only because L == S. kLineResWait is that count.
+constexpr int kLineBlocks = 8;
+constexpr int kLineLoadsPerBlock = 2;
+constexpr int kLineStoresPerBlock = 2;
+constexpr int kLineResWait = kLineLoadsPerBlock * (kLineBlocks - 1);
+static_assert(kLineLoadsPerBlock == kLineStoresPerBlock,
+              "vmcnt(kLineResWait) is exact for every block only when each block issues as many stores as loads");
+static_assert(kLineResWait == 14, "the counted residual wait assumes 8 blocks x 2 loads");
+static_assert(kLineResWait < 64, "vmcnt field is 6 bits on gfx950");
+
 template <int EPI, bool NT>
 __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int m0, int n0, int wm, int wn, int lane,
                                                   bf16* __restrict__ C, int ldc, const bf16* __restrict__ R, int ldr,
@@ -783,7 +802,7 @@ __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int 
       // pending: blocks 0-1 (issued in the last MMA phase) are followed by the
       // other pre load pair and 12 loads; block i >= 2 by 2 (7 - i) loads; and
       // every earlier block added its 2 stores -> 14 for every i
-      asm volatile("s_waitcnt vmcnt(14)" : "+v"(res[i][0]), "+v"(res[i][1]) :: "memory");
+      asm volatile("s_waitcnt vmcnt(%2)" : "+v"(res[i][0]), "+v"(res[i][1]) : "n"(kLineResWait) : "memory");
       __builtin_amdgcn_sched_barrier(0);
       *reinterpret_cast<u32x4*>(scratch + line_off0) = res[i][0];
       *reinterpret_cast<u32x4*>(scratch + line_off1) = res[i][1];
@@ -838,7 +857,10 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
     const float* __restrict__ bias, const bf16* __restrict__ R, int ldr, int M, int N, int K) {
   using namespace g2;
   constexpr int kImg = 256 * 128;
-  constexpr int kEpiOps = 16;  // VMEM ops per wave the epilogue leaves in flight (16-B stores)
+  // VMEM ops per wave the epilogue leaves in flight: its 16-B stores (every residual load
+  // has been waited for by then). The relaxed phase-0/1 waits below add this to their count.
+  constexpr int kEpiOps = kLineBlocks * kLineStoresPerBlock;
+  static_assert(kEpiOps == 16, "epilogue store count changed: re-derive the relaxed waits");
   constexpr int kBiasOff = 2 * 2 * kImg;  // [2 tiles][256] fp32 bias after the operand buffers
   // ONE __shared__ array: a second LDS object makes hipcc drain vmcnt before ds_reads
   constexpr int kEpiOff = kBiasOff + 2 * 256 * 4;  // LINE epilogue: 2 KiB scratch per wave

@@ -179,14 +179,15 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const int32_t* __restrict
                                                        const bf16* __restrict__ word, const bf16* __restrict__ pos,
                                                        const bf16* __restrict__ type, const float* __restrict__ gamma,
                                                        const float* __restrict__ beta, bf16* __restrict__ out,
-                                                       int tokens, int S, int vocab, float eps) {
+                                                       int tokens, int S, int vocab, int type_vocab, float eps) {
   const int lane = threadIdx.x & 63;
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= tokens) return;
   constexpr int N = NG * 256;
   int id = ids[t];
   id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
-  const int tt = type_ids ? type_ids[t] : 0;
+  int tt = type_ids ? type_ids[t] : 0;  // clamped like the word id: a bad type id never reads past the table
+  tt = tt < 0 ? 0 : (tt >= type_vocab ? type_vocab - 1 : tt);
   float v[NG * 4];
   load_row<NG>(word + (size_t)id * N, v, lane);
   add_row<NG>(pos + (size_t)(t % S) * N, v, lane);
@@ -263,14 +264,15 @@ void rmsnorm_bf16(const bf16* x, const float* gamma, bf16* out, int rows, int N,
 }
 
 void embed_layernorm(const int32_t* ids, const int32_t* type_ids, const bf16* word, const bf16* pos, const bf16* type,
-                     const float* gamma, const float* beta, bf16* out, int B, int S, int N, int vocab, float eps,
-                     hipStream_t stream) {
+                     const float* gamma, const float* beta, bf16* out, int B, int S, int N, int vocab, int type_vocab,
+                     float eps, hipStream_t stream) {
   check_width(N);
+  ATPU_CHECK(vocab > 0 && type_vocab > 0, "embedding tables must be non-empty");
   const int tokens = B * S;
   if (tokens <= 0) return;
   const dim3 grid((tokens + 3) / 4);
   ATPU_NG_DISPATCH(N, hipLaunchKernelGGL(embed_ln_kernel<NG>, grid, dim3(256), 0, stream, ids, type_ids, word, pos,
-                                         type, gamma, beta, out, tokens, S, vocab, eps));
+                                         type, gamma, beta, out, tokens, S, vocab, type_vocab, eps));
   ATPU_HIP_CHECK(hipGetLastError());
 }
 

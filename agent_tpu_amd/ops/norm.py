@@ -18,6 +18,13 @@ def _f32(t: torch.Tensor, n: int, name: str) -> None:
     check(t.dtype == torch.float32 and t.is_contiguous() and t.numel() == n, f"{name} must be fp32 [{n}]")
 
 
+def _check_out(out: torch.Tensor, shape, like: torch.Tensor) -> None:
+    """A caller-provided output must be a contiguous bf16 tensor of the result's shape on the input's device."""
+    check(tuple(out.shape) == tuple(shape), f"out must be {list(shape)}, got {list(out.shape)}")
+    check(out.dtype == torch.bfloat16 and out.is_contiguous(), "out must be contiguous bf16")
+    check(out.device == like.device, f"out is on {out.device}, inputs on {like.device}")
+
+
 def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-12,
               residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     rows, N = x.shape
@@ -32,7 +39,10 @@ def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: flo
     if residual is not None:
         check_bf16_dev(residual, "residual")
         check(residual.is_contiguous() and residual.shape == x.shape, "residual must match x")
-    out = torch.empty_like(x) if out is None else out
+    if out is None:
+        out = torch.empty_like(x)
+    else:
+        _check_out(out, x.shape, x)
     native().layernorm(ptr(x), ptr(residual), ptr(gamma), ptr(beta), ptr(out), rows, N, float(eps), stream_handle())
     return out
 
@@ -46,7 +56,10 @@ def rmsnorm(x: torch.Tensor, gamma: torch.Tensor, eps: float = 1e-6, out: Option
     check_bf16_dev(x, "x")
     check(x.is_contiguous(), "x must be contiguous")
     _f32(gamma, N, "gamma")
-    out = torch.empty_like(x) if out is None else out
+    if out is None:
+        out = torch.empty_like(x)
+    else:
+        _check_out(out, x.shape, x)
     native().rmsnorm(ptr(x), ptr(gamma), ptr(out), rows, N, float(eps), stream_handle())
     return out
 
@@ -59,7 +72,8 @@ def embed_layernorm(ids: torch.Tensor, word: torch.Tensor, pos: torch.Tensor, ty
     V, N = word.shape
     if not ids.is_cuda:
         tt = type_ids if type_ids is not None else torch.zeros_like(ids)
-        x = word.float()[ids.long().clamp(0, V - 1)] + pos.float()[:S].unsqueeze(0) + type_.float()[tt.long()]
+        x = (word.float()[ids.long().clamp(0, V - 1)] + pos.float()[:S].unsqueeze(0)
+             + type_.float()[tt.long().clamp(0, type_.shape[0] - 1)])
         y = F.layer_norm(x, (N,), gamma.float(), beta.float(), eps).to(word.dtype).view(B * S, N)
         return out.copy_(y) if out is not None else y
     check(ids.dtype == torch.int32 and ids.is_contiguous(), "ids must be contiguous int32")
@@ -70,9 +84,14 @@ def embed_layernorm(ids: torch.Tensor, word: torch.Tensor, pos: torch.Tensor, ty
     _f32(beta, N, "beta")
     if type_ids is not None:
         check(type_ids.dtype == torch.int32 and type_ids.shape == ids.shape, "type_ids must be int32 [B,S]")
-    out = torch.empty((B * S, N), dtype=torch.bfloat16, device=ids.device) if out is None else out
+    check(tuple(pos.shape[1:]) == (N,) and tuple(type_.shape[1:]) == (N,) and type_.shape[0] > 0,
+          "pos/type tables must be [*, N]")
+    if out is None:
+        out = torch.empty((B * S, N), dtype=torch.bfloat16, device=ids.device)
+    else:
+        _check_out(out, (B * S, N), word)
     native().embed_layernorm(ptr(ids), ptr(type_ids), ptr(word), ptr(pos), ptr(type_), ptr(gamma), ptr(beta),
-                             ptr(out), B, S, N, V, float(eps), stream_handle())
+                             ptr(out), B, S, N, V, type_.shape[0], float(eps), stream_handle())
     return out
 
 
@@ -84,6 +103,9 @@ def embed_gather(ids: torch.Tensor, table: torch.Tensor, out: Optional[torch.Ten
         return out.copy_(y) if out is not None else y
     check(ids.dtype == torch.int32 and ids.is_contiguous(), "ids must be contiguous int32")
     check_bf16_dev(table, "table")
-    out = torch.empty((flat.numel(), N), dtype=torch.bfloat16, device=ids.device) if out is None else out
+    if out is None:
+        out = torch.empty((flat.numel(), N), dtype=torch.bfloat16, device=ids.device)
+    else:
+        _check_out(out, (flat.numel(), N), table)
     native().embed_gather(ptr(flat), ptr(table), ptr(out), flat.numel(), N, V, stream_handle())
     return out

@@ -107,8 +107,8 @@ def broadcast_pack(pack, cfg, device: torch.device, src: int = 0, builder=None):
     if rank == src:
         assert pack is not None
         out = pack if pack.buffer.device == device else pack.to(device)
-    else:
-        out = ParamPack(specs, device=device)
+    else:  # destination: preallocated by the caller (dp_ops.load_collectively) or here
+        out = pack if pack is not None and pack.buffer.device == device else ParamPack(specs, device=device)
     if is_dist():
         cdev = comm_device(device)
         buf = out.buffer if out.buffer.device == cdev else out.buffer.to(cdev)

@@ -19,9 +19,10 @@ Registered bodies: ``map_classify_csv`` (C2 all-gather of top-k),
 from __future__ import annotations
 
 import os
+import threading
 import time
 import traceback
-from typing import Any, Callable, Dict, Tuple
+from typing import Any, Callable, Dict, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -68,7 +69,14 @@ def is_device_fault(msg: str) -> bool:
     return any(m in msg for m in FAULT_MARKERS)
 
 
-class LeftGroup(Exception):
+class DPError(RuntimeError):
+    """A DP job failed on one or more ranks; the message names each rank.
+
+    Ops must not turn this into a soft result (``map_classify``'s fallback
+    stub): the agent has to see it to mark faulted devices unhealthy."""
+
+
+class LeftGroup(DPError):
     """This rank's device faulted and it was dropped from the DP group."""
 
 
@@ -94,7 +102,8 @@ def maybe_inject_fault(stage: str) -> None:
     raise RuntimeError(f"injected fault ({spec}) at {stage}")
 
 
-_ERR_TYPES = {"ValueError": ValueError, "TypeError": TypeError, "KeyError": KeyError}
+_ERR_TYPES = {"ValueError": ValueError, "TypeError": TypeError, "KeyError": KeyError,
+              "FileNotFoundError": FileNotFoundError}
 
 
 def _check_errors(err: str) -> None:
@@ -125,12 +134,69 @@ def _check_errors(err: str) -> None:
         if dist.get_rank() in faulted:
             raise LeftGroup(msg)
         msg += f" (dropped from the DP group: ranks {faulted}; DP world now {len(members())})"
-    raise RuntimeError(msg)
+    raise DPError(msg)
+
+
+def _err_str(exc: BaseException) -> str:
+    return f"{type(exc).__name__}: {exc}"
+
+
+_CTX = threading.local()
+
+
+def in_task() -> bool:
+    """True while this rank executes a dispatched DP task body (every rank of
+    the group runs the same body, so collectives inside it pair up)."""
+    return getattr(_CTX, "depth", 0) > 0
 
 
 def run_collective(name: str, payload: Dict[str, Any]) -> Any:
     fn = _TASKS[name]
-    return fn(payload)
+    _CTX.depth = getattr(_CTX, "depth", 0) + 1
+    try:
+        return fn(payload)
+    finally:
+        _CTX.depth -= 1
+
+
+def load_collectively(local: Callable[[], Any], collective: Callable[[Any], Any],
+                      post: Optional[Callable[[Any], Any]] = None) -> Any:
+    """Model-load protocol of a DP task: no rank enters the C1 broadcast
+    unless every rank is ready for it.
+
+    1. ``local()`` on every rank: rank 0 builds the source weights on the
+       host (seeded init or a safetensors load), the others allocate the
+       destination; either may raise (bad path, missing tensor, HBM OOM).
+    2. Errors are exchanged (:func:`_check_errors`): one failure fails the
+       job on EVERY rank before any collective is issued, so a rank that
+       leaves early never pairs a later broadcast with a stale one.
+    3. ``collective(state)``: the broadcast itself, reached by all or none.
+    4. ``post(result)`` (engine / graph build, local) with a second exchange,
+       so a per-rank OOM there also fails every rank together.
+
+    Outside a process group it is just ``post(collective(local()))`` with the
+    error raised directly.
+    """
+    err, state = "", None
+    try:
+        state = local()
+    except Exception as exc:
+        err = _err_str(exc)
+        if not is_dist():
+            raise
+    _check_errors(err)
+    out = collective(state)
+    if post is None:
+        return out
+    err, res = "", None
+    try:
+        res = post(out)
+    except Exception as exc:
+        err = _err_str(exc)
+        if not is_dist():
+            raise
+    _check_errors(err)
+    return res
 
 
 def dispatch(name: str, payload: Dict[str, Any]) -> Any:
@@ -178,7 +244,7 @@ def classify_csv_task(payload: Dict[str, Any]) -> Any:
 
     rank, ws = world()
     timing: Dict[str, float] = {}
-    # model load is itself collective (C1 broadcast), so it happens on every rank
+    # model load is itself collective (C1 broadcast, errors exchanged before it), on every rank
     with span("load_ms", timing):
         h = get_gpu_handle(get_model_path(payload.get("model_path")))
     err, idx, sc, meta = "", None, None, {}
@@ -211,6 +277,36 @@ def classify_csv_task(payload: Dict[str, Any]) -> Any:
     from ops.map_classify import csv_result
 
     return csv_result(h, idx.cpu(), sc.cpu(), meta, payload)
+
+
+@dp_task("map_classify_rows")
+def classify_rows_task(payload: Dict[str, Any]) -> Any:
+    """``input`` (one pre-tokenized row: rank 0 computes it) and ``texts``
+    (rows split over the ranks, top-k all-gathered, C2) forms of map_classify.
+    The model load is collective on every rank either way."""
+    from ops import map_classify as mc
+    from ops._gpu_runtime import get_gpu_handle, get_model_path
+
+    rank, ws = world()
+    h = get_gpu_handle(get_model_path(payload.get("model_path")))
+    op, t0 = payload.get("_op", mc.OP_NAME), float(payload.get("_t0", time.time()))
+    if "input" in payload:
+        return mc.classify_ids(h, payload, op, t0) if rank == 0 else None
+    texts = mc.check_texts(payload)  # same payload on every rank: same outcome, no exchange needed
+    k = max(1, min(int(payload.get("topk", 5)), h.cfg.num_labels))
+    err, idx, sc = "", None, None
+    try:
+        s_r, n_r = split_range(0, len(texts), ws, rank)
+        maybe_inject_fault("classify")
+        res = h.engine.classify_texts(texts[s_r:s_r + n_r], k)
+        idx, sc = res.idx[:, :k].contiguous(), res.score[:, :k].contiguous()
+    except Exception as exc:
+        err = _err_str(exc)
+    _check_errors(err)
+    idx, sc = all_gather_rows(idx, sc)
+    if rank != 0:
+        return None
+    return mc.texts_result(h, idx.cpu(), sc.cpu(), payload, ws)
 
 
 # ---------------------------------------------------------- risk_accumulate

@@ -287,12 +287,20 @@ def build_model(name: str, pack=None, device: Optional[torch.device] = None, see
     mod = bart if fam == "bart" else t5
     cfg = mod.config_for(name)
     if broadcast:
+        from ..models.params import ParamPack
         from ..parallel.dp import broadcast_pack, world
+        from ..parallel.dp_ops import load_collectively
 
-        if world()[0] == 0 and pack is None:
-            pack = mod.init_random(cfg, seed=seed)
-        pack = broadcast_pack(pack, cfg, device if device is not None else torch.device("cpu"),
-                              builder=mod.param_specs)
+        dev = device if device is not None else torch.device("cpu")
+        src = pack
+
+        def local():  # rank 0: seeded init + H2D; others: the destination buffer (either may OOM)
+            if world()[0] == 0:
+                p = src if src is not None else mod.init_random(cfg, seed=seed)
+                return p if p.buffer.device == dev else p.to(dev)
+            return ParamPack(mod.param_specs(cfg), device=dev)
+
+        pack = load_collectively(local, lambda p: broadcast_pack(p, cfg, dev, builder=mod.param_specs))
     pack = pack if pack is not None else mod.init_random(cfg, seed=seed)
     if device is not None and pack.buffer.device != device:
         pack = pack.to(device)

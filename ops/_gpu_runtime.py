@@ -65,38 +65,71 @@ def parse_spec(path: str) -> ModelSpec:
 
 
 class GpuHandle:
-    """A loaded model: config + device engine (built lazily per device)."""
+    """A loaded model: config + device engine."""
 
-    def __init__(self, spec: ModelSpec, device):
-        from agent_tpu_amd.models.bert import config_for, init_random
-        from agent_tpu_amd.parallel.dp import broadcast_pack, is_dist, world
-        from agent_tpu_amd.runtime.classify import ClassifyEngine
-
+    def __init__(self, spec: ModelSpec, cfg, engine):
         self.spec = spec
         self.model_path = spec.path
-        self.cfg = config_for(spec.preset, num_labels=spec.labels)
-        rank, _ = world()
-        pack = None
-        if rank == 0 or not is_dist():
-            pack = self._load_pack(init_random)
-        pack = broadcast_pack(pack, self.cfg, device) if is_dist() else pack.to(device)
+        self.cfg = cfg
+        self.engine = engine
+
+
+def _load_host_pack(spec: ModelSpec, cfg):
+    from agent_tpu_amd.models.bert import init_random
+
+    if spec.file:
+        from safetensors.torch import load_file
+
+        from agent_tpu_amd.models.bert import param_specs
+        from agent_tpu_amd.models.params import ParamPack
+
+        pack = ParamPack(param_specs(cfg))
+        tensors = load_file(spec.file)
+        missing = [n for n in pack.names() if n not in tensors]
+        if missing:
+            raise KeyError(f"{spec.file}: missing tensors {missing[:4]}{' ...' if len(missing) > 4 else ''}")
+        for name in pack.names():
+            pack[name].copy_(tensors[name])
+        return pack
+    return init_random(cfg, seed=spec.seed)
+
+
+def _build_handle(model_path: str, device) -> GpuHandle:
+    """Load a model on this rank, or on every rank of the DP group together.
+
+    Under a process group the load follows ``dp_ops.load_collectively``: rank 0
+    builds the weights on the host and copies them to its GPU, the other ranks
+    allocate the destination, errors are exchanged, and only then does the C1
+    broadcast run (all ranks or none); the engine build is exchanged again.
+    """
+    from agent_tpu_amd.models.bert import config_for, param_specs
+    from agent_tpu_amd.models.params import ParamPack
+    from agent_tpu_amd.parallel.dp import broadcast_pack, is_dist, world
+    from agent_tpu_amd.parallel.dp_ops import load_collectively
+    from agent_tpu_amd.runtime.classify import ClassifyEngine
+
+    dist_on = is_dist()
+    box = {}
+
+    def local():
+        spec = parse_spec(model_path)
+        cfg = config_for(spec.preset, num_labels=spec.labels)
+        box.update(spec=spec, cfg=cfg)
+        if dist_on and world()[0] != 0:
+            return ParamPack(param_specs(cfg), device=device)
+        return _load_host_pack(spec, cfg).to(device)
+
+    def collective(pack):
+        return broadcast_pack(pack, box["cfg"], device) if dist_on else pack
+
+    def post(pack):
+        spec, cfg = box["spec"], box["cfg"]
         batch = spec.batch_rows or _auto_batch_rows()
-        self.engine = ClassifyEngine(self.cfg, pack, device, batch_rows=batch, seq_len=spec.seq_len,
-                                     topk=min(self.cfg.num_labels, 64))
+        eng = ClassifyEngine(cfg, pack, device, batch_rows=batch, seq_len=spec.seq_len,
+                             topk=min(cfg.num_labels, 64))
+        return GpuHandle(spec, cfg, eng)
 
-    def _load_pack(self, init_random):
-        if self.spec.file:
-            from safetensors.torch import load_file
-
-            from agent_tpu_amd.models.params import ParamPack
-            from agent_tpu_amd.models.bert import param_specs
-
-            pack = ParamPack(param_specs(self.cfg))
-            tensors = load_file(self.spec.file)
-            for name in pack.names():
-                pack[name].copy_(tensors[name])
-            return pack
-        return init_random(self.cfg, seed=self.spec.seed)
+    return load_collectively(local, collective, post)
 
 
 def _auto_batch_rows() -> int:
@@ -137,6 +170,8 @@ def lru_budget_bytes(device) -> int:
 def device_for_rank():
     import torch
 
+    if os.getenv("CLASSIFY_DEVICE", "").strip().lower() == "cpu":
+        return torch.device("cpu")  # fp32 PyTorch oracle path (CPU tests of the op forms)
     if not torch.cuda.is_available():
         raise RuntimeError("No ROCm GPU available (torch.cuda.is_available() is False)")
     # modulo: ranks may share a device in single-GPU rehearsals (gloo backend)
@@ -146,6 +181,20 @@ def device_for_rank():
 
 
 def get_gpu_handle(model_path: str, device=None) -> GpuHandle:
+    """Cached handle for ``model_path``.
+
+    Under a DP process group this is a collective: call it only from a
+    dispatched DP task body (``dp_ops.dispatch``), where every rank asks for
+    the same models in the same order. The caches of all ranks then hold the
+    same keys, so they agree on hit or miss, and a miss broadcasts the
+    weights from rank 0 (C1) with every rank taking part.
+    """
+    from agent_tpu_amd.parallel.dp import is_dist
+    from agent_tpu_amd.parallel.dp_ops import in_task
+
+    if is_dist() and not in_task():
+        raise RuntimeError("get_gpu_handle under a DP process group must run inside a dispatched DP task "
+                           "(dp_ops.dispatch), so that every rank loads the model together")
     device = device if device is not None else device_for_rank()
     key = (model_path, str(device))
     with _lock:
@@ -153,7 +202,7 @@ def get_gpu_handle(model_path: str, device=None) -> GpuHandle:
         if h is not None:
             _cache.move_to_end(key)
             return h
-        h = GpuHandle(parse_spec(model_path), device)
+        h = _build_handle(model_path, device)
         _cache[key] = h
         budget = lru_budget_bytes(device)
         evicted = False

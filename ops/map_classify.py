@@ -23,7 +23,6 @@ import time
 from typing import Any, Dict, List
 
 from . import register_op
-from ._gpu_runtime import get_gpu_handle, get_model_path
 
 OP_NAME = "map_classify_tpu"
 
@@ -37,9 +36,11 @@ def _fallback(payload: Dict[str, Any], reason: str, t0: float, op: str) -> Dict[
             "elapsed_ms": (time.time() - t0) * 1000.0}
 
 
-def _classify_ids(h, payload: Dict[str, Any], k: int, op: str, t0: float) -> Dict[str, Any]:
+def classify_ids(h, payload: Dict[str, Any], op: str, t0: float) -> Dict[str, Any]:
+    """The reference form: one pre-tokenized row (``input``) -> reference keys."""
     import torch
 
+    k = max(1, min(int(payload.get("topk", 5)), h.cfg.num_labels))
     S = h.engine.S
     raw = payload["input"]
     ids = torch.tensor(raw, dtype=torch.int64)
@@ -54,6 +55,20 @@ def _classify_ids(h, payload: Dict[str, Any], k: int, op: str, t0: float) -> Dic
                                          torch.tensor([max(1, n)], dtype=torch.int32, device=dev), k)
     return {"op": op, "model_path": h.model_path, "topk": _topk_list(idx[0].tolist(), sc[0].tolist()),
             "elapsed_ms": (time.time() - t0) * 1000.0}
+
+
+def check_texts(payload: Dict[str, Any]) -> List[str]:
+    texts = payload["texts"]
+    if not isinstance(texts, list):
+        raise ValueError("payload.texts must be a list of strings")
+    return ["" if t is None else str(t) for t in texts]
+
+
+def texts_result(h, idx, sc, payload: Dict[str, Any], dp_world: int) -> Dict[str, Any]:
+    k = max(1, min(int(payload.get("topk", 5)), h.cfg.num_labels))
+    extra = {"dp_world_size": dp_world} if dp_world > 1 else {}
+    return _rows_result(h, idx[:, :k], sc[:, :k], 0, k, payload.get("_op", OP_NAME),
+                        float(payload.get("_t0", time.time())), extra)
 
 
 def csv_result(h, idx, sc, meta: Dict[str, Any], payload: Dict[str, Any]) -> Dict[str, Any]:
@@ -86,31 +101,32 @@ def _rows_result(h, idx, sc, start: int, k: int, op: str, t0: float, extra: Dict
     return out
 
 
+def hard_failure(exc: BaseException) -> bool:
+    """Failures the fallback stub must not hide: a HIP device fault (the agent
+    marks the device unhealthy from the raised error) and any DP job failure
+    (it names the ranks; a faulted rank has already left the DP group)."""
+    from agent_tpu_amd.parallel.dp_ops import DPError, is_device_fault
+
+    return isinstance(exc, DPError) or is_device_fault(str(exc))
+
+
 def run(payload: Dict[str, Any], ctx: Dict[str, Any] = None, op: str = OP_NAME) -> Dict[str, Any]:
     payload = payload or {}
     t0 = time.time()
     allow_fallback = payload.get("allow_fallback", True)
     try:
-        if "source_uri" in payload and "input" not in payload:
-            # DP path: every rank (not only this one) must load the model, so
-            # the task descriptor is broadcast before anything touches the GPU
-            from agent_tpu_amd.parallel.dp_ops import dispatch
+        # Every form runs as a DP task: under torchrun the descriptor is
+        # broadcast first, so all ranks load (and cache) the same models in the
+        # same order and the C1 weight broadcast always has every rank in it.
+        from agent_tpu_amd.parallel.dp_ops import dispatch
 
-            out = dispatch("map_classify_csv", dict(payload, _op=op, _t0=t0))
-            return out
-        h = get_gpu_handle(get_model_path(payload.get("model_path")))
-        k = max(1, min(int(payload.get("topk", 5)), h.cfg.num_labels))
-        if "input" in payload:
-            return _classify_ids(h, payload, k, op, t0)
-        if "texts" in payload:
-            texts = payload["texts"]
-            if not isinstance(texts, list):
-                raise ValueError("payload.texts must be a list of strings")
-            res = h.engine.classify_texts(["" if t is None else str(t) for t in texts], k)
-            return _rows_result(h, res.idx[:, :k], res.score[:, :k], 0, k, op, t0, {})
-        raise ValueError('payload missing required key: "input" (or "texts" / "source_uri")')
+        if "source_uri" in payload and "input" not in payload:
+            return dispatch("map_classify_csv", dict(payload, _op=op, _t0=t0))
+        if "input" not in payload and "texts" not in payload:
+            raise ValueError('payload missing required key: "input" (or "texts" / "source_uri")')
+        return dispatch("map_classify_rows", dict(payload, _op=op, _t0=t0))
     except Exception as exc:
-        if allow_fallback:
+        if allow_fallback and not hard_failure(exc):
             return _fallback(payload, str(exc), t0, op)
         raise
 

@@ -1,51 +1,64 @@
-"""``map_tokenize`` — fixed-size character chunking.
+"""``map_tokenize`` — fixed-size character chunking (the reference's "tokens").
 
-Parity with ``/root/reference/ops/map_tokenize.py:6-61``. The reference's
-"tokens" are character chunks (not subwords); the subword/word ids that feed
-BERT are produced on the GPU by ``map_classify`` (see map_classify.CONTRACT.md).
-Errors are *returned* as ``{"ok": False, "error": ...}``, never raised.
+Behaviour pinned to ``/root/reference/ops/map_tokenize.py:6-61`` by the
+golden table in ``tests/contract/test_simple_ops.py``:
+a "token" is a run of at most ``chunk_size`` characters, not a subword. The
+word-piece ids that BERT consumes are produced on the GPU by ``map_classify``
+(tokenizer kernel K1). Bad input is *returned* as ``{"ok": False, "error"}``.
+
+Design: both payload shapes are normalised to one list of source strings
+(``items`` entries, or the single ``text``/``data`` string), cut by a single
+slicing pass; only the result keys differ between the two shapes.
 """
 from __future__ import annotations
 
-from typing import Any, Dict, List
+from itertools import chain
+from typing import Any, Dict, Iterable, List, Optional, Tuple
 
 from . import register_op
 
 DEFAULT_CHUNK = 1024
+_ERR_SIZE = "payload.chunk_size must be a positive integer"
+_ERR_ITEMS = "payload.items must be a list of strings"
+_ERR_TEXT = "payload.text must be a string"
 
 
 def chunk_text(text: str, size: int) -> List[str]:
-    """Split ``text`` into consecutive ``size``-character pieces."""
-    return [text[pos:pos + size] for pos in range(0, len(text), size)] if text else []
+    """Consecutive ``size``-character slices of ``text`` (``[]`` for ``""``)."""
+    return list(_slices(text, size))
 
 
-def _bad(msg: str) -> Dict[str, Any]:
-    return {"ok": False, "error": msg}
+def _slices(text: str, size: int) -> Iterable[str]:
+    return (text[lo:lo + size] for lo in range(0, len(text), size))
+
+
+def _sources(payload: Dict[str, Any]) -> Tuple[Optional[List[str]], bool, Optional[str]]:
+    """-> (source strings, came from ``items``, error message)."""
+    if payload.get("items") is not None:
+        items = payload["items"]
+        if not isinstance(items, list):
+            return None, True, _ERR_ITEMS
+        return ["" if it is None else str(it) for it in items], True, None
+    # a falsy ``text`` ("" or None) falls through to ``data`` (reference behaviour)
+    text = payload.get("text") or payload.get("data", "")
+    if not isinstance(text, str):
+        return None, False, _ERR_TEXT
+    return [text], False, None
 
 
 @register_op("map_tokenize")
 def map_tokenize(payload: Any) -> Dict[str, Any]:
-    payload = payload or {}
+    payload = payload if payload is not None else {}
     size = payload.get("chunk_size", DEFAULT_CHUNK)
-    # bool is an int subclass in Python; the reference accepts it (True == 1)
-    if not isinstance(size, int) or size <= 0:
-        return _bad("payload.chunk_size must be a positive integer")
-
-    items = payload.get("items")
-    if "items" in payload and items is not None:
-        if not isinstance(items, list):
-            return _bad("payload.items must be a list of strings")
-        pieces: List[str] = []
-        n_chars = 0
-        for item in items:
-            s = "" if item is None else str(item)
-            n_chars += len(s)
-            pieces += chunk_text(s, size)
-        return {"ok": True, "tokens": pieces, "count": len(pieces),
-                "total_chars": n_chars, "items_count": len(items)}
-
-    text = payload.get("text") or payload.get("data", "")
-    if not isinstance(text, str):
-        return _bad("payload.text must be a string")
-    pieces = chunk_text(text, size)
-    return {"ok": True, "tokens": pieces, "count": len(pieces), "total_chars": len(text)}
+    # ``bool`` subclasses ``int``: True is accepted as size 1, like the reference
+    if not (isinstance(size, int) and size > 0):
+        return {"ok": False, "error": _ERR_SIZE}
+    srcs, from_items, err = _sources(payload)
+    if err is not None:
+        return {"ok": False, "error": err}
+    tokens = list(chain.from_iterable(_slices(s, size) for s in srcs))
+    out: Dict[str, Any] = {"ok": True, "tokens": tokens, "count": len(tokens),
+                           "total_chars": sum(map(len, srcs))}
+    if from_items:
+        out["items_count"] = len(srcs)
+    return out

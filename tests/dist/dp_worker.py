@@ -155,6 +155,50 @@ def scen_shrink():
     return out
 
 
+def scen_classify():
+    """map_classify's ``input`` and ``texts`` forms under DP (CPU engines via
+    CLASSIFY_DEVICE=cpu): every rank takes part in the model load (C1), texts
+    are split and all-gathered (C2), and load failures, on every rank or on
+    rank 0 only, fail the job on all ranks without desynchronising the group."""
+    rank, ws = dp.world()
+    if rank != 0:
+        dp_ops.worker_loop()
+        return None
+    from agent_tpu_amd.models.bert import config_for, init_random
+    from agent_tpu_amd.runtime.classify import ClassifyEngine
+    from ops import map_classify as mc
+
+    model = "bert-tiny?labels=3&batch=4&seq=32"
+    out = {}
+    ids = [101] + [1000 + 37 * i for i in range(20)] + [102] + [0] * 10
+    out["input"] = mc.map_classify({"input": ids, "model_path": model, "topk": 3, "allow_fallback": False})
+    texts = [f"row {i} " + "lorem ipsum dolor sit amet " * (i % 4) for i in range(7)]
+    got = mc.map_classify({"texts": texts, "model_path": model, "topk": 2, "allow_fallback": False})
+    cfg = config_for("bert-tiny", num_labels=3)
+    eng = ClassifyEngine(cfg, init_random(cfg, seed=0), torch.device("cpu"), batch_rows=4, seq_len=32, topk=3)
+    ref = eng.classify_texts(texts, 2)
+    out["texts_world"] = got["dp_world_size"]
+    out["texts_rows"] = got["row_count"]
+    out["texts_idx_match"] = [[t["index"] for t in r["topk"]] for r in got["rows"]] == ref.idx.tolist()
+    out["texts_score_err"] = max(abs(t["score"] - s) for r, rs in zip(got["rows"], ref.score.tolist())
+                                 for t, s in zip(r["topk"], rs))
+    # every rank fails the load the same way -> the op's own error type, then the fallback stub
+    out["missing"] = mc.map_classify({"texts": ["x"], "model_path": "/nope/model.safetensors"})
+    # rank 0 alone fails (its safetensors lacks tensors; the others only allocate): the job
+    # fails on every rank before the broadcast, naming rank 0
+    bad = os.environ["DP_TEST_BAD_MODEL"]
+    try:
+        mc.map_classify({"texts": ["x"], "model_path": bad, "allow_fallback": False})
+        out["rank0_only"] = None
+    except Exception as exc:
+        out["rank0_only"] = f"{type(exc).__name__}: {exc}"
+    # the group is still in step: the next load + job works
+    again = mc.map_classify({"texts": texts[:3], "model_path": model, "topk": 2, "allow_fallback": False})
+    out["again_rows"] = again["row_count"]
+    dp_ops.shutdown_workers()
+    return out
+
+
 def main():
     scen = sys.argv[1]
     dist.init_process_group("gloo")
@@ -162,7 +206,7 @@ def main():
         res = globals()[f"scen_{scen}"]()
     finally:
         if dist.is_initialized():
-            if scen not in ("risk", "fault", "summarize", "shrink"):  # worker_loop ranks already left the group
+            if scen not in ("risk", "fault", "summarize", "shrink", "classify"):  # worker_loop ranks already left the group
                 dist.barrier()
             dist.destroy_process_group()
     if int(os.environ.get("RANK", "0")) == 0:

@@ -97,3 +97,24 @@ def test_device_fault_shrinks_dp_world():
     assert res["after_ok"] and res["after_world"] == 2
     assert res["bad"] == "payload.values must be a list"
     assert res["members_after_bad"] == [0, 1]
+
+
+def test_classify_input_and_texts_forms_under_dp(tmp_path):
+    """ADVICE r1 (high/medium): the ``input``/``texts`` forms are dispatched to every
+    rank (no rank-0-only collective), and model-load failures are exchanged before
+    the weight broadcast (on all ranks, or on rank 0 alone) instead of hanging."""
+    import torch
+    from safetensors.torch import save_file
+
+    bad = tmp_path / "partial.safetensors"
+    save_file({"emb.word": torch.zeros(4, 4)}, str(bad))
+    (tmp_path / "partial.safetensors.json").write_text('{"preset": "bert-tiny", "num_labels": 2}')
+    res = run_ranks("classify", 2, {"CLASSIFY_DEVICE": "cpu", "DP_TEST_BAD_MODEL": str(bad)})
+    inp = res["input"]
+    assert set(inp) == {"op", "model_path", "topk", "elapsed_ms"} and len(inp["topk"]) == 3
+    assert res["texts_world"] == 2 and res["texts_rows"] == 7
+    assert res["texts_idx_match"] and res["texts_score_err"] < 1e-5
+    assert res["missing"]["fallback"] == "cpu" and "GPU model not found" in res["missing"]["reason"]
+    assert res["rank0_only"] is not None and res["rank0_only"].startswith("DPError: rank 0: KeyError")
+    assert "rank 1" not in res["rank0_only"]
+    assert res["again_rows"] == 3

@@ -72,3 +72,53 @@ def test_dp_agent_risk_reduce_and_shutdown(ctl, tmp_path):
     assert res["after"]["result"]["sum"] == 10.0  # the DP group survived the failed job
     assert p.returncode == 0, out[-3000:]
     assert "dp worker rank=1 ready" in out and "stopped" in out
+
+
+def test_dp_agent_classify_input_first_and_device_fault(ctl):
+    """under torchrun the FIRST job is a reference-form ``input``
+    classify (the model load must involve every rank, or the DP group hangs),
+    and a device fault on rank 1 with the default ``allow_fallback`` fails the
+    job (it is not swallowed into the fallback stub), drops rank 1, and later
+    jobs still run."""
+    model = "bert-tiny?labels=3&batch=4&seq=32"
+    ids = [101] + [1000 + 13 * i for i in range(12)] + [102] + [0] * 18
+    ctl.lease({"id": "in", "op": "map_classify", "payload": {"input": ids, "model_path": model, "topk": 2}})
+    ctl.lease({"id": "tx", "op": "map_classify", "payload": {"texts": ["a b c", "d e", "f"], "model_path": model}})
+    ctl.lease({"id": "tx2", "op": "map_classify", "payload": {"texts": ["g h", "i"], "model_path": model}})
+    ctl.lease({"id": "e", "op": "echo", "payload": {"k": 2}})
+    env = dict(os.environ, CONTROLLER_URL=ctl.url, TASKS="echo,map_classify", IDLE_SLEEP_SEC="0.02",
+               ERROR_LOG_EVERY_SEC="0", ATPU_DP_BACKEND="gloo", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="",
+               GPU_DISABLED="1", OMP_NUM_THREADS="1", PYTHONUNBUFFERED="1", CLASSIFY_DEVICE="cpu",
+               MI355X_FAULT="rank:1:classify:1:device")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", "app.py"]
+    p = subprocess.Popen(cmd, cwd=REPO, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    try:
+        assert ctl.wait(lambda c: "e" in {r["job_id"] for r in c.results}, 180), ctl.results
+        # rank 1 left the DP group after its fault and exits on its own: let it finish
+        # (a SIGTERM during interpreter teardown would be reported as a failed rank)
+        for r in psutil.Process(p.pid).children(recursive=True):
+            try:
+                if r.environ().get("LOCAL_RANK") == "1":
+                    r.wait(timeout=90)
+            except (psutil.NoSuchProcess, psutil.AccessDenied):
+                pass
+    finally:
+        for r in psutil.Process(p.pid).children(recursive=True):
+            try:
+                r.send_signal(signal.SIGTERM)
+            except psutil.NoSuchProcess:
+                pass
+        out, _ = p.communicate(timeout=120)
+    res = {r["job_id"]: r for r in ctl.results}
+    first = res["in"]
+    assert first["status"] == "succeeded", first
+    assert set(first["result"]) == {"op", "model_path", "topk", "elapsed_ms"} and len(first["result"]["topk"]) == 2
+    tx = res["tx"]
+    assert tx["status"] == "failed", tx
+    assert "rank 1" in tx["error"]["message"] and "hipError" in tx["error"]["message"]
+    assert "dropped from the DP group" in tx["error"]["message"]
+    tx2 = res["tx2"]
+    assert tx2["status"] == "succeeded" and tx2["result"]["row_count"] == 2, tx2
+    assert res["e"]["result"] == {"ok": True, "echo": {"k": 2}}
+    assert p.returncode == 0, out[-3000:]
