@@ -73,6 +73,29 @@ PYBIND11_MODULE(_atpu, m) {
       "bf16 MFMA GEMM C = epi(A @ Bt^T)", py::arg("A"), py::arg("lda"), py::arg("Bt"), py::arg("ldb"), py::arg("C"),
       py::arg("ldc"), py::arg("bias"), py::arg("R"), py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"),
       py::arg("epi"), py::arg("stream"), py::arg("splits") = 1, py::arg("ws") = 0);
+  m.def(
+      "gemm_ln",
+      [](uintptr_t A, int lda, uintptr_t Bt, int ldb, uintptr_t C, int ldc, uintptr_t bias, uintptr_t R, int ldr, int M,
+         int N, int K, int epi, uintptr_t in_fin, uintptr_t colsum, uintptr_t res_fin, uintptr_t gamma,
+         uintptr_t part_out, uintptr_t stream) {
+        GemmArgs g;
+        g.A = P<const bf16>(A); g.lda = lda; g.Bt = P<const bf16>(Bt); g.ldb = ldb; g.C = P<bf16>(C); g.ldc = ldc;
+        g.bias = P<const float>(bias); g.R = P<const bf16>(R); g.ldr = ldr; g.M = M; g.N = N; g.K = K; g.epi = epi;
+        g.in_fin = P<const float>(in_fin); g.colsum = P<const float>(colsum); g.res_fin = P<const float>(res_fin);
+        g.gamma = P<const float>(gamma); g.part_out = P<float>(part_out);
+        gemm_bf16(g, S(stream));
+      },
+      "bf16 MFMA GEMM with LayerNorm folding epilogues (InNorm / ResNorm / StatsOut)", py::arg("A"), py::arg("lda"),
+      py::arg("Bt"), py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("bias"), py::arg("R"), py::arg("ldr"),
+      py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("in_fin"), py::arg("colsum"),
+      py::arg("res_fin"), py::arg("gamma"), py::arg("part_out"), py::arg("stream"));
+  m.def(
+      "ln_stats_finalize",
+      [](uintptr_t part, int slots, int M, int K, float eps, uintptr_t fin, uintptr_t stream) {
+        ln_stats_finalize(P<const float>(part), slots, M, K, eps, P<float>(fin), S(stream));
+      },
+      "fin[m] = (rstd, rstd*mu) from StatsOut partials [slots][M][2]", py::arg("part"), py::arg("slots"),
+      py::arg("M"), py::arg("K"), py::arg("eps"), py::arg("fin"), py::arg("stream"));
   m.def("trace_enabled", &trace_enabled, "roctx tracing active (MI355X_TRACE=1 and roctx loadable)");
   m.def("trace_push", [](const std::string& n) { trace_push(n.c_str()); });
   m.def("trace_pop", &trace_pop);
@@ -83,6 +106,9 @@ PYBIND11_MODULE(_atpu, m) {
   m.def("gemm_256_variant", &gemm_256_variant, py::arg("set") = -1,
         "256x256 GEMM schedule: 0 = 256b, 1 = 256p ping-pong, 2 = 256s persistent, 3 = 256l full-line "
         "epilogue, 4 = 256n full-line + nt stores (default); set >= 0 switches, returns the current");
+  m.def("gemm_ablate", &gemm_ablate, py::arg("set") = -1,
+        "timing-only ablations of the persistent 256x256 GEMM (results WRONG): 4 no epilogue, 5 no stores, "
+        "6 no VALU, 7 LN-folding structure with the plain epilogue; 0 off; returns the current");
   m.def("cu_budget", &cu_budget, py::arg("set") = -1,
         "get/set the CU count persistent grids are sized for (0 = the device's; set it to the CU share of "
         "CU-masked streams)");

@@ -19,6 +19,14 @@ enum GemmEpilogue : int {
   kEpiResidual = 8,
   kEpiRelu = 16,
   kEpiOutF32 = 32,  // C is float* (128x128 kernel only; LM-head logits)
+  // LayerNorm folding (post-LN encoders; persistent 256x256 full-line kernel only,
+  // M, N, K multiples of 256). LN(x) = (x - mu) * rstd * gamma + beta is never
+  // materialised: its producer emits row statistics, its consumers apply them.
+  kEpiInNorm = 64,     // A rows are raw LN inputs, gamma folded into Bt, beta into bias:
+                       //   C = rstd*acc - rstd*mu*colsum + bias    (rstd, mu from in_fin)
+  kEpiResNorm = 128,   // R rows are raw LN inputs (beta folded into bias):
+                       //   C = ... + (R*rstd - rstd*mu) * gamma     (rstd, mu from res_fin)
+  kEpiStatsOut = 256,  // also write per-row partial (sum, sum of squares) of C, one per 256 columns
 };
 
 struct GemmArgs {
@@ -36,6 +44,12 @@ struct GemmArgs {
   // split-K (skinny M): splits > 1 needs ws = fp32 [splits, M, N]
   int splits = 1;
   float* ws = nullptr;
+  // LayerNorm folding (see kEpiInNorm / kEpiResNorm / kEpiStatsOut)
+  const float* in_fin = nullptr;   // InNorm: [M][2] (rstd, rstd*mu) of A's rows
+  const float* colsum = nullptr;   // InNorm: [N] fp32, colsum[n] = sum_k Bt[n][k]
+  const float* res_fin = nullptr;  // ResNorm: [M][2] (rstd, rstd*mu) of R's rows
+  const float* gamma = nullptr;    // ResNorm: [N] LN gamma of R
+  float* part_out = nullptr;       // StatsOut: [N/256][M][2] partial (sum, sumsq) of C's rows (fp32 values)
 };
 void gemm_bf16(const GemmArgs& g, hipStream_t stream);
 // split count the library picks for an [M,N,K] problem (1 = no split-K)
@@ -44,6 +58,7 @@ int gemm_splitk_splits(int M, int N, int K);
 int gemm_dec_mode(int set);
 // 256x256 schedule selector (benchmarks): set >= 0 switches; returns the current
 int gemm_256_variant(int set);
+int gemm_ablate(int set);  // timing-only ablations of the persistent 256x256 kernel (results wrong); -1 reads
 int attention_persist_mode(int set);  // packed BERT attention: 1 persistent (default), 0 per-item
 int num_cus();                        // CUs a persistent grid is sized for (device count, or the budget below)
 int cu_budget(int set);               // >0: size persistent grids for this many CUs (CU-masked streams)
@@ -91,6 +106,9 @@ void rmsnorm_bf16(const bf16* x, const float* gamma, bf16* out, int rows, int N,
 void embed_layernorm(const int32_t* ids, const int32_t* type_ids, const bf16* word, const bf16* pos,
                      const bf16* type, const float* gamma, const float* beta, bf16* out, int B, int S, int N,
                      int vocab, int type_vocab, float eps, hipStream_t stream);
+// LayerNorm folding: fin[m] = (rstd, rstd*mu) of rows of width K from the StatsOut
+// partials part[slots][M][2] (sum, sumsq), slots summed in order (deterministic)
+void ln_stats_finalize(const float* part, int slots, int M, int K, float eps, float* fin, hipStream_t stream);
 // Plain embedding gather (T5 encoder/decoder input): out[t] = table[ids[t]] * scale
 void embed_gather(const int32_t* ids, const bf16* table, bf16* out, int tokens, int N, int vocab,
                   hipStream_t stream);

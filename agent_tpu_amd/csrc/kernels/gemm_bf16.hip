@@ -736,18 +736,41 @@ static_assert(kLineLoadsPerBlock == kLineStoresPerBlock,
 static_assert(kLineResWait == 14, "the counted residual wait assumes 8 blocks x 2 loads");
 static_assert(kLineResWait < 64, "vmcnt field is 6 bits on gfx950");
 
+// LayerNorm folding state of the line epilogue, all in the kernel's LDS array:
+//   fin[256][2]  (rstd, rstd*mu) of the tile's rows: of A (InNorm) or of R (ResNorm)
+//   col[256]     colsum of the folded weights (InNorm) or the residual's gamma (ResNorm)
+//   st[4][256][2] per-wave-column partial (sum, sumsq) of the output rows (StatsOut),
+//                slot wn written by wave (wm, wn) for its 128 rows; summed in slot
+//                order when flushed (deterministic, no atomics)
+struct LnLds {
+  const float* fin = nullptr;
+  const float* col = nullptr;
+  float* st = nullptr;
+};
+
 template <int EPI, bool NT>
 __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int m0, int n0, int wm, int wn, int lane,
                                                   bf16* __restrict__ C, int ldc, const bf16* __restrict__ R, int ldr,
                                                   const float* lds_bias, char* scratch,
-                                                  const u32x4 (&pre)[2][2]) {
+                                                  const u32x4 (&pre)[2][2], LnLds ln = {}) {
+  constexpr bool kIn = EPI & kEpiInNorm, kRes = EPI & kEpiResNorm, kSt = EPI & kEpiStatsOut;
   const int fr = lane & 15, fc = lane >> 4;
-  f32x4 b4[4];
+  // per-column LDS vectors (bias, colsum, gamma) at this lane's 4 columns of fragment j
+  auto col4 = [&](const float* v, int j) {
+    return *reinterpret_cast<const f32x4*>(v + wn * 64 + j * 16 + fc * 4);
+  };
+  f32x4 b4[4], g4[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    if constexpr (EPI & kEpiBias) b4[j] = *reinterpret_cast<const f32x4*>(lds_bias + wn * 64 + j * 16 + fc * 4);
-    else b4[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    b4[j] = (EPI & kEpiBias) ? col4(lds_bias, j) : f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (kRes) g4[j] = col4(ln.col, j);  // ResNorm's caller adds the bias in the accumulator init
   }
+  // (rstd, rstd*mu) of the lane's row in block i, read one block ahead: the residual
+  // wait (asm with a memory clobber) would otherwise pin each read behind it
+  auto row_fin = [&](int i) {
+    return (kIn || kRes) ? *reinterpret_cast<const f32x2*>(ln.fin + (wm * 128 + i * 16 + fr) * 2) : f32x2{1.f, 0.f};
+  };
+  f32x2 rsm_next = row_fin(0);
   // line layout: lane -> row lr (+8 for the second half), 16-B chunk lc
   const int lr = lane >> 3, lc = lane & 7;
   const int line_off0 = lr * 128 + ((lc ^ (lr & 7)) << 4);
@@ -778,9 +801,28 @@ __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int 
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     float v[4][4];
+    const int lrow = wm * 128 + i * 16 + fr;  // tile-local row of this lane's fragment row
+    const f32x2 rsm = rsm_next;               // (rstd, rstd*mu) of that row (InNorm / ResNorm)
+    if (i + 1 < 8) rsm_next = row_fin(i + 1);
+    // the LN math runs on value PAIRS (v_pk_fma_f32 with the row scalars broadcast):
+    // written per element, hipcc packed it with a v_mov per operand pair
+    const f32x2 rs2 = f32x2{rsm[0], rsm[0]}, nrm2 = f32x2{-rsm[1], -rsm[1]};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const f32x4 t = acc[i][j] + b4[j];
+      f32x4 t;
+      if constexpr (kIn) {
+        // LN(a) . W = rstd * (a . (gamma o W) - mu * colsum(gamma o W)) + beta . W (in the bias);
+        // the caller started acc at -mu * colsum
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x2 o = __builtin_elementwise_fma(f32x2{acc[i][j][2 * h], acc[i][j][2 * h + 1]}, rs2,
+                                                    f32x2{b4[j][2 * h], b4[j][2 * h + 1]});
+          t[2 * h] = o[0];
+          t[2 * h + 1] = o[1];
+        }
+      } else {
+        t = acc[i][j] + b4[j];
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[j][e] = t[e];
     }
@@ -809,9 +851,40 @@ __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int 
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const bf16x4 r = *reinterpret_cast<const bf16x4*>(scratch + frag_off(j));
+        if constexpr (kRes) {
+          // residual = LN(r) = (r*rstd - rstd*mu) * gamma (+ beta, folded into the bias)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[j][e] += bf2f(r[e]);
+          for (int h = 0; h < 2; ++h) {
+            const f32x2 t2 = __builtin_elementwise_fma(f32x2{bf2f(r[2 * h]), bf2f(r[2 * h + 1])}, rs2, nrm2);
+            const f32x2 o = __builtin_elementwise_fma(t2, f32x2{g4[j][2 * h], g4[j][2 * h + 1]},
+                                                      f32x2{v[j][2 * h], v[j][2 * h + 1]});
+            v[j][2 * h] = o[0];
+            v[j][2 * h + 1] = o[1];
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[j][e] += bf2f(r[e]);
+        }
       }
+    }
+    if constexpr (kSt) {
+      // row partials over this wave's 64 columns: 16 values per lane, then the 4
+      // lanes sharing the row (fc = 0..3: lanes fr, fr+16, fr+32, fr+48), fixed order
+      f32x2 s1 = f32x2{0.f, 0.f}, s2 = f32x2{0.f, 0.f};  // over value pairs: packed add / fma
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x2 p2 = f32x2{v[j][2 * h], v[j][2 * h + 1]};
+          s1 += p2;
+          s2 = __builtin_elementwise_fma(p2, p2, s2);
+        }
+      f32x2 s = f32x2{s1[0] + s1[1], s2[0] + s2[1]};
+      s[0] += __shfl_xor(s[0], 16, 64);
+      s[1] += __shfl_xor(s[1], 16, 64);
+      s[0] += __shfl_xor(s[0], 32, 64);
+      s[1] += __shfl_xor(s[1], 32, 64);
+      if (fc == 0) *reinterpret_cast<f32x2*>(ln.st + (wn * 256 + lrow) * 2) = s;
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -850,11 +923,33 @@ __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int 
 // The phase/quarter program and its hazard argument are those of 256p; the
 // epilogue has no barrier, so the two wave groups stay staggered across tiles.
 // ============================================================================
+// Kernel arguments of the LayerNorm folding epilogues (GemmArgs fields of the same names).
+struct LnFold {
+  const float* in_fin;
+  const float* colsum;
+  const float* res_fin;
+  const float* gamma;
+  float* part_out;
+};
+
 // DBG (timing-only ablation, results WRONG): 1 = skip the epilogue (acc kept live)
+//
+// LayerNorm folding (EPI & (kEpiInNorm | kEpiResNorm | kEpiStatsOut), LINE only, K >= 256):
+//  * K-tile 1, phase 0: the tile's per-row / per-column LN data is staged by 4-byte
+//    LDS-DMA (as the bias is at K-tile 0): the finalized (rstd, rstd*mu) of the 256
+//    A rows (InNorm) or R rows (ResNorm), and colsum (InNorm) or gamma (ResNorm) of
+//    columns n0..+256. Every wave issues the same op count; the later counted waits
+//    only get stricter. Single buffers: by K-tile 1 both (staggered) wave groups
+//    have left the previous tile's epilogue. K-tiles 0-1 are peeled, so the K loop
+//    itself has no branch.
+//  * StatsOut: the epilogue writes per-wave row partials to LDS; K-tile 1 of the
+//    NEXT tile (or a barrier after the loop, for the last tile) sums the 4 column
+//    slots in order and stores the tile's 256 (sum, sumsq) pairs. The statistics are
+//    finalized between the kernels (ln_stats_finalize, norm_embed.hip).
 template <int EPI, int DBG = 0, bool NT = false, bool LINE = false>
 __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
     const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C, int ldc,
-    const float* __restrict__ bias, const bf16* __restrict__ R, int ldr, int M, int N, int K) {
+    const float* __restrict__ bias, const bf16* __restrict__ R, int ldr, int M, int N, int K, LnFold lf) {
   using namespace g2;
   constexpr int kImg = 256 * 128;
   // VMEM ops per wave the epilogue leaves in flight: its 16-B stores (every residual load
@@ -864,7 +959,16 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
   constexpr int kBiasOff = 2 * 2 * kImg;  // [2 tiles][256] fp32 bias after the operand buffers
   // ONE __shared__ array: a second LDS object makes hipcc drain vmcnt before ds_reads
   constexpr int kEpiOff = kBiasOff + 2 * 256 * 4;  // LINE epilogue: 2 KiB scratch per wave
-  __shared__ __attribute__((aligned(16))) char lds[kEpiOff + (LINE ? 8 * 2048 : 0)];
+  constexpr bool kIn = EPI & kEpiInNorm, kRes = EPI & kEpiResNorm, kSt = EPI & kEpiStatsOut;
+  static_assert(!(kIn || kRes || kSt) || LINE, "LayerNorm folding needs the full-line epilogue");
+  static_assert(!(kIn && (kRes || kSt)), "InNorm and ResNorm/StatsOut do not share one kernel (LDS budget)");
+  constexpr int kXOff = kEpiOff + (LINE ? 8 * 2048 : 0);
+  constexpr int kFinOff = kXOff;                                    // [2 tiles (InNorm)][256][2] (rstd, rstd*mu)
+  constexpr int kColOff = kFinOff + (kIn ? 4096 : kRes ? 2048 : 0); // [256] colsum | gamma
+  constexpr int kStOff = kColOff + ((kIn || kRes) ? 1024 : 0);      // StatsOut: [4][256][2]
+  constexpr int kLdsBytes = kStOff + (kSt ? 4 * 2048 : 0);
+  static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ntn = N / 256, ntm = (M + 255) / 256, ntiles = ntm * ntn;
@@ -886,22 +990,50 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
   for (int q = 0; q < 4; ++q)
 #pragma unroll
     for (int i = 0; i < 2; ++i) dst[q][i] = (q == 0 || q == 3 ? 0 : kImg) + qrow(q, (i * 8 + wave) * 8) * 128;
+  // lane ids are made opaque per use (recomputed by mbcnt, never hoisted): with the
+  // LayerNorm-folding epilogues the per-lane staging rows kept live across the tile
+  // loop spilled, and a scratch reload is a VMEM load the waitcnt pass drains the
+  // LDS-DMA stream for (vmcnt(0) in the last K-tile)
+  auto opaque_lane = [] {
+    int l = __lane_id();
+    asm volatile("" : "+v"(l));
+    return l;
+  };
+  // staging sources: 64-bit per-lane pointers, or (LN-folding variants, whose
+  // epilogue is the register peak) 32-bit byte offsets from the uniform A / Bt
+  // base, which the DMA takes in its saddr form: 8 VGPRs instead of 16 live over
+  // the whole tile loop (host: A and Bt each < 4 GiB)
+  constexpr bool kFold = kIn || kRes || kSt;
+  // ResNorm / StatsOut variants start each tile's accumulators at the bias (read from
+  // LDS, where the previous tile's last K-tile staged it) instead of adding it in the
+  // epilogue: 16 fewer VGPRs and one op fewer per value pair on the epilogue chain
+  constexpr bool kBiasAcc = (kRes || kSt) && (EPI & kEpiBias);
   const bf16* src[4][2];
+  uint32_t soff[4][2];
   auto set_src = [&](int tm0, int tn0) {
+    const int ln = kFold ? opaque_lane() : lane;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const int r = qrow(q, (i * 8 + wave) * 8 + (lane >> 3));
-        src[q][i] = (q == 0 || q == 3) ? A + (size_t)min(tm0 + r, M - 1) * lda + sw(r, spos) * 8
-                                       : Bt + (size_t)(tn0 + r) * ldb + sw(r, spos) * 8;
+        const int r = qrow(q, (i * 8 + wave) * 8 + (ln >> 3));
+        const size_t e = (q == 0 || q == 3) ? (size_t)min(tm0 + r, M - 1) * lda + sw(r, ln & 7) * 8
+                                            : (size_t)(tn0 + r) * ldb + sw(r, ln & 7) * 8;
+        if constexpr (kFold) soff[q][i] = (uint32_t)(e * 2);
+        else src[q][i] = ((q == 0 || q == 3) ? A : Bt) + e;
       }
   };
   auto stage = [&](int q, int kt, int buf) {
     char* base = lds + buf * 2 * kImg;
     const int koff = kt * 64;
-    glds16(src[q][0] + koff, base + dst[q][0]);
-    glds16(src[q][1] + koff, base + dst[q][1]);
+    if constexpr (kFold) {
+      const char* g = reinterpret_cast<const char*>((q == 0 || q == 3) ? A : Bt) + koff * 2;
+      glds16(g + soff[q][0], base + dst[q][0]);
+      glds16(g + soff[q][1], base + dst[q][1]);
+    } else {
+      glds16(src[q][0] + koff, base + dst[q][0]);
+      glds16(src[q][1] + koff, base + dst[q][1]);
+    }
   };
 
   const int fr = lane & 15, fc = lane >> 4;
@@ -939,9 +1071,50 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
   };
 
   const int nk = K / 64;
+  // ---- LayerNorm folding (see the kernel comment) ----
+  // LN data staging: uniform base + 32-bit lane offset (saddr form, no 64-bit
+  // per-lane address kept live)
+  auto glds4 = [&](const float* ubase, char* ldst) {
+    const uint32_t lo = (uint32_t)opaque_lane() * 4u;
+    __builtin_amdgcn_global_load_lds((const ATPU_GLOBAL_AS void*)(reinterpret_cast<const char*>(ubase) + lo),
+                                     (ATPU_LDS_AS void*)ldst, 4, 0, 0);
+  };
+  auto ln_stage = [&](int tm0, int tn0) {  // ResNorm, at K-tile 1 of the tile
+    if constexpr (kRes) {
+      glds4(lf.res_fin + (size_t)tm0 * 2 + wave * 64, lds + kFinOff + wave * 256);
+      glds4(lf.gamma + tn0 + (wave & 3) * 64, lds + kColOff + (wave & 3) * 256);
+    }
+  };
+  // InNorm: a tile's row statistics and colsum are staged ahead of the tile (prologue,
+  // or the previous tile's last K-tile, like kBiasAcc's bias): the accumulators start
+  // at -mu*colsum, so the epilogue is one packed FMA per value pair, rstd*acc + bias.
+  // The statistics are double-buffered (the epilogue of the tile before reads its own).
+  auto ln_stage_in = [&](int tm0, int tn0, int par) {
+    if constexpr (kIn) {
+      glds4(lf.in_fin + (size_t)tm0 * 2 + wave * 64, lds + kFinOff + par * 2048 + wave * 256);
+      glds4(lf.colsum + tn0 + (wave & 3) * 64, lds + kColOff + (wave & 3) * 256);
+    }
+  };
+  auto ln_flush = [&](int fm0, int fn0) {
+    if constexpr (kSt) {
+      const int l = opaque_lane();
+      if (l < 32) {
+        const int r = wave * 32 + l;
+        f32x2 s = f32x2{0.f, 0.f};
+#pragma unroll
+        for (int w = 0; w < 4; ++w) s += *reinterpret_cast<const f32x2*>(lds + kStOff + (w * 256 + r) * 8);
+        float* ub = lf.part_out + ((size_t)(fn0 >> 8) * M + fm0 + wave * 32) * 2;
+        *reinterpret_cast<f32x2*>(reinterpret_cast<char*>(ub) + (uint32_t)l * 8u) = s;
+      }
+    }
+  };
+  int pm0 = 0, pn0 = 0;  // StatsOut: the tile whose row partials sit in LDS
+
   int tile = xcd_remap(v, ntiles);
   int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 256;
   set_src(m0, n0);
+  if constexpr (kBiasAcc) glds4(bias + n0 + (wave & 3) * 64, lds + kBiasOff + (wave & 3) * 256);
+  ln_stage_in(m0, n0, 0);
 #pragma unroll
   for (int q = 0; q < 4; ++q) stage(q, 0, 0);
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
@@ -964,10 +1137,36 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
   int tile_par = 0;   // bias buffer of the current tile
   bool first = true;  // no epilogue stores in flight before the first tile
   for (;;) {
+    if constexpr (kBiasAcc) {
+      // this tile's bias landed before a barrier of the previous tile's last K-tile
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 b = *reinterpret_cast<const f32x4*>(lds + kBiasOff + (wn * 64 + j * 16 + fc * 4) * 4);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < 8; ++i) acc[i][j] = b;
+      }
+    } else if constexpr (kIn) {
+      // acc = -mu * colsum: rstd * acc_final = rstd*(a.W') - rstd*mu*colsum(W').
+      // LDS offsets from an opaque lane id (the hoisted lane-derived offsets spilled)
+      const int ol = opaque_lane();
+      f32x4 c4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        c4[j] = *reinterpret_cast<const f32x4*>(lds + kColOff + (wn * 64 + j * 16 + (ol >> 4) * 4) * 4);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const f32x2 f = *reinterpret_cast<const f32x2*>(lds + kFinOff + tile_par * 2048 +
+                                                        (wm * 128 + i * 16 + (ol & 15)) * 8);
+        const float nmu = -f[1] * __builtin_amdgcn_rcpf(f[0]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = c4[j] * nmu;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     const int vn = v + G;
     const bool has_next = vn < ntiles;
     const int cm0 = m0, cn0 = n0;
@@ -975,8 +1174,13 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
     // one K-tile; the last one is a separate instantiation so that pre[] is
     // live only from its p3 to the epilogue (assigned in a loop iteration it
     // would be live around the whole K loop and spill)
-    auto kstep = [&](int t, auto last_c) {
+    // peel_c: std::integral_constant<int, P>; P >= 0 = this is K-tile P (compile time,
+    // the ResNorm/StatsOut variants peel K-tiles 0-1 so no per-tile branch sits in the K loop),
+    // -1 = a K-tile >= 2 of a peeled loop, -2 = runtime t (non-folding variants)
+    auto kstep = [&](int t, auto last_c, auto peel_c) {
       constexpr bool last = decltype(last_c)::value;
+      constexpr int P = decltype(peel_c)::value;
+      const bool is_t0 = P == -2 ? t == 0 : P == 0;
       const bool more = !last || has_next;
       int kn = t + 1;  // K-tile staged during this one
       if (last && has_next) {
@@ -987,16 +1191,31 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
         set_src(m0, n0);
         kn = 0;
       }
-      const bool relax = t == 0 && !first;  // epilogue stores of the previous tile may be in flight
+      const bool relax = is_t0 && !first;  // epilogue stores of the previous tile may be in flight
       // p0
       read_a(buf, 0);
       read_b(bl, buf, 0);
-      if ((EPI & kEpiBias) && t == 0) {
+      if constexpr (kBiasAcc) {
+        // the next tile's bias, ahead of its K-tile 0 (older than every quarter of
+        // it, so retired by the waits that retire them; single buffer: this tile's
+        // bias was consumed by the accumulator init)
+        if (last && has_next) glds4(bias + n0 + (wave & 3) * 64, lds + kBiasOff + (wave & 3) * 256);
+      } else if ((EPI & kEpiBias) && is_t0) {
         // this tile's bias -> LDS (waves w, w+4 write the same 256 B: every wave
         // issues the same op count). Only makes the waits below stricter.
-        __builtin_amdgcn_global_load_lds((const ATPU_GLOBAL_AS void*)(bias + cn0 + (wave & 3) * 64 + lane),
+        const int bl_lane = (kIn || kRes || kSt) ? opaque_lane() : lane;
+        __builtin_amdgcn_global_load_lds((const ATPU_GLOBAL_AS void*)(bias + cn0 + (wave & 3) * 64 + bl_lane),
                                          (ATPU_LDS_AS void*)(lds + kBiasOff + (tile_par * 256 + (wave & 3) * 64) * 4),
                                          4, 0, 0);
+      }
+      if constexpr (kIn) {
+        if (last && has_next) ln_stage_in(m0, n0, tile_par ^ 1);
+      }
+      if constexpr (kRes || kSt) {
+        if constexpr (P == 1) {
+          ln_stage(cm0, cn0);
+          if (!first) ln_flush(pm0, pn0);
+        }
       }
       if (more) {
         stage(0, kn, buf ^ 1);
@@ -1054,22 +1273,38 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
       ATPU_PS_SYNC_MMA(bl, 1, 0);
       buf ^= 1;
     };
-    for (int t = 0; t + 1 < nk; ++t) kstep(t, std::false_type{});
-    kstep(nk - 1, std::true_type{});
+    if constexpr (kRes || kSt) {  // host: K >= 256, so K-tiles 0-1 are never the last
+      kstep(0, std::false_type{}, std::integral_constant<int, 0>{});
+      kstep(1, std::false_type{}, std::integral_constant<int, 1>{});
+      for (int t = 2; t + 1 < nk; ++t) kstep(t, std::false_type{}, std::integral_constant<int, -1>{});
+      kstep(nk - 1, std::true_type{}, std::integral_constant<int, -1>{});
+    } else {
+      for (int t = 0; t + 1 < nk; ++t) kstep(t, std::false_type{}, std::integral_constant<int, -2>{});
+      kstep(nk - 1, std::true_type{}, std::integral_constant<int, -2>{});
+    }
     if constexpr (DBG & 1) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
     } else {
+      // DBG & 8 (timing-only ablation of the LN-folding variants): their staging and
+      // tile-loop structure, the plain epilogue (no LN math, no statistics)
+      constexpr int kEpiRun0 = kBiasAcc ? (EPI & ~kEpiBias) : EPI;
+      constexpr int kEpiRun = (DBG & 8) ? (kEpiRun0 & ~(kEpiInNorm | kEpiResNorm | kEpiStatsOut)) : kEpiRun0;
       if constexpr (LINE)
-        epilogue_256_line<EPI, NT>(acc, cm0, cn0, wm, wn, lane, C, ldc, R, ldr,
+        epilogue_256_line<kEpiRun, NT>(acc, cm0, cn0, wm, wn, (kIn || kRes || kSt) ? opaque_lane() : lane, C, ldc, R, ldr,
                                    reinterpret_cast<const float*>(lds + kBiasOff) + tile_par * 256,
-                                   lds + kEpiOff + wave * 2048, pre);
+                                   lds + kEpiOff + wave * 2048, pre,
+                                   LnLds{reinterpret_cast<const float*>(lds + kFinOff + (kIn ? tile_par * 2048 : 0)),
+                                         reinterpret_cast<const float*>(lds + kColOff),
+                                         reinterpret_cast<float*>(lds + kStOff)});
       else
         epilogue_256<EPI, true, (DBG >> 1), NT>(acc, cm0, cn0, wm, wn, lane, C, ldc, bias, R, ldr, M,
                                             reinterpret_cast<const float*>(lds + kBiasOff) + tile_par * 256);
     }
+    pm0 = cm0;
+    pn0 = cn0;
     if (!has_next) break;
     v = vn;
     first = false;
@@ -1077,6 +1312,12 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
   }
 #undef ATPU_PS_SYNC_MMA
   if (wm == 0) __builtin_amdgcn_s_barrier();  // close the stagger (equal barrier counts)
+  if constexpr (kSt) {
+    // the last tile's row partials: every wave's epilogue LDS writes done, then flushed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    ln_flush(pm0, pn0);
+  }
 }
 
 }  // namespace
@@ -1111,6 +1352,16 @@ int64_t make_cu_mask_stream(int first_bit, int nbits) {
   return reinterpret_cast<int64_t>(s);
 }
 
+int gemm_ablate(int set) {
+  // timing-only ablations of the persistent kernel (results WRONG): ATPU_GEMM_ABLATE=4|5|6|7
+  static int v = [] {
+    const char* f = std::getenv("ATPU_GEMM_ABLATE");
+    return f ? std::atoi(f) : 0;
+  }();
+  if (set >= 0) v = set;
+  return v;
+}
+
 namespace {
 
 template <bool NT, bool LINE = false>
@@ -1119,22 +1370,47 @@ void launch_256s(const GemmArgs& g, hipStream_t s) {
   // one workgroup per CU; a multiple of 8 so v % 8 keeps naming the XCD
   int nb = std::min(tiles, num_cus());
   if (nb >= 8) nb &= ~7;
-  static const int ablate = [] {
-    const char* f = std::getenv("ATPU_GEMM_ABLATE");
-    return f ? std::atoi(f) : 0;
-  }();
+  const int ablate = gemm_ablate(-1);
+  const LnFold lf{g.in_fin, g.colsum, g.res_fin, g.gamma, g.part_out};
   if (ablate == 4 || ablate == 5 || ablate == 6) {  // timing only: no epilogue / no stores / no VALU
     auto k = ablate == 4 ? gemm256s_kernel<kEpiBias, 1> : ablate == 5 ? gemm256s_kernel<kEpiBias, 2>
                                                                        : gemm256s_kernel<kEpiBias, 4>;
     hipLaunchKernelGGL(k, dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M,
-                       g.N, g.K);
+                       g.N, g.K, lf);
     return;
   }
 #define ATPU_G256S(E)                                                                                          \
   case E:                                                                                                      \
     hipLaunchKernelGGL((gemm256s_kernel<E, 0, NT, LINE>), dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, \
-                       g.bias, g.R, g.ldr, g.M, g.N, g.K);                                                     \
+                       g.bias, g.R, g.ldr, g.M, g.N, g.K, lf);                                                 \
     break;
+  if constexpr (LINE) {
+    if (ablate == 7) {  // timing only: LN-folding structure without its epilogue math
+#define ATPU_G256S_A(E)                                                                                        \
+  case E:                                                                                                      \
+    hipLaunchKernelGGL((gemm256s_kernel<E, 8, NT, LINE>), dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, \
+                       g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, lf);                                          \
+    return;
+      switch (g.epi) {
+        ATPU_G256S_A(kEpiBias | kEpiInNorm)
+        ATPU_G256S_A(kEpiBias | kEpiInNorm | kEpiGelu)
+        ATPU_G256S_A(kEpiBias | kEpiResidual | kEpiStatsOut)
+        ATPU_G256S_A(kEpiBias | kEpiResidual | kEpiResNorm | kEpiStatsOut)
+        default:
+          break;
+      }
+#undef ATPU_G256S_A
+    }
+    switch (g.epi) {
+      ATPU_G256S(kEpiBias | kEpiInNorm)
+      ATPU_G256S(kEpiBias | kEpiInNorm | kEpiGelu)
+      ATPU_G256S(kEpiBias | kEpiResidual | kEpiStatsOut)
+      ATPU_G256S(kEpiBias | kEpiResidual | kEpiResNorm | kEpiStatsOut)
+      default:
+        break;
+    }
+    if (g.epi & (kEpiInNorm | kEpiResNorm | kEpiStatsOut)) return;
+  }
   switch (g.epi) {
     ATPU_G256S(0)
     ATPU_G256S(kEpiBias)
@@ -1575,6 +1851,27 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
   const int kernel256 = gemm_256_variant(-1);
   const bool big_ok = g.N % 256 == 0 && g.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(g.C) & 15) == 0 &&
                       (!(g.epi & kEpiResidual) || (g.ldr % 8 == 0 && (reinterpret_cast<uintptr_t>(g.R) & 15) == 0));
+  if (g.epi & (kEpiInNorm | kEpiResNorm | kEpiStatsOut)) {
+    // LayerNorm folding: persistent full-line kernel only (ops.linear checks the same
+    // conditions and falls back to a materialised LayerNorm)
+    const int fe = g.epi;
+    ATPU_CHECK(fe == (kEpiBias | kEpiInNorm) || fe == (kEpiBias | kEpiInNorm | kEpiGelu) ||
+                   fe == (kEpiBias | kEpiResidual | kEpiStatsOut) ||
+                   fe == (kEpiBias | kEpiResidual | kEpiResNorm | kEpiStatsOut),
+               "gemm: unsupported LayerNorm-folding epilogue " + std::to_string(fe));
+    ATPU_CHECK(big_ok && g.M % 256 == 0 && g.K % 256 == 0 && g.K >= 256, "gemm: LN folding needs M, N, K % 256 == 0");
+    ATPU_CHECK(kernel256 >= 3, "gemm: LN folding needs the full-line 256x256 kernel (ATPU_GEMM_256=n|l)");
+    ATPU_CHECK(!(fe & kEpiInNorm) || (g.in_fin && g.colsum), "gemm: InNorm needs in_fin and colsum");
+    // staging offsets are 32-bit byte offsets from A / Bt
+    ATPU_CHECK((size_t)g.M * g.lda * 2 < (1ull << 32) && (size_t)g.N * g.ldb * 2 < (1ull << 32),
+               "gemm: LN folding needs A and Bt under 4 GiB");
+    ATPU_CHECK(!(fe & kEpiResNorm) || (g.res_fin && g.gamma), "gemm: ResNorm needs res_fin and gamma");
+    ATPU_CHECK(!(fe & kEpiStatsOut) || g.part_out, "gemm: StatsOut needs part_out");
+    if (kernel256 == 3) launch_256s<false, true>(g, stream);
+    else launch_256s<true, true>(g, stream);
+    ATPU_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const bool use_big = !(g.epi & kEpiOutF32) && (forced ? (forced == 256 && big_ok) : (g.M >= 2048 && big_ok));
   // 256s counts its epilogue's stores in the next tile's waits: whole row tiles only
   const bool persistent_ok = g.M % 256 == 0;

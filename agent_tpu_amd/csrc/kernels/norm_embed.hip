@@ -223,6 +223,20 @@ __global__ __launch_bounds__(256) void embed_gather_kernel(const int32_t* __rest
     default: throw std::invalid_argument("atpu: unsupported row width " + std::to_string(N)); \
   }
 
+// LayerNorm folding: one thread per row turns the GEMM StatsOut partials
+// (sum, sumsq per 256-column tile, slots summed in order) into (rstd, rstd*mu).
+// 8 B in + 8 B out per slot and row: a few microseconds at BERT sizes.
+__global__ __launch_bounds__(256) void ln_stats_finalize_kernel(const float* __restrict__ part, int slots, int M,
+                                                                 float inv_k, float eps, float* __restrict__ fin) {
+  const int m = blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  f32x2 s = *reinterpret_cast<const f32x2*>(part + (size_t)m * 2);
+  for (int k = 1; k < slots; ++k) s += *reinterpret_cast<const f32x2*>(part + ((size_t)k * M + m) * 2);
+  const float mu = s[0] * inv_k;
+  const float rs = rsqrtf(fmaxf(s[1] * inv_k - mu * mu, 0.f) + eps);
+  *reinterpret_cast<f32x2*>(fin + (size_t)m * 2) = f32x2{rs, rs * mu};
+}
+
 inline void check_width(int N) { ATPU_CHECK(N % 256 == 0 && N <= 2048, "row width must be a multiple of 256, <= 2048"); }
 
 }  // namespace
@@ -273,6 +287,14 @@ void embed_layernorm(const int32_t* ids, const int32_t* type_ids, const bf16* wo
   const dim3 grid((tokens + 3) / 4);
   ATPU_NG_DISPATCH(N, hipLaunchKernelGGL(embed_ln_kernel<NG>, grid, dim3(256), 0, stream, ids, type_ids, word, pos,
                                          type, gamma, beta, out, tokens, S, vocab, type_vocab, eps));
+  ATPU_HIP_CHECK(hipGetLastError());
+}
+
+void ln_stats_finalize(const float* part, int slots, int M, int K, float eps, float* fin, hipStream_t stream) {
+  ATPU_CHECK(slots >= 1 && K > 0, "ln_stats_finalize: bad shape");
+  if (M <= 0) return;
+  hipLaunchKernelGGL(ln_stats_finalize_kernel, dim3((M + 255) / 256), dim3(256), 0, stream, part, slots, M,
+                     1.0f / static_cast<float>(K), eps, fin);
   ATPU_HIP_CHECK(hipGetLastError());
 }
 

@@ -188,12 +188,106 @@ class BertClassifier:
         if cls_only_last is None:
             cls_only_last = os.getenv("ATPU_CLS_ONLY_LAST", "1") not in ("0", "false", "no")
         self.cls_only_last = bool(cls_only_last)
+        # LayerNorm folding (GPU): no LayerNorm pass inside the encoder; see encode_folded
+        self.ln_fold = (self.device.type == "cuda" and not fp32
+                        and os.getenv("ATPU_LN_FOLD", "1") not in ("0", "false", "no"))
+        self._folded: Optional[Dict[str, torch.Tensor]] = None
+
+    # ------------------------------------------------------------ LN folding
+    def folded(self) -> Dict[str, torch.Tensor]:
+        """Weights with the preceding LayerNorm folded in (built once, on the device).
+
+        QKV of layer i >= 1 consumes LN2 of layer i-1 and FFN1 of layer i consumes LN1
+        of layer i: gamma goes into the weight, beta into the bias, plus the weight's
+        column sums (:func:`ops.fold_ln_into_linear`). The out-proj / FFN2 residual is
+        the same LayerNorm's output: its beta is added to their bias.
+        """
+        if self._folded is None:
+            p, f = self.p, {}
+            for i in range(self.cfg.layers):
+                q = f"l{i}."
+                if i > 0:
+                    g2, b2 = p[f"l{i - 1}.ln2_g"], p[f"l{i - 1}.ln2_b"]
+                    f[q + "qkv_w"], f[q + "qkv_c"], f[q + "qkv_b"] = ops.fold_ln_into_linear(
+                        p[q + "qkv_w"], p[q + "qkv_b"], g2, b2)
+                    f[q + "o_b"] = (p[q + "o_b"] + b2).contiguous()
+                f[q + "f1_w"], f[q + "f1_c"], f[q + "f1_b"] = ops.fold_ln_into_linear(
+                    p[q + "f1_w"], p[q + "f1_b"], p[q + "ln1_g"], p[q + "ln1_b"])
+                f[q + "f2_b"] = (p[q + "f2_b"] + p[q + "ln1_b"]).contiguous()
+            self._folded = f
+        return self._folded
+
+    def can_fold(self, B: int, S: int) -> bool:
+        M, H, I = B * S, self.cfg.hidden, self.cfg.intermediate
+        return (self.ln_fold and self.cfg.layers >= 2 and ops.fold_ok(M, 3 * H, H) and ops.fold_ok(M, I, H)
+                and ops.fold_ok(M, H, I))
+
+    def encode_folded(self, ids: torch.Tensor, lens: torch.Tensor, type_ids: Optional[torch.Tensor] = None,
+                      cls_only_last: bool = False) -> torch.Tensor:
+        """:meth:`encode` with every encoder LayerNorm folded into the GEMMs around it.
+
+        The post-LN residual stream stays raw (pre-LN sums). The out-proj / FFN2
+        epilogues emit per-row partial (sum, sumsq) of their output; a finalize pass
+        turns them into (rstd, rstd*mu), which FFN1 / the next QKV apply to the
+        folded weights' product and FFN2 / the next out-proj apply to their residual.
+        Removes 2 LayerNorm passes per layer (each a full read + write of the hidden
+        states); the logits match the unfolded encoder to bf16 rounding."""
+        cfg, p, f = self.cfg, self.p, self.folded()
+        B, S = ids.shape
+        H, M, eps = cfg.hidden, B * S, cfg.eps
+        dev = ids.device
+        h0 = ops.embed_layernorm(ids, p["emb.word"], p["emb.pos"], p["emb.type"], p["emb.ln_g"], p["emb.ln_b"],
+                                 eps, type_ids=type_ids)
+        part = torch.empty((H // 256, M, 2), dtype=torch.float32, device=dev)  # raw rows' partials
+        fin = torch.empty((M, 2), dtype=torch.float32, device=dev)             # (rstd, rstd*mu)
+        last_full = cfg.layers - 1 if cls_only_last else cfg.layers
+        g = h0
+        for i in range(last_full):
+            q = f"l{i}."
+            if i == 0:
+                qkv = ops.linear(h0, p[q + "qkv_w"], p[q + "qkv_b"])
+            else:  # consumes LN2_{i-1}(g); fin = its statistics (also the out-proj residual's)
+                qkv = ops.linear_ln(g, f[q + "qkv_w"], f[q + "qkv_b"], in_fin=fin, colsum=f[q + "qkv_c"])
+            ctx = ops.attention_packed(qkv, lens, B, S, cfg.heads)
+            if i == 0:
+                a = ops.linear_ln(ctx, p[q + "o_w"], p[q + "o_b"], residual=h0, part_out=part)
+            else:
+                a = ops.linear_ln(ctx, p[q + "o_w"], f[q + "o_b"], residual=g, res_fin=fin,
+                                  res_gamma=p[f"l{i - 1}.ln2_g"], part_out=part)
+            ops.ln_finalize(part, H, eps, out=fin)  # LN1 statistics of a
+            ff = ops.linear_ln(a, f[q + "f1_w"], f[q + "f1_b"], act="gelu", in_fin=fin, colsum=f[q + "f1_c"])
+            g = ops.linear_ln(ff, p[q + "f2_w"], f[q + "f2_b"], residual=a, res_fin=fin,
+                              res_gamma=p[q + "ln1_g"], part_out=part)
+            ops.ln_finalize(part, H, eps, out=fin)  # LN2 statistics of g
+        ln2 = f"l{last_full - 1}."
+        if not cls_only_last:
+            return ops.layernorm(g, p[ln2 + "ln2_g"], p[ln2 + "ln2_b"], eps)
+        # last layer on the [CLS] rows (see encode): K/V over every token from the raw g
+        q = f"l{cfg.layers - 1}."
+        kv = ops.linear_ln(g, f[q + "qkv_w"][H:], f[q + "qkv_b"][H:], in_fin=fin, colsum=f[q + "qkv_c"][H:])
+        h_cls = ops.layernorm(g.view(B, S, H)[:, 0, :].contiguous(), p[ln2 + "ln2_g"], p[ln2 + "ln2_b"], eps)
+        return self._cls_layer(h_cls, kv, lens, B, S)
+
+    def _cls_layer(self, h_cls: torch.Tensor, kv: torch.Tensor, lens: torch.Tensor, B: int, S: int) -> torch.Tensor:
+        """Last encoder layer on the [CLS] rows given their input and every token's K/V."""
+        cfg, p, H = self.cfg, self.p, self.cfg.hidden
+        q = f"l{cfg.layers - 1}."
+        qc = ops.linear(h_cls, p[q + "qkv_w"][:H], p[q + "qkv_b"][:H])
+        ctx = ops.decode_attention(qc, kv[:, :H], kv[:, H:], cfg.heads, S, 1, lens=lens,
+                                   scale=1.0 / math.sqrt(cfg.head_dim))
+        h1 = ops.linear(ctx, p[q + "o_w"], p[q + "o_b"], residual=h_cls.contiguous())
+        h1 = ops.layernorm(h1, p[q + "ln1_g"], p[q + "ln1_b"], cfg.eps)
+        f = ops.linear(h1, p[q + "f1_w"], p[q + "f1_b"], act="gelu")
+        h2 = ops.linear(f, p[q + "f2_w"], p[q + "f2_b"], residual=h1)
+        return ops.layernorm(h2, p[q + "ln2_g"], p[q + "ln2_b"], cfg.eps)
 
     def encode(self, ids: torch.Tensor, lens: torch.Tensor, type_ids: Optional[torch.Tensor] = None,
                cls_only_last: bool = False) -> torch.Tensor:
         """Hidden states ``[B*S, H]``, or ``[B, H]`` [CLS] states with ``cls_only_last``."""
         cfg, p = self.cfg, self.p
         B, S = ids.shape
+        if ids.is_cuda and self.can_fold(B, S):
+            return self.encode_folded(ids, lens, type_ids, cls_only_last)
         H = cfg.hidden
         h = ops.embed_layernorm(ids, p["emb.word"], p["emb.pos"], p["emb.type"], p["emb.ln_g"], p["emb.ln_b"],
                                 cfg.eps, type_ids=type_ids)
@@ -212,17 +306,9 @@ class BertClassifier:
         # last layer on the [CLS] rows: K/V GEMM over every token (rows H..3H of
         # the fused weight), Q GEMM over the B [CLS] rows, single-query attention
         q = f"l{cfg.layers - 1}."
-        w, b = p[q + "qkv_w"], p[q + "qkv_b"]
-        kv = ops.linear(h, w[H:], b[H:])
+        kv = ops.linear(h, p[q + "qkv_w"][H:], p[q + "qkv_b"][H:])
         h_cls = h.view(B, S, H)[:, 0, :]  # strided view: row stride S*H
-        qc = ops.linear(h_cls, w[:H], b[:H])
-        ctx = ops.decode_attention(qc, kv[:, :H], kv[:, H:], cfg.heads, S, 1, lens=lens,
-                                   scale=1.0 / math.sqrt(cfg.head_dim))
-        h1 = ops.linear(ctx, p[q + "o_w"], p[q + "o_b"], residual=h_cls.contiguous())
-        h1 = ops.layernorm(h1, p[q + "ln1_g"], p[q + "ln1_b"], cfg.eps)
-        f = ops.linear(h1, p[q + "f1_w"], p[q + "f1_b"], act="gelu")
-        h2 = ops.linear(f, p[q + "f2_w"], p[q + "f2_b"], residual=h1)
-        return ops.layernorm(h2, p[q + "ln2_g"], p[q + "ln2_b"], cfg.eps)
+        return self._cls_layer(h_cls, kv, lens, B, S)
 
     def pooled(self, h: torch.Tensor, B: int, S: int) -> torch.Tensor:
         cls_rows = h if h.shape[0] == B else h.view(B, S, self.cfg.hidden)[:, 0, :]  # strided: row stride S*H

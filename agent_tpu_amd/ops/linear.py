@@ -81,3 +81,136 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     native().gemm(ptr(x), lda, ptr(w), ldb, ptr(out), ldc, ptr(bias), ptr(residual), ldr, M, N, K, epi,
                   stream_handle(), splits, ptr(ws))
     return out
+
+
+# ---------------------------------------------------------------- LayerNorm folding
+# A post-LN encoder's LayerNorm never materialised (kernel: gemm256s with the
+# kEpiInNorm / kEpiResNorm / kEpiStatsOut epilogues, csrc/kernels/gemm_bf16.hip):
+#   producer (attention out-proj, FFN2):  C = raw pre-LN sum, plus per-row partial
+#       (sum, sumsq) of C for each 256-column tile          -> part  [N/256, M, 2]
+#   ln_finalize (norm_embed.hip): part -> (rstd, rstd*mu)    -> fin   [M, 2]
+#   consumer of LN(x) as GEMM input (QKV, FFN1):  gamma folded into the weight,
+#       beta into the bias:  LN(x).W^T = rstd*(x.W'^T) - rstd*mu*colsum(W') + b'
+#   consumer of LN(x) as the residual (out-proj, FFN2 of the next step):
+#       + (x*rstd - rstd*mu)*gamma, beta folded into the bias
+EPI_IN_NORM, EPI_RES_NORM, EPI_STATS_OUT = 64, 128, 256
+
+
+def ln_partials_ref(y: torch.Tensor) -> torch.Tensor:
+    """[N/256, M, 2] per-row (sum, sum of squares) of ``y`` over each 256-column tile (fp32)."""
+    M, N = y.shape
+    t = y.float().view(M, N // 256, 256).transpose(0, 1)
+    return torch.stack([t.sum(-1), (t * t).sum(-1)], -1).contiguous()
+
+
+def ln_finalize(part: torch.Tensor, K: int, eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[M, 2] (rstd, rstd*mu) of rows of width K from their StatsOut partials ``part [slots, M, 2]``."""
+    slots, M, two = part.shape
+    check(two == 2 and part.dtype == torch.float32 and part.is_contiguous(), "part must be contiguous fp32 [S, M, 2]")
+    if out is None:
+        out = torch.empty((M, 2), dtype=torch.float32, device=part.device)
+    check(tuple(out.shape) == (M, 2) and out.dtype == torch.float32 and out.is_contiguous(), "out must be fp32 [M, 2]")
+    if not part.is_cuda:
+        s = part.sum(0)
+        mu = s[:, 0] * (1.0 / K)
+        rs = torch.rsqrt((s[:, 1] * (1.0 / K) - mu * mu).clamp_min(0.0) + eps)
+        return out.copy_(torch.stack([rs, rs * mu], -1))
+    same_device(part, out)
+    native().ln_stats_finalize(ptr(part), slots, M, int(K), float(eps), ptr(out), stream_handle())
+    return out
+
+
+def fold_ln_into_linear(w: torch.Tensor, b: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor):
+    """``LN(x) @ w.T + b == rstd*(x @ w_f.T) - rstd*mu*colsum + b_f`` -> ``(w_f, colsum fp32, b_f fp32)``.
+
+    ``colsum`` is taken over the (bf16-rounded) ``w_f`` the GEMM multiplies with."""
+    wf = (w.float() * gamma.float().unsqueeze(0)).to(w.dtype)
+    colsum = wf.float().sum(1).contiguous()
+    bf = (b.float() + w.float() @ beta.float()).contiguous()
+    return wf.contiguous(), colsum, bf
+
+
+def fold_ok(M: int, N: int, K: int) -> bool:
+    """Shapes (and GEMM build) the LN-folding epilogues support."""
+    if M % 256 or N % 256 or K % 256 or M < 2048:
+        return False
+    try:
+        return native().gemm_256_variant(-1) >= 3
+    except Exception:
+        return False
+
+
+def linear_ln(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, *, act: Optional[str] = None,
+              in_fin: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None,
+              residual: Optional[torch.Tensor] = None, res_fin: Optional[torch.Tensor] = None,
+              res_gamma: Optional[torch.Tensor] = None, part_out: Optional[torch.Tensor] = None,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Linear layer of a LayerNorm-folded encoder (see the block comment above).
+
+    * ``in_fin [M, 2]`` (+ ``colsum``): ``x`` holds raw LN inputs whose (rstd, rstd*mu)
+      are ``in_fin``; ``w``/``bias`` are folded (:func:`fold_ln_into_linear`).
+    * ``res_fin`` + ``res_gamma``: ``residual`` holds raw LN inputs; the bias carries beta.
+    * ``part_out [N/256, M, 2]``: row partials of the output (fp32, before bf16 rounding).
+    """
+    in_norm, res_norm = in_fin is not None, res_fin is not None
+    check(act in (None, "gelu"), f"linear_ln: activation {act!r} not supported")
+    check(not (in_norm and (res_norm or part_out is not None or residual is not None)),
+          "linear_ln: an input-normalising GEMM has no residual / output statistics")
+    check(not res_norm or residual is not None, "linear_ln: res_fin needs a residual")
+    M, K = x.shape
+    N = w.shape[0]
+    if not x.is_cuda:
+        y = x.float() @ w.float().t()
+        if in_norm:
+            y = y * in_fin[:, :1] - in_fin[:, 1:] * colsum.float().unsqueeze(0)
+        y = y + bias.float()
+        if act == "gelu":
+            y = F.gelu(y)
+        if residual is not None:
+            r = residual.float()
+            if res_norm:
+                r = (r * res_fin[:, :1] - res_fin[:, 1:]) * res_gamma.float().unsqueeze(0)
+            y = y + r
+        if part_out is not None:
+            part_out.copy_(ln_partials_ref(y))
+        y = y.to(x.dtype)
+        return out.copy_(y) if out is not None else y
+    check_bf16_dev(x, "x")
+    check_bf16_dev(w, "w")
+    same_device(x, w, bias, residual, in_fin, colsum, res_fin, res_gamma, part_out, out)
+    check(w.shape[1] == K, f"inner dims differ: x {tuple(x.shape)} w {tuple(w.shape)}")
+    check(fold_ok(M, N, K), f"linear_ln: unsupported shape M={M} N={N} K={K} (needs multiples of 256, M >= 2048)")
+
+    def f32(t, shape, name):
+        check(t is not None and t.dtype == torch.float32 and t.is_contiguous() and tuple(t.shape) == tuple(shape),
+              f"linear_ln: {name} must be contiguous fp32 {list(shape)}")
+
+    f32(bias, (N,), "bias")
+    epi = EPI_BIAS | (EPI_GELU if act == "gelu" else 0)
+    if in_norm:
+        f32(in_fin, (M, 2), "in_fin")
+        f32(colsum, (N,), "colsum")
+        epi |= EPI_IN_NORM
+    ldr = 0
+    if residual is not None:
+        check_bf16_dev(residual, "residual")
+        check(tuple(residual.shape) == (M, N), "residual must be [M, N]")
+        ldr = row_stride(residual, "residual")
+        epi |= EPI_RESIDUAL
+    if res_norm:
+        f32(res_fin, (M, 2), "res_fin")
+        f32(res_gamma, (N,), "res_gamma")
+        epi |= EPI_RES_NORM
+    if part_out is not None:
+        f32(part_out, (N // 256, M, 2), "part_out")
+        epi |= EPI_STATS_OUT
+    check(epi in (EPI_BIAS | EPI_IN_NORM, EPI_BIAS | EPI_IN_NORM | EPI_GELU,
+                  EPI_BIAS | EPI_RESIDUAL | EPI_STATS_OUT, EPI_BIAS | EPI_RESIDUAL | EPI_RES_NORM | EPI_STATS_OUT),
+          f"linear_ln: unsupported epilogue combination {epi}")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    check(tuple(out.shape) == (M, N) and out.dtype == torch.bfloat16, "out must be bf16 [M, N]")
+    native().gemm_ln(ptr(x), row_stride(x, "x"), ptr(w), row_stride(w, "w"), ptr(out), row_stride(out, "out"),
+                     ptr(bias), ptr(residual), ldr, M, N, K, epi, ptr(in_fin), ptr(colsum), ptr(res_fin),
+                     ptr(res_gamma), ptr(part_out), stream_handle())
+    return out

@@ -1,0 +1,81 @@
+"""LayerNorm folding algebra (CPU reference path of ops.linear_ln, the oracle of the GPU epilogues).
+
+A post-LN encoder never materialises its LayerNorms on the GPU: producers emit row
+partial (sum, sumsq), consumers apply (rstd, mu) to folded weights or to the residual.
+These tests pin the algebra in fp32 against the plain LayerNorm formulation.
+"""
+import torch
+import torch.nn.functional as F
+
+from agent_tpu_amd import ops
+from agent_tpu_amd.models.bert import BertClassifier, config_for, init_random
+
+
+def _ln(x, g, b, eps):
+    return F.layer_norm(x, (x.shape[1],), g, b, eps)
+
+
+def test_partials_and_finalize_match_layernorm_stats():
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(64, 768, generator=g) * 3 + 0.5
+    part = ops.ln_partials_ref(x)
+    assert part.shape == (3, 64, 2)
+    fin = ops.ln_finalize(part, 768, 1e-12)
+    mu, var = x.mean(1), x.var(1, unbiased=False)
+    torch.testing.assert_close(fin[:, 0], torch.rsqrt(var + 1e-12), rtol=1e-4, atol=0)
+    torch.testing.assert_close(fin[:, 1], torch.rsqrt(var + 1e-12) * mu, rtol=1e-4, atol=1e-6)
+
+
+def test_input_norm_fold_equals_ln_then_linear():
+    g = torch.Generator().manual_seed(1)
+    M, K, N, eps = 32, 512, 256, 1e-12
+    x = torch.randn(M, K, generator=g) * 2 + 1.0
+    w = torch.randn(N, K, generator=g) * 0.05
+    b = torch.randn(N, generator=g) * 0.1
+    gam = 1 + 0.2 * torch.randn(K, generator=g)
+    bet = 0.1 * torch.randn(K, generator=g)
+    ref = _ln(x, gam, bet, eps) @ w.t() + b
+    wf, colsum, bf = ops.fold_ln_into_linear(w, b, gam, bet)
+    fin = ops.ln_finalize(ops.ln_partials_ref(x), K, eps)
+    y = ops.linear_ln(x, wf, bf, in_fin=fin, colsum=colsum)
+    torch.testing.assert_close(y, ref, rtol=1e-4, atol=1e-4)
+    yg = ops.linear_ln(x, wf, bf, act="gelu", in_fin=fin, colsum=colsum)
+    torch.testing.assert_close(yg, F.gelu(ref), rtol=1e-4, atol=1e-4)
+
+
+def test_residual_norm_and_stats_out():
+    g = torch.Generator().manual_seed(2)
+    M, K, N, eps = 16, 256, 512, 1e-5
+    ctx = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) * 0.05
+    b = torch.randn(N, generator=g) * 0.1
+    r = torch.randn(M, N, generator=g) * 1.5 - 0.3  # raw pre-LN residual stream
+    gam = 1 + 0.2 * torch.randn(N, generator=g)
+    bet = 0.1 * torch.randn(N, generator=g)
+    fin = ops.ln_finalize(ops.ln_partials_ref(r), N, eps)
+    part = torch.empty(N // 256, M, 2)
+    y = ops.linear_ln(ctx, w, b + bet, residual=r, res_fin=fin, res_gamma=gam, part_out=part)
+    ref = ctx @ w.t() + b + _ln(r, gam, bet, eps)
+    torch.testing.assert_close(y, ref, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(part, ops.ln_partials_ref(ref), rtol=1e-4, atol=1e-3)
+
+
+def test_folded_encoder_equals_layernorm_encoder_fp32():
+    """The whole folded BERT encoder (CPU fp32) == the LayerNorm encoder, incl. the
+    [CLS]-only last layer, with non-trivial LN gamma/beta."""
+    cfg = config_for("bert-tiny", num_labels=3)  # hidden 256, intermediate 1024
+    pack = init_random(cfg, seed=5, bias_std=0.02)
+    g = torch.Generator().manual_seed(7)
+    for name in pack.names():
+        if name.endswith("_g"):
+            pack[name].copy_(1 + 0.1 * torch.randn(pack[name].shape, generator=g))
+        elif name.endswith("ln_b") or name.endswith("ln1_b") or name.endswith("ln2_b"):
+            pack[name].copy_(0.05 * torch.randn(pack[name].shape, generator=g))
+    m = BertClassifier(cfg, pack, fp32=True)
+    B, S = 4, 32
+    ids = torch.randint(1000, cfg.vocab_size, (B, S), generator=g, dtype=torch.int32)
+    lens = torch.tensor([32, 20, 9, 32], dtype=torch.int32)
+    for cls_only in (False, True):
+        ref = m.encode(ids, lens, cls_only_last=cls_only)
+        got = m.encode_folded(ids, lens, cls_only_last=cls_only)
+        torch.testing.assert_close(got, ref, rtol=2e-4, atol=2e-4)

@@ -1,0 +1,109 @@
+"""LayerNorm-folding GEMM epilogues (gemm256s InNorm / ResNorm / StatsOut) vs fp32 references.
+
+References are plain PyTorch fp32 on the same device (LayerNorm materialised, then
+the linear layer). M is chosen so that the persistent grid walks several tiles per
+workgroup: the row statistics of tile i are flushed during tile i+1.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from agent_tpu_amd import ops
+from agent_tpu_amd.models.bert import BertClassifier, config_for, init_random
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand(shape, gen, scale=1.0, shift=0.0, dtype=torch.bfloat16, dev="cuda"):
+    return (torch.randn(shape, generator=gen) * scale + shift).to(dtype).to(dev)
+
+
+def _ln_vecs(K, gen, dev):
+    return ((1 + 0.2 * torch.randn(K, generator=gen)).to(dev), (0.1 * torch.randn(K, generator=gen)).to(dev))
+
+
+@pytest.mark.parametrize("M,K,N,act", [(4096, 768, 2304, None), (65536, 768, 3072, "gelu"),
+                                       (8192, 1024, 1024, None), (32768, 256, 1024, "gelu")])
+def test_input_norm_epilogue(gpu, M, K, N, act):
+    gen = torch.Generator().manual_seed(M + K + N)
+    x = _rand((M, K), gen, 2.0, 0.5, dev=gpu)  # raw pre-LN rows
+    w = _rand((N, K), gen, 0.05, dev=gpu)
+    b = (0.1 * torch.randn(N, generator=gen)).to(gpu)
+    gam, bet = _ln_vecs(K, gen, gpu)
+    wf, colsum, bf = ops.fold_ln_into_linear(w, b, gam, bet)
+    part = ops.ln_partials_ref(x.float())
+    fin = ops.ln_finalize(part, K, 1e-12)  # the HIP finalize kernel
+    torch.testing.assert_close(fin, ops.ln_finalize(part.cpu(), K, 1e-12).to(gpu), rtol=2e-6, atol=1e-6)
+    y = ops.linear_ln(x, wf, bf, act=act, in_fin=fin, colsum=colsum)
+    ref = F.layer_norm(x.float(), (K,), gam, bet, 1e-12) @ w.float().t() + b
+    if act == "gelu":
+        ref = F.gelu(ref)
+    err = (y.float() - ref).abs().max().item()
+    assert err < 3e-2 * max(1.0, ref.abs().max().item()), err
+    # deterministic: no atomics anywhere
+    y2 = ops.linear_ln(x, wf, bf, act=act, in_fin=fin, colsum=colsum)
+    assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("M,K,N,res_norm", [(4096, 768, 768, False), (65536, 768, 768, True),
+                                            (32768, 3072, 768, True), (8192, 4096, 1024, True)])
+def test_residual_norm_and_stats_epilogue(gpu, M, K, N, res_norm):
+    gen = torch.Generator().manual_seed(M + K + N + res_norm)
+    ctx = _rand((M, K), gen, 1.0, dev=gpu)
+    w = _rand((N, K), gen, 0.03, dev=gpu)
+    b = (0.1 * torch.randn(N, generator=gen)).to(gpu)
+    r = _rand((M, N), gen, 1.5, -0.2, dev=gpu)
+    part = torch.full((N // 256, M, 2), float("nan"), device=gpu)
+    if res_norm:
+        gam, bet = _ln_vecs(N, gen, gpu)
+        fin = ops.ln_finalize(ops.ln_partials_ref(r.float()), N, 1e-12)
+        y = ops.linear_ln(ctx, w, b + bet, residual=r, res_fin=fin, res_gamma=gam, part_out=part)
+        ref = ctx.float() @ w.float().t() + b + F.layer_norm(r.float(), (N,), gam, bet, 1e-12)
+    else:
+        y = ops.linear_ln(ctx, w, b, residual=r, part_out=part)
+        ref = ctx.float() @ w.float().t() + b + r.float()
+    err = (y.float() - ref).abs().max().item()
+    assert err < 2e-2 * max(1.0, ref.abs().max().item()), err
+    # partials are of the fp32 outputs: compare with the reference's, scaled by the row mass
+    rp = ops.ln_partials_ref(ref)
+    assert torch.isfinite(part).all()
+    tol = 2e-3 * rp.abs().amax(dim=1, keepdim=True) + 1e-2
+    assert ((part - rp).abs() <= tol).all(), (part - rp).abs().max().item()
+    part2 = torch.empty_like(part)
+    if res_norm:
+        y2 = ops.linear_ln(ctx, w, b + bet, residual=r, res_fin=fin, res_gamma=gam, part_out=part2)
+    else:
+        y2 = ops.linear_ln(ctx, w, b, residual=r, part_out=part2)
+    assert torch.equal(y, y2) and torch.equal(part, part2)
+
+
+def test_folded_bert_matches_layernorm_bert(gpu):
+    """BERT-base at a production batch: the LN-folded encoder vs the materialised-LN
+    encoder on the same GPU, with non-trivial LN gamma/beta, and vs the fp32 oracle."""
+    cfg = config_for("bert-base", num_labels=5)
+    pack = init_random(cfg, seed=21, bias_std=0.02)
+    g = torch.Generator().manual_seed(8)
+    for name in pack.names():
+        if name.endswith("_g"):
+            pack[name].copy_(1 + 0.1 * torch.randn(pack[name].shape, generator=g))
+        elif name.endswith("ln_b") or name.endswith("ln1_b") or name.endswith("ln2_b"):
+            pack[name].copy_(0.05 * torch.randn(pack[name].shape, generator=g))
+    B, S = 32, 128
+    ids = torch.randint(1000, cfg.vocab_size, (B, S), generator=g, dtype=torch.int32)
+    ids[:, 0] = 101
+    lens = torch.randint(16, S + 1, (B,), generator=g, dtype=torch.int32)
+    ids[torch.arange(S).view(1, S) >= lens.view(B, 1)] = 0
+    m = BertClassifier(cfg, pack.to(gpu))
+    assert m.can_fold(B, S)
+    for cls_only in (True, False):
+        m.cls_only_last = cls_only
+        m.ln_fold = True
+        fl, fi, fs = m.forward(ids.to(gpu), lens.to(gpu), k=3)
+        m.ln_fold = False
+        ul, ui, us = m.forward(ids.to(gpu), lens.to(gpu), k=3)
+        assert (fl - ul).abs().max().item() < 2e-2 * max(1.0, ul.abs().max().item())
+        ok = (us[:, 0] - us[:, 1]) > 0.02
+        assert torch.equal(fi[ok, 0], ui[ok, 0])
+    oracle = BertClassifier(cfg, pack, fp32=True)
+    rl, _, _ = oracle.forward(ids[:4], lens[:4], k=3)
+    assert (fl[:4].cpu() - rl).abs().max().item() < 5e-2 * max(1.0, rl.abs().max().item())
