@@ -247,7 +247,8 @@ __device__ __forceinline__ bf16x4 lds_read_tr16_asm(const char* p) {
   return __builtin_bit_cast(bf16x4, r);
 }
 
-template <int CPOL>
+// HOT (timing-only diagnostic, results WRONG): every item reads batch row 0's Q/K/V (L2-resident)
+template <int CPOL, bool HOT = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void attention_packed_persist_kernel(
     const bf16* __restrict__ QKV, int ldq, bf16* __restrict__ O, int ldo, const int32_t* __restrict__ lens, int S,
     int H, int items, float scale) {
@@ -262,7 +263,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   if (item >= items) return;
 
   auto stage = [&](int it, int buf) {
-    const int b = __builtin_amdgcn_readfirstlane(it / H), h = __builtin_amdgcn_readfirstlane(it % H);
+    const int b = HOT ? 0 : __builtin_amdgcn_readfirstlane(it / H), h = __builtin_amdgcn_readfirstlane(it % H);
     // buffer resource over this item's rows (scalar base + 32-bit lane offsets,
     // guide T8): one VGPR per DMA. The lane offsets are recomputed per item from
     // the lane id (v_mbcnt, rematerialisable): kept live across the loop they were
@@ -464,7 +465,14 @@ void attention_fwd_strided(const bf16* q, int ldq, const bf16* k, int ldk, const
       const char* f = std::getenv("ATPU_ATTN_NT");
       return !(f && f[0] == '0');
     }();
-    if (nt)
+    static const bool hot = [] {
+      const char* f = std::getenv("ATPU_ATTN_HOT");
+      return f && f[0] == '1';
+    }();
+    if (hot)
+      hipLaunchKernelGGL((attention_packed_persist_kernel<2, true>), dim3(std::min(items, nb)), dim3(kThreads), 0,
+                         stream, q, ldq, out, ldo, lens, Sq, H, items, scale);
+    else if (nt)
       hipLaunchKernelGGL(attention_packed_persist_kernel<2>, dim3(std::min(items, nb)), dim3(kThreads), 0, stream, q,
                          ldq, out, ldo, lens, Sq, H, items, scale);
     else
