@@ -736,6 +736,23 @@ static_assert(kLineLoadsPerBlock == kLineStoresPerBlock,
 static_assert(kLineResWait == 14, "the counted residual wait assumes 8 blocks x 2 loads");
 static_assert(kLineResWait < 64, "vmcnt field is 6 bits on gfx950");
 
+// Sum of x over the 4 lanes l, l^16, l^32, l^48 (one 16-lane row each), in registers:
+// v_permlane16_swap of two copies leaves row pairs (0,1) and (2,3) exchanged across the
+// copies, so their sum is x + x^16; v_permlane32_swap does the same for the halves.
+// The copies are made inside the asm into early-clobber outputs: as plain copies of one
+// value hipcc allocated both operands to ONE register (docs/PERF_NOTES.md, permlane).
+// Same bits on all 4 lanes ((a+b)+(c+d) in either operand order). Replaces 2 LDS
+// round trips (ds_bpermute) per value on the epilogue's dependency chain.
+__device__ __forceinline__ float sum_lane_rows(float x) {
+  float a, b, c, d;
+  asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %2\n\ts_nop 1\n\tv_permlane16_swap_b32 %0, %1"
+               : "=&v"(a), "=&v"(b) : "v"(x));
+  const float y = a + b;
+  asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %2\n\ts_nop 1\n\tv_permlane32_swap_b32 %0, %1"
+               : "=&v"(c), "=&v"(d) : "v"(y));
+  return c + d;
+}
+
 // LayerNorm folding state of the line epilogue, all in the kernel's LDS array:
 //   fin[256][2]  (rstd, rstd*mu) of the tile's rows: of A (InNorm) or of R (ResNorm)
 //   col[256]     colsum of the folded weights (InNorm) or the residual's gamma (ResNorm)
@@ -879,11 +896,7 @@ __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int 
           s1 += p2;
           s2 = __builtin_elementwise_fma(p2, p2, s2);
         }
-      f32x2 s = f32x2{s1[0] + s1[1], s2[0] + s2[1]};
-      s[0] += __shfl_xor(s[0], 16, 64);
-      s[1] += __shfl_xor(s[1], 16, 64);
-      s[0] += __shfl_xor(s[0], 32, 64);
-      s[1] += __shfl_xor(s[1], 32, 64);
+      const f32x2 s = f32x2{sum_lane_rows(s1[0] + s1[1]), sum_lane_rows(s2[0] + s2[1])};
       if (fc == 0) *reinterpret_cast<f32x2*>(ln.st + (wn * 256 + lrow) * 2) = s;
     }
 #pragma unroll
