@@ -765,7 +765,9 @@ struct LnLds {
   float* st = nullptr;
 };
 
-template <int EPI, bool NT>
+// IN_ACC (InNorm): the caller started the accumulators at -mu*colsum (else the
+// epilogue applies -rstd*mu*colsum itself, from LDS colsum)
+template <int EPI, bool NT, bool IN_ACC = true>
 __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int m0, int n0, int wm, int wn, int lane,
                                                   bf16* __restrict__ C, int ldc, const bf16* __restrict__ R, int ldr,
                                                   const float* lds_bias, char* scratch,
@@ -780,7 +782,9 @@ __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int 
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     b4[j] = (EPI & kEpiBias) ? col4(lds_bias, j) : f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (kRes) g4[j] = col4(ln.col, j);  // ResNorm's caller adds the bias in the accumulator init
+    // ResNorm: gamma (its caller adds the bias in the accumulator init); InNorm without
+    // IN_ACC: colsum
+    if constexpr (kRes || (kIn && !IN_ACC)) g4[j] = col4(ln.col, j);
   }
   // (rstd, rstd*mu) of the lane's row in block i, read one block ahead: the residual
   // wait (asm with a memory clobber) would otherwise pin each read behind it
@@ -829,11 +833,12 @@ __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int 
       f32x4 t;
       if constexpr (kIn) {
         // LN(a) . W = rstd * (a . (gamma o W) - mu * colsum(gamma o W)) + beta . W (in the bias);
-        // the caller started acc at -mu * colsum
+        // IN_ACC: the caller started acc at -mu * colsum
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const f32x2 o = __builtin_elementwise_fma(f32x2{acc[i][j][2 * h], acc[i][j][2 * h + 1]}, rs2,
-                                                    f32x2{b4[j][2 * h], b4[j][2 * h + 1]});
+          f32x2 c2 = f32x2{b4[j][2 * h], b4[j][2 * h + 1]};
+          if constexpr (!IN_ACC) c2 = __builtin_elementwise_fma(nrm2, f32x2{g4[j][2 * h], g4[j][2 * h + 1]}, c2);
+          const f32x2 o = __builtin_elementwise_fma(f32x2{acc[i][j][2 * h], acc[i][j][2 * h + 1]}, rs2, c2);
           t[2 * h] = o[0];
           t[2 * h + 1] = o[1];
         }
@@ -1017,6 +1022,14 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
   // base, which the DMA takes in its saddr form: 8 VGPRs instead of 16 live over
   // the whole tile loop (host: A and Bt each < 4 GiB)
   constexpr bool kFold = kIn || kRes || kSt;
+  // InNorm: statistics and colsum staged at K-tile 1 (peeled), the epilogue applies
+  // rstd*acc - rstd*mu*colsum + bias (two packed FMAs per value pair). DBG & 16 (A/B
+  // variant, gemm_ablate(8)): statistics staged ahead of the tile and the accumulators
+  // started at -mu*colsum, one FMA in the epilogue; measured slower (tools/bench_fold.py:
+  // qkv +9.4 vs +4.7 us, ffn1 +13 vs +6 us over the plain kernel), the extra LDS reads
+  // sit on the tile-start path
+  constexpr bool kInAcc = kIn && (DBG & 16);
+  constexpr bool kPeel = kRes || kSt || (kIn && !kInAcc);
   // ResNorm / StatsOut variants start each tile's accumulators at the bias (read from
   // LDS, where the previous tile's last K-tile staged it) instead of adding it in the
   // epilogue: 16 fewer VGPRs and one op fewer per value pair on the epilogue chain
@@ -1092,10 +1105,10 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
     __builtin_amdgcn_global_load_lds((const ATPU_GLOBAL_AS void*)(reinterpret_cast<const char*>(ubase) + lo),
                                      (ATPU_LDS_AS void*)ldst, 4, 0, 0);
   };
-  auto ln_stage = [&](int tm0, int tn0) {  // ResNorm, at K-tile 1 of the tile
-    if constexpr (kRes) {
-      glds4(lf.res_fin + (size_t)tm0 * 2 + wave * 64, lds + kFinOff + wave * 256);
-      glds4(lf.gamma + tn0 + (wave & 3) * 64, lds + kColOff + (wave & 3) * 256);
+  auto ln_stage = [&](int tm0, int tn0) {  // ResNorm (and InNorm without kInAcc), at K-tile 1
+    if constexpr (kRes || (kIn && !kInAcc)) {
+      glds4((kRes ? lf.res_fin : lf.in_fin) + (size_t)tm0 * 2 + wave * 64, lds + kFinOff + wave * 256);
+      glds4((kRes ? lf.gamma : lf.colsum) + tn0 + (wave & 3) * 64, lds + kColOff + (wave & 3) * 256);
     }
   };
   // InNorm: a tile's row statistics and colsum are staged ahead of the tile (prologue,
@@ -1103,7 +1116,7 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
   // at -mu*colsum, so the epilogue is one packed FMA per value pair, rstd*acc + bias.
   // The statistics are double-buffered (the epilogue of the tile before reads its own).
   auto ln_stage_in = [&](int tm0, int tn0, int par) {
-    if constexpr (kIn) {
+    if constexpr (kInAcc) {
       glds4(lf.in_fin + (size_t)tm0 * 2 + wave * 64, lds + kFinOff + par * 2048 + wave * 256);
       glds4(lf.colsum + tn0 + (wave & 3) * 64, lds + kColOff + (wave & 3) * 256);
     }
@@ -1158,7 +1171,7 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc[i][j] = b;
       }
-    } else if constexpr (kIn) {
+    } else if constexpr (kInAcc) {
       // acc = -mu * colsum: rstd * acc_final = rstd*(a.W') - rstd*mu*colsum(W').
       // LDS offsets from an opaque lane id (the hoisted lane-derived offsets spilled)
       const int ol = opaque_lane();
@@ -1221,10 +1234,10 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
                                          (ATPU_LDS_AS void*)(lds + kBiasOff + (tile_par * 256 + (wave & 3) * 64) * 4),
                                          4, 0, 0);
       }
-      if constexpr (kIn) {
+      if constexpr (kInAcc) {
         if (last && has_next) ln_stage_in(m0, n0, tile_par ^ 1);
       }
-      if constexpr (kRes || kSt) {
+      if constexpr (kPeel) {
         if constexpr (P == 1) {
           ln_stage(cm0, cn0);
           if (!first) ln_flush(pm0, pn0);
@@ -1286,7 +1299,7 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
       ATPU_PS_SYNC_MMA(bl, 1, 0);
       buf ^= 1;
     };
-    if constexpr (kRes || kSt) {  // host: K >= 256, so K-tiles 0-1 are never the last
+    if constexpr (kPeel) {  // host: K >= 256, so K-tiles 0-1 are never the last
       kstep(0, std::false_type{}, std::integral_constant<int, 0>{});
       kstep(1, std::false_type{}, std::integral_constant<int, 1>{});
       for (int t = 2; t + 1 < nk; ++t) kstep(t, std::false_type{}, std::integral_constant<int, -1>{});
@@ -1306,10 +1319,10 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
       constexpr int kEpiRun0 = kBiasAcc ? (EPI & ~kEpiBias) : EPI;
       constexpr int kEpiRun = (DBG & 8) ? (kEpiRun0 & ~(kEpiInNorm | kEpiResNorm | kEpiStatsOut)) : kEpiRun0;
       if constexpr (LINE)
-        epilogue_256_line<kEpiRun, NT>(acc, cm0, cn0, wm, wn, (kIn || kRes || kSt) ? opaque_lane() : lane, C, ldc, R, ldr,
+        epilogue_256_line<kEpiRun, NT, kInAcc>(acc, cm0, cn0, wm, wn, (kIn || kRes || kSt) ? opaque_lane() : lane, C, ldc, R, ldr,
                                    reinterpret_cast<const float*>(lds + kBiasOff) + tile_par * 256,
                                    lds + kEpiOff + wave * 2048, pre,
-                                   LnLds{reinterpret_cast<const float*>(lds + kFinOff + (kIn ? tile_par * 2048 : 0)),
+                                   LnLds{reinterpret_cast<const float*>(lds + kFinOff + (kInAcc ? tile_par * 2048 : 0)),
                                          reinterpret_cast<const float*>(lds + kColOff),
                                          reinterpret_cast<float*>(lds + kStOff)});
       else
@@ -1398,6 +1411,15 @@ void launch_256s(const GemmArgs& g, hipStream_t s) {
                        g.bias, g.R, g.ldr, g.M, g.N, g.K, lf);                                                 \
     break;
   if constexpr (LINE) {
+    if (ablate == 8 && (g.epi & kEpiInNorm)) {  // A/B: InNorm with the accumulators started at -mu*colsum
+      if (g.epi & kEpiGelu)
+        hipLaunchKernelGGL((gemm256s_kernel<kEpiBias | kEpiInNorm | kEpiGelu, 16, NT, LINE>), dim3(nb), dim3(512), 0, s,
+                           g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, lf);
+      else
+        hipLaunchKernelGGL((gemm256s_kernel<kEpiBias | kEpiInNorm, 16, NT, LINE>), dim3(nb), dim3(512), 0, s, g.A,
+                           g.lda, g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, lf);
+      return;
+    }
     if (ablate == 7) {  // timing only: LN-folding structure without its epilogue math
 #define ATPU_G256S_A(E)                                                                                        \
   case E:                                                                                                      \

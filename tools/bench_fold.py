@@ -59,7 +59,7 @@ def main():
                          lambda: ops.linear_ln(x3072, w2, b2, residual=res, res_fin=fin, res_gamma=gam, part_out=part),
                          2 * M * I * H),
     }
-    times = {k: {"plain": [], "fold": [], "struct": []} for k in cases}
+    times = {k: {"plain": [], "fold": [], "struct": [], "accinit": []} for k in cases}
     extra = {"layernorm": [], "finalize": []}
     for rd in range(a.rounds):
         for k in (list(cases) if rd % 2 == 0 else list(reversed(cases))):
@@ -68,12 +68,15 @@ def main():
             times[k]["fold"].append(timeit(fold, a.iters))
             nat.gemm_ablate(7)
             times[k]["struct"].append(timeit(fold, a.iters))
+            if k in ("qkv", "ffn1"):  # InNorm variant: accumulators started at -mu*colsum
+                nat.gemm_ablate(8)
+                times[k]["accinit"].append(timeit(fold, a.iters))
             nat.gemm_ablate(0)
         extra["layernorm"].append(timeit(lambda: ops.layernorm(x768, gam, bet, 1e-12), a.iters))
         extra["finalize"].append(timeit(lambda: ops.ln_finalize(part, H, 1e-12, out=fin), a.iters))
     out = {}
     for k, (_, _, fl) in cases.items():
-        med = {v: statistics.median(t) for v, t in times[k].items()}
+        med = {v: statistics.median(t) for v, t in times[k].items() if t}
         out[k] = {f"{v}_us": round(t * 1000, 1) for v, t in med.items()}
         out[k].update({f"{v}_tflops": round(fl / t / 1e9, 1) for v, t in med.items()})
         print(k, json.dumps(out[k]), flush=True)
