@@ -10,7 +10,9 @@ silent eager fallback); ``ATPU_REQUIRE_NATIVE=1`` forces that everywhere.
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
+import sys
 from typing import Any, Optional
 
 import torch  # noqa: F401  (must precede the extension import)
@@ -35,6 +37,13 @@ def native() -> Any:
     """Return the ``_atpu`` module, building it in-tree if it is missing."""
     global _mod, _err
     if _mod is not None:
+        return _mod
+    alt = os.environ.get("ATPU_NATIVE_PATH")
+    if alt:  # development A/B: load another build of the extension (same module name)
+        spec = importlib.util.spec_from_file_location("agent_tpu_amd._atpu", alt)
+        _mod = importlib.util.module_from_spec(spec)
+        sys.modules["agent_tpu_amd._atpu"] = _mod
+        spec.loader.exec_module(_mod)
         return _mod
     try:
         _mod = importlib.import_module("agent_tpu_amd._atpu")

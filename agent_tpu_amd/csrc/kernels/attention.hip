@@ -333,28 +333,50 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     // every wave's K reads have retired (its MFMAs consumed them): the K half
     // of this buffer becomes the O staging area below
     __builtin_amdgcn_s_barrier();
-    float mx = -1e30f;
+    // softmax over the keys (unscaled scores: scale > 0, so max(s)*scale = max(s*scale)).
+    // exp((s - max)*scale) = exp2(s*c - max*c), c = scale*log2(e): one FMA + v_exp per
+    // score. When all 128 key slots are valid keys (S == 128 and a full-length row) the
+    // wave-uniform branch skips the per-score mask compares and selects; for S < 128 the
+    // slots past S hold clamped duplicate rows and are always masked.
+    const float c = scale * 1.4426950408889634f;
+    float mx = -1e30f, psum = 0.f;
+    if (len >= 8 * 16) {
 #pragma unroll
-    for (int kt = 0; kt < 8; ++kt)
+      for (int kt = 0; kt < 8; ++kt) mx = fmaxf(mx, fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3])));
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float moff = mx * c;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kt * 16 + fg * 4 + r;
-        const float x = key < len ? s[kt][r] * scale : -1e30f;
-        s[kt][r] = x;
-        mx = fmaxf(mx, x);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    float psum = 0.f;
+      for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
-    for (int kt = 0; kt < 8; ++kt)
+        for (int r = 0; r < 4; ++r) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[kt][r], c, -moff));
+          s[kt][r] = p;
+          psum += p;
+        }
+    } else {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float x = s[kt][r];
-        const float p = x <= -1e29f ? 0.f : __expf(x - mx);
-        s[kt][r] = p;
-        psum += p;
-      }
+      for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kt * 16 + fg * 4 + r;
+          const float x = key < len ? s[kt][r] : -1e30f;
+          s[kt][r] = x;
+          mx = fmaxf(mx, x);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float moff = mx * c;
+#pragma unroll
+      for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = s[kt][r];
+          const float p = x <= -1e29f ? 0.f : __builtin_amdgcn_exp2f(fmaf(x, c, -moff));
+          s[kt][r] = p;
+          psum += p;
+        }
+    }
     psum += __shfl_xor(psum, 16, 64);
     psum += __shfl_xor(psum, 32, 64);
 

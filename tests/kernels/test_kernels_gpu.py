@@ -160,7 +160,9 @@ def test_attention_persistent_matches_per_item(gpu, nat, S):
         nat.attention_persist_mode(1)
         for _ in range(3):
             out = ops.attention_packed(qkv, lens, B, S, H)
-            assert _rel_err(out, ref) < 1e-3
+            # the persistent kernel's softmax is exp2(s*c - max*c) (FMA form), the per-item
+            # kernel's exp(s*scale - max): bf16 outputs differ by rounding flips only
+            assert _rel_err(out, ref) < 2e-3
     finally:
         nat.attention_persist_mode(prev)
     hd = H * 64
