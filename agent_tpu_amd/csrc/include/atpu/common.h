@@ -40,6 +40,31 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Reductions over the 4 lanes l, l^16, l^32, l^48 (the 4 lane rows holding one
+// MFMA 16x16 fragment row/column), registers only: v_permlane16_swap then
+// v_permlane32_swap, no ds_bpermute round trips. Every lane gets the result.
+// The operands are laundered through v_mov into early-clobber outputs: the
+// two-result builtin let hipcc allocate both to ONE register (ROCm 7.2).
+__device__ __forceinline__ float lane_rows_sum(float x) {
+  float a, b, c, d;
+  asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %2\n\ts_nop 1\n\tv_permlane16_swap_b32 %0, %1"
+               : "=&v"(a), "=&v"(b) : "v"(x));
+  const float y = a + b;
+  asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %2\n\ts_nop 1\n\tv_permlane32_swap_b32 %0, %1"
+               : "=&v"(c), "=&v"(d) : "v"(y));
+  return c + d;
+}
+
+__device__ __forceinline__ float lane_rows_max(float x) {
+  float a, b, c, d;
+  asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %2\n\ts_nop 1\n\tv_permlane16_swap_b32 %0, %1"
+               : "=&v"(a), "=&v"(b) : "v"(x));
+  const float y = fmaxf(a, b);
+  asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %2\n\ts_nop 1\n\tv_permlane32_swap_b32 %0, %1"
+               : "=&v"(c), "=&v"(d) : "v"(y));
+  return fmaxf(c, d);
+}
+
 __device__ __forceinline__ double wave_sum_f64(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -130,6 +155,62 @@ __device__ __forceinline__ void gelu_poly16(float (&v)[16]) {
     const f32x2 g = f32x2{v[2 * e], v[2 * e + 1]} * __builtin_elementwise_fma(xc[e], p[e], f32x2{0.5f, 0.5f});
     v[2 * e] = g[0];
     v[2 * e + 1] = g[1];
+  }
+}
+
+// A/B variants of gelu_poly16 (gemm_ablate 9-11, ffn1 only): MODE & 1 = scalar
+// v_fma_f32 instead of packed pairs (a v_pk_fma_f32 issued beside another wave's
+// MFMAs costs more than its two scalar halves); MODE & 2 = degree 8 on
+// |x/sqrt2| <= 3 (max |err| 5.2e-5, tools/gelu_fit.py --deg 8 --a 3.0).
+template <int MODE>
+__device__ __forceinline__ void gelu_poly16_v(float (&v)[16]) {
+  if constexpr (MODE == 0) {
+    gelu_poly16(v);
+  } else {
+    constexpr bool kD8 = MODE & 2;
+    constexpr int kDeg = kD8 ? 8 : 10;
+    constexpr float kQ10[11] = {1.536687613e-01f,  -7.178471889e-03f, 4.856055602e-04f, -3.426085095e-05f,
+                                2.347781901e-06f,  -1.526724844e-07f, 8.713541888e-09f, -4.079194205e-10f,
+                                2.366933385e-11f,  -1.725522828e-12f, 5.926992431e-14f};
+    constexpr float kQ8[11] = {1.662152261e-01f, -8.985635825e-03f, 6.880812580e-04f, -5.386176053e-05f,
+                               3.873941750e-06f, -2.390964369e-07f, 1.633439162e-08f, -1.310694664e-09f,
+                               5.403365602e-11f, 0.f, 0.f};
+    constexpr float kClamp = kD8 ? 4.242640495e+00f : 4.596194267e+00f;
+    constexpr float kH = kD8 ? 9.0f : 1.056250000e+01f;
+    if constexpr (MODE & 1) {
+      float xc[16], w[16], p[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        xc[e] = __builtin_amdgcn_fmed3f(v[e], -kClamp, kClamp);
+        w[e] = fmaf(xc[e], xc[e], -kH);
+        p[e] = kD8 ? kQ8[kDeg] : kQ10[kDeg];
+      }
+#pragma unroll
+      for (int k = kDeg - 1; k >= 0; --k)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) p[e] = fmaf(p[e], w[e], kD8 ? kQ8[k] : kQ10[k]);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v[e] = v[e] * fmaf(xc[e], p[e], 0.5f);
+    } else {
+      f32x2 xc[8], w[8], p[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        xc[e] = f32x2{__builtin_amdgcn_fmed3f(v[2 * e], -kClamp, kClamp),
+                      __builtin_amdgcn_fmed3f(v[2 * e + 1], -kClamp, kClamp)};
+        w[e] = __builtin_elementwise_fma(xc[e], xc[e], f32x2{-kH, -kH});
+        p[e] = f32x2{kQ8[kDeg], kQ8[kDeg]};
+      }
+#pragma unroll
+      for (int k = kDeg - 1; k >= 0; --k)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) p[e] = __builtin_elementwise_fma(p[e], w[e], f32x2{kQ8[k], kQ8[k]});
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const f32x2 g = f32x2{v[2 * e], v[2 * e + 1]} * __builtin_elementwise_fma(xc[e], p[e], f32x2{0.5f, 0.5f});
+        v[2 * e] = g[0];
+        v[2 * e + 1] = g[1];
+      }
+    }
   }
 }
 

@@ -248,7 +248,9 @@ __device__ __forceinline__ bf16x4 lds_read_tr16_asm(const char* p) {
 }
 
 // HOT (timing-only diagnostic, results WRONG): every item reads batch row 0's Q/K/V (L2-resident)
-template <int CPOL, bool HOT = false>
+// PL: row max / sum over the 4 lanes of a query by v_permlane16/32_swap (registers
+// only) instead of the ds_bpermute round trips __shfl_xor compiles to
+template <int CPOL, bool HOT = false, bool PL = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void attention_packed_persist_kernel(
     const bf16* __restrict__ QKV, int ldq, bf16* __restrict__ O, int ldo, const int32_t* __restrict__ lens, int S,
     int H, int items, float scale) {
@@ -343,8 +345,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     if (len >= 8 * 16) {
 #pragma unroll
       for (int kt = 0; kt < 8; ++kt) mx = fmaxf(mx, fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3])));
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if constexpr (PL) {
+        mx = lane_rows_max(mx);
+      } else {
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      }
       const float moff = mx * c;
 #pragma unroll
       for (int kt = 0; kt < 8; ++kt)
@@ -364,8 +370,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
           s[kt][r] = x;
           mx = fmaxf(mx, x);
         }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if constexpr (PL) {
+        mx = lane_rows_max(mx);
+      } else {
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      }
       const float moff = mx * c;
 #pragma unroll
       for (int kt = 0; kt < 8; ++kt)
@@ -377,8 +387,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
           psum += p;
         }
     }
-    psum += __shfl_xor(psum, 16, 64);
-    psum += __shfl_xor(psum, 32, 64);
+    if constexpr (PL) {
+      psum = lane_rows_sum(psum);
+    } else {
+      psum += __shfl_xor(psum, 16, 64);
+      psum += __shfl_xor(psum, 32, 64);
+    }
 
     f32x4 o[4];
 #pragma unroll
@@ -459,10 +473,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 }  // namespace
 
 int attention_persist_mode(int set) {
-  // 1 = persistent prefetching kernel for the packed BERT case (default), 0 = one item per workgroup
+  // packed BERT case: 2 = persistent kernel with register-only row reductions (default),
+  // 1 = persistent kernel with ds_bpermute reductions, 0 = one item per workgroup
   static int v = [] {
     const char* f = std::getenv("ATPU_ATTN_PERSIST");
-    return (f && f[0] == '0') ? 0 : 1;
+    return (f && (f[0] == '0' || f[0] == '1')) ? f[0] - '0' : 2;
   }();
   if (set >= 0) v = set;
   return v;
@@ -479,10 +494,16 @@ void attention_fwd_strided(const bf16* q, int ldq, const bf16* k, int ldk, const
   // one key chunk, whole 16-query tiles: the persistent prefetching kernel
   const bool packed = k == q + H * kD && v == k + H * kD && ldk == ldq && ldv == ldq;
   if (packed && !bias && !causal && lens && Sq == Skv && Sq <= kKC && Sq % 16 == 0 &&
-      attention_persist_mode(-1) == 1) {
-    const int nb = 2 * num_cus();  // two workgroups per CU (<= 128 VGPRs, 80 KiB LDS each)
+      attention_persist_mode(-1) >= 1) {
+    const int nb = 2 * num_cus();  // two workgroups per CU (80 KiB LDS each)
 
     const int items = B * H;
+    if (attention_persist_mode(-1) == 2) {
+      hipLaunchKernelGGL((attention_packed_persist_kernel<2, false, true>), dim3(std::min(items, nb)), dim3(kThreads),
+                         0, stream, q, ldq, out, ldo, lens, Sq, H, items, scale);
+      ATPU_HIP_CHECK(hipGetLastError());
+      return;
+    }
     static const bool nt = [] {
       const char* f = std::getenv("ATPU_ATTN_NT");
       return !(f && f[0] == '0');

@@ -743,15 +743,7 @@ static_assert(kLineResWait < 64, "vmcnt field is 6 bits on gfx950");
 // value hipcc allocated both operands to ONE register (docs/PERF_NOTES.md, permlane).
 // Same bits on all 4 lanes ((a+b)+(c+d) in either operand order). Replaces 2 LDS
 // round trips (ds_bpermute) per value on the epilogue's dependency chain.
-__device__ __forceinline__ float sum_lane_rows(float x) {
-  float a, b, c, d;
-  asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %2\n\ts_nop 1\n\tv_permlane16_swap_b32 %0, %1"
-               : "=&v"(a), "=&v"(b) : "v"(x));
-  const float y = a + b;
-  asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %2\n\ts_nop 1\n\tv_permlane32_swap_b32 %0, %1"
-               : "=&v"(c), "=&v"(d) : "v"(y));
-  return c + d;
-}
+__device__ __forceinline__ float sum_lane_rows(float x) { return lane_rows_sum(x); }
 
 // LayerNorm folding state of the line epilogue, all in the kernel's LDS array:
 //   fin[256][2]  (rstd, rstd*mu) of the tile's rows: of A (InNorm) or of R (ResNorm)
@@ -767,7 +759,7 @@ struct LnLds {
 
 // IN_ACC (InNorm): the caller started the accumulators at -mu*colsum (else the
 // epilogue applies -rstd*mu*colsum itself, from LDS colsum)
-template <int EPI, bool NT, bool IN_ACC = true>
+template <int EPI, bool NT, bool IN_ACC = true, int GM = 0>
 __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int m0, int n0, int wm, int wn, int lane,
                                                   bf16* __restrict__ C, int ldc, const bf16* __restrict__ R, int ldr,
                                                   const float* lds_bias, char* scratch,
@@ -848,7 +840,7 @@ __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int 
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[j][e] = t[e];
     }
-    if constexpr (EPI & kEpiGelu) gelu_poly16(*reinterpret_cast<float(*)[16]>(&v[0][0]));
+    if constexpr (EPI & kEpiGelu) gelu_poly16_v<GM>(*reinterpret_cast<float(*)[16]>(&v[0][0]));
     if constexpr (EPI & kEpiTanh) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -1319,7 +1311,7 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
       constexpr int kEpiRun0 = kBiasAcc ? (EPI & ~kEpiBias) : EPI;
       constexpr int kEpiRun = (DBG & 8) ? (kEpiRun0 & ~(kEpiInNorm | kEpiResNorm | kEpiStatsOut)) : kEpiRun0;
       if constexpr (LINE)
-        epilogue_256_line<kEpiRun, NT, kInAcc>(acc, cm0, cn0, wm, wn, (kIn || kRes || kSt) ? opaque_lane() : lane, C, ldc, R, ldr,
+        epilogue_256_line<kEpiRun, NT, kInAcc, ((DBG >> 5) & 3)>(acc, cm0, cn0, wm, wn, (kIn || kRes || kSt) ? opaque_lane() : lane, C, ldc, R, ldr,
                                    reinterpret_cast<const float*>(lds + kBiasOff) + tile_par * 256,
                                    lds + kEpiOff + wave * 2048, pre,
                                    LnLds{reinterpret_cast<const float*>(lds + kFinOff + (kInAcc ? tile_par * 2048 : 0)),
@@ -1418,6 +1410,15 @@ void launch_256s(const GemmArgs& g, hipStream_t s) {
       else
         hipLaunchKernelGGL((gemm256s_kernel<kEpiBias | kEpiInNorm, 16, NT, LINE>), dim3(nb), dim3(512), 0, s, g.A,
                            g.lda, g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, lf);
+      return;
+    }
+    if (ablate >= 9 && ablate <= 11 && g.epi == (kEpiBias | kEpiInNorm | kEpiGelu)) {
+      // A/B of the GELU evaluation (gelu_poly16_v): 9 scalar, 10 packed degree 8, 11 scalar degree 8
+      auto k = ablate == 9 ? gemm256s_kernel<kEpiBias | kEpiInNorm | kEpiGelu, 32, NT, LINE>
+               : ablate == 10 ? gemm256s_kernel<kEpiBias | kEpiInNorm | kEpiGelu, 64, NT, LINE>
+                              : gemm256s_kernel<kEpiBias | kEpiInNorm | kEpiGelu, 96, NT, LINE>;
+      hipLaunchKernelGGL(k, dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M,
+                         g.N, g.K, lf);
       return;
     }
     if (ablate == 7) {  // timing only: LN-folding structure without its epilogue math

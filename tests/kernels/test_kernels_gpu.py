@@ -146,8 +146,9 @@ def test_attention_packed(gpu, B, S, H):
     assert _rel_err(out, ref) < 2e-2
 
 
+@pytest.mark.parametrize("mode", [1, 2])  # ds_bpermute / permlane row reductions
 @pytest.mark.parametrize("S", [128, 64])
-def test_attention_persistent_matches_per_item(gpu, nat, S):
+def test_attention_persistent_matches_per_item(gpu, nat, S, mode):
     # the persistent prefetching kernel walks several (batch, head) items per
     # workgroup here (B*H > 2 workgroups per CU), with ragged key lengths
     B, H = 96, 12
@@ -157,7 +158,7 @@ def test_attention_persistent_matches_per_item(gpu, nat, S):
     try:
         nat.attention_persist_mode(0)
         ref = ops.attention_packed(qkv, lens, B, S, H)
-        nat.attention_persist_mode(1)
+        nat.attention_persist_mode(mode)
         for _ in range(3):
             out = ops.attention_packed(qkv, lens, B, S, H)
             # the persistent kernel's softmax is exp2(s*c - max*c) (FMA form), the per-item

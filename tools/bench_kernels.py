@@ -81,7 +81,8 @@ def main():
                           0)
     sel = [k for k in cases if not a.only or k in a.only.split(",")]
     variants = [int(v) for v in a.variants.split(",") if v]
-    times = {k: {"ours": [], "lib": [], **{f"v{v}": [] for v in variants}} for k in sel}
+    times = {k: {"ours": [], "lib": [], "p16": [], **{f"v{v}": [] for v in variants}} for k in sel}
+    prev_var = nat.gemm_256_variant(-1)
     for rd in range(a.rounds):
         for k in (sel if rd % 2 == 0 else list(reversed(sel))):
             ours, lib, _ = cases[k]
@@ -91,7 +92,12 @@ def main():
                 for v in variants:
                     nat.gemm_256_variant(v)
                     times[k][f"v{v}"].append(timeit(ours, a.iters))
-                    nat.gemm_256_variant(1)
+                    nat.gemm_256_variant(prev_var)
+            if k == "attention":  # A/B: the 16-query persistent kernel (mode 1)
+                prev = nat.attention_persist_mode(-1)
+                nat.attention_persist_mode(1)
+                times[k]["p16"].append(timeit(ours, a.iters))
+                nat.attention_persist_mode(prev)
     for k in sel:
         fl = cases[k][2]
         o, l = statistics.median(times[k]["ours"]), statistics.median(times[k]["lib"])
@@ -99,6 +105,8 @@ def main():
         if fl:
             out[k]["ours_tflops"] = round(fl / o / 1e9, 1)
             out[k]["lib_tflops"] = round(fl / l / 1e9, 1)
+        if times[k]["p16"]:
+            out[k]["p16_ms"] = round(statistics.median(times[k]["p16"]), 4)
         for v in variants:
             if times[k][f"v{v}"]:
                 out[k][f"v{v}_tflops"] = round(fl / statistics.median(times[k][f"v{v}"]) / 1e9, 1)
