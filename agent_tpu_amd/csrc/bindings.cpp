@@ -63,16 +63,16 @@ PYBIND11_MODULE(_atpu, m) {
   m.def(
       "gemm",
       [](uintptr_t A, int lda, uintptr_t Bt, int ldb, uintptr_t C, int ldc, uintptr_t bias, uintptr_t R, int ldr, int M,
-         int N, int K, int epi, uintptr_t stream, int splits, uintptr_t ws) {
+         int N, int K, int epi, uintptr_t stream, int splits, uintptr_t ws, float rms_eps) {
         GemmArgs g;
         g.A = P<const bf16>(A); g.lda = lda; g.Bt = P<const bf16>(Bt); g.ldb = ldb; g.C = P<bf16>(C); g.ldc = ldc;
         g.bias = P<const float>(bias); g.R = P<const bf16>(R); g.ldr = ldr; g.M = M; g.N = N; g.K = K; g.epi = epi;
-        g.splits = splits; g.ws = P<float>(ws);
+        g.splits = splits; g.ws = P<float>(ws); g.rms_eps = rms_eps;
         gemm_bf16(g, S(stream));
       },
       "bf16 MFMA GEMM C = epi(A @ Bt^T)", py::arg("A"), py::arg("lda"), py::arg("Bt"), py::arg("ldb"), py::arg("C"),
       py::arg("ldc"), py::arg("bias"), py::arg("R"), py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"),
-      py::arg("epi"), py::arg("stream"), py::arg("splits") = 1, py::arg("ws") = 0);
+      py::arg("epi"), py::arg("stream"), py::arg("splits") = 1, py::arg("ws") = 0, py::arg("rms_eps") = 0.f);
   m.def(
       "gemm_ln",
       [](uintptr_t A, int lda, uintptr_t Bt, int ldb, uintptr_t C, int ldc, uintptr_t bias, uintptr_t R, int ldr, int M,

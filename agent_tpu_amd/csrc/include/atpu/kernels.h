@@ -27,6 +27,9 @@ enum GemmEpilogue : int {
   kEpiResNorm = 128,   // R rows are raw LN inputs (beta folded into bias):
                        //   C = ... + (R*rstd - rstd*mu) * gamma     (rstd, mu from res_fin)
   kEpiStatsOut = 256,  // also write per-row partial (sum, sum of squares) of C, one per 256 columns
+  kEpiRowRms = 512,    // A rows are raw RMSNorm inputs (gamma folded into Bt): the kernel sums A^2
+                       //   over its K loop, C = rsqrt(mean_k A^2 + rms_eps) * (A . Bt^T) ... (128x128 and
+                       //   skinny "dec" kernels, no split-K; T5 decoder steps)
 };
 
 struct GemmArgs {
@@ -50,6 +53,7 @@ struct GemmArgs {
   const float* res_fin = nullptr;  // ResNorm: [M][2] (rstd, rstd*mu) of R's rows
   const float* gamma = nullptr;    // ResNorm: [N] LN gamma of R
   float* part_out = nullptr;       // StatsOut: [N/256][M][2] partial (sum, sumsq) of C's rows (fp32 values)
+  float rms_eps = 0.f;             // RowRms
 };
 void gemm_bf16(const GemmArgs& g, hipStream_t stream);
 // split count the library picks for an [M,N,K] problem (1 = no split-K)

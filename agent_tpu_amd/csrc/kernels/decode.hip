@@ -246,7 +246,7 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const bf16* __restrict
   }
 }
 
-constexpr int kTopkThreads = 1024;
+constexpr int kTopkThreads = 256;
 constexpr int kTopkWaves = kTopkThreads / 64;
 constexpr int kMaxBeamK = 16;
 
@@ -298,7 +298,7 @@ template <int K>
 __global__ __launch_bounds__(kTopkThreads) void beam_topk_kernel(const float* __restrict__ logits, int V,
                                                                  const float* __restrict__ beam_scores, int eos,
                                                                  int mask_eos, float* __restrict__ out_score,
-                                                                 int32_t* __restrict__ out_token) {
+                                                                 int32_t* __restrict__ out_token, int vec4) {
   __shared__ float wm[kTopkWaves], ws[kTopkWaves];
   constexpr int KM = K;
   __shared__ float cv[kTopkWaves * KM];
@@ -310,9 +310,42 @@ __global__ __launch_bounds__(kTopkThreads) void beam_topk_kernel(const float* __
 #pragma unroll
   for (int r = 0; r < KM; ++r) { tv[r] = -FLT_MAX; ti[r] = 0x7fffffff; }
   // normaliser over ALL tokens; the min-length EOS mask applies to selection
-  // only (HF applies MinLengthLogitsProcessor after log_softmax)
+  // only (HF applies MinLengthLogitsProcessor after log_softmax).
+  // 16-B loads, 4 per thread in flight per round (the scalar, branchy loop ran at
+  // ~1 TB/s); the running (max, sum) is rescaled once per 16 values.
   float m = -FLT_MAX, s = 0.f;
-  for (int i = tid; i < V; i += kTopkThreads) {
+  auto take = [&](float val, int i) {
+    const float sel = (mask_eos && i == eos) ? -FLT_MAX : val;
+    if (better(sel, i, tv[KM - 1], ti[KM - 1])) list_insert<KM>(tv, ti, sel, i);
+  };
+  const int nv4 = vec4 ? V / 4 : 0;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  for (int j0 = tid; j0 < nv4; j0 += 4 * kTopkThreads) {
+    float4 v[4];
+    bool ok[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = j0 + u * kTopkThreads;
+      ok[u] = j < nv4;
+      v[u] = ok[u] ? x4[j] : make_float4(-FLT_MAX, -FLT_MAX, -FLT_MAX, -FLT_MAX);
+    }
+    float cm = m;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) cm = fmaxf(cm, fmaxf(fmaxf(v[u].x, v[u].y), fmaxf(v[u].z, v[u].w)));
+    s *= __expf(m - cm);  // m == -FLT_MAX: s is 0 either way
+    m = cm;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (!ok[u]) continue;
+      s += (__expf(v[u].x - m) + __expf(v[u].y - m)) + (__expf(v[u].z - m) + __expf(v[u].w - m));
+      const int i = 4 * (j0 + u * kTopkThreads);
+      take(v[u].x, i);
+      take(v[u].y, i + 1);
+      take(v[u].z, i + 2);
+      take(v[u].w, i + 3);
+    }
+  }
+  for (int i = 4 * nv4 + tid; i < V; i += kTopkThreads) {  // tail (or every element without vec4)
     const float val = x[i];
     if (val > m) {
       s = s * __expf(m - val) + 1.f;
@@ -320,8 +353,7 @@ __global__ __launch_bounds__(kTopkThreads) void beam_topk_kernel(const float* __
     } else {
       s += __expf(val - m);
     }
-    const float sel = (mask_eos && i == eos) ? -FLT_MAX : val;
-    if (better(sel, i, tv[KM - 1], ti[KM - 1])) list_insert<KM>(tv, ti, sel, i);
+    take(val, i);
   }
   // block log-sum-exp
   const float wmax = wave_max(m);
@@ -416,10 +448,11 @@ void gather_rows(const bf16* src, bf16* dst, const int32_t* parent, int nrows, i
 void beam_topk_rows(const float* logits, int rows, int V, const float* beam_scores, int eos, int mask_eos, int K,
                     float* out_score, int32_t* out_token, hipStream_t stream) {
   ATPU_CHECK(K >= 1 && K <= kMaxBeamK && K <= V, "beam_topk: 1 <= K <= 16");
+  const int vec4 = V % 4 == 0 && (reinterpret_cast<uintptr_t>(logits) & 15) == 0;
 #define ATPU_TK(KK)                                                                                               \
   case KK:                                                                                                        \
     hipLaunchKernelGGL(beam_topk_kernel<KK>, dim3(rows), dim3(kTopkThreads), 0, stream, logits, V, beam_scores,   \
-                       eos, mask_eos, out_score, out_token);                                                      \
+                       eos, mask_eos, out_score, out_token, vec4);                                                \
     break;
   switch (K) {
     ATPU_TK(1) ATPU_TK(2) ATPU_TK(3) ATPU_TK(4) ATPU_TK(5) ATPU_TK(6) ATPU_TK(7) ATPU_TK(8)

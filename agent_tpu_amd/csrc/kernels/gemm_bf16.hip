@@ -46,11 +46,26 @@ __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >>
 // order (deterministic) with the epilogue fused. (An in-kernel "last block
 // reduces" fixup was measured 10x slower: the device-scope fence it needs
 // writes back the XCD's whole L2 on gfx950.)
+// RowRms (EPI & kEpiRowRms): every lane sums the squares of the A fragments it reads
+// (v_dot2c_f32_bf16); the 4 lanes of a row (its 4 k-chunks) complete the row's sum over
+// the whole K loop, and the accumulator of that row is scaled by rsqrt(mean + eps).
+// MFMA operands are swapped (Bt as "A"), so an accumulator's row is the lane's A
+// fragment row: no transposition of the statistics.
+__device__ __forceinline__ float sumsq_bf16x8(bf16x8 a, float acc) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const bf16x2_t p = bf16x2_t{a[2 * e], a[2 * e + 1]};
+    acc = __builtin_amdgcn_fdot2_f32_bf16(p, p, acc, false);
+  }
+  return acc;
+}
+
 template <int BM, int BN, int WM, int WN, int EPI, int SPLIT = 0>
 __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
     const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C, int ldc,
     const float* __restrict__ bias, const bf16* __restrict__ R, int ldr, int M, int N, int K,
-    float* __restrict__ ws = nullptr) {
+    float* __restrict__ ws = nullptr, float rms_eps = 0.f) {
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 16;
   constexpr int TN = BN / WN / 16;
@@ -110,6 +125,9 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int frow = lane & 15, fchunk = lane >> 4;
+  float ssq[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) ssq[i] = 0.f;
   auto compute = [&](int buf) {
     const char* base = lds + buf * STAGE_BYTES;
 #pragma unroll
@@ -119,6 +137,7 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
       for (int i = 0; i < TM; ++i) {
         const int r = arow0 + i * 16 + frow;
         af[i] = *reinterpret_cast<const bf16x8*>(base + r * kRowBytes + swz(r, ks * 4 + fchunk) * 16);
+        if constexpr (EPI & kEpiRowRms) ssq[i] = sumsq_bf16x8(af[i], ssq[i]);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
@@ -160,6 +179,10 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
   }
 
   // ---- epilogue: lane owns C[m][n..n+3] for each (i, j) fragment ----
+  float rstd[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+    rstd[i] = (EPI & kEpiRowRms) ? __builtin_amdgcn_rsqf(lane_rows_sum(ssq[i]) * (1.f / K) + rms_eps) : 1.f;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = m0 + arow0 + i * 16 + frow;
@@ -169,6 +192,7 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
       const int n = n0 + brow0 + j * 16 + fchunk * 4;
       if (n >= N) continue;
       f32x4 v = acc[i][j];
+      if constexpr (EPI & kEpiRowRms) v *= rstd[i];
       if constexpr (EPI & kEpiBias) {
         const f32x4 b = *reinterpret_cast<const f32x4*>(bias + n);
         v += b;
@@ -1527,7 +1551,8 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
                                                           const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C,
                                                           int ldc, const float* __restrict__ bias,
                                                           const bf16* __restrict__ R, int ldr, int M, int N, int K,
-                                                          float* __restrict__ ws) {
+                                                          float* __restrict__ ws, float rms_eps = 0.f) {
+  static_assert(!(SPLIT && (EPI & kEpiRowRms)), "RowRms needs the whole K loop in one block");
   constexpr int BM = 64, BN = 64;
   constexpr int STAGE = (BM + BN) * kRowBytes;  // 16 KiB: A rows 0-63, B rows 64-127
   constexpr int LPS = (BM + BN) / 8 / 4;        // DMA instructions per wave per stage (4)
@@ -1571,6 +1596,7 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  float ssq[2] = {0.f, 0.f};  // RowRms: this lane's share of its A rows' sum of squares
   auto compute = [&](int slot) {
     const char* base = lds + slot * STAGE;
 #pragma unroll
@@ -1580,6 +1606,7 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
       for (int i = 0; i < 2; ++i) {
         const int r = wm * 32 + i * 16 + frow;
         af[i] = *reinterpret_cast<const bf16x8*>(base + r * kRowBytes + swz(r, ks * 4 + fchunk) * 16);
+        if constexpr (EPI & kEpiRowRms) ssq[i] = sumsq_bf16x8(af[i], ssq[i]);
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -1625,6 +1652,10 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
     }
     return;
   }
+  float rstd[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    rstd[i] = (EPI & kEpiRowRms) ? __builtin_amdgcn_rsqf(lane_rows_sum(ssq[i]) * (1.f / K) + rms_eps) : 1.f;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int m = m0 + wm * 32 + i * 16 + frow;
@@ -1634,6 +1665,7 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
       const int n = n0 + wn * 32 + j * 16 + fchunk * 4;
       if (n >= N) continue;
       f32x4 v = acc[i][j];
+      if constexpr (EPI & kEpiRowRms) v *= rstd[i];
       if constexpr (EPI & kEpiBias) v += *reinterpret_cast<const f32x4*>(bias + n);
       if constexpr (EPI & kEpiGelu) {
 #pragma unroll
@@ -1674,9 +1706,12 @@ void launch_dec(const GemmArgs& g, hipStream_t s) {
 #define ATPU_DEC_CASE(E)                                                                                       \
   case E:                                                                                                      \
     hipLaunchKernelGGL((gemm_dec_kernel<E, kDecStages, 0>), grid, block, 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, \
-                       g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, nullptr);                                    \
+                       g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, nullptr, g.rms_eps);                         \
     break;
   switch (g.epi) {
+    ATPU_DEC_CASE(kEpiRowRms)
+    ATPU_DEC_CASE(kEpiRowRms | kEpiRelu)
+    ATPU_DEC_CASE(kEpiRowRms | kEpiOutF32)
     ATPU_DEC_CASE(0)
     ATPU_DEC_CASE(kEpiBias)
     ATPU_DEC_CASE(kEpiBias | kEpiGelu)
@@ -1777,9 +1812,12 @@ void launch_tile(const GemmArgs& g, hipStream_t s) {
 #define ATPU_GEMM_CASE(E)                                                                             \
   case E:                                                                                             \
     hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, E>), grid, block, 0, s, g.A, g.lda, g.Bt, g.ldb, \
-                       g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K);                                 \
+                       g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, nullptr, g.rms_eps);             \
     break;
   switch (g.epi) {
+    ATPU_GEMM_CASE(kEpiRowRms)
+    ATPU_GEMM_CASE(kEpiRowRms | kEpiRelu)
+    ATPU_GEMM_CASE(kEpiRowRms | kEpiOutF32)
     ATPU_GEMM_CASE(0)
     ATPU_GEMM_CASE(kEpiBias)
     ATPU_GEMM_CASE(kEpiBias | kEpiGelu)
@@ -1879,6 +1917,7 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
     return f ? std::atoi(f) : 0;
   }();
   if (g.splits > 1) {
+    ATPU_CHECK(!(g.epi & kEpiRowRms), "gemm: RowRms cannot split K");
     ATPU_CHECK(g.ws && (g.K / kBK) % g.splits == 0, "gemm: split-K needs a workspace and K/64 % splits == 0");
     launch_splitk(g, g.splits, gemm_dec_mode(-1) == 1 && skinny(g.M, g.N), stream);
     ATPU_HIP_CHECK(hipGetLastError());
@@ -1905,6 +1944,19 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
     ATPU_CHECK(!(fe & kEpiStatsOut) || g.part_out, "gemm: StatsOut needs part_out");
     if (kernel256 == 3) launch_256s<false, true>(g, stream);
     else launch_256s<true, true>(g, stream);
+    ATPU_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  if (g.epi & kEpiRowRms) {
+    // RMSNorm folded into the GEMM (T5 decoder steps): the 128x128 and skinny kernels
+    // sum the A rows' squares over their whole K loop (no split-K)
+    const int fe = g.epi & ~kEpiRowRms;
+    ATPU_CHECK(fe == 0 || fe == kEpiRelu || fe == kEpiOutF32, "gemm: unsupported RowRms epilogue " + std::to_string(g.epi));
+    ATPU_CHECK(g.rms_eps > 0.f, "gemm: RowRms needs rms_eps > 0");
+    if (gemm_dec_mode(-1) == 1 && skinny(g.M, g.N))
+      launch_dec(g, stream);
+    else
+      launch_tile<128, 128, 2, 2>(g, stream);
     ATPU_HIP_CHECK(hipGetLastError());
     return;
   }

@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, Optional
 
@@ -197,6 +198,24 @@ class T5Model:
         self.device = pack.buffer.device
         self._enc_bias: Dict[int, torch.Tensor] = {}
         self._dec_bias: Optional[torch.Tensor] = None
+        # decoder steps: every RMSNorm folded into the GEMM that consumes it (gamma in the
+        # weight, the row statistics summed in the GEMM's K loop; ops.linear rms_eps)
+        self.rms_fold = (self.device.type == "cuda" and not fp32
+                         and os.getenv("ATPU_RMS_FOLD", "1") not in ("0", "false", "no"))
+        self._rfold: Optional[Dict[str, torch.Tensor]] = None
+
+    def rms_folded(self) -> Dict[str, torch.Tensor]:
+        """Decoder weights with the preceding RMSNorm's gamma folded in (built once)."""
+        if self._rfold is None:
+            p, f = self.p, {}
+            for i in range(self.cfg.dec_layers):
+                q = f"dec.l{i}."
+                f[q + "qkv"] = ops.fold_rms_into_linear(p[q + "qkv"], p[q + "ln1"])
+                f[q + "cq"] = ops.fold_rms_into_linear(p[q + "cq"], p[q + "ln2"])
+                f[q + "wi"] = ops.fold_rms_into_linear(p[q + "wi"], p[q + "ln3"])
+            f["lm"] = ops.fold_rms_into_linear(p["lm"], p["dec.ln_f"])
+            self._rfold = f
+        return self._rfold
 
     def wrap_source(self, toks):
         return list(toks) + [self.cfg.eos_id]
@@ -262,6 +281,8 @@ class T5Model:
         x = ops.embed_gather(tokens, p["shared"])
         if x.dtype != p["dec.l0.qkv"].dtype:
             x = x.to(p["dec.l0.qkv"].dtype)
+        if self.rms_fold:
+            return self._step_folded(x, step, cache, T, ckv, src_lens, S, group, hist, dbias)
         for i in range(cfg.dec_layers):
             q = f"dec.l{i}."
             c = cache[i]
@@ -280,3 +301,23 @@ class T5Model:
             x = ops.linear(f, p[q + "wo"], residual=x)
         y = ops.rmsnorm(x, p["dec.ln_f"], cfg.eps)
         return ops.linear(y, p["lm"], out_f32=True)
+
+    def _step_folded(self, x, step, cache, T, ckv, src_lens, S, group, hist, dbias) -> torch.Tensor:
+        """:meth:`step` with each RMSNorm folded into its consumer GEMM (37 fewer launches
+        per step, no normalised copy of x); logits equal the unfolded step to bf16 rounding."""
+        cfg, p, f = self.cfg, self.p, self.rms_folded()
+        d, H, eps = cfg.d_model, cfg.heads, cfg.eps
+        for i in range(cfg.dec_layers):
+            q = f"dec.l{i}."
+            c = cache[i]
+            qkv = ops.linear(x, f[q + "qkv"], rms_eps=eps)
+            ops.kv_append(qkv, d, 2 * d, c, T, step)
+            ctx = ops.decode_attention(qkv[:, :d], c[:, :d], c[:, d:], H, T, 1, step=step, bias_dist=dbias, hist=hist)
+            x = ops.linear(ctx, p[q + "o"], residual=x)
+            cq = ops.linear(x, f[q + "cq"], rms_eps=eps)
+            kv = ckv[:, i * 2 * d:(i + 1) * 2 * d]
+            ctx = ops.decode_attention(cq, kv[:, :d], kv[:, d:], H, S, group, lens=src_lens)
+            x = ops.linear(ctx, p[q + "co"], residual=x)
+            h = ops.linear(x, f[q + "wi"], act="relu", rms_eps=eps)
+            x = ops.linear(h, p[q + "wo"], residual=x)
+        return ops.linear(x, f["lm"], out_f32=True, rms_eps=eps)

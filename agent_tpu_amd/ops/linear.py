@@ -21,8 +21,13 @@ EPI_BIAS, EPI_GELU, EPI_TANH, EPI_RESIDUAL, EPI_RELU, EPI_OUT_F32 = 1, 2, 4, 8, 
 _ACTS = {None: 0, "none": 0, "gelu": EPI_GELU, "tanh": EPI_TANH, "relu": EPI_RELU}
 
 
-def linear_ref(x, w, bias=None, act=None, residual=None, out_f32=False):
+EPI_ROW_RMS = 512
+
+
+def linear_ref(x, w, bias=None, act=None, residual=None, out_f32=False, rms_eps=None):
     y = x.float() @ w.float().t()
+    if rms_eps is not None:
+        y = y * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + rms_eps)
     if bias is not None:
         y = y + bias.float()
     if act == "gelu":
@@ -43,11 +48,19 @@ def _splits(M: int, N: int, K: int) -> int:
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: Optional[str] = None,
            residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-           out_f32: bool = False) -> torch.Tensor:
-    """``act(x @ w.T + bias) + residual``; ``out_f32`` returns fp32 (LM-head logits)."""
+           out_f32: bool = False, rms_eps: Optional[float] = None) -> torch.Tensor:
+    """``act(x @ w.T + bias) + residual``; ``out_f32`` returns fp32 (LM-head logits).
+
+    ``rms_eps``: ``x`` rows are raw RMSNorm inputs and ``w`` carries the norm's gamma
+    (:func:`fold_rms_into_linear`): ``y = rsqrt(mean(x^2) + eps) * (x @ w.T)``, the row
+    statistics summed inside the GEMM's K loop (no bias / residual with it)."""
     check(act in _ACTS, f"unknown activation {act!r}")
+    if rms_eps is not None:
+        check(bias is None and residual is None and act in (None, "none", "relu"),
+              "linear: rms_eps takes no bias / residual and only a ReLU")
+        check(rms_eps > 0, "linear: rms_eps must be > 0")
     if not x.is_cuda:
-        y = linear_ref(x, w, bias, act, residual, out_f32)
+        y = linear_ref(x, w, bias, act, residual, out_f32, rms_eps)
         if out is not None:
             out.copy_(y)
             return out
@@ -76,11 +89,20 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         out = torch.empty((M, N), dtype=odt, device=x.device)
     check(tuple(out.shape) == (M, N) and out.dtype == odt, "out must be [M, N] of the output dtype")
     ldc = row_stride(out, "out")
-    splits = _splits(M, N, K)
+    if rms_eps is not None:
+        epi |= EPI_ROW_RMS
+        splits = 1
+    else:
+        splits = _splits(M, N, K)
     ws = torch.empty(splits * M * N, dtype=torch.float32, device=x.device) if splits > 1 else None
     native().gemm(ptr(x), lda, ptr(w), ldb, ptr(out), ldc, ptr(bias), ptr(residual), ldr, M, N, K, epi,
-                  stream_handle(), splits, ptr(ws))
+                  stream_handle(), splits, ptr(ws), float(rms_eps or 0.0))
     return out
+
+
+def fold_rms_into_linear(w: torch.Tensor, gamma: torch.Tensor) -> torch.Tensor:
+    """``RMSNorm(x; gamma) @ w.T == rstd(x) * (x @ (w * gamma).T)``: the folded weight (``w``'s dtype)."""
+    return (w.float() * gamma.float().unsqueeze(0)).to(w.dtype).contiguous()
 
 
 # ---------------------------------------------------------------- LayerNorm folding

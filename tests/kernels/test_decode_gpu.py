@@ -235,3 +235,53 @@ def test_bart_step_and_generate_gpu(gpu):
                                                               use_graph=False))
     assert r1.sequences == r2.sequences
     assert all(s[0] == 2 and s[1] == 0 and len(s) <= 20 for s in r1.sequences)
+
+
+@pytest.mark.parametrize("M,N,K,act,out_f32", [(1024, 2304, 768, None, False), (1024, 3072, 768, "relu", False),
+                                               (256, 768, 768, None, False), (4096, 768, 768, None, False),
+                                               (1024, 32128, 768, None, True), (77, 192, 256, "relu", False)])
+def test_gemm_row_rms_fold(gpu, M, N, K, act, out_f32):
+    # RMSNorm folded into the GEMM (skinny dec kernel, 128x128 kernel, LM-head fp32 out):
+    # rsqrt(mean(x^2) + eps) * (x @ (w*gamma).T) against the fp32 norm-then-linear reference
+    x = _r((M, K), gpu, 2.0, seed=21)
+    w = _r((N, K), gpu, 0.05, seed=22)
+    gamma = 1 + _r((K,), gpu, 0.3, torch.float32, seed=23)
+    eps = 1e-6
+    wf = ops.fold_rms_into_linear(w, gamma)
+    y = ops.linear(x, wf, act=act, out_f32=out_f32, rms_eps=eps)
+    xf = x.cpu().float()
+    xn = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * gamma.cpu()
+    ref = xn @ w.cpu().float().t()
+    if act == "relu":
+        ref = torch.relu(ref)
+    assert y.dtype == (torch.float32 if out_f32 else torch.bfloat16)
+    assert _rel(y, ref) < 2e-2
+
+
+def test_t5_step_rms_fold_matches_unfolded(gpu):
+    # non-trivial RMSNorm gammas: the folded decoder step vs the rmsnorm + linear step (GPU) and the fp32 oracle
+    from agent_tpu_amd.models.t5 import T5Model, config_for, init_random
+
+    cfg = config_for("t5-tiny")
+    pack = init_random(cfg, seed=3)
+    g = torch.Generator().manual_seed(4)
+    for n in pack.names():
+        if n.split(".")[-1].startswith("ln"):
+            pack[n].copy_(1 + 0.3 * torch.randn(pack[n].shape, generator=g))
+    cpu_m = T5Model(cfg, pack, fp32=True)
+    gp = pack.to(gpu)
+    fold_m, plain_m = T5Model(cfg, gp), T5Model(cfg, gp)
+    plain_m.rms_fold = False
+    assert fold_m.rms_fold
+    B, S, T = 3, 16, 8
+    ids = torch.randint(2, cfg.vocab_size, (B, S), generator=g, dtype=torch.int32)
+    lens = torch.tensor([16, 9, 12], dtype=torch.int32)
+    _, kc = cpu_m.encode(ids, lens)
+    _, kg = fold_m.encode(ids.to(gpu), lens.to(gpu))
+    tok = torch.randint(2, cfg.vocab_size, (B,), generator=g, dtype=torch.int32)
+    step = torch.zeros(1, dtype=torch.int32)
+    lc = cpu_m.step(tok, step, cpu_m.new_cache(B, T), T, kc, lens, S, 1)
+    lf = fold_m.step(tok.to(gpu), step.to(gpu), fold_m.new_cache(B, T), T, kg, lens.to(gpu), S, 1)
+    lp = plain_m.step(tok.to(gpu), step.to(gpu), plain_m.new_cache(B, T), T, kg, lens.to(gpu), S, 1)
+    assert _rel(lf, lc) < 5e-2 and _rel(lp, lc) < 5e-2
+    assert _rel(lf, lp) < 3e-2
