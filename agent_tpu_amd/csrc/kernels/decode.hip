@@ -50,7 +50,11 @@ __global__ __launch_bounds__(NW * 64) void decode_attention_kernel(
   __shared__ float po[NW][GM][kD];
   __shared__ float red[NW][16];
   __shared__ int prow[GM == 1 ? kMaxKeys : 1];  // self attention: physical cache row of key j
-  const int seq = blockIdx.x, h = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // self attention: the beams of one item mostly share their history (backpointers
+  // to the same physical cache rows), so consecutive rows go to ONE XCD (bijective
+  // remap of the row index, guide T1) and re-read each other's K/V rows from its L2
+  const int seq = (GM == 1 && hist) ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int h = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int G = min(group, nrows - seq * group);
   int len = lens ? lens[seq] : (*step_dev + 1);
   len = min(len, kMaxKeys);
