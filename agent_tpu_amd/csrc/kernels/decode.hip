@@ -26,6 +26,7 @@
 #include "atpu/kernels.h"
 
 #include <cfloat>
+#include <cstdlib>
 
 namespace atpu {
 namespace {
@@ -199,6 +200,103 @@ __global__ __launch_bounds__(NW * 64) void decode_attention_kernel(
       acc += po[x][g][d];
     }
     out[(size_t)(seq * group + g) * ldo + h * kD + d] = f2bf(s > 0.f ? acc / s : 0.f);
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Self-attention decode step, ONE workgroup per sequence row for ALL heads
+// (default; ATPU_DEC_SELF=0 restores decode_attention_kernel<1, 4>).
+// The per-(row, head) kernel above spends a 16-key MFMA tile and three block
+// barriers on ~65 keys of one query, and every one of its rows x heads blocks
+// walks the same dependent chain: backpointer load -> K row -> barrier ->
+// V row -> barrier (206 us per call at 4096 rows, far from any bandwidth
+// bound). Here the backpointer row is resolved once into LDS for all heads,
+// and each wave owns whole heads, so nothing crosses waves after that:
+//   scores : lane = key, the key's 128-B K row in 8 x 16-B loads, 32 v_dot2
+//            with the (uniform) query, wave max / sum reductions;
+//   P.V    : lane = (key sub 0..7, 8 dims), probabilities through a per-wave
+//            LDS row, 16-B V loads kUnrollV deep, xor-reduce over key subs.
+// ----------------------------------------------------------------------------
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void decode_self_attention_kernel(
+    const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k, const bf16* __restrict__ v, int ldkv,
+    int seq_stride, const int32_t* __restrict__ step_dev, const int32_t* __restrict__ hist, int hist_stride,
+    const float* __restrict__ bias_dist, int bias_stride, bf16* __restrict__ out, int ldo, int H, float scale) {
+  extern __shared__ __attribute__((aligned(16))) char dsm[];
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  const int seq = xcd_remap(blockIdx.x, gridDim.x);  // beams of one item on one XCD (shared history rows)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int len = min(*step_dev + 1, seq_stride);
+  const int cap = (seq_stride + 3) & ~3;
+  int* prow = reinterpret_cast<int*>(dsm);                  // physical cache row of key j
+  float* pw = reinterpret_cast<float*>(dsm) + cap * (1 + w);  // this wave's scores / probabilities
+  for (int j = tid; j < len; j += NW * 64) prow[j] = (hist && j < len - 1) ? hist[(size_t)seq * hist_stride + j] : seq;
+  __syncthreads();
+  auto at = [&](int r, int j, int h) -> size_t { return ((size_t)r * seq_stride + j) * ldkv + h * kD; };
+  const int ksub = lane >> 3, dc = (lane & 7) * 8;
+  for (int h = w; h < H; h += NW) {
+    bf16x8 qq[8];  // the head's query, identical in every lane
+    const bf16* qr = q + (size_t)seq * ldq + h * kD;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) qq[c] = *reinterpret_cast<const bf16x8*>(qr + c * 8);
+    float mx = -FLT_MAX;
+    for (int j0 = 0; j0 < len; j0 += 64) {
+      const int j = j0 + lane;
+      if (j < len) {
+        const bf16* kr = k + at(prow[j], j, h);
+        bf16x8 kk[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) kk[c] = *reinterpret_cast<const bf16x8*>(kr + c * 8);
+        float d[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            d[e & 3] = __builtin_amdgcn_fdot2_f32_bf16(bf16x2_t{kk[c][2 * e], kk[c][2 * e + 1]},
+                                                       bf16x2_t{qq[c][2 * e], qq[c][2 * e + 1]}, d[e & 3], false);
+        const float sj = ((d[0] + d[1]) + (d[2] + d[3])) * scale +
+                         (bias_dist ? bias_dist[h * bias_stride + (len - 1 - j)] : 0.f);
+        pw[j] = sj;
+        mx = fmaxf(mx, sj);
+      }
+    }
+    mx = wave_max(mx);
+    float sum = 0.f;
+    for (int j = lane; j < len; j += 64) {
+      const float e = __expf(pw[j] - mx);
+      pw[j] = e;
+      sum += e;
+    }
+    sum = wave_sum(sum);
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = 0.f;
+    for (int j0 = 0; j0 < len; j0 += 8 * kUnrollV) {
+      bf16x8 vv[kUnrollV];
+#pragma unroll
+      for (int u = 0; u < kUnrollV; ++u) {
+        const int j = min(j0 + u * 8 + ksub, len - 1);
+        vv[u] = *reinterpret_cast<const bf16x8*>(v + at(prow[j], j, h) + dc);
+      }
+#pragma unroll
+      for (int u = 0; u < kUnrollV; ++u) {
+        const int j = j0 + u * 8 + ksub;
+        const float pj = j < len ? pw[j] : 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += pj * bf2f(vv[u][e]);
+      }
+    }
+    const float inv = sum > 0.f ? 1.f / sum : 0.f;
+    bf16x8 ov;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float x = o[e];
+      x += __shfl_xor(x, 8);
+      x += __shfl_xor(x, 16);
+      x += __shfl_xor(x, 32);
+      ov[e] = f2bf(x * inv);
+    }
+    if (ksub == 0) *reinterpret_cast<bf16x8*>(out + (size_t)seq * ldo + h * kD + dc) = ov;
   }
 }
 
@@ -405,6 +503,21 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
   ATPU_CHECK(ldq % 8 == 0 && ldkv % 8 == 0, "decode_attention: 16-B rows required");
   ATPU_CHECK((reinterpret_cast<uintptr_t>(k) & 15) == 0 && (reinterpret_cast<uintptr_t>(v) & 15) == 0,
              "decode_attention: K/V must be 16-byte aligned");
+  static const bool row_kernel = [] {
+    const char* f = std::getenv("ATPU_DEC_SELF");
+    return !(f && f[0] == '0');
+  }();
+  if (group == 1 && step_dev && !lens && row_kernel) {
+    ATPU_CHECK(seq_stride <= kMaxKeys, "decode_attention: cache length above 2048");
+    ATPU_CHECK(ldo % 8 == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 && (reinterpret_cast<uintptr_t>(q) & 15) == 0,
+               "decode_attention: q / out need 16-B rows");
+    constexpr int NW = 4;
+    const size_t smem = (size_t)((seq_stride + 3) & ~3) * 4 * (1 + NW);
+    hipLaunchKernelGGL((decode_self_attention_kernel<NW>), dim3(rows), dim3(NW * 64), smem, stream, q, ldq, k, v, ldkv,
+                       seq_stride, step_dev, hist, hist_stride, bias_dist, bias_stride, out, ldo, H, scale);
+    ATPU_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const int nseq = (rows + group - 1) / group;
   const dim3 grid(nseq, H);
 #define ATPU_DA(GM, NW)                                                                                          \

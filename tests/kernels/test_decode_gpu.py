@@ -75,6 +75,25 @@ def test_decode_self_hist_backpointers(gpu):
     assert torch.equal(dst[:, t], parent) and torch.equal(dst[:, :t], hist[parent.long(), :t])
 
 
+@pytest.mark.parametrize("rows,H,T,t,scale", [(9, 16, 300, 257, 0.125), (64, 12, 130, 64, 1.0), (5, 12, 131, 0, 1.0),
+                                              (3, 2, 2048, 2047, 0.125)])
+def test_decode_self_rows_all_heads(gpu, rows, H, T, t, scale):
+    # per-row all-heads self-attention kernel: > 64 keys (several score passes), 16 heads over 4 waves,
+    # the first step (one key), the longest cache; random backpointers, no bias / T5 bias
+    d = H * 64
+    cache = _r((rows * T, 2 * d), gpu, seed=31)
+    q = _r((rows, 3 * d), gpu, seed=32)[:, :d]  # strided like the fused QKV output
+    g = torch.Generator().manual_seed(5)
+    hist = torch.randint(0, rows, (rows, T), generator=g, dtype=torch.int32)
+    step = torch.tensor([t], dtype=torch.int32)
+    for bias in (None, _r((H, T), gpu, 1.0, torch.float32, seed=33)):
+        out = ops.decode_attention(q, cache[:, :d], cache[:, d:], H, T, 1, step=step.to(gpu), bias_dist=bias,
+                                   hist=hist.to(gpu), scale=scale)
+        ref = _decode_attention_ref(q.cpu(), cache.cpu()[:, :d], cache.cpu()[:, d:], H, T, 1, None, step,
+                                    None if bias is None else bias.cpu(), scale, None, hist)
+        assert _rel(out, ref) < 2e-2
+
+
 @pytest.mark.parametrize("rows,group,seqlen", [(256, 4, 512), (40, 4, 100), (24, 8, 7), (9, 3, 2048), (10, 4, 64),
                                                (13, 5, 300)])
 def test_decode_cross_grouped_shapes(gpu, rows, group, seqlen):
