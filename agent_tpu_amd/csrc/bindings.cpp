@@ -146,11 +146,16 @@ PYBIND11_MODULE(_atpu, m) {
     gather_rows(P<const bf16>(src), P<bf16>(dst), P<const int32_t>(parent), nrows, seq_stride, ldc,
                 P<const int32_t>(step_dev), slabs, slab_elems, S(stream));
   });
-  m.def("beam_topk_rows", [](uintptr_t logits, int rows, int V, uintptr_t beam_scores, int eos, int mask_eos, int K,
-                             uintptr_t out_score, uintptr_t out_token, uintptr_t stream) {
-    beam_topk_rows(P<const float>(logits), rows, V, P<const float>(beam_scores), eos, mask_eos, K, P<float>(out_score),
-                   P<int32_t>(out_token), S(stream));
-  });
+  m.def(
+      "beam_topk_rows",
+      [](uintptr_t logits, int rows, int V, uintptr_t beam_scores, int eos, int mask_eos, int K, uintptr_t out_score,
+         uintptr_t out_token, uintptr_t stream, uintptr_t bans, int nbmax) {
+        beam_topk_rows(P<const float>(logits), rows, V, P<const float>(beam_scores), eos, mask_eos, K,
+                       P<float>(out_score), P<int32_t>(out_token), S(stream), P<const int32_t>(bans), nbmax);
+      },
+      py::arg("logits"), py::arg("rows"), py::arg("V"), py::arg("beam_scores"), py::arg("eos"), py::arg("mask_eos"),
+      py::arg("K"), py::arg("out_score"), py::arg("out_token"), py::arg("stream"), py::arg("bans") = 0,
+      py::arg("nbmax") = 0);
 
   m.def("attention", [](uintptr_t qkv, uintptr_t lens, uintptr_t bias, uintptr_t out, int B, int Sq, int H, int D,
                         float scale, uintptr_t stream) {

@@ -88,7 +88,8 @@ void kv_append(const bf16* src, int lds, int col0, int ncols, bf16* cache, int s
 void gather_rows(const bf16* src, bf16* dst, const int32_t* parent, int nrows, int seq_stride, int ldc,
                  const int32_t* step_dev, int slabs, size_t slab_elems, hipStream_t stream);
 void beam_topk_rows(const float* logits, int rows, int V, const float* beam_scores, int eos, int mask_eos, int K,
-                    float* out_score, int32_t* out_token, hipStream_t stream);
+                    float* out_score, int32_t* out_token, hipStream_t stream,
+                    const int32_t* bans = nullptr, int nbmax = 0);
 
 // ------------------------------------------------------------- attention (K4)
 // qkv: [B*S, 3*H*D] packed per token as [q(H*D) | k(H*D) | v(H*D)];

@@ -351,6 +351,7 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const bf16* __restrict
 constexpr int kTopkThreads = 256;
 constexpr int kTopkWaves = kTopkThreads / 64;
 constexpr int kMaxBeamK = 16;
+constexpr int kMaxBans = 512;  // banned tokens per row (beam_topk_rows); more -> the caller's exact path
 
 // (value desc, index asc) ordering
 __device__ __forceinline__ bool better(float a, int ia, float b, int ib) { return a > b || (a == b && ia < ib); }
@@ -400,7 +401,8 @@ template <int K>
 __global__ __launch_bounds__(kTopkThreads) void beam_topk_kernel(const float* __restrict__ logits, int V,
                                                                  const float* __restrict__ beam_scores, int eos,
                                                                  int mask_eos, float* __restrict__ out_score,
-                                                                 int32_t* __restrict__ out_token, int vec4) {
+                                                                 int32_t* __restrict__ out_token, int vec4,
+                                                                 const int32_t* __restrict__ bans, int nbmax) {
   __shared__ float wm[kTopkWaves], ws[kTopkWaves];
   constexpr int KM = K;
   __shared__ float cv[kTopkWaves * KM];
@@ -415,10 +417,21 @@ __global__ __launch_bounds__(kTopkThreads) void beam_topk_kernel(const float* __
   // only (HF applies MinLengthLogitsProcessor after log_softmax).
   // 16-B loads, 4 per thread in flight per round (the scalar, branchy loop ran at
   // ~1 TB/s); the running (max, sum) is rescaled once per 16 values.
+  // no-repeat-n-gram bans: the row's banned token ids (-1 padded), tested only for a
+  // value that would enter the thread's list (rare after the first few), so the
+  // kernel returns the top K among the allowed tokens (HF applies the processor
+  // after log_softmax: the normaliser still covers every token)
+  __shared__ int ban_s[kMaxBans];
+  for (int b = tid; b < nbmax; b += kTopkThreads) ban_s[b] = bans[(size_t)row * nbmax + b];
+  if (nbmax > 0) __syncthreads();
   float m = -FLT_MAX, s = 0.f;
   auto take = [&](float val, int i) {
     const float sel = (mask_eos && i == eos) ? -FLT_MAX : val;
-    if (better(sel, i, tv[KM - 1], ti[KM - 1])) list_insert<KM>(tv, ti, sel, i);
+    if (better(sel, i, tv[KM - 1], ti[KM - 1])) {
+      for (int b = 0; b < nbmax; ++b)
+        if (ban_s[b] == i) return;
+      list_insert<KM>(tv, ti, sel, i);
+    }
   };
   const int nv4 = vec4 ? V / 4 : 0;
   const float4* x4 = reinterpret_cast<const float4*>(x);
@@ -563,13 +576,14 @@ void gather_rows(const bf16* src, bf16* dst, const int32_t* parent, int nrows, i
 }
 
 void beam_topk_rows(const float* logits, int rows, int V, const float* beam_scores, int eos, int mask_eos, int K,
-                    float* out_score, int32_t* out_token, hipStream_t stream) {
+                    float* out_score, int32_t* out_token, hipStream_t stream, const int32_t* bans, int nbmax) {
   ATPU_CHECK(K >= 1 && K <= kMaxBeamK && K <= V, "beam_topk: 1 <= K <= 16");
+  ATPU_CHECK(nbmax >= 0 && nbmax <= kMaxBans && (nbmax == 0 || bans), "beam_topk: 0 <= banned tokens per row <= 512");
   const int vec4 = V % 4 == 0 && (reinterpret_cast<uintptr_t>(logits) & 15) == 0;
 #define ATPU_TK(KK)                                                                                               \
   case KK:                                                                                                        \
     hipLaunchKernelGGL(beam_topk_kernel<KK>, dim3(rows), dim3(kTopkThreads), 0, stream, logits, V, beam_scores,   \
-                       eos, mask_eos, out_score, out_token, vec4);                                                \
+                       eos, mask_eos, out_score, out_token, vec4, bans, nbmax);                                   \
     break;
   switch (K) {
     ATPU_TK(1) ATPU_TK(2) ATPU_TK(3) ATPU_TK(4) ATPU_TK(5) ATPU_TK(6) ATPU_TK(7) ATPU_TK(8)

@@ -119,20 +119,36 @@ def gather_rows(src: torch.Tensor, dst: torch.Tensor, parent: torch.Tensor, nrow
                          nrows * seq_stride * C, stream_handle())
 
 
-def beam_topk_rows(logits: torch.Tensor, beam_scores: torch.Tensor, k: int, eos: int, mask_eos: bool
-                   ) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Per row: top-k of ``log_softmax(logits) + beam_score`` (EOS masked if asked)."""
+MAX_BANS = 512  # banned tokens per row the kernel filters (decode.hip kMaxBans)
+
+
+def beam_topk_rows(logits: torch.Tensor, beam_scores: torch.Tensor, k: int, eos: int, mask_eos: bool,
+                   bans: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per row: top-k of ``log_softmax(logits) + beam_score`` (EOS masked if asked).
+
+    ``bans`` (int32 ``[R, nb]``, -1 padded): token ids excluded from row r's selection
+    (no-repeat-n-gram processor; the log-softmax normaliser still covers every token)."""
     R, V = logits.shape
+    nbmax = 0 if bans is None else int(bans.shape[1])
     if not logits.is_cuda:
         lp = torch.log_softmax(logits.float(), dim=-1)
         if mask_eos:
             lp[:, eos] = float("-inf")
+        if nbmax:
+            b = bans.to(torch.int64).cpu()
+            r = torch.arange(R).view(-1, 1).expand_as(b)
+            ok = b >= 0
+            lp[r[ok], b[ok]] = float("-inf")
         lp = lp + beam_scores.float().view(-1, 1)
         sc, idx = torch.topk(lp, k, dim=-1)
         return sc, idx.to(torch.int32)
     check(logits.dtype == torch.float32 and logits.is_contiguous(), "logits must be contiguous fp32")
+    if nbmax:
+        check(nbmax <= MAX_BANS, f"beam_topk_rows: at most {MAX_BANS} banned tokens per row")
+        check(bans.dtype == torch.int32 and bans.is_contiguous() and bans.shape[0] == R and bans.device == logits.device,
+              "bans must be contiguous int32 [R, n] on the logits' device")
     sc = torch.empty((R, k), dtype=torch.float32, device=logits.device)
     idx = torch.empty((R, k), dtype=torch.int32, device=logits.device)
     native().beam_topk_rows(ptr(logits), R, V, ptr(beam_scores), int(eos), int(mask_eos), int(k), ptr(sc), ptr(idx),
-                            stream_handle())
+                            stream_handle(), ptr(bans) if nbmax else 0, nbmax)
     return sc, idx

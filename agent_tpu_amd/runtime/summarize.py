@@ -113,8 +113,18 @@ def _select(logits: torch.Tensor, run_scores: torch.Tensor, K2: int, cfg, gen: G
         return sc, tk
     mask_eos = cur < gen.min_length
     br, bt = ngram_bans(run_seq.view(rows, -1)[:, :cur], gen.no_repeat_ngram_size)
-    nban = int(torch.bincount(br, minlength=rows).max()) if br.numel() else 0
+    counts = torch.bincount(br, minlength=rows) if br.numel() else None
+    nban = int(counts.max()) if counts is not None else 0
     scores_dev = run_scores.view(-1).to(logits.device)
+    if logits.is_cuda and 0 < nban <= ops.MAX_BANS:
+        # the kernel skips each row's banned tokens itself: exactly K2 per row come back
+        starts = torch.cumsum(counts, 0) - counts
+        bans = torch.full((rows, nban), -1, dtype=torch.int32)
+        bans[br, torch.arange(br.numel()) - starts[br]] = bt.to(torch.int32)
+        sc, tk = ops.beam_topk_rows(logits, scores_dev, K2, cfg.eos_id, mask_eos,
+                                    bans=bans.to(logits.device, non_blocking=False))
+        both = torch.cat([sc, tk.view(torch.float32)], 1).cpu()
+        return both[:, :K2].contiguous(), both[:, K2:].contiguous().view(torch.int32).long()
     if K2 + nban <= 16:
         sc, tk = ops.beam_topk_rows(logits, scores_dev, K2 + nban, cfg.eos_id, mask_eos)
         if sc.is_cuda:  # one D2H copy (one sync) for scores and token ids

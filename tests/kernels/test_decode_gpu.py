@@ -123,6 +123,26 @@ def test_beam_topk_rows(gpu, V, k, mask):
         assert not (idx == 1).any()
 
 
+@pytest.mark.parametrize("V,k,nb", [(50264, 8, 12), (32128, 8, 1), (4096, 3, 300)])
+def test_beam_topk_rows_bans(gpu, V, k, nb):
+    # per-row banned tokens filtered inside the kernel: equal to the CPU path, and the
+    # best raw candidates of each row are banned on purpose (so the filter must act)
+    R = 16
+    logits = _r((R, V), gpu, 3.0, torch.float32, seed=41)
+    bs = _r((R,), gpu, 1.0, torch.float32, seed=42)
+    g = torch.Generator().manual_seed(6)
+    bans = torch.randint(0, V, (R, nb), generator=g, dtype=torch.int32)
+    top = torch.topk(logits.cpu(), min(nb, 4), dim=-1).indices.to(torch.int32)
+    bans[:, :top.shape[1]] = top
+    bans[::3, -1] = -1  # padding
+    sc, idx = ops.beam_topk_rows(logits, bs, k, eos=1, mask_eos=True, bans=bans.to(gpu))
+    rsc, ridx = ops.beam_topk_rows(logits.cpu(), bs.cpu(), k, eos=1, mask_eos=True, bans=bans)
+    torch.testing.assert_close(sc.cpu(), rsc, atol=2e-4, rtol=1e-5)
+    assert torch.equal(idx.cpu(), ridx)
+    for r in range(R):
+        assert not set(idx[r].tolist()) & set(b for b in bans[r].tolist() if b >= 0)
+
+
 @pytest.mark.parametrize("M,N,K,act,res,bias", [(256, 768, 3072, None, True, False), (256, 3072, 768, "relu", False, False),
                                                 (256, 2304, 768, None, False, True), (96, 768, 768, "gelu", False, True),
                                                 (512, 768, 768, None, True, False)])
