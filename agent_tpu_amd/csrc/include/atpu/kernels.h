@@ -27,6 +27,8 @@ enum GemmEpilogue : int {
   kEpiResNorm = 128,   // R rows are raw LN inputs (beta folded into bias):
                        //   C = ... + (R*rstd - rstd*mu) * gamma     (rstd, mu from res_fin)
   kEpiStatsOut = 256,  // also write per-row partial (sum, sum of squares) of C, one per 256 columns
+  kEpiKvScatter = 1024,  // decode QKV: columns >= kv_col0 (K|V) go to the KV cache at row m*kv_T + *kv_step
+                         //   (leading dim kv_ld), columns < kv_col0 (Q) to C (128x128 / "dec" kernels)
   kEpiRowRms = 512,    // A rows are raw RMSNorm inputs (gamma folded into Bt): the kernel sums A^2
                        //   over its K loop, C = rsqrt(mean_k A^2 + rms_eps) * (A . Bt^T) ... (128x128 and
                        //   skinny "dec" kernels, no split-K; T5 decoder steps)
@@ -54,6 +56,9 @@ struct GemmArgs {
   const float* gamma = nullptr;    // ResNorm: [N] LN gamma of R
   float* part_out = nullptr;       // StatsOut: [N/256][M][2] partial (sum, sumsq) of C's rows (fp32 values)
   float rms_eps = 0.f;             // RowRms
+  bf16* kv_cache = nullptr;        // KvScatter: cache [rows * kv_T, kv_ld]
+  int kv_ld = 0, kv_T = 0, kv_col0 = 0;
+  const int32_t* kv_step = nullptr;  // device scalar: the position being written
 };
 void gemm_bf16(const GemmArgs& g, hipStream_t stream);
 // split count the library picks for an [M,N,K] problem (1 = no split-K)

@@ -46,6 +46,13 @@ __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >>
 // order (deterministic) with the epilogue fused. (An in-kernel "last block
 // reduces" fixup was measured 10x slower: the device-scope fence it needs
 // writes back the XCD's whole L2 on gfx950.)
+// KvScatter destination (decode QKV GEMM writes K|V straight into the KV cache)
+struct KvOut {
+  bf16* cache = nullptr;
+  int ld = 0, T = 0, col0 = 0;
+  const int32_t* step = nullptr;
+};
+
 // RowRms (EPI & kEpiRowRms): every lane sums the squares of the A fragments it reads
 // (v_dot2c_f32_bf16); the 4 lanes of a row (its 4 k-chunks) complete the row's sum over
 // the whole K loop, and the accumulator of that row is scaled by rsqrt(mean + eps).
@@ -65,7 +72,7 @@ template <int BM, int BN, int WM, int WN, int EPI, int SPLIT = 0>
 __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
     const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C, int ldc,
     const float* __restrict__ bias, const bf16* __restrict__ R, int ldr, int M, int N, int K,
-    float* __restrict__ ws = nullptr, float rms_eps = 0.f) {
+    float* __restrict__ ws = nullptr, float rms_eps = 0.f, KvOut kvo = {}) {
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 16;
   constexpr int TN = BN / WN / 16;
@@ -179,6 +186,7 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
   }
 
   // ---- epilogue: lane owns C[m][n..n+3] for each (i, j) fragment ----
+  const int kv_pos = (EPI & kEpiKvScatter) ? *kvo.step : 0;
   float rstd[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -220,7 +228,14 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
         bf16x4 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
-        *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
+        if (EPI & kEpiKvScatter) {
+          // the tile is all Q or all K|V (host: kv_col0 % 128 == 0)
+          bf16* dst = n >= kvo.col0 ? kvo.cache + ((size_t)m * kvo.T + kv_pos) * kvo.ld + (n - kvo.col0)
+                                    : C + (size_t)m * ldc + n;
+          *reinterpret_cast<bf16x4*>(dst) = o;
+        } else {
+          *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
+        }
       }
     }
   }
@@ -1551,7 +1566,8 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
                                                           const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C,
                                                           int ldc, const float* __restrict__ bias,
                                                           const bf16* __restrict__ R, int ldr, int M, int N, int K,
-                                                          float* __restrict__ ws, float rms_eps = 0.f) {
+                                                          float* __restrict__ ws, float rms_eps = 0.f,
+                                                          KvOut kvo = {}) {
   static_assert(!(SPLIT && (EPI & kEpiRowRms)), "RowRms needs the whole K loop in one block");
   constexpr int BM = 64, BN = 64;
   constexpr int STAGE = (BM + BN) * kRowBytes;  // 16 KiB: A rows 0-63, B rows 64-127
@@ -1652,6 +1668,7 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
     }
     return;
   }
+  const int kv_pos = (EPI & kEpiKvScatter) ? *kvo.step : 0;
   float rstd[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -1690,7 +1707,14 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
         bf16x4 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
-        *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
+        if (EPI & kEpiKvScatter) {
+          // the tile is all Q or all K|V (host: kv_col0 % 128 == 0)
+          bf16* dst = n >= kvo.col0 ? kvo.cache + ((size_t)m * kvo.T + kv_pos) * kvo.ld + (n - kvo.col0)
+                                    : C + (size_t)m * ldc + n;
+          *reinterpret_cast<bf16x4*>(dst) = o;
+        } else {
+          *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
+        }
       }
     }
   }
@@ -1706,9 +1730,12 @@ void launch_dec(const GemmArgs& g, hipStream_t s) {
 #define ATPU_DEC_CASE(E)                                                                                       \
   case E:                                                                                                      \
     hipLaunchKernelGGL((gemm_dec_kernel<E, kDecStages, 0>), grid, block, 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, \
-                       g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, nullptr, g.rms_eps);                         \
+                       g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, nullptr, g.rms_eps,                          \
+                       KvOut{g.kv_cache, g.kv_ld, g.kv_T, g.kv_col0, g.kv_step});                             \
     break;
   switch (g.epi) {
+    ATPU_DEC_CASE(kEpiRowRms | kEpiKvScatter)
+    ATPU_DEC_CASE(kEpiBias | kEpiKvScatter)
     ATPU_DEC_CASE(kEpiRowRms)
     ATPU_DEC_CASE(kEpiRowRms | kEpiRelu)
     ATPU_DEC_CASE(kEpiRowRms | kEpiOutF32)
@@ -1812,9 +1839,12 @@ void launch_tile(const GemmArgs& g, hipStream_t s) {
 #define ATPU_GEMM_CASE(E)                                                                             \
   case E:                                                                                             \
     hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, E>), grid, block, 0, s, g.A, g.lda, g.Bt, g.ldb, \
-                       g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, nullptr, g.rms_eps);             \
+                       g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, nullptr, g.rms_eps,              \
+                       KvOut{g.kv_cache, g.kv_ld, g.kv_T, g.kv_col0, g.kv_step});                     \
     break;
   switch (g.epi) {
+    ATPU_GEMM_CASE(kEpiRowRms | kEpiKvScatter)
+    ATPU_GEMM_CASE(kEpiBias | kEpiKvScatter)
     ATPU_GEMM_CASE(kEpiRowRms)
     ATPU_GEMM_CASE(kEpiRowRms | kEpiRelu)
     ATPU_GEMM_CASE(kEpiRowRms | kEpiOutF32)
@@ -1917,7 +1947,7 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
     return f ? std::atoi(f) : 0;
   }();
   if (g.splits > 1) {
-    ATPU_CHECK(!(g.epi & kEpiRowRms), "gemm: RowRms cannot split K");
+    ATPU_CHECK(!(g.epi & (kEpiRowRms | kEpiKvScatter)), "gemm: RowRms / KvScatter cannot split K");
     ATPU_CHECK(g.ws && (g.K / kBK) % g.splits == 0, "gemm: split-K needs a workspace and K/64 % splits == 0");
     launch_splitk(g, g.splits, gemm_dec_mode(-1) == 1 && skinny(g.M, g.N), stream);
     ATPU_HIP_CHECK(hipGetLastError());
@@ -1947,12 +1977,22 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
     ATPU_HIP_CHECK(hipGetLastError());
     return;
   }
-  if (g.epi & kEpiRowRms) {
+  if (g.epi & kEpiKvScatter) {
+    // decode QKV straight into the KV cache (128x128 / dec kernels; every 64- and
+    // 128-column tile must be all Q or all K|V)
+    const int fe = g.epi & ~kEpiKvScatter;
+    ATPU_CHECK(fe == kEpiRowRms || fe == kEpiBias, "gemm: unsupported KvScatter epilogue " + std::to_string(g.epi));
+    ATPU_CHECK(g.kv_cache && g.kv_step && g.kv_T > 0 && g.kv_col0 % 128 == 0 && g.kv_col0 > 0 && g.kv_col0 < g.N &&
+                   g.kv_ld >= g.N - g.kv_col0 && g.kv_ld % 4 == 0,
+               "gemm: KvScatter needs a cache, a device step, kv_col0 % 128 == 0 and kv_ld >= N - kv_col0");
+  }
+  if (g.epi & (kEpiRowRms | kEpiKvScatter)) {
     // RMSNorm folded into the GEMM (T5 decoder steps): the 128x128 and skinny kernels
     // sum the A rows' squares over their whole K loop (no split-K)
-    const int fe = g.epi & ~kEpiRowRms;
-    ATPU_CHECK(fe == 0 || fe == kEpiRelu || fe == kEpiOutF32, "gemm: unsupported RowRms epilogue " + std::to_string(g.epi));
-    ATPU_CHECK(g.rms_eps > 0.f, "gemm: RowRms needs rms_eps > 0");
+    const int fe = g.epi & ~(kEpiRowRms | kEpiKvScatter);
+    ATPU_CHECK(fe == 0 || fe == kEpiRelu || fe == kEpiOutF32 || fe == kEpiBias,
+               "gemm: unsupported RowRms / KvScatter epilogue " + std::to_string(g.epi));
+    ATPU_CHECK(!(g.epi & kEpiRowRms) || g.rms_eps > 0.f, "gemm: RowRms needs rms_eps > 0");
     if (gemm_dec_mode(-1) == 1 && skinny(g.M, g.N))
       launch_dec(g, stream);
     else

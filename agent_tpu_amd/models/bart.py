@@ -23,6 +23,7 @@ Parameter layout follows HF ``BartForConditionalGeneration`` (Linear weights
 from __future__ import annotations
 
 import dataclasses
+import os
 from dataclasses import dataclass
 from typing import Dict, Optional
 
@@ -188,6 +189,9 @@ class BartModel:
         dt = self.p["shared"].dtype
         self._type0 = torch.zeros((2, cfg.d_model), dtype=dt, device=self.device)
         self._pos_off = torch.tensor([POS_OFFSET], dtype=torch.int64, device=self.device)
+        # decode QKV GEMM writes K|V straight into the KV cache (no kv_append pass)
+        self.kv_scatter = (self.device.type == "cuda" and not fp32
+                           and os.getenv("ATPU_KV_SCATTER", "1") not in ("0", "false", "no"))
 
     def wrap_source(self, toks):
         return [self.cfg.bos_id] + list(toks) + [self.cfg.eos_id]
@@ -230,9 +234,13 @@ class BartModel:
         for i in range(cfg.dec_layers):
             q = f"dec.l{i}."
             c = cache[i]
-            qkv = ops.linear(x, p[q + "qkv_w"], p[q + "qkv_b"])
-            ops.kv_append(qkv, d, 2 * d, c, T, step)
-            ctx = ops.decode_attention(qkv[:, :d], c[:, :d], c[:, d:], H, T, 1, step=step, scale=scale, hist=hist)
+            if self.kv_scatter:  # K|V written straight into the cache by the GEMM (no kv_append)
+                qh = ops.linear(x, p[q + "qkv_w"], p[q + "qkv_b"], kv_cache=(c, T, step, d))
+            else:
+                qkv = ops.linear(x, p[q + "qkv_w"], p[q + "qkv_b"])
+                ops.kv_append(qkv, d, 2 * d, c, T, step)
+                qh = qkv[:, :d]
+            ctx = ops.decode_attention(qh, c[:, :d], c[:, d:], H, T, 1, step=step, scale=scale, hist=hist)
             x = ops.layernorm(ops.linear(ctx, p[q + "o_w"], p[q + "o_b"], residual=x), p[q + "ln1_g"],
                               p[q + "ln1_b"], cfg.eps)
             cq = ops.linear(x, p[q + "cq_w"], p[q + "cq_b"])

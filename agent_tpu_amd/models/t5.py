@@ -203,6 +203,8 @@ class T5Model:
         self.rms_fold = (self.device.type == "cuda" and not fp32
                          and os.getenv("ATPU_RMS_FOLD", "1") not in ("0", "false", "no"))
         self._rfold: Optional[Dict[str, torch.Tensor]] = None
+        self.kv_scatter = (self.device.type == "cuda" and not fp32
+                           and os.getenv("ATPU_KV_SCATTER", "1") not in ("0", "false", "no"))
 
     def rms_folded(self) -> Dict[str, torch.Tensor]:
         """Decoder weights with the preceding RMSNorm's gamma folded in (built once)."""
@@ -310,9 +312,13 @@ class T5Model:
         for i in range(cfg.dec_layers):
             q = f"dec.l{i}."
             c = cache[i]
-            qkv = ops.linear(x, f[q + "qkv"], rms_eps=eps)
-            ops.kv_append(qkv, d, 2 * d, c, T, step)
-            ctx = ops.decode_attention(qkv[:, :d], c[:, :d], c[:, d:], H, T, 1, step=step, bias_dist=dbias, hist=hist)
+            if self.kv_scatter:  # K|V written straight into the cache by the GEMM (no kv_append)
+                qh = ops.linear(x, f[q + "qkv"], rms_eps=eps, kv_cache=(c, T, step, d))
+            else:
+                qkv = ops.linear(x, f[q + "qkv"], rms_eps=eps)
+                ops.kv_append(qkv, d, 2 * d, c, T, step)
+                qh = qkv[:, :d]
+            ctx = ops.decode_attention(qh, c[:, :d], c[:, d:], H, T, 1, step=step, bias_dist=dbias, hist=hist)
             x = ops.linear(ctx, p[q + "o"], residual=x)
             cq = ops.linear(x, f[q + "cq"], rms_eps=eps)
             kv = ckv[:, i * 2 * d:(i + 1) * 2 * d]

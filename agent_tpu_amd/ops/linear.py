@@ -22,6 +22,7 @@ _ACTS = {None: 0, "none": 0, "gelu": EPI_GELU, "tanh": EPI_TANH, "relu": EPI_REL
 
 
 EPI_ROW_RMS = 512
+EPI_KV_SCATTER = 1024
 
 
 def linear_ref(x, w, bias=None, act=None, residual=None, out_f32=False, rms_eps=None):
@@ -48,13 +49,30 @@ def _splits(M: int, N: int, K: int) -> int:
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: Optional[str] = None,
            residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-           out_f32: bool = False, rms_eps: Optional[float] = None) -> torch.Tensor:
+           out_f32: bool = False, rms_eps: Optional[float] = None, kv_cache=None) -> torch.Tensor:
     """``act(x @ w.T + bias) + residual``; ``out_f32`` returns fp32 (LM-head logits).
 
     ``rms_eps``: ``x`` rows are raw RMSNorm inputs and ``w`` carries the norm's gamma
     (:func:`fold_rms_into_linear`): ``y = rsqrt(mean(x^2) + eps) * (x @ w.T)``, the row
-    statistics summed inside the GEMM's K loop (no bias / residual with it)."""
+    statistics summed inside the GEMM's K loop (no bias / residual with it).
+
+    ``kv_cache = (cache, T, step, col0)`` (decode QKV): output columns ``>= col0`` (K|V)
+    are written to ``cache[m*T + step, :]`` (``step`` a 1-element int32 device tensor),
+    the Q columns to ``out [M, col0]``, which is returned (no kv_append pass)."""
     check(act in _ACTS, f"unknown activation {act!r}")
+    if kv_cache is not None:
+        cache, T, step, col0 = kv_cache
+        N0 = w.shape[0]
+        check(residual is None and act in (None, "none") and not out_f32, "linear: kv_cache takes no residual / act")
+        check(0 < col0 < N0 and col0 % 128 == 0, "linear: kv_cache col0 must be a positive multiple of 128 below N")
+        check(cache.dim() == 2 and cache.shape[1] >= N0 - col0 and cache.shape[0] == x.shape[0] * T
+              and cache.dtype == torch.bfloat16, "linear: cache must be bf16 [M*T, >= N-col0]")
+        if not x.is_cuda:
+            y = linear_ref(x, w, bias, act, None, False, rms_eps)
+            rows = torch.arange(x.shape[0]) * T + int(step.reshape(-1)[0])
+            cache[rows, :N0 - col0] = y[:, col0:]
+            q = y[:, :col0]
+            return out.copy_(q) if out is not None else q.contiguous()
     if rms_eps is not None:
         check(bias is None and residual is None and act in (None, "none", "relu"),
               "linear: rms_eps takes no bias / residual and only a ReLU")
@@ -85,18 +103,27 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     if out_f32:
         epi |= EPI_OUT_F32
     odt = torch.float32 if out_f32 else torch.bfloat16
+    NC = kv_cache[3] if kv_cache is not None else N  # columns that land in ``out``
     if out is None:
-        out = torch.empty((M, N), dtype=odt, device=x.device)
-    check(tuple(out.shape) == (M, N) and out.dtype == odt, "out must be [M, N] of the output dtype")
+        out = torch.empty((M, NC), dtype=odt, device=x.device)
+    check(tuple(out.shape) == (M, NC) and out.dtype == odt, "out must be [M, N] of the output dtype")
     ldc = row_stride(out, "out")
-    if rms_eps is not None:
-        epi |= EPI_ROW_RMS
+    kv_args = ()
+    if kv_cache is not None:
+        cache, T, step, col0 = kv_cache
+        same_device(x, cache, step)
+        check(step.dtype == torch.int32, "linear: kv step must be an int32 device tensor")
+        epi |= EPI_KV_SCATTER
+        kv_args = (ptr(cache), row_stride(cache, "cache"), int(T), int(col0), ptr(step))
+    if rms_eps is not None or kv_cache is not None:
+        if rms_eps is not None:
+            epi |= EPI_ROW_RMS
         splits = 1
     else:
         splits = _splits(M, N, K)
     ws = torch.empty(splits * M * N, dtype=torch.float32, device=x.device) if splits > 1 else None
     native().gemm(ptr(x), lda, ptr(w), ldb, ptr(out), ldc, ptr(bias), ptr(residual), ldr, M, N, K, epi,
-                  stream_handle(), splits, ptr(ws), float(rms_eps or 0.0))
+                  stream_handle(), splits, ptr(ws), float(rms_eps or 0.0), *kv_args)
     return out
 
 

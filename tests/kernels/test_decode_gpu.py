@@ -324,3 +324,21 @@ def test_t5_step_rms_fold_matches_unfolded(gpu):
     lp = plain_m.step(tok.to(gpu), step.to(gpu), plain_m.new_cache(B, T), T, kg, lens.to(gpu), S, 1)
     assert _rel(lf, lc) < 5e-2 and _rel(lp, lc) < 5e-2
     assert _rel(lf, lp) < 3e-2
+
+
+@pytest.mark.parametrize("M,d,rms", [(1024, 768, True), (256, 1024, False), (4096, 768, True), (77, 256, False)])
+def test_gemm_kv_scatter(gpu, M, d, rms):
+    # decode QKV GEMM writing K|V into the cache row m*T + step and Q into out, vs the plain GEMM
+    T, t = 9, 5
+    x = _r((M, d), gpu, 1.0, seed=51)
+    w = _r((3 * d, d), gpu, 0.05, seed=52)
+    b = None if rms else _r((3 * d,), gpu, 0.1, torch.float32, seed=53)
+    cache = torch.zeros((M * T, 2 * d), dtype=torch.bfloat16, device=gpu)
+    step = torch.tensor([t], dtype=torch.int32, device=gpu)
+    eps = 1e-6 if rms else None
+    q = ops.linear(x, w, b, rms_eps=eps, kv_cache=(cache, T, step, d))
+    full = ops.linear(x, w, b, rms_eps=eps)
+    assert torch.equal(q, full[:, :d])
+    kv = cache.view(M, T, 2 * d)
+    assert torch.equal(kv[:, t], full[:, d:])
+    assert kv[:, :t].abs().sum().item() == 0 and kv[:, t + 1:].abs().sum().item() == 0
