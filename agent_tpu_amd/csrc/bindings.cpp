@@ -106,6 +106,7 @@ PYBIND11_MODULE(_atpu, m) {
   m.def("trace_pop", &trace_pop);
   m.def("trace_mark", [](const std::string& n) { trace_mark(n.c_str()); });
   m.def("gemm_splitk_splits", &gemm_splitk_splits, "split-K factor chosen for an [M,N,K] GEMM");
+  m.def("gemm_force_tile", &gemm_force_tile, py::arg("set") = -1, "GEMM kernel family override: 0 auto, 64, 128, 256");
   m.def("gemm_dec_mode", &gemm_dec_mode, py::arg("set") = -1,
         "skinny-M GEMM path: 1 = 64x64 multi-stage dec kernel, 0 = 128x128 split-K; returns the current");
   m.def("gemm_256_variant", &gemm_256_variant, py::arg("set") = -1,

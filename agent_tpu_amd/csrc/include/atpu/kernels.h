@@ -65,6 +65,8 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream);
 int gemm_splitk_splits(int M, int N, int K);
 // skinny-M selector (benchmarks): 1 = 64x64 multi-stage dec kernel, 0 = 128x128 split-K
 int gemm_dec_mode(int set);
+// kernel family override (benchmarks/tests): 0 auto, 64 dec, 128, 256; -1 reads
+int gemm_force_tile(int set);
 // 256x256 schedule selector (benchmarks): set >= 0 switches; returns the current
 int gemm_256_variant(int set);
 int gemm_ablate(int set);  // timing-only ablations of the persistent 256x256 kernel (results wrong); -1 reads

@@ -522,6 +522,7 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
   }();
   if (group == 1 && step_dev && !lens && row_kernel) {
     ATPU_CHECK(seq_stride <= kMaxKeys, "decode_attention: cache length above 2048");
+    ATPU_CHECK(!hist || hist_stride >= seq_stride, "decode_attention: hist rows shorter than the cache");
     ATPU_CHECK(ldo % 8 == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 && (reinterpret_cast<uintptr_t>(q) & 15) == 0,
                "decode_attention: q / out need 16-B rows");
     constexpr int NW = 4;

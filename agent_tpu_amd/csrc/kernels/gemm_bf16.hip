@@ -186,7 +186,7 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
   }
 
   // ---- epilogue: lane owns C[m][n..n+3] for each (i, j) fragment ----
-  const int kv_pos = (EPI & kEpiKvScatter) ? *kvo.step : 0;
+  const int kv_pos = (EPI & kEpiKvScatter) ? max(*kvo.step, 0) : 0;
   float rstd[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -230,9 +230,11 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
         for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
         if (EPI & kEpiKvScatter) {
           // the tile is all Q or all K|V (host: kv_col0 % 128 == 0)
-          bf16* dst = n >= kvo.col0 ? kvo.cache + ((size_t)m * kvo.T + kv_pos) * kvo.ld + (n - kvo.col0)
-                                    : C + (size_t)m * ldc + n;
-          *reinterpret_cast<bf16x4*>(dst) = o;
+          // a step past the cache (caller bug) drops the K|V write instead of writing out of bounds
+          if (n < kvo.col0)
+            *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
+          else if (kv_pos < kvo.T)
+            *reinterpret_cast<bf16x4*>(kvo.cache + ((size_t)m * kvo.T + kv_pos) * kvo.ld + (n - kvo.col0)) = o;
         } else {
           *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
         }
@@ -1668,7 +1670,7 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
     }
     return;
   }
-  const int kv_pos = (EPI & kEpiKvScatter) ? *kvo.step : 0;
+  const int kv_pos = (EPI & kEpiKvScatter) ? max(*kvo.step, 0) : 0;
   float rstd[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -1709,9 +1711,11 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
         for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
         if (EPI & kEpiKvScatter) {
           // the tile is all Q or all K|V (host: kv_col0 % 128 == 0)
-          bf16* dst = n >= kvo.col0 ? kvo.cache + ((size_t)m * kvo.T + kv_pos) * kvo.ld + (n - kvo.col0)
-                                    : C + (size_t)m * ldc + n;
-          *reinterpret_cast<bf16x4*>(dst) = o;
+          // a step past the cache (caller bug) drops the K|V write instead of writing out of bounds
+          if (n < kvo.col0)
+            *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
+          else if (kv_pos < kvo.T)
+            *reinterpret_cast<bf16x4*>(kvo.cache + ((size_t)m * kvo.T + kv_pos) * kvo.ld + (n - kvo.col0)) = o;
         } else {
           *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
         }
@@ -1887,6 +1891,16 @@ int gemm_256_variant(int set) {
   return v;
 }
 
+int gemm_force_tile(int set) {
+  // kernel family override (benchmarks / tests): 0 = auto, 64 = skinny "dec", 128, 256; ATPU_GEMM_TILE
+  static int v = [] {
+    const char* f = std::getenv("ATPU_GEMM_TILE");
+    return f ? std::atoi(f) : 0;
+  }();
+  if (set >= 0) v = set;
+  return v;
+}
+
 int gemm_dec_mode(int set) {
   // skinny-M path: 1 = 64x64 multi-stage "dec" kernel (default), 0 = 128x128 split-K; ATPU_GEMM_DEC=0|1
   static int v = [] {
@@ -1899,7 +1913,13 @@ int gemm_dec_mode(int set) {
 
 namespace {
 // problems the 128x128 grid would leave under two blocks per CU
-bool skinny(int M, int N) { return M <= 2048 && ((M + 127) / 128) * ((N + 127) / 128) < 512; }
+// Kernel family by how well each fills the 256 CUs (tools/bench_tile_choice.py, decode
+// shapes at M = 1024 / 2048 / 4096): the 64x64 "dec" kernel while the 128x128 grid is
+// small, the 128x128 kernel above that, the persistent 256x256 kernel once it has at
+// more than half a tile per CU (e.g. N = 768 at M = 4096 is 48 tiles: 20 us there, 13.7 us
+// on 128x128; at M = 2048 the dec kernel takes 8.7 us).
+bool skinny(int M, int N) { return ((M + 127) / 128) * ((N + 127) / 128) < (M <= 1024 ? 512 : 192); }
+bool big_fills(int M, int N) { return 2 * ((M + 255) / 256) * (N / 256) > num_cus(); }
 }  // namespace
 
 int gemm_splitk_splits(int M, int N, int K) {
@@ -1942,10 +1962,7 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
   // 256x256 full-line-staged kernel once the grid fills the chip several
   // times over; the 128x128 kernel (2 blocks/CU) covers small M and odd N.
   // ATPU_GEMM_TILE=128|256 forces one (benchmarks/tests).
-  static const int forced = [] {
-    const char* f = std::getenv("ATPU_GEMM_TILE");
-    return f ? std::atoi(f) : 0;
-  }();
+  const int forced = gemm_force_tile(-1);
   if (g.splits > 1) {
     ATPU_CHECK(!(g.epi & (kEpiRowRms | kEpiKvScatter)), "gemm: RowRms / KvScatter cannot split K");
     ATPU_CHECK(g.ws && (g.K / kBK) % g.splits == 0, "gemm: split-K needs a workspace and K/64 % splits == 0");
@@ -1993,14 +2010,15 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
     ATPU_CHECK(fe == 0 || fe == kEpiRelu || fe == kEpiOutF32 || fe == kEpiBias,
                "gemm: unsupported RowRms / KvScatter epilogue " + std::to_string(g.epi));
     ATPU_CHECK(!(g.epi & kEpiRowRms) || g.rms_eps > 0.f, "gemm: RowRms needs rms_eps > 0");
-    if (gemm_dec_mode(-1) == 1 && skinny(g.M, g.N))
+    if (forced == 64 || (forced != 128 && gemm_dec_mode(-1) == 1 && skinny(g.M, g.N)))
       launch_dec(g, stream);
     else
       launch_tile<128, 128, 2, 2>(g, stream);
     ATPU_HIP_CHECK(hipGetLastError());
     return;
   }
-  const bool use_big = !(g.epi & kEpiOutF32) && (forced ? (forced == 256 && big_ok) : (g.M >= 2048 && big_ok));
+  const bool use_big = !(g.epi & kEpiOutF32) &&
+                       (forced ? (forced == 256 && big_ok) : (g.M >= 2048 && big_ok && big_fills(g.M, g.N)));
   // 256s counts its epilogue's stores in the next tile's waits: whole row tiles only
   const bool persistent_ok = g.M % 256 == 0;
   if (use_big && persistent_ok && kernel256 >= 2) {
@@ -2011,7 +2029,7 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
     launch_256p(g, stream);
   else if (use_big)
     launch_256b(g, stream);
-  else if (!forced && gemm_dec_mode(-1) == 1 && skinny(g.M, g.N))
+  else if ((forced == 64 || (!forced && gemm_dec_mode(-1) == 1 && skinny(g.M, g.N))))
     launch_dec(g, stream);
   else
     launch_tile<128, 128, 2, 2>(g, stream);
