@@ -137,6 +137,11 @@ PYBIND11_MODULE(_atpu, m) {
                      P<const int32_t>(lens), P<const int32_t>(step_dev), P<const int32_t>(hist), hist_stride,
                      P<const float>(bias), bias_stride, P<bf16>(out), ldo, rows, H, scale, S(stream));
   });
+  m.def("beam_select", [](uintptr_t sc, uintptr_t tk, int B, int nb, int K2, int V, int eos, int hit_all, float neg,
+                          uintptr_t stage, uintptr_t rec, uintptr_t stream) {
+    beam_select(P<const float>(sc), P<const int32_t>(tk), B, nb, K2, V, eos, hit_all, neg, P<int32_t>(stage),
+                P<int32_t>(rec), S(stream));
+  });
   m.def("beam_reorder_hist", [](uintptr_t src, uintptr_t dst, uintptr_t parent, int rows, int stride,
                                 uintptr_t step_dev, uintptr_t stream) {
     beam_reorder_hist(P<const int32_t>(src), P<int32_t>(dst), P<const int32_t>(parent), rows, stride,

@@ -88,6 +88,10 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
                       const float* bias_dist, int bias_stride, bf16* out, int ldo, int rows, int H, float scale,
                       hipStream_t stream);
 // dst[r][j] = src[parent[r]][j] (j < t), dst[r][t] = parent[r]; t = *step_dev
+// device beam selection (runtime/summarize.py): item top-K2 over its beams' candidates, hits,
+// next running beams -> stage [parents | tokens | score bits] and a host record per item
+void beam_select(const float* sc, const int32_t* tk, int B, int nb, int K2, int V, int eos, int hit_all, float neg,
+                 int32_t* stage, int32_t* rec, hipStream_t stream);
 void beam_reorder_hist(const int32_t* src, int32_t* dst, const int32_t* parent, int rows, int stride,
                        const int32_t* step_dev, hipStream_t stream);
 void kv_append(const bf16* src, int lds, int col0, int ncols, bf16* cache, int seq_stride, int ldc,

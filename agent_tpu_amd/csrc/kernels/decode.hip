@@ -504,6 +504,74 @@ __global__ __launch_bounds__(kTopkThreads) void beam_topk_kernel(const float* __
   }
 }
 
+// ----------------------------------------------------------------------------
+// Beam selection on the device (one workgroup per batch item): from each beam
+// row's top K2 continuations (beam_topk_rows) pick the item's global top K2 by
+// (score desc, beam*V + token asc), mark hits (EOS, or the last position), keep
+// the best nb non-hits (stable) as the next running beams and write the next
+// step's inputs straight into the device staging row [parent rows | tokens |
+// running scores]. The host gets a per-item record [top score bits K2 | top
+// tokens K2 | top beams K2 | kept slots nb] by async D2H for its finished-
+// hypothesis bookkeeping, so the next decoder step is enqueued without a host
+// round trip (runtime/summarize.py, device selection).
+// ----------------------------------------------------------------------------
+constexpr int kSelMax = 256;  // nb * K2 candidates per item
+__global__ __launch_bounds__(kSelMax) void beam_select_kernel(const float* __restrict__ sc,
+                                                              const int32_t* __restrict__ tk, int nb, int K2, int V,
+                                                              int eos, int hit_all, float neg,
+                                                              int32_t* __restrict__ stage, int rows,
+                                                              int32_t* __restrict__ rec) {
+  __shared__ float cs[kSelMax];
+  __shared__ long long cf[kSelMax];
+  __shared__ int ctok[kSelMax];
+  __shared__ float ts[kSelMax];
+  __shared__ int tt[kSelMax], tb[kSelMax];
+  __shared__ float rc[kSelMax];
+  const int b = blockIdx.x, c = threadIdx.x, n = nb * K2;
+  if (c < n) {
+    const size_t src = (size_t)b * n + c;  // rows b*nb .. b*nb+nb-1, K2 each: contiguous
+    cs[c] = sc[src];
+    ctok[c] = tk[src];
+    cf[c] = (long long)(c / K2) * V + tk[src];
+  }
+  __syncthreads();
+  if (c < n) {
+    const float s = cs[c];
+    const long long f = cf[c];
+    int rank = 0;
+    // (score desc, flat asc, candidate index asc): np.lexsort's order, total even for
+    // duplicate (score, token) pairs
+    for (int o = 0; o < n; ++o) rank += (cs[o] > s || (cs[o] == s && (cf[o] < f || (cf[o] == f && o < c)))) ? 1 : 0;
+    if (rank < K2) {
+      ts[rank] = s;
+      tt[rank] = ctok[c];
+      tb[rank] = c / K2;
+    }
+  }
+  __syncthreads();
+  if (c < K2) {
+    const bool hit = hit_all || tt[c] == eos;
+    rc[c] = hit ? ts[c] + neg : ts[c];
+  }
+  __syncthreads();
+  int32_t* r = rec + (size_t)b * (3 * K2 + nb);
+  if (c < K2) {
+    const float x = rc[c];
+    int rank = 0;
+    for (int o = 0; o < K2; ++o) rank += (rc[o] > x || (rc[o] == x && o < c)) ? 1 : 0;
+    if (rank < nb) {
+      const int row = b * nb + rank;
+      stage[row] = b * nb + tb[c];
+      stage[rows + row] = tt[c];
+      stage[2 * rows + row] = __float_as_int(x);
+      r[3 * K2 + rank] = c;
+    }
+    r[c] = __float_as_int(ts[c]);
+    r[K2 + c] = tt[c];
+    r[2 * K2 + c] = tb[c];
+  }
+}
+
 }  // namespace
 
 void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int ldkv, int seq_stride, int group,
@@ -592,6 +660,14 @@ void beam_topk_rows(const float* logits, int rows, int V, const float* beam_scor
     default: break;
   }
 #undef ATPU_TK
+  ATPU_HIP_CHECK(hipGetLastError());
+}
+
+void beam_select(const float* sc, const int32_t* tk, int B, int nb, int K2, int V, int eos, int hit_all, float neg,
+                 int32_t* stage, int32_t* rec, hipStream_t stream) {
+  ATPU_CHECK(B > 0 && nb >= 1 && K2 >= nb && nb * K2 <= kSelMax, "beam_select: need nb <= K2 and nb*K2 <= 256");
+  hipLaunchKernelGGL(beam_select_kernel, dim3(B), dim3(kSelMax), 0, stream, sc, tk, nb, K2, V, eos, hit_all, neg,
+                     stage, B * nb, rec);
   ATPU_HIP_CHECK(hipGetLastError());
 }
 

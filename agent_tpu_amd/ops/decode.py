@@ -15,10 +15,12 @@ from __future__ import annotations
 import math
 from typing import Optional, Tuple
 
+import numpy as np
+
 import torch
 
 from .._native import native, ptr, stream_handle
-from ._util import check, check_bf16_dev, row_stride
+from ._util import check, check_bf16_dev, row_stride, same_device
 
 HEAD_DIM = 64
 
@@ -152,3 +154,59 @@ def beam_topk_rows(logits: torch.Tensor, beam_scores: torch.Tensor, k: int, eos:
     native().beam_topk_rows(ptr(logits), R, V, ptr(beam_scores), int(eos), int(mask_eos), int(k), ptr(sc), ptr(idx),
                             stream_handle(), ptr(bans) if nbmax else 0, nbmax)
     return sc, idx
+
+
+def beam_select_ref(sc: np.ndarray, tk: np.ndarray, nb: int, V: int, eos: int, hit_all: bool, neg: float):
+    """Host reference of the device beam selection for ``B`` items.
+
+    ``sc``/``tk`` [B*nb, K2]: each beam row's top continuations (accumulated score, token).
+    Returns ``(top_sc [B,K2] f32, top_tok [B,K2], top_beam [B,K2], nxt [B,nb])``: the item's top K2 by
+    (score desc, beam*V + token asc), and the K2 slots of the next running beams (best nb after hits
+    get ``+neg``, stable)."""
+    rows, K2 = sc.shape
+    B = rows // nb
+    s = np.ascontiguousarray(sc, dtype=np.float32).reshape(B, nb * K2)
+    t = np.asarray(tk).astype(np.int64).reshape(B, nb * K2)
+    beam_of = np.broadcast_to(np.repeat(np.arange(nb, dtype=np.int64), K2)[None, :], (B, nb * K2))
+    rb = np.arange(B)[:, None]
+    order = np.lexsort((beam_of * V + t, -s), axis=1)[:, :K2]
+    top_sc, top_tok, top_beam = s[rb, order], t[rb, order], beam_of[rb, order]
+    hits = (top_tok == eos) | bool(hit_all)
+    run_cand = np.where(hits, top_sc + np.float32(neg), top_sc)
+    nxt = np.argsort(-run_cand, axis=1, kind="stable")[:, :nb]
+    return top_sc, top_tok, top_beam, nxt
+
+
+def beam_select(sc: torch.Tensor, tk: torch.Tensor, nb: int, V: int, eos: int, hit_all: bool, neg: float,
+                stage: torch.Tensor, rec: torch.Tensor) -> None:
+    """Device beam selection (kernel ``beam_select_kernel``) for ``B = rows / nb`` items.
+
+    Writes the next step's inputs into ``stage`` (int32 [3*rows]: parent rows | tokens | running-score
+    bits) and per item ``rec`` (int32 [B, 3*K2 + nb]: top score bits | top tokens | top beams | kept
+    slots) — the values of :func:`beam_select_ref`."""
+    rows, K2 = sc.shape
+    B = rows // nb
+    check(rows % nb == 0 and K2 >= nb and tuple(tk.shape) == (rows, K2), "beam_select: sc/tk must be [B*nb, K2]")
+    check(stage.numel() == 3 * rows and stage.dtype == torch.int32 and stage.is_contiguous(), "stage: int32 [3*rows]")
+    check(tuple(rec.shape) == (B, 3 * K2 + nb) and rec.dtype == torch.int32 and rec.is_contiguous(),
+          "rec: int32 [B, 3*K2 + nb]")
+    if not sc.is_cuda:
+        top_sc, top_tok, top_beam, nxt = beam_select_ref(sc.numpy(), tk.numpy(), nb, V, eos, hit_all, neg)
+        rb = np.arange(B)[:, None]
+        hits = (top_tok == eos) | bool(hit_all)
+        run_cand = np.where(hits, top_sc + np.float32(neg), top_sc)
+        st = stage.numpy()
+        st[:rows] = (rb * nb + top_beam[rb, nxt]).reshape(-1)
+        st[rows:2 * rows] = top_tok[rb, nxt].reshape(-1)
+        st[2 * rows:] = run_cand[rb, nxt].astype(np.float32).reshape(-1).view(np.int32)
+        r = rec.numpy()
+        r[:, :K2] = top_sc.astype(np.float32).view(np.int32)
+        r[:, K2:2 * K2] = top_tok
+        r[:, 2 * K2:3 * K2] = top_beam
+        r[:, 3 * K2:] = nxt
+        return
+    check(sc.dtype == torch.float32 and tk.dtype == torch.int32 and sc.is_contiguous() and tk.is_contiguous(),
+          "beam_select: sc fp32 / tk int32, contiguous")
+    same_device(sc, tk, stage, rec)
+    native().beam_select(ptr(sc), ptr(tk), B, nb, K2, int(V), int(eos), int(bool(hit_all)), float(neg), ptr(stage),
+                         ptr(rec), stream_handle())

@@ -41,6 +41,8 @@ from ..tokenizer import pack_rows
 from ..utils.trace import span
 
 NEG = -1.0e9
+# host-side step timing (tools/host_prof_summ.py): a dict to accumulate into, or None
+HOST_PROF: Optional[Dict[str, float]] = None
 
 
 @dataclass
@@ -54,6 +56,7 @@ class GenConfig:
     forced_bos_id: Optional[int] = None  # None -> model default (bart-large-cnn 0)
     forced_eos_id: Optional[int] = None  # None -> model default (bart-large-cnn 2)
     use_graph: bool = True  # replay the decoder step as one hipGraph (device runs only)
+    device_select: bool = True  # beam selection on the device, host bookkeeping one step behind
 
     def resolved(self, cfg) -> "GenConfig":
         def pick(v, name, default):
@@ -63,7 +66,7 @@ class GenConfig:
                          float(pick(self.length_penalty, "length_penalty", 1.0)), self.early_stopping,
                          int(pick(self.no_repeat_ngram_size, "no_repeat_ngram_size", 0) or 0),
                          pick(self.forced_bos_id, "forced_bos_id", None),
-                         pick(self.forced_eos_id, "forced_eos_id", None), self.use_graph)
+                         pick(self.forced_eos_id, "forced_eos_id", None), self.use_graph, self.device_select)
 
 
 def ngram_bans(seq: torch.Tensor, n: int) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -94,10 +97,12 @@ class GenResult:
 
 
 def _select(logits: torch.Tensor, run_scores: torch.Tensor, K2: int, cfg, gen: GenConfig, cur: int, T: int,
-            run_seq: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+            run_seq: torch.Tensor, scores_dev: Optional[torch.Tensor] = None,
+            on_device: bool = False, bans_buf=None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Per beam row: the top ``K2`` continuations ``(score [rows, K2], token [rows, K2])``
     after log-softmax and the logits processors (min-length EOS mask, n-gram bans,
-    forced BOS/EOS), on the host."""
+    forced BOS/EOS), on the host; ``on_device``: left on the logits' device (fp32 /
+    int32, for :func:`ops.beam_select`), no D2H."""
     rows, V = logits.shape
     forced = None
     if gen.forced_bos_id is not None and cur == 1:
@@ -110,23 +115,39 @@ def _select(logits: torch.Tensor, run_scores: torch.Tensor, K2: int, cfg, gen: G
         tk = torch.arange(K2).view(1, -1).expand(rows, -1).clone()
         tk[:, 1:] += (tk[:, 1:] >= forced).long()  # placeholders distinct from the forced token
         tk[:, 0] = forced
+        if on_device:
+            return sc.to(logits.device), tk.to(device=logits.device, dtype=torch.int32)
         return sc, tk
     mask_eos = cur < gen.min_length
     br, bt = ngram_bans(run_seq.view(rows, -1)[:, :cur], gen.no_repeat_ngram_size)
     counts = torch.bincount(br, minlength=rows) if br.numel() else None
     nban = int(counts.max()) if counts is not None else 0
-    scores_dev = run_scores.view(-1).to(logits.device)
+    if scores_dev is None:  # the caller keeps a device copy of the running scores when it can
+        scores_dev = run_scores.view(-1).to(logits.device)
     if logits.is_cuda and 0 < nban <= ops.MAX_BANS:
         # the kernel skips each row's banned tokens itself: exactly K2 per row come back
         starts = torch.cumsum(counts, 0) - counts
-        bans = torch.full((rows, nban), -1, dtype=torch.int32)
+        if bans_buf is not None:  # (pinned host, device) staging: async H2D, nothing waits for it
+            bh, bd = bans_buf
+            bans = bh[:rows * nban].view(rows, nban)
+            bans.fill_(-1)
+        else:
+            bans = torch.full((rows, nban), -1, dtype=torch.int32)
         bans[br, torch.arange(br.numel()) - starts[br]] = bt.to(torch.int32)
-        sc, tk = ops.beam_topk_rows(logits, scores_dev, K2, cfg.eos_id, mask_eos,
-                                    bans=bans.to(logits.device, non_blocking=False))
+        if bans_buf is not None:
+            bans_dev = bd[:rows * nban].view(rows, nban)
+            bans_dev.copy_(bans, non_blocking=True)
+        else:
+            bans_dev = bans.to(logits.device)
+        sc, tk = ops.beam_topk_rows(logits, scores_dev, K2, cfg.eos_id, mask_eos, bans=bans_dev)
+        if on_device:
+            return sc, tk
         both = torch.cat([sc, tk.view(torch.float32)], 1).cpu()
         return both[:, :K2].contiguous(), both[:, K2:].contiguous().view(torch.int32).long()
     if K2 + nban <= 16:
         sc, tk = ops.beam_topk_rows(logits, scores_dev, K2 + nban, cfg.eos_id, mask_eos)
+        if on_device and nban == 0:
+            return sc, tk
         if sc.is_cuda:  # one D2H copy (one sync) for scores and token ids
             both = torch.cat([sc, tk.view(torch.float32)], 1).cpu()
             sc, tk = both[:, :K2 + nban].contiguous(), both[:, K2 + nban:].contiguous().view(torch.int32).long()
@@ -149,6 +170,8 @@ def _select(logits: torch.Tensor, run_scores: torch.Tensor, K2: int, cfg, gen: G
         lp[:, cfg.eos_id] = float("-inf")
     lp[br.to(lp.device), bt.to(lp.device)] = float("-inf")
     sc, tk = torch.topk(lp + scores_dev.view(-1, 1), K2, dim=-1)
+    if on_device:
+        return sc.contiguous(), tk.to(torch.int32).contiguous()
     return sc.cpu(), tk.cpu().long()
 
 
@@ -192,13 +215,18 @@ def generate(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfi
     unsat = np.ones((B, 1), dtype=bool)
     top_mask = np.arange(K2) < nb
     rowsB = np.arange(B)[:, None]
-    beam_of0 = np.broadcast_to(np.repeat(np.arange(nb, dtype=np.int64), K2)[None, :], (B, nb * K2))
     neg = np.float32(NEG)
     tokens = torch.full((rows,), cfg.decoder_start_id, dtype=torch.int32, device=dev)
     pin = dev.type == "cuda"
-    par_host = torch.empty(rows, dtype=torch.int32, pin_memory=pin)
-    tok_host = torch.empty(rows, dtype=torch.int32, pin_memory=pin)
-    par_dev = torch.empty(rows, dtype=torch.int32, device=dev)
+    # one pinned staging row per step: [parent rows | new tokens | running beam scores]
+    # -> ONE async H2D; everything after it (history reorder, token copy, step advance,
+    # decoder step) is a single graph replay, and the next top-k finds the beam scores
+    # already on the device (no synchronous pageable copy in front of it)
+    stage_host = torch.empty(3 * rows, dtype=torch.int32, pin_memory=pin)
+    stage_dev = torch.zeros(3 * rows, dtype=torch.int32, device=dev)
+    par_dev, tok_dev = stage_dev[:rows], stage_dev[rows:2 * rows]
+    score_dev = stage_dev[2 * rows:].view(torch.float32)
+    score_dev.copy_(torch.from_numpy(run_scores.reshape(-1)).to(dev))
     lp = float(gen.length_penalty)
     # Every step input is a static device buffer (tokens, step, cache, hist), so
     # after one eager step the whole decoder step (~13 launches x L layers) is
@@ -206,55 +234,37 @@ def generate(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfi
     use_graph = gen.use_graph and dev.type == "cuda"
     graph, g_logits = None, None
 
-    def launch(length: int) -> torch.Tensor:
-        """Enqueue the decoder step for sequence length ``length`` -> logits."""
+    def advance() -> torch.Tensor:
+        """Histories follow their parent beams (backpointers, no KV copy), new tokens in,
+        position + 1, decoder step -> logits. Static buffers only (graph-capturable)."""
+        ops.beam_reorder_hist(hist, hist_alt, par_dev, step_dev)
+        hist.copy_(hist_alt)  # keep the captured buffer address
+        tokens.copy_(tok_dev)
+        step_dev.add_(1)
+        return model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist)
+
+    def launch_next() -> torch.Tensor:
         nonlocal graph, g_logits
-        step_dev.fill_(length - 1)
         if graph is not None:
             graph.replay()
             return g_logits
-        out = model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist)
+        out = advance()
         if use_graph:
+            # capture records without executing: the state stays at the eager step's
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
-                g_logits = model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist)
+                g_logits = advance()
         return out
 
-    cur = 1  # sequence length so far (decoder start token included)
-    steps = 0
-    logits = launch(cur)
-    while True:
-        with span("beam_select"):
-            sc_t, tk_t = _select(logits, torch.from_numpy(run_scores), K2, cfg, gen, cur, T,
-                                 torch.from_numpy(run_seq))
-        sc = sc_t.numpy().reshape(B, nb * K2)
-        tk = tk_t.numpy().astype(np.int64, copy=False).reshape(B, nb * K2)
-        steps += 1
-        # global top-K2 per item, ties -> lower flat index (beam * V + token),
-        # like torch.topk over the item's [nb * V] scores: score desc, flat asc
-        order = np.lexsort((beam_of0 * V + tk, -sc), axis=1)[:, :K2]
-        top_sc, top_tok, top_beam = sc[rowsB, order], tk[rowsB, order], beam_of0[rowsB, order]
+    def apply(cur: int, top_sc, top_tok, top_beam, nxt) -> bool:
+        """Fold step ``cur``'s selection into the host state (sequences, finished
+        hypotheses); True when the search is over (HF's stopping rules)."""
+        nonlocal run_seq, run_alt, run_scores, fin_seq, fin_scores, fin_done, fin_len, unsat
         hits = (top_tok == cfg.eos_id) | (cur + 1 >= T)
-
-        # running beams for the next step: best nb non-hit continuations
         run_cand = np.where(hits, top_sc + neg, top_sc)
-        nxt = np.argsort(-run_cand, axis=1, kind="stable")[:, :nb]
         parent = top_beam[rowsB, nxt]  # beam index within the item
         new_tok = top_tok[rowsB, nxt]
         run_scores = run_cand[rowsB, nxt]
-
-        if cur + 1 < T:
-            # enqueue step cur+1 NOW: histories follow their parent beams
-            # (backpointers, no KV copy), new tokens, decoder-step graph
-            par_host.numpy()[:] = (rowsB * nb + parent).reshape(-1)
-            tok_host.numpy()[:] = new_tok.reshape(-1)
-            par_dev.copy_(par_host, non_blocking=True)
-            tokens.copy_(tok_host, non_blocking=True)
-            ops.beam_reorder_hist(hist, hist_alt, par_dev, step_dev)
-            hist.copy_(hist_alt)  # keep the captured buffer address
-            logits = launch(cur + 1)
-
-        # ---- under the GPU step: sequences, finished hypotheses, early stop ----
         prev_seq, run_seq = run_seq, run_alt
         run_alt = prev_seq
         run_seq[:, :, :cur] = prev_seq[rowsB, parent, :cur]
@@ -275,17 +285,96 @@ def generate(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfi
         fin_scores = m_sc[rowsB, keep]
         fin_done = np.where(from_fin, fin_done[rowsB, np.minimum(keep, nb - 1)], did[rowsB, kc])
         fin_len = np.where(from_fin, fin_len[rowsB, np.minimum(keep, nb - 1)], cur + 1)
-
-        cur += 1
-        if cur >= T:
-            break
+        if cur + 1 >= T:
+            return True
         # early-stop heuristic (early_stopping=True: best running at current length)
-        best_run = run_scores[:, :1] / np.float32(float(cur - 1) ** lp)
+        best_run = run_scores[:, :1] / np.float32(float(cur) ** lp)
         worst_fin = np.where(fin_done, fin_scores.min(axis=1, keepdims=True), neg)
         unsat = unsat & (best_run > worst_fin).any(axis=1, keepdims=True)
         open_beam = not (bool(fin_done.all()) and bool(gen.early_stopping))
-        if not (bool(unsat.any()) and open_beam and not bool(hits.all())):
-            break
+        return not (bool(unsat.any()) and open_beam and not bool(hits.all()))
+
+    def prof(tp0, tp1, tp2):
+        if HOST_PROF is not None:  # (select incl. the wait for the GPU, select -> next launch, after launch)
+            tp3 = time.perf_counter()
+            for key, dt in (("select", tp1 - tp0), ("to_launch", tp2 - tp1), ("after_launch", tp3 - tp2)):
+                HOST_PROF[key] = HOST_PROF.get(key, 0.0) + dt
+            HOST_PROF["steps"] = HOST_PROF.get("steps", 0) + 1
+
+    cur = 1  # sequence length so far (decoder start token included)
+    steps = 0
+    step_dev.fill_(0)
+    logits = model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist)
+    if pin and gen.device_select:
+        # Device selection: top-k -> beam_select -> next decoder step are enqueued back to
+        # back; the host folds step t's record into its state while the GPU runs step t+1
+        # (the sequences it needs for step t+1's n-gram bans are complete by then).
+        rec_dev = torch.empty((B, 3 * K2 + nb), dtype=torch.int32, device=dev)
+        rec_host = torch.empty((B, 3 * K2 + nb), dtype=torch.int32, pin_memory=True)
+        rec_ev = torch.cuda.Event()
+        # n-gram ban staging (free again once the previous step's record event has passed)
+        bans_buf = ((torch.empty(rows * ops.MAX_BANS, dtype=torch.int32, pin_memory=True),
+                     torch.empty(rows * ops.MAX_BANS, dtype=torch.int32, device=dev))
+                    if gen.no_repeat_ngram_size else None)
+        pending = None
+        while True:
+            tp0 = time.perf_counter()
+            if pending is not None:
+                rec_ev.synchronize()
+                r = rec_host.numpy()
+                rs = (r[:, :K2].copy().view(np.float32), r[:, K2:2 * K2].astype(np.int64),
+                      r[:, 2 * K2:3 * K2].astype(np.int64), r[:, 3 * K2:].astype(np.int64))
+                steps += 1
+                if apply(pending, *rs):
+                    break
+            tp1 = time.perf_counter()
+            with span("beam_select"):
+                sc_d, tk_d = _select(logits, torch.from_numpy(run_scores), K2, cfg, gen, cur, T,
+                                     torch.from_numpy(run_seq), scores_dev=score_dev, on_device=True,
+                                     bans_buf=bans_buf)
+                ops.beam_select(sc_d, tk_d, nb, V, cfg.eos_id, cur + 1 >= T, NEG, stage_dev, rec_dev)
+                rec_host.copy_(rec_dev, non_blocking=True)
+                rec_ev.record()
+            pending = cur
+            if cur + 1 < T:
+                logits = launch_next()
+            tp2 = time.perf_counter()
+            prof(tp0, tp1, tp2)
+            cur += 1
+            if cur >= T:  # the last selection: fold it in and stop
+                rec_ev.synchronize()
+                r = rec_host.numpy()
+                steps += 1
+                apply(pending, r[:, :K2].copy().view(np.float32), r[:, K2:2 * K2].astype(np.int64),
+                      r[:, 2 * K2:3 * K2].astype(np.int64), r[:, 3 * K2:].astype(np.int64))
+                break
+    else:
+        while True:
+            tp0 = time.perf_counter()
+            with span("beam_select"):
+                sc_t, tk_t = _select(logits, torch.from_numpy(run_scores), K2, cfg, gen, cur, T,
+                                     torch.from_numpy(run_seq), scores_dev=score_dev if pin else None)
+            tp1 = time.perf_counter()
+            top_sc, top_tok, top_beam, nxt = ops.beam_select_ref(sc_t.numpy(), tk_t.numpy(), nb, V, cfg.eos_id,
+                                                                 cur + 1 >= T, NEG)
+            steps += 1
+            if cur + 1 < T:
+                # enqueue step cur+1 NOW (the staging row is free: the top-k D2H of this
+                # step synchronised past its previous H2D)
+                hits = (top_tok == cfg.eos_id) | (cur + 1 >= T)
+                run_cand = np.where(hits, top_sc + neg, top_sc)
+                st = stage_host.numpy()
+                st[:rows] = (rowsB * nb + top_beam[rowsB, nxt]).reshape(-1)
+                st[rows:2 * rows] = top_tok[rowsB, nxt].reshape(-1)
+                st[2 * rows:] = run_cand[rowsB, nxt].reshape(-1).view(np.int32)
+                stage_dev.copy_(stage_host, non_blocking=True)
+                logits = launch_next()
+            tp2 = time.perf_counter()
+            stop = apply(cur, top_sc, top_tok, top_beam, nxt)  # under the GPU step
+            prof(tp0, tp1, tp2)
+            cur += 1
+            if stop:
+                break
     t_dec = time.perf_counter()
     seqs = [fin_seq[b, 0, :int(fin_len[b, 0])].tolist() for b in range(B)]
     scores = [float(fin_scores[b, 0]) for b in range(B)]

@@ -342,3 +342,40 @@ def test_gemm_kv_scatter(gpu, M, d, rms):
     kv = cache.view(M, T, 2 * d)
     assert torch.equal(kv[:, t], full[:, d:])
     assert kv[:, :t].abs().sum().item() == 0 and kv[:, t + 1:].abs().sum().item() == 0
+
+
+@pytest.mark.parametrize("B,nb,K2", [(7, 4, 8), (64, 4, 8), (3, 8, 16), (5, 1, 2)])
+def test_beam_select_kernel(gpu, B, nb, K2):
+    # device beam selection vs the host reference, with many exact score ties (the
+    # (score desc, beam*V + token asc) order and the stable non-hit ranking must agree)
+    V, eos = 1000, 1
+    g = torch.Generator().manual_seed(B * 10 + nb)
+    sc = (torch.randint(-6, 1, (B * nb, K2), generator=g).float() * 0.5).contiguous()
+    tk = torch.randint(0, 40, (B * nb, K2), generator=g, dtype=torch.int32)
+    tk[::3, 0] = eos
+    for hit_all in (False, True):
+        st_g = torch.zeros(3 * B * nb, dtype=torch.int32, device=gpu)
+        rec_g = torch.zeros((B, 3 * K2 + nb), dtype=torch.int32, device=gpu)
+        ops.beam_select(sc.to(gpu), tk.to(gpu), nb, V, eos, hit_all, -1e9, st_g, rec_g)
+        st_c = torch.zeros(3 * B * nb, dtype=torch.int32)
+        rec_c = torch.zeros((B, 3 * K2 + nb), dtype=torch.int32)
+        ops.beam_select(sc, tk, nb, V, eos, hit_all, -1e9, st_c, rec_c)
+        assert torch.equal(rec_g.cpu(), rec_c) and torch.equal(st_g.cpu(), st_c)
+
+
+@pytest.mark.parametrize("family", ["t5-tiny", "bart-tiny"])
+def test_generate_device_select_matches_host(gpu, family):
+    # the device-selection beam loop (host bookkeeping one step behind) returns exactly the
+    # host-selection loop's sequences and scores (BART: n-gram bans, forced BOS/EOS)
+    from agent_tpu_amd.runtime.summarize import GenConfig, build_model, generate
+
+    model, _ = build_model(family, device=gpu, seed=3)
+    g = torch.Generator().manual_seed(7)
+    B, S = 5, 32
+    ids = torch.randint(5, model.cfg.vocab_size, (B, S), generator=g, dtype=torch.int32)
+    lens = torch.tensor([32, 20, 31, 9, 27], dtype=torch.int32)
+    for ml in (24, 40):
+        a = generate(model, ids.to(gpu), lens.to(gpu), GenConfig(num_beams=4, max_length=ml, min_length=5))
+        b = generate(model, ids.to(gpu), lens.to(gpu),
+                     GenConfig(num_beams=4, max_length=ml, min_length=5, device_select=False))
+        assert a.sequences == b.sequences and a.scores == b.scores and a.steps == b.steps
