@@ -348,6 +348,9 @@ def generate(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfi
                 apply(pending, r[:, :K2].copy().view(np.float32), r[:, K2:2 * K2].astype(np.int64),
                       r[:, 2 * K2:3 * K2].astype(np.int64), r[:, 3 * K2:].astype(np.int64))
                 break
+        # an early stop leaves the speculatively launched step in flight: let it drain
+        # before its graph and buffers go out of scope
+        torch.cuda.current_stream(dev).synchronize()
     else:
         while True:
             tp0 = time.perf_counter()
