@@ -417,19 +417,28 @@ __global__ __launch_bounds__(kTopkThreads) void beam_topk_kernel(const float* __
   // only (HF applies MinLengthLogitsProcessor after log_softmax).
   // 16-B loads, 4 per thread in flight per round (the scalar, branchy loop ran at
   // ~1 TB/s); the running (max, sum) is rescaled once per 16 values.
-  // no-repeat-n-gram bans: the row's banned token ids (-1 padded), tested only for a
-  // value that would enter the thread's list (rare after the first few), so the
-  // kernel returns the top K among the allowed tokens (HF applies the processor
-  // after log_softmax: the normaliser still covers every token)
-  __shared__ int ban_s[kMaxBans];
-  for (int b = tid; b < nbmax; b += kTopkThreads) ban_s[b] = bans[(size_t)row * nbmax + b];
-  if (nbmax > 0) __syncthreads();
+  // no-repeat-n-gram bans: the row's banned token ids (-1 padded) become a V-bit LDS
+  // bitmap, tested (one ds_read) only for a value that would enter the thread's list,
+  // so the kernel returns the top K among the allowed tokens (HF applies the processor
+  // after log_softmax: the normaliser still covers every token). A per-candidate scan of
+  // the ban list diverged: some lane of a wave inserts at almost every value, so every
+  // wave ran the whole scan per value (584 us per BART step).
+  extern __shared__ uint32_t ban_bits[];  // (V + 31) / 32 words when nbmax > 0
+  if (nbmax > 0) {
+    const int nw = (V + 31) / 32;
+    for (int w2 = tid; w2 < nw; w2 += kTopkThreads) ban_bits[w2] = 0u;
+    __syncthreads();
+    for (int b = tid; b < nbmax; b += kTopkThreads) {
+      const int t = bans[(size_t)row * nbmax + b];
+      if (t >= 0 && t < V) atomicOr(&ban_bits[t >> 5], 1u << (t & 31));
+    }
+    __syncthreads();
+  }
   float m = -FLT_MAX, s = 0.f;
   auto take = [&](float val, int i) {
     const float sel = (mask_eos && i == eos) ? -FLT_MAX : val;
     if (better(sel, i, tv[KM - 1], ti[KM - 1])) {
-      for (int b = 0; b < nbmax; ++b)
-        if (ban_s[b] == i) return;
+      if (nbmax > 0 && ((ban_bits[i >> 5] >> (i & 31)) & 1u)) return;
       list_insert<KM>(tv, ti, sel, i);
     }
   };
@@ -649,9 +658,11 @@ void beam_topk_rows(const float* logits, int rows, int V, const float* beam_scor
   ATPU_CHECK(K >= 1 && K <= kMaxBeamK && K <= V, "beam_topk: 1 <= K <= 16");
   ATPU_CHECK(nbmax >= 0 && nbmax <= kMaxBans && (nbmax == 0 || bans), "beam_topk: 0 <= banned tokens per row <= 512");
   const int vec4 = V % 4 == 0 && (reinterpret_cast<uintptr_t>(logits) & 15) == 0;
+  const size_t smem = nbmax > 0 ? (size_t)((V + 31) / 32) * 4 : 0;
+  ATPU_CHECK(smem <= 64 * 1024, "beam_topk: vocabulary too large for the ban bitmap (2M tokens)");
 #define ATPU_TK(KK)                                                                                               \
   case KK:                                                                                                        \
-    hipLaunchKernelGGL(beam_topk_kernel<KK>, dim3(rows), dim3(kTopkThreads), 0, stream, logits, V, beam_scores,   \
+    hipLaunchKernelGGL(beam_topk_kernel<KK>, dim3(rows), dim3(kTopkThreads), smem, stream, logits, V, beam_scores, \
                        eos, mask_eos, out_score, out_token, vec4, bans, nbmax);                                   \
     break;
   switch (K) {
