@@ -199,9 +199,9 @@ PYBIND11_MODULE(_atpu, m) {
     embed_gather(P<const int32_t>(ids), P<const bf16>(table), P<bf16>(out), tokens, N, vocab, S(stream));
   });
   m.def("tokenize", [](uintptr_t text, uintptr_t offsets, uintptr_t ids, uintptr_t lens, int B, int Sq, int vocab,
-                       int max_row_bytes, uintptr_t stream) {
+                       int max_row_bytes, uintptr_t stream, long long text_bytes) {
     tokenize_hash(P<const uint8_t>(text), P<const int32_t>(offsets), P<int32_t>(ids), P<int32_t>(lens), B, Sq, vocab,
-                  max_row_bytes, S(stream));
+                  max_row_bytes, S(stream), text_bytes);
   });
   m.def("head_topk", [](uintptr_t pooled, int ldp, uintptr_t Wc, uintptr_t bc, uintptr_t logits, uintptr_t idx,
                         uintptr_t score, int B, int N, int C, int k, uintptr_t stream) {

@@ -133,7 +133,8 @@ void embed_gather(const int32_t* ids, const bf16* table, bf16* out, int tokens, 
 // Deterministic hash word-piece tokenizer (see agent_tpu_amd/tokenizer.py for
 // the exact spec and the CPU twin). text: packed UTF-8 bytes; offsets[B+1].
 void tokenize_hash(const uint8_t* text, const int32_t* offsets, int32_t* ids, int32_t* lens, int B, int S,
-                   int vocab, int max_row_bytes, hipStream_t stream);
+                   int vocab, int max_row_bytes, hipStream_t stream,
+                   long long text_bytes);
 
 // ------------------------------------------------ classify head + top-k (K7)
 // logits[b, c] = pooled[b] · Wc[c] + bc[c]; probs = softmax(logits);

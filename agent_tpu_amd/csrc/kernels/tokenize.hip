@@ -52,15 +52,26 @@ __device__ __forceinline__ int wave_inclusive_scan(int v, int lane) {
 __global__ __launch_bounds__(256) void tokenize_kernel(const uint8_t* __restrict__ text,
                                                        const int32_t* __restrict__ offsets, int32_t* __restrict__ ids,
                                                        int32_t* __restrict__ lens, int B, int S, int vocab,
-                                                       int max_row_bytes) {
-  __shared__ uint8_t rowbuf[4][kMaxRowBytes];
+                                                       int max_row_bytes, long long text_bytes) {
+  __shared__ __attribute__((aligned(16))) uint8_t rowbuf[4][kMaxRowBytes + 16];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int row = blockIdx.x * 4 + w;
   if (row >= B) return;
-  uint8_t* buf = rowbuf[w];
   const int start = offsets[row];
   const int n = min(offsets[row + 1] - start, max_row_bytes);
-  for (int i = lane; i < n; i += 64) buf[i] = text[start + i];
+  // the row's bytes arrive as aligned 16-B pieces (one load per lane for a 1 KiB row;
+  // byte loads were 16 dependent round trips), the row itself starts sh bytes in; the
+  // last piece is clipped at the end of the text buffer
+  const int a0 = start & ~15, sh = start - a0;
+  for (int c = lane; c < (sh + n + 15) >> 4; c += 64) {
+    const long long g = (long long)a0 + 16 * c;
+    if (g + 16 <= text_bytes) {
+      *reinterpret_cast<uint4*>(rowbuf[w] + 16 * c) = *reinterpret_cast<const uint4*>(text + g);
+    } else {
+      for (int k = 0; k < 16 && g + k < text_bytes; ++k) rowbuf[w][16 * c + k] = text[g + k];
+    }
+  }
+  uint8_t* buf = rowbuf[w] + sh;
   // each wave reads only its own LDS slice: a wave-level fence suffices
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -121,13 +132,14 @@ __global__ __launch_bounds__(256) void tokenize_kernel(const uint8_t* __restrict
 }  // namespace
 
 void tokenize_hash(const uint8_t* text, const int32_t* offsets, int32_t* ids, int32_t* lens, int B, int S, int vocab,
-                   int max_row_bytes, hipStream_t stream) {
+                   int max_row_bytes, hipStream_t stream, long long text_bytes) {
+  ATPU_CHECK((reinterpret_cast<uintptr_t>(text) & 15) == 0, "tokenize: text buffer must be 16-byte aligned");
   ATPU_CHECK(S >= 2, "tokenize: S must be >= 2");
   ATPU_CHECK(vocab > 1000, "tokenize: vocab must exceed the 1000 reserved ids");
   ATPU_CHECK(max_row_bytes > 0 && max_row_bytes <= kMaxRowBytes, "tokenize: max_row_bytes must be in (0, 4096]");
   if (B <= 0) return;
   hipLaunchKernelGGL(tokenize_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, text, offsets, ids, lens, B, S, vocab,
-                     max_row_bytes);
+                     max_row_bytes, text_bytes);
   ATPU_HIP_CHECK(hipGetLastError());
 }
 

@@ -35,5 +35,5 @@ def tokenize(text: torch.Tensor, offsets: torch.Tensor, seq_len: int, vocab: int
         lens = torch.empty((B,), dtype=torch.int32, device=text.device)
     check(ids.shape[1] == seq_len and ids.shape[0] >= B and lens.numel() >= B, "ids/lens too small")
     native().tokenize(ptr(text), ptr(offsets), ptr(ids), ptr(lens), B, seq_len, vocab, max_row_bytes,
-                      stream_handle())
+                      stream_handle(), int(text.numel()))
     return ids, lens
