@@ -29,7 +29,7 @@ BASELINE_DOCS_PER_SEC = {"t5": 0.269, "bart": 0.155}
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="t5-base")
-    ap.add_argument("--docs", type=int, default=64, help="documents per step (batch)")
+    ap.add_argument("--docs", type=int, default=256, help="documents per step (batch)")
     ap.add_argument("--src-len", type=int, default=512)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
