@@ -374,8 +374,8 @@ def test_generate_device_select_matches_host(gpu, family):
     B, S = 5, 32
     ids = torch.randint(5, model.cfg.vocab_size, (B, S), generator=g, dtype=torch.int32)
     lens = torch.tensor([32, 20, 31, 9, 27], dtype=torch.int32)
-    for ml in (24, 40):
-        a = generate(model, ids.to(gpu), lens.to(gpu), GenConfig(num_beams=4, max_length=ml, min_length=5))
+    for ml, nbm, mn in ((24, 4, 5), (40, 4, 5), (2, 4, 0), (3, 2, 1), (12, 1, 3)):
+        a = generate(model, ids.to(gpu), lens.to(gpu), GenConfig(num_beams=nbm, max_length=ml, min_length=mn))
         b = generate(model, ids.to(gpu), lens.to(gpu),
-                     GenConfig(num_beams=4, max_length=ml, min_length=5, device_select=False))
-        assert a.sequences == b.sequences and a.scores == b.scores and a.steps == b.steps
+                     GenConfig(num_beams=nbm, max_length=ml, min_length=mn, device_select=False))
+        assert a.sequences == b.sequences and a.scores == b.scores and a.steps == b.steps, (ml, nbm)
