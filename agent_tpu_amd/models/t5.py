@@ -222,6 +222,14 @@ class T5Model:
     def wrap_source(self, toks):
         return list(toks) + [self.cfg.eos_id]
 
+    def prepare_decode(self, S: int, T: int) -> None:
+        """Build the lazily cached tensors a search of source length S / length T reads, on
+        the caller's stream (concurrent searches on other streams then only read them)."""
+        self.enc_bias(S)
+        self.dec_bias(T)
+        if self.rms_fold:
+            self.rms_folded()
+
     # ------------------------------------------------------------- biases
     def enc_bias(self, S: int) -> torch.Tensor:
         if S not in self._enc_bias:

@@ -29,6 +29,7 @@ position ``pos``) and only that int table is gathered by parent beam (K11).
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -177,6 +178,56 @@ def _select(logits: torch.Tensor, run_scores: torch.Tensor, K2: int, cfg, gen: G
 
 def generate(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfig) -> GenResult:
     """Beam search for a batch. ``src_ids`` [B, S] int32 (on the model device)."""
+    return _drive([_generate_iter(model, src_ids, src_lens, gen)])[0]
+
+
+def generate_concurrent(model, parts: Sequence[Tuple[torch.Tensor, torch.Tensor]], gen: GenConfig) -> List[GenResult]:
+    """Beam search for several batches at once, each on its own HIP stream.
+
+    A decode step of one batch is a chain of small latency-bound launches (skinny GEMMs,
+    per-row attention) next to one bandwidth-bound kernel (cross attention); two batches
+    on two streams fill each other's gaps (two 128-doc T5 runs side by side: 779 docs/s
+    against 666 for one 256-doc run). The host interleaves the runs' device-selection
+    loops: each yields before it waits for its own step's record."""
+    dev = model.device
+    caller = torch.cuda.current_stream(dev)
+    prep = getattr(model, "prepare_decode", None)
+    if prep is not None:  # lazily built weights / biases: once, before the streams fork
+        for ids, _ in parts:
+            prep(int(ids.shape[1]), int(gen.resolved(model.cfg).max_length))
+    streams = [torch.cuda.Stream(dev) for _ in parts]
+    for st in streams:  # the inputs were produced on the caller's stream
+        st.wait_stream(caller)
+    try:
+        return _drive([_generate_iter(model, ids, lens, gen, stream=st) for (ids, lens), st in zip(parts, streams)])
+    finally:
+        torch.cuda.set_stream(caller)
+        for st in streams:
+            caller.wait_stream(st)
+
+
+def _drive(iters) -> List[GenResult]:
+    """Run generate iterators round robin until each returns its GenResult."""
+    results: List[Optional[GenResult]] = [None] * len(iters)
+    active = list(range(len(iters)))
+    while active:
+        for i in list(active):
+            try:
+                next(iters[i])
+            except StopIteration as stop:
+                results[i] = stop.value
+                active.remove(i)
+    return results  # type: ignore[return-value]
+
+
+def _generate_iter(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfig, stream=None):
+    """:func:`generate` as a generator: yields where it would wait for its device step
+    (device selection only), returns the GenResult. ``stream``: the HIP stream to run on."""
+    def on_stream():
+        if stream is not None:
+            torch.cuda.set_stream(stream)
+
+    on_stream()
     cfg = model.cfg
     gen = gen.resolved(cfg)
     dev = model.device
@@ -306,6 +357,8 @@ def generate(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfi
     step_dev.fill_(0)
     logits = model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist)
     if pin and gen.device_select:
+        yield  # let other runs start their encoders / first steps
+        on_stream()
         # Device selection: top-k -> beam_select -> next decoder step are enqueued back to
         # back; the host folds step t's record into its state while the GPU runs step t+1
         # (the sequences it needs for step t+1's n-gram bans are complete by then).
@@ -320,6 +373,8 @@ def generate(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfi
         while True:
             tp0 = time.perf_counter()
             if pending is not None:
+                yield  # other runs enqueue their next step while this one's selection lands
+                on_stream()
                 rec_ev.synchronize()
                 r = rec_host.numpy()
                 rs = (r[:, :K2].copy().view(np.float32), r[:, K2:2 * K2].astype(np.int64),
@@ -512,16 +567,37 @@ class SummarizeEngine:
         hit = (vmap.ids[i] == q) if len(vmap.ids) else np.zeros(len(q), bool)
         return " ".join(vmap.words[vmap.word_of[j]] if h else f"<{t}>" for t, j, h in zip(keep, i, hit))
 
+    def run(self, ids: torch.Tensor, lens: torch.Tensor, gen: GenConfig) -> GenResult:
+        """Beam search over a tokenized batch. On a GPU with device selection the batch is
+        split into ``ATPU_SUMM_STREAMS`` (default 2) contiguous parts searched concurrently
+        on their own streams (:func:`generate_concurrent`), each part >= ``ATPU_SUMM_PART_MIN``
+        (default 512) documents. One host thread runs every part's bookkeeping, so the
+        split only pays once a part's GPU step outlasts the other parts' host work
+        (T5-base, MI355X: 1024 docs 819 -> 845 docs/s; 256 docs as 2x128: 668 -> 654)."""
+        n = int(os.getenv("ATPU_SUMM_STREAMS", "2"))
+        B = int(ids.shape[0])
+        n = max(1, min(n, B // max(1, int(os.getenv("ATPU_SUMM_PART_MIN", "512")))))
+        if n < 2 or self.device.type != "cuda" or not gen.device_select:
+            return generate(self.model, ids, lens, gen)
+        cuts = [B * i // n for i in range(n + 1)]
+        parts = [(ids[a:b], lens[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+        t0 = time.perf_counter()
+        outs = generate_concurrent(self.model, parts, gen)
+        wall = (time.perf_counter() - t0) * 1e3
+        enc = max(o.timing_ms["encode_ms"] for o in outs)
+        return GenResult([s for o in outs for s in o.sequences], [s for o in outs for s in o.scores],
+                         max(o.steps for o in outs), {"encode_ms": enc, "decode_ms": wall - enc})
+
     def generate_ids(self, texts: Sequence[str], gen: GenConfig) -> GenResult:
         """Token sequences only (a DP rank's shard; rank 0 detokenizes)."""
         ids, lens, _ = self.encode_texts(texts, with_maps=False)
-        return generate(self.model, ids, lens, gen)
+        return self.run(ids, lens, gen)
 
     def detokenize_all(self, texts: Sequence[str], seqs: List[List[int]]) -> List[str]:
         return [self.detokenize(s, m) for s, m in zip(seqs, self.word_maps(texts))]
 
     def summarize(self, texts: Sequence[str], gen: GenConfig) -> Tuple[List[str], GenResult]:
         ids, lens, _ = self.encode_texts(texts, with_maps=False)
-        res = generate(self.model, ids, lens, gen)
+        res = self.run(ids, lens, gen)
         maps = self.word_maps(texts)
         return [self.detokenize(s, m) for s, m in zip(res.sequences, maps)], res

@@ -379,3 +379,42 @@ def test_generate_device_select_matches_host(gpu, family):
         b = generate(model, ids.to(gpu), lens.to(gpu),
                      GenConfig(num_beams=nbm, max_length=ml, min_length=mn, device_select=False))
         assert a.sequences == b.sequences and a.scores == b.scores and a.steps == b.steps, (ml, nbm)
+
+
+@pytest.mark.parametrize("family", ["t5-tiny", "bart-tiny"])
+def test_generate_concurrent_matches_serial(gpu, family):
+    # two (or three) batches searched concurrently on their own streams, host loops
+    # interleaved, return exactly what one search per batch returns
+    from agent_tpu_amd.runtime.summarize import GenConfig, build_model, generate, generate_concurrent
+
+    model, _ = build_model(family, device=gpu, seed=5)
+    g = torch.Generator().manual_seed(11)
+    B, S = 9, 40
+    ids = torch.randint(5, model.cfg.vocab_size, (B, S), generator=g, dtype=torch.int32).to(gpu)
+    lens = torch.tensor([40, 12, 33, 9, 27, 40, 3, 18, 25], dtype=torch.int32).to(gpu)
+    for cuts, (ml, nbm, mn) in (((0, 4, 9), (30, 4, 5)), ((0, 2, 5, 9), (20, 2, 1)), ((0, 5, 9), (3, 4, 0))):
+        gen = GenConfig(num_beams=nbm, max_length=ml, min_length=mn)
+        parts = [(ids[a:b], lens[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+        ref = [generate(model, i, l, gen) for i, l in parts]
+        got = generate_concurrent(model, parts, gen)
+        for r, o in zip(ref, got):
+            assert r.sequences == o.sequences and r.scores == o.scores and r.steps == o.steps, (cuts, ml)
+
+
+def test_engine_stream_split_matches_single(gpu, monkeypatch):
+    # SummarizeEngine.run split over two streams: same output as one search
+    from agent_tpu_amd.runtime.summarize import GenConfig, SummarizeEngine, build_model
+
+    model, _ = build_model("t5-tiny", device=gpu, seed=2)
+    eng = SummarizeEngine(model, 64)
+    g = torch.Generator().manual_seed(4)
+    B, S = 70, 24
+    ids = torch.randint(5, model.cfg.vocab_size, (B, S), generator=g, dtype=torch.int32).to(gpu)
+    lens = torch.randint(2, S + 1, (B,), generator=g, dtype=torch.int32).to(gpu)
+    gen = GenConfig(num_beams=4, max_length=16, min_length=2)
+    monkeypatch.setenv("ATPU_SUMM_STREAMS", "1")
+    a = eng.run(ids, lens, gen)
+    monkeypatch.setenv("ATPU_SUMM_STREAMS", "2")
+    monkeypatch.setenv("ATPU_SUMM_PART_MIN", "32")
+    b = eng.run(ids, lens, gen)
+    assert a.sequences == b.sequences and a.scores == b.scores

@@ -1,10 +1,9 @@
+#!/bin/bash
+# ad-hoc GPU step: concurrent-stream summarize tests + A/B
 set -o pipefail
-export HSA_ENABLE_IPC_MODE_LEGACY=0
-R=$PWD
-rm -rf gpurun_out/prof_serial gpurun_out/prof_conc
-mkdir -p gpurun_out/prof_serial gpurun_out/prof_conc
-cd /tmp && export TMPDIR=/tmp
-ATPU_CONCURRENT_SLOTS=0 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format rocpd csv -d $R/gpurun_out/prof_serial -o run -- python3 $R/bench.py --steps 5 --warmup 1 > $R/gpurun_out/prof_serial.log 2>&1 || { tail -30 $R/gpurun_out/prof_serial.log; exit 1; }
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format rocpd csv -d $R/gpurun_out/prof_conc -o run -- python3 $R/bench.py --steps 5 --warmup 1 > $R/gpurun_out/prof_conc.log 2>&1 || { tail -30 $R/gpurun_out/prof_conc.log; exit 1; }
-cd $R
-for d in prof_serial prof_conc; do f=$(find gpurun_out/$d -name '*.db' | head -1); (python tools/kstats.py $f 16 > gpurun_out/$d.txt && head -8 gpurun_out/$d.txt) || find gpurun_out/$d; done
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/kernels/test_decode_gpu.py -k "concurrent or stream_split or device_select" > gpurun_out/adhoc_tests.log 2>&1 || { tail -30 gpurun_out/adhoc_tests.log; exit 1; }
+tail -2 gpurun_out/adhoc_tests.log
+CMD="python bench/summarize.py --docs 256" A="ATPU_SUMM_STREAMS=1" B="ATPU_SUMM_STREAMS=2" ROUNDS=2 bash tools/ab_env.sh || exit 1
+CMD="python bench/summarize.py --docs 256 --model bart-large-cnn" A="ATPU_SUMM_STREAMS=1" B="ATPU_SUMM_STREAMS=2" ROUNDS=1 bash tools/ab_env.sh || exit 1
+CMD="python bench/summarize.py --docs 1024" A="ATPU_SUMM_STREAMS=1" B="ATPU_SUMM_STREAMS=2" ROUNDS=1 bash tools/ab_env.sh
