@@ -397,7 +397,7 @@ __device__ __forceinline__ void wave_topk(float (&tv)[KM], int (&ti)[KM], float&
   }
 }
 
-template <int K>
+template <int K, bool BANS>
 __global__ __launch_bounds__(kTopkThreads) void beam_topk_kernel(const float* __restrict__ logits, int V,
                                                                  const float* __restrict__ beam_scores, int eos,
                                                                  int mask_eos, float* __restrict__ out_score,
@@ -418,13 +418,13 @@ __global__ __launch_bounds__(kTopkThreads) void beam_topk_kernel(const float* __
   // 16-B loads, 4 per thread in flight per round (the scalar, branchy loop ran at
   // ~1 TB/s); the running (max, sum) is rescaled once per 16 values.
   // no-repeat-n-gram bans: the row's banned token ids (-1 padded) become a V-bit LDS
-  // bitmap, tested (one ds_read) only for a value that would enter the thread's list,
+  // bitmap, tested (one ds_read) only for a value that would enter the candidates,
   // so the kernel returns the top K among the allowed tokens (HF applies the processor
   // after log_softmax: the normaliser still covers every token). A per-candidate scan of
   // the ban list diverged: some lane of a wave inserts at almost every value, so every
   // wave ran the whole scan per value (584 us per BART step).
   extern __shared__ uint32_t ban_bits[];  // (V + 31) / 32 words when nbmax > 0
-  if (nbmax > 0) {
+  if (BANS) {
     const int nw = (V + 31) / 32;
     for (int w2 = tid; w2 < nw; w2 += kTopkThreads) ban_bits[w2] = 0u;
     __syncthreads();
@@ -435,59 +435,174 @@ __global__ __launch_bounds__(kTopkThreads) void beam_topk_kernel(const float* __
     __syncthreads();
   }
   float m = -FLT_MAX, s = 0.f;
-  auto take = [&](float val, int i) {
-    const float sel = (mask_eos && i == eos) ? -FLT_MAX : val;
-    if (better(sel, i, tv[KM - 1], ti[KM - 1])) {
-      if (nbmax > 0 && ((ban_bits[i >> 5] >> (i & 31)) & 1u)) return;
-      list_insert<KM>(tv, ti, sel, i);
+  // Selection (per wave, exact): a value enters the wave's candidate buffer (LDS,
+  // ballot + mbcnt compaction) only if it is >= thr, a lower bound of the wave's K-th
+  // best allowed value: every value below thr has K strictly better ones. thr starts
+  // at the K-th largest lane maximum of the first 16 values per lane and rises when a
+  // nearly full buffer is cut back to the candidates >= the K-th largest of their
+  // per-lane maxima. A float4 costs a max, a compare and a ballot unless one of the
+  // wave's is a candidate. The per-lane sorted-list insert this replaces ran on every
+  // value some lane of the wave inserted (60 of 90 us per 1024 x 32128 step); a
+  // sorted cut-back (list insert + K-round wave top-K) per refill cost as much again.
+  constexpr int kBuf = 16 * 64 + 64;
+  __shared__ float bufv[kTopkWaves][kBuf];
+  __shared__ int bufi[kTopkWaves][kBuf];
+  float* bv = bufv[w];
+  int* bi = bufi[w];
+  float thr = -FLT_MAX;
+  int cnt = 0;  // wave-uniform
+  float rv;
+  int ri;
+  // K-th largest of one value per lane (duplicates count), -FLT_MAX if fewer than K
+  auto kth_lane_max = [&](float x) __attribute__((always_inline)) -> float {
+    float t = -FLT_MAX;
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+      t = wave_max(x);
+      const unsigned long long hit = __ballot(x == t);
+      if (lane == (int)__builtin_ctzll(hit | (1ull << 63))) x = -FLT_MAX;
     }
+    return t;
   };
+  // sorted top K of the buffer -> (rv, ri) in lanes 0..K-1, buffer = those K
+  auto exact_cut = [&]() __attribute__((always_inline)) {
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < KM; ++r) { tv[r] = -FLT_MAX; ti[r] = 0x7fffffff; }
+    for (int c = lane; c < cnt; c += 64) list_insert<KM>(tv, ti, bv[c], bi[c]);
+    wave_topk<KM>(tv, ti, rv, ri);
+    __builtin_amdgcn_wave_barrier();
+    if (lane < K) { bv[lane] = rv; bi[lane] = ri; }
+    thr = fmaxf(thr, __shfl(rv, K - 1, 64));
+    cnt = K;
+    __builtin_amdgcn_wave_barrier();
+  };
+  // room for one more chunk (1024 values): raise thr, keep the candidates >= thr
+  auto make_room = [&]() __attribute__((always_inline)) {
+    if (cnt <= kBuf - 16 * 64) return;
+    float lmx = -FLT_MAX;
+    for (int c = lane; c < cnt; c += 64) lmx = fmaxf(lmx, bv[c]);
+    thr = fmaxf(thr, kth_lane_max(lmx));
+    int n = 0;
+    for (int c0 = 0; c0 < cnt; c0 += 64) {  // in place: round r writes below (r + 1) * 64
+      const int c = c0 + lane;
+      const bool in = c < cnt;
+      const float val = in ? bv[c] : -FLT_MAX;
+      const int id = in ? bi[c] : 0;
+      const bool keep = in && val >= thr;
+      const unsigned long long bal = __ballot(keep);
+      __builtin_amdgcn_wave_barrier();
+      if (keep) {
+        const int pos = n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        bv[pos] = val;
+        bi[pos] = id;
+      }
+      __builtin_amdgcn_wave_barrier();
+      n += __popcll(bal);
+    }
+    cnt = n;
+    if (cnt > kBuf - 16 * 64) exact_cut();  // candidates held by fewer than K lanes
+  };
+  auto push = [&](float sel, int i, bool p) __attribute__((always_inline)) {
+    if (BANS && p) p = !((ban_bits[i >> 5] >> (i & 31)) & 1u);
+    const unsigned long long bal = __ballot(p);
+    if (bal == 0) return;
+    if (p) {
+      const int pos = cnt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+      bv[pos] = sel;
+      bi[pos] = i;
+    }
+    cnt += __popcll(bal);
+  };
+  // Loops run over block-uniform ranges (ballots and cut-backs need the whole wave).
+  // Two register sets alternate: loads are unconditional (index clamped, value
+  // masked), so the next 16 values per lane are in flight under the current 16 and
+  // the compiler's counted waits stay exact (a conditional or copied prefetch made
+  // it wait for everything).
   const int nv4 = vec4 ? V / 4 : 0;
   const float4* x4 = reinterpret_cast<const float4*>(x);
-  for (int j0 = tid; j0 < nv4; j0 += 4 * kTopkThreads) {
+  const int eos4 = mask_eos ? (eos >> 2) : -1;
+  auto load4 = [&](float4 (&dst)[4], int jb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dst[u] = x4[min(jb + tid + u * kTopkThreads, nv4 - 1)];
+  };
+  auto process = [&](const float4 (&src)[4], int jb) __attribute__((always_inline)) {
+    make_room();
     float4 v[4];
-    bool ok[4];
+    float lm[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int j = j0 + u * kTopkThreads;
-      ok[u] = j < nv4;
-      v[u] = ok[u] ? x4[j] : make_float4(-FLT_MAX, -FLT_MAX, -FLT_MAX, -FLT_MAX);
+      const bool ok = jb + tid + u * kTopkThreads < nv4;
+      v[u] = ok ? src[u] : make_float4(-FLT_MAX, -FLT_MAX, -FLT_MAX, -FLT_MAX);
+      lm[u] = fmaxf(fmaxf(v[u].x, v[u].y), fmaxf(v[u].z, v[u].w));
     }
-    float cm = m;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) cm = fmaxf(cm, fmaxf(fmaxf(v[u].x, v[u].y), fmaxf(v[u].z, v[u].w)));
+    const float cm = fmaxf(m, fmaxf(fmaxf(lm[0], lm[1]), fmaxf(lm[2], lm[3])));
     s *= __expf(m - cm);  // m == -FLT_MAX: s is 0 either way
     m = cm;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (!ok[u]) continue;
+    for (int u = 0; u < 4; ++u)
       s += (__expf(v[u].x - m) + __expf(v[u].y - m)) + (__expf(v[u].z - m) + __expf(v[u].w - m));
-      const int i = 4 * (j0 + u * kTopkThreads);
-      take(v[u].x, i);
-      take(v[u].y, i + 1);
-      take(v[u].z, i + 2);
-      take(v[u].w, i + 3);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (__builtin_expect(jb + tid + u * kTopkThreads == eos4, 0)) {  // selection only: the normaliser keeps EOS
+        const int c = eos & 3;
+        if (c == 0) v[u].x = -FLT_MAX;
+        if (c == 1) v[u].y = -FLT_MAX;
+        if (c == 2) v[u].z = -FLT_MAX;
+        if (c == 3) v[u].w = -FLT_MAX;
+        lm[u] = fmaxf(fmaxf(v[u].x, v[u].y), fmaxf(v[u].z, v[u].w));
+      }
+    }
+    // first chunk: no candidates yet; K lanes hold values >= the K-th largest lane
+    // maximum (banned tokens would not count: rows with bans start from -FLT_MAX)
+    if (!BANS && jb == 0) thr = kth_lane_max(fmaxf(fmaxf(lm[0], lm[1]), fmaxf(lm[2], lm[3])));
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      // a float4 of the wave enters the per-value path only if one of its values can
+      // be a candidate
+      if (__ballot(lm[u] >= thr) == 0) continue;
+      const bool ok = jb + tid + u * kTopkThreads < nv4;
+      const int i = 4 * (jb + tid + u * kTopkThreads);
+      push(v[u].x, i, ok && v[u].x >= thr);
+      push(v[u].y, i + 1, ok && v[u].y >= thr);
+      push(v[u].z, i + 2, ok && v[u].z >= thr);
+      push(v[u].w, i + 3, ok && v[u].w >= thr);
+    }
+  };
+  if (nv4 > 0) {
+    float4 ra[4], rb[4];
+    load4(ra, 0);
+    for (int jb = 0; jb < nv4; jb += 8 * kTopkThreads) {  // an odd chunk count runs one masked chunk
+      load4(rb, jb + 4 * kTopkThreads);
+      process(ra, jb);
+      load4(ra, jb + 8 * kTopkThreads);
+      process(rb, jb + 4 * kTopkThreads);
     }
   }
-  for (int i = 4 * nv4 + tid; i < V; i += kTopkThreads) {  // tail (or every element without vec4)
-    const float val = x[i];
-    if (val > m) {
-      s = s * __expf(m - val) + 1.f;
-      m = val;
-    } else {
-      s += __expf(val - m);
+  for (int ib = 4 * nv4; ib < V; ib += kTopkThreads) {  // tail (or every element without vec4)
+    if (cnt > kBuf - 64) exact_cut();
+    const int i = ib + tid;
+    const bool ok = i < V;
+    const float val = ok ? x[i] : -FLT_MAX;
+    if (ok) {
+      if (val > m) {
+        s = s * __expf(m - val) + 1.f;
+        m = val;
+      } else {
+        s += __expf(val - m);
+      }
     }
-    take(val, i);
+    const float sel = (mask_eos && i == eos) ? -FLT_MAX : val;
+    push(sel, i, ok && sel >= thr);
   }
+  exact_cut();  // lanes 0..K-1: the wave's top K in (rv, ri)
   // block log-sum-exp
   const float wmax = wave_max(m);
   float sa = (m == -FLT_MAX) ? 0.f : s * __expf(m - wmax);
   sa = wave_sum(sa);
   if (lane == 0) { wm[w] = wmax; ws[w] = sa; }
-  // wave-level top-K
-  float rv;
-  int ri;
-  wave_topk<KM>(tv, ti, rv, ri);
   if (lane < K) { cv[w * KM + lane] = rv; ci[w * KM + lane] = ri; }
   __syncthreads();
   if (w == 0) {
@@ -660,10 +775,14 @@ void beam_topk_rows(const float* logits, int rows, int V, const float* beam_scor
   const int vec4 = V % 4 == 0 && (reinterpret_cast<uintptr_t>(logits) & 15) == 0;
   const size_t smem = nbmax > 0 ? (size_t)((V + 31) / 32) * 4 : 0;
   ATPU_CHECK(smem <= 64 * 1024, "beam_topk: vocabulary too large for the ban bitmap (2M tokens)");
-#define ATPU_TK(KK)                                                                                               \
-  case KK:                                                                                                        \
-    hipLaunchKernelGGL(beam_topk_kernel<KK>, dim3(rows), dim3(kTopkThreads), smem, stream, logits, V, beam_scores, \
-                       eos, mask_eos, out_score, out_token, vec4, bans, nbmax);                                   \
+#define ATPU_TK(KK)                                                                                             \
+  case KK:                                                                                                      \
+    if (nbmax > 0)                                                                                              \
+      hipLaunchKernelGGL((beam_topk_kernel<KK, true>), dim3(rows), dim3(kTopkThreads), smem, stream, logits, V, \
+                         beam_scores, eos, mask_eos, out_score, out_token, vec4, bans, nbmax);                  \
+    else                                                                                                        \
+      hipLaunchKernelGGL((beam_topk_kernel<KK, false>), dim3(rows), dim3(kTopkThreads), smem, stream, logits,   \
+                         V, beam_scores, eos, mask_eos, out_score, out_token, vec4, bans, nbmax);               \
     break;
   switch (K) {
     ATPU_TK(1) ATPU_TK(2) ATPU_TK(3) ATPU_TK(4) ATPU_TK(5) ATPU_TK(6) ATPU_TK(7) ATPU_TK(8)

@@ -1,4 +1,5 @@
 """Decode kernels (K9-K11) and the T5 HIP path vs the fp32 CPU references."""
+import numpy as np
 import pytest
 import torch
 
@@ -121,6 +122,23 @@ def test_beam_topk_rows(gpu, V, k, mask):
     assert torch.equal(idx.cpu(), ridx)
     if mask:
         assert not (idx == 1).any()
+
+
+@pytest.mark.parametrize("V,k", [(32128, 8), (50264, 16), (1002, 4), (7, 5)])
+def test_beam_topk_rows_ties(gpu, V, k):
+    # coarse logits: many exact ties at the top; the order is (value desc, index asc)
+    R = 9
+    logits = (_r((R, V), gpu, 3.0, torch.float32, seed=8) * 2).round() / 2
+    logits[3] = 1.0  # a row of one value
+    bs = _r((R,), gpu, 1.0, torch.float32, seed=9)
+    sc, idx = ops.beam_topk_rows(logits, bs, k, eos=1, mask_eos=True)
+    rsc, _ = ops.beam_topk_rows(logits.cpu(), bs.cpu(), k, eos=1, mask_eos=True)
+    torch.testing.assert_close(sc.cpu(), rsc, atol=2e-4, rtol=1e-5)
+    x = logits.cpu().numpy().copy()
+    x[:, 1] = -np.inf
+    for r in range(R):
+        want = np.lexsort((np.arange(V), -x[r]))[:k]
+        assert idx[r].tolist() == want.tolist(), r
 
 
 @pytest.mark.parametrize("V,k,nb", [(50264, 8, 12), (32128, 8, 1), (4096, 3, 300)])
