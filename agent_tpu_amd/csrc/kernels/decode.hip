@@ -47,7 +47,12 @@ __global__ __launch_bounds__(NW * 64) void decode_attention_kernel(
     int seq_stride, int group, int nrows, const int32_t* __restrict__ lens, const int32_t* __restrict__ step_dev,
     const int32_t* __restrict__ hist, int hist_stride, const float* __restrict__ bias_dist, int bias_stride,
     bf16* __restrict__ out, int ldo, float scale) {
-  __shared__ float p[GM][kMaxKeys];
+  // scores / probabilities, GM rows of pst = seq_stride rounded to 4 (dynamic: sized
+  // to the cache, not kMaxKeys -- 32 KiB static held the cross-attention launch to 4
+  // workgroups per CU)
+  extern __shared__ float p_dyn[];
+  const int pst = (seq_stride + 3) & ~3;
+  auto P = [&](int g, int j) -> float& { return p_dyn[g * pst + j]; };
   __shared__ float po[NW][GM][kD];
   __shared__ float red[NW][16];
   __shared__ int prow[GM == 1 ? kMaxKeys : 1];  // self attention: physical cache row of key j
@@ -58,7 +63,7 @@ __global__ __launch_bounds__(NW * 64) void decode_attention_kernel(
   const int h = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int G = min(group, nrows - seq * group);
   int len = lens ? lens[seq] : (*step_dev + 1);
-  len = min(len, kMaxKeys);
+  len = min(len, seq_stride);  // <= kMaxKeys (host check)
   const bool use_hist = GM == 1 && hist != nullptr;
   auto row_of = [&](int j) -> int {
     return (use_hist && j < len - 1) ? hist[(size_t)seq * hist_stride + j] : seq;
@@ -78,20 +83,23 @@ __global__ __launch_bounds__(NW * 64) void decode_attention_kernel(
 #pragma unroll
     for (int e = 0; e < 8; ++e) { qb0[e] = f2bf(0.f); qb1[e] = f2bf(0.f); }
   }
+  // (8 tiles / slabs in flight per wave for cross attention measured the same as 4)
+  constexpr int US = kUnrollS;
+  constexpr int UV = kUnrollV;
   float mxl = -FLT_MAX;
-  for (int t0 = w; t0 * 16 < len; t0 += NW * kUnrollS) {
-    bf16x8 a0[kUnrollS], a1[kUnrollS];
-    int rr[kUnrollS];
+  for (int t0 = w; t0 * 16 < len; t0 += NW * US) {
+    bf16x8 a0[US], a1[US];
+    int rr[US];
 #pragma unroll
-    for (int u = 0; u < kUnrollS; ++u) rr[u] = row_of(min((t0 + u * NW) * 16 + li, len - 1));
+    for (int u = 0; u < US; ++u) rr[u] = row_of(min((t0 + u * NW) * 16 + li, len - 1));
 #pragma unroll
-    for (int u = 0; u < kUnrollS; ++u) {
+    for (int u = 0; u < US; ++u) {
       const bf16* kr = k + at(rr[u], min((t0 + u * NW) * 16 + li, len - 1));
       a0[u] = *reinterpret_cast<const bf16x8*>(kr + kq);
       a1[u] = *reinterpret_cast<const bf16x8*>(kr + 32 + kq);
     }
 #pragma unroll
-    for (int u = 0; u < kUnrollS; ++u) {
+    for (int u = 0; u < US; ++u) {
       const int t = t0 + u * NW;
       if (t * 16 >= len) break;
       if (GM == 1 && lane < 16 && t * 16 + lane < len) prow[t * 16 + lane] = rr[u];
@@ -104,7 +112,7 @@ __global__ __launch_bounds__(NW * 64) void decode_attention_kernel(
           const int j = t * 16 + (lane >> 4) * 4 + e;
           if (j < len) {
             const float sj = acc[e] * scale + (bias_dist ? bias_dist[h * bias_stride + (len - 1 - j)] : 0.f);
-            p[li][j] = sj;
+            P(li, j) = sj;
             mxl = fmaxf(mxl, sj);
           }
         }
@@ -115,6 +123,18 @@ __global__ __launch_bounds__(NW * 64) void decode_attention_kernel(
   mxl = fmaxf(mxl, __shfl_xor(mxl, 32));
   if (lane < 16) red[w][lane] = mxl;
   __syncthreads();
+  // ---- P·V operands: lane = (key sub 0..7, dims (lane&7)*8 .. +8) ----
+  const int ksub = lane >> 3, dc = (lane & 7) * 8;
+  bf16x8 vv[UV];
+  auto load_v = [&](int j0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < UV; ++u) {
+      const int j = min(j0 + u * NW * 8 + ksub, len - 1);
+      const int r = use_hist ? prow[j] : seq;
+      vv[u] = *reinterpret_cast<const bf16x8*>(v + at(r, j) + dc);
+    }
+  };
+  load_v(w * 8);  // in flight under the softmax
   float mx[GM];
 #pragma unroll
   for (int g = 0; g < GM; ++g) {
@@ -131,8 +151,8 @@ __global__ __launch_bounds__(NW * 64) void decode_attention_kernel(
 #pragma unroll
     for (int g = 0; g < GM; ++g) {
       if (g < G) {
-        const float e = __expf(p[g][j] - mx[g]);
-        p[g][j] = e;
+        const float e = __expf(P(g, j) - mx[g]);
+        P(g, j) = e;
         sm[g] += e;
       }
     }
@@ -143,29 +163,22 @@ __global__ __launch_bounds__(NW * 64) void decode_attention_kernel(
     if (lane == 0) red[w][g] = s;
   }
   __syncthreads();
-  // ---- P·V: lane = (key sub 0..7, dims (lane&7)*8 .. +8) ----
-  const int ksub = lane >> 3, dc = (lane & 7) * 8;
+  // ---- P·V ----
   float o[GM][8];
 #pragma unroll
   for (int g = 0; g < GM; ++g)
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[g][e] = 0.f;
-  for (int j0 = w * 8; j0 < len; j0 += NW * 8 * kUnrollV) {
-    bf16x8 vv[kUnrollV];
+  for (int j0 = w * 8; j0 < len; j0 += NW * 8 * UV) {
+    if (j0 != w * 8) load_v(j0);
 #pragma unroll
-    for (int u = 0; u < kUnrollV; ++u) {
-      const int j = min(j0 + u * NW * 8 + ksub, len - 1);
-      const int r = use_hist ? prow[j] : seq;
-      vv[u] = *reinterpret_cast<const bf16x8*>(v + at(r, j) + dc);
-    }
-#pragma unroll
-    for (int u = 0; u < kUnrollV; ++u) {
+    for (int u = 0; u < UV; ++u) {
       const int j = j0 + u * NW * 8 + ksub;
       if (j < len) {
 #pragma unroll
         for (int g = 0; g < GM; ++g) {
           if (g < G) {
-            const float pj = p[g][j];
+            const float pj = P(g, j);
 #pragma unroll
             for (int e = 0; e < 8; ++e) o[g][e] += pj * bf2f(vv[u][e]);
           }
@@ -724,10 +737,11 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
     ATPU_HIP_CHECK(hipGetLastError());
     return;
   }
+  ATPU_CHECK(seq_stride <= kMaxKeys, "decode_attention: cache length above 2048");
   const int nseq = (rows + group - 1) / group;
-  const dim3 grid(nseq, H);
 #define ATPU_DA(GM, NW)                                                                                          \
-  hipLaunchKernelGGL((decode_attention_kernel<GM, NW>), grid, dim3(NW * 64), 0, stream, q, ldq, k, v, ldkv,       \
+  hipLaunchKernelGGL((decode_attention_kernel<GM, NW>), dim3(nseq, H), dim3(NW * 64),                           \
+                     (size_t)GM * ((seq_stride + 3) & ~3) * sizeof(float), stream, q, ldq, k, v, ldkv,          \
                      seq_stride, group, rows, lens, step_dev, hist, hist_stride, bias_dist, bias_stride, out, ldo, \
                      scale)
   if (group == 1)
