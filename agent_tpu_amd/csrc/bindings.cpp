@@ -142,11 +142,15 @@ PYBIND11_MODULE(_atpu, m) {
     beam_select(P<const float>(sc), P<const int32_t>(tk), B, nb, K2, V, eos, hit_all, neg, P<int32_t>(stage),
                 P<int32_t>(rec), S(stream));
   });
-  m.def("beam_reorder_hist", [](uintptr_t src, uintptr_t dst, uintptr_t parent, int rows, int stride,
-                                uintptr_t step_dev, uintptr_t stream) {
-    beam_reorder_hist(P<const int32_t>(src), P<int32_t>(dst), P<const int32_t>(parent), rows, stride,
-                      P<const int32_t>(step_dev), S(stream));
-  });
+  m.def(
+      "beam_reorder_hist",
+      [](uintptr_t src, uintptr_t dst, uintptr_t parent, int rows, int stride, uintptr_t step_dev, uintptr_t stream,
+         uintptr_t last, int off) {
+        beam_reorder_hist(P<const int32_t>(src), P<int32_t>(dst), P<const int32_t>(parent), rows, stride,
+                          P<const int32_t>(step_dev), S(stream), P<const int32_t>(last), off);
+      },
+      py::arg("src"), py::arg("dst"), py::arg("parent"), py::arg("rows"), py::arg("stride"), py::arg("step_dev"),
+      py::arg("stream"), py::arg("last") = 0, py::arg("off") = 0);
   m.def("kv_append", [](uintptr_t src, int lds, int col0, int ncols, uintptr_t cache, int seq_stride, int ldc,
                         uintptr_t step_dev, int rows, uintptr_t stream) {
     kv_append(P<const bf16>(src), lds, col0, ncols, P<bf16>(cache), seq_stride, ldc, P<const int32_t>(step_dev), rows,
@@ -160,13 +164,15 @@ PYBIND11_MODULE(_atpu, m) {
   m.def(
       "beam_topk_rows",
       [](uintptr_t logits, int rows, int V, uintptr_t beam_scores, int eos, int mask_eos, int K, uintptr_t out_score,
-         uintptr_t out_token, uintptr_t stream, uintptr_t bans, int nbmax) {
+         uintptr_t out_token, uintptr_t stream, uintptr_t bans, int nbmax, uintptr_t seq, int seq_stride, int cur,
+         int ngram) {
         beam_topk_rows(P<const float>(logits), rows, V, P<const float>(beam_scores), eos, mask_eos, K,
-                       P<float>(out_score), P<int32_t>(out_token), S(stream), P<const int32_t>(bans), nbmax);
+                       P<float>(out_score), P<int32_t>(out_token), S(stream), P<const int32_t>(bans), nbmax,
+                       P<const int32_t>(seq), seq_stride, cur, ngram);
       },
       py::arg("logits"), py::arg("rows"), py::arg("V"), py::arg("beam_scores"), py::arg("eos"), py::arg("mask_eos"),
       py::arg("K"), py::arg("out_score"), py::arg("out_token"), py::arg("stream"), py::arg("bans") = 0,
-      py::arg("nbmax") = 0);
+      py::arg("nbmax") = 0, py::arg("seq") = 0, py::arg("seq_stride") = 0, py::arg("cur") = 0, py::arg("ngram") = 0);
 
   m.def("attention", [](uintptr_t qkv, uintptr_t lens, uintptr_t bias, uintptr_t out, int B, int Sq, int H, int D,
                         float scale, uintptr_t stream) {

@@ -87,20 +87,21 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
                       const int32_t* lens, const int32_t* step_dev, const int32_t* hist, int hist_stride,
                       const float* bias_dist, int bias_stride, bf16* out, int ldo, int rows, int H, float scale,
                       hipStream_t stream);
-// dst[r][j] = src[parent[r]][j] (j < t), dst[r][t] = parent[r]; t = *step_dev
+// dst[r][j] = src[parent[r]][j] (j < t), dst[r][t] = last ? last[r] : parent[r]; t = *step_dev + off
 // device beam selection (runtime/summarize.py): item top-K2 over its beams' candidates, hits,
 // next running beams -> stage [parents | tokens | score bits] and a host record per item
 void beam_select(const float* sc, const int32_t* tk, int B, int nb, int K2, int V, int eos, int hit_all, float neg,
                  int32_t* stage, int32_t* rec, hipStream_t stream);
 void beam_reorder_hist(const int32_t* src, int32_t* dst, const int32_t* parent, int rows, int stride,
-                       const int32_t* step_dev, hipStream_t stream);
+                       const int32_t* step_dev, hipStream_t stream, const int32_t* last = nullptr, int off = 0);
 void kv_append(const bf16* src, int lds, int col0, int ncols, bf16* cache, int seq_stride, int ldc,
                const int32_t* step_dev, int rows, hipStream_t stream);
 void gather_rows(const bf16* src, bf16* dst, const int32_t* parent, int nrows, int seq_stride, int ldc,
                  const int32_t* step_dev, int slabs, size_t slab_elems, hipStream_t stream);
 void beam_topk_rows(const float* logits, int rows, int V, const float* beam_scores, int eos, int mask_eos, int K,
                     float* out_score, int32_t* out_token, hipStream_t stream,
-                    const int32_t* bans = nullptr, int nbmax = 0);
+                    const int32_t* bans = nullptr, int nbmax = 0, const int32_t* seq = nullptr, int seq_stride = 0,
+                    int cur = 0, int ngram = 0);
 
 // ------------------------------------------------------------- attention (K4)
 // qkv: [B*S, 3*H*D] packed per token as [q(H*D) | k(H*D) | v(H*D)];

@@ -313,17 +313,19 @@ __global__ __launch_bounds__(NW * 64) void decode_self_attention_kernel(
   }
 }
 
-// hist'[r][j] = hist[parent[r]][j] for j < t; hist'[r][t] = parent[r]
+// hist'[r][j] = hist[parent[r]][j] for j < t; hist'[r][t] = last ? last[r] : parent[r],
+// t = *step_dev + off (token histories: last = the new tokens, off = 1)
 __global__ __launch_bounds__(256) void beam_reorder_hist_kernel(const int32_t* __restrict__ src,
                                                                 int32_t* __restrict__ dst,
                                                                 const int32_t* __restrict__ parent, int rows,
-                                                                int stride, const int32_t* __restrict__ step_dev) {
-  const int t = *step_dev;
+                                                                int stride, const int32_t* __restrict__ step_dev,
+                                                                const int32_t* __restrict__ last, int off) {
+  const int t = min(*step_dev + off, stride - 1);
   const int n = rows * (t + 1);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int r = i / (t + 1), j = i % (t + 1);
     const int pr = parent[r];
-    dst[(size_t)r * stride + j] = j < t ? src[(size_t)pr * stride + j] : pr;
+    dst[(size_t)r * stride + j] = j < t ? src[(size_t)pr * stride + j] : (last ? last[r] : pr);
   }
 }
 
@@ -415,7 +417,9 @@ __global__ __launch_bounds__(kTopkThreads) void beam_topk_kernel(const float* __
                                                                  const float* __restrict__ beam_scores, int eos,
                                                                  int mask_eos, float* __restrict__ out_score,
                                                                  int32_t* __restrict__ out_token, int vec4,
-                                                                 const int32_t* __restrict__ bans, int nbmax) {
+                                                                 const int32_t* __restrict__ bans, int nbmax,
+                                                                 const int32_t* __restrict__ seq, int seq_stride,
+                                                                 int cur, int ngram) {
   __shared__ float wm[kTopkWaves], ws[kTopkWaves];
   constexpr int KM = K;
   __shared__ float cv[kTopkWaves * KM];
@@ -444,6 +448,18 @@ __global__ __launch_bounds__(kTopkThreads) void beam_topk_kernel(const float* __
     for (int b = tid; b < nbmax; b += kTopkThreads) {
       const int t = bans[(size_t)row * nbmax + b];
       if (t >= 0 && t < V) atomicOr(&ban_bits[t >> 5], 1u << (t & 31));
+    }
+    // no-repeat-n-gram from the device token history (HF NoRepeatNGramLogitsProcessor):
+    // the row's first cur tokens; window i bans its last token when its first n-1
+    // match the row's last n-1
+    if (ngram > 0 && cur >= ngram) {
+      const int32_t* sr = seq + (size_t)row * seq_stride;
+      for (int i = tid; i + ngram <= cur; i += kTopkThreads) {
+        bool eq = true;
+        for (int e = 0; e + 1 < ngram; ++e) eq = eq && sr[i + e] == sr[cur - ngram + 1 + e];
+        const int t = sr[i + ngram - 1];
+        if (eq && t >= 0 && t < V) atomicOr(&ban_bits[t >> 5], 1u << (t & 31));
+      }
     }
     __syncthreads();
   }
@@ -757,11 +773,11 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
 }
 
 void beam_reorder_hist(const int32_t* src, int32_t* dst, const int32_t* parent, int rows, int stride,
-                       const int32_t* step_dev, hipStream_t stream) {
-  ATPU_CHECK(rows > 0 && stride > 0, "beam_reorder_hist: bad shape");
+                       const int32_t* step_dev, hipStream_t stream, const int32_t* last, int off) {
+  ATPU_CHECK(rows > 0 && stride > 0 && off >= 0, "beam_reorder_hist: bad shape");
   const int blocks = std::max(1, std::min(1024, (rows * stride + 255) / 256));
   hipLaunchKernelGGL(beam_reorder_hist_kernel, dim3(blocks), dim3(256), 0, stream, src, dst, parent, rows, stride,
-                     step_dev);
+                     step_dev, last, off);
   ATPU_HIP_CHECK(hipGetLastError());
 }
 
@@ -783,20 +799,26 @@ void gather_rows(const bf16* src, bf16* dst, const int32_t* parent, int nrows, i
 }
 
 void beam_topk_rows(const float* logits, int rows, int V, const float* beam_scores, int eos, int mask_eos, int K,
-                    float* out_score, int32_t* out_token, hipStream_t stream, const int32_t* bans, int nbmax) {
+                    float* out_score, int32_t* out_token, hipStream_t stream, const int32_t* bans, int nbmax,
+                    const int32_t* seq, int seq_stride, int cur, int ngram) {
   ATPU_CHECK(K >= 1 && K <= kMaxBeamK && K <= V, "beam_topk: 1 <= K <= 16");
   ATPU_CHECK(nbmax >= 0 && nbmax <= kMaxBans && (nbmax == 0 || bans), "beam_topk: 0 <= banned tokens per row <= 512");
+  ATPU_CHECK(ngram <= 0 || (seq && cur <= seq_stride), "beam_topk: n-gram bans need the token history [rows, >= cur]");
+  if (ngram > 0 && cur < ngram) ngram = 0;
+  const bool any_bans = nbmax > 0 || ngram > 0;
   const int vec4 = V % 4 == 0 && (reinterpret_cast<uintptr_t>(logits) & 15) == 0;
-  const size_t smem = nbmax > 0 ? (size_t)((V + 31) / 32) * 4 : 0;
+  const size_t smem = any_bans ? (size_t)((V + 31) / 32) * 4 : 0;
   ATPU_CHECK(smem <= 64 * 1024, "beam_topk: vocabulary too large for the ban bitmap (2M tokens)");
 #define ATPU_TK(KK)                                                                                             \
   case KK:                                                                                                      \
-    if (nbmax > 0)                                                                                              \
+    if (any_bans)                                                                                               \
       hipLaunchKernelGGL((beam_topk_kernel<KK, true>), dim3(rows), dim3(kTopkThreads), smem, stream, logits, V, \
-                         beam_scores, eos, mask_eos, out_score, out_token, vec4, bans, nbmax);                  \
+                         beam_scores, eos, mask_eos, out_score, out_token, vec4, bans, nbmax, seq, seq_stride,  \
+                         cur, ngram);                                                                           \
     else                                                                                                        \
       hipLaunchKernelGGL((beam_topk_kernel<KK, false>), dim3(rows), dim3(kTopkThreads), smem, stream, logits,   \
-                         V, beam_scores, eos, mask_eos, out_score, out_token, vec4, bans, nbmax);               \
+                         V, beam_scores, eos, mask_eos, out_score, out_token, vec4, bans, nbmax, seq,           \
+                         seq_stride, cur, ngram);                                                               \
     break;
   switch (K) {
     ATPU_TK(1) ATPU_TK(2) ATPU_TK(3) ATPU_TK(4) ATPU_TK(5) ATPU_TK(6) ATPU_TK(7) ATPU_TK(8)

@@ -92,19 +92,24 @@ def kv_append(src: torch.Tensor, col0: int, ncols: int, cache: torch.Tensor, seq
                        row_stride(cache, "cache"), ptr(step), R, stream_handle())
 
 
-def beam_reorder_hist(src: torch.Tensor, dst: torch.Tensor, parent: torch.Tensor, step: torch.Tensor) -> None:
-    """dst[r, :t] = src[parent[r], :t]; dst[r, t] = parent[r] (t = step); [R, T] int32."""
+def beam_reorder_hist(src: torch.Tensor, dst: torch.Tensor, parent: torch.Tensor, step: torch.Tensor,
+                      last: Optional[torch.Tensor] = None, off: int = 0) -> None:
+    """dst[r, :t] = src[parent[r], :t]; dst[r, t] = last[r] if given else parent[r];
+    t = step + off (clamped to T - 1); [R, T] int32. Cache backpointers: last None, off 0;
+    token histories: last = the new tokens, off 1."""
     R, T = src.shape
     if not src.is_cuda:
-        t = int(step.reshape(-1)[0])
+        t = min(int(step.reshape(-1)[0]) + off, T - 1)
         pl = parent.long().cpu()
         dst[:, :t] = src[pl, :t]
-        dst[:, t] = parent.to(dst.dtype)
+        dst[:, t] = (last if last is not None else parent).to(dst.dtype)
         return
     check(src.dtype == torch.int32 and dst.dtype == torch.int32 and parent.dtype == torch.int32,
           "hist/parent must be int32")
     check(src.is_contiguous() and dst.is_contiguous() and tuple(dst.shape) == (R, T), "hist must be contiguous [R, T]")
-    native().beam_reorder_hist(ptr(src), ptr(dst), ptr(parent), R, T, ptr(step), stream_handle())
+    check(last is None or (last.dtype == torch.int32 and last.is_cuda and last.numel() >= R), "last: int32 [R] on device")
+    native().beam_reorder_hist(ptr(src), ptr(dst), ptr(parent), R, T, ptr(step), stream_handle(),
+                               ptr(last) if last is not None else 0, int(off))
 
 
 def gather_rows(src: torch.Tensor, dst: torch.Tensor, parent: torch.Tensor, nrows: int, seq_stride: int,
@@ -124,12 +129,34 @@ def gather_rows(src: torch.Tensor, dst: torch.Tensor, parent: torch.Tensor, nrow
 MAX_BANS = 512  # banned tokens per row the kernel filters (decode.hip kMaxBans)
 
 
+def ngram_bans(seq: torch.Tensor, n: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """HF NoRepeatNGramLogitsProcessor for every row of ``seq`` [R, cur] at once.
+
+    Returns ``(rows, tokens)``: token t is banned for row r when the row's last
+    n-1 tokens followed by t already occur in the row.
+    """
+    R, cur = seq.shape
+    if n <= 0 or cur + 1 < n or cur < n:
+        return torch.empty(0, dtype=torch.long), torch.empty(0, dtype=torch.long)
+    if n == 1:
+        rows = torch.arange(R).repeat_interleave(cur)
+        return rows, seq.reshape(-1)
+    ng = seq.unfold(1, n, 1)  # [R, cur-n+1, n]
+    prefix = seq[:, cur - n + 1:]  # [R, n-1]
+    match = (ng[:, :, :n - 1] == prefix.unsqueeze(1)).all(-1)
+    r, c = match.nonzero(as_tuple=True)
+    return r, ng[r, c, n - 1]
+
+
 def beam_topk_rows(logits: torch.Tensor, beam_scores: torch.Tensor, k: int, eos: int, mask_eos: bool,
-                   bans: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                   bans: Optional[torch.Tensor] = None,
+                   ngram: Optional[Tuple[torch.Tensor, int, int]] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Per row: top-k of ``log_softmax(logits) + beam_score`` (EOS masked if asked).
 
     ``bans`` (int32 ``[R, nb]``, -1 padded): token ids excluded from row r's selection
-    (no-repeat-n-gram processor; the log-softmax normaliser still covers every token)."""
+    (no-repeat-n-gram processor; the log-softmax normaliser still covers every token).
+    ``ngram = (seq, cur, n)``: the same processor computed in the kernel from the
+    device token history ``seq`` (int32 ``[R, T]``, the first ``cur`` columns valid)."""
     R, V = logits.shape
     nbmax = 0 if bans is None else int(bans.shape[1])
     if not logits.is_cuda:
@@ -141,6 +168,10 @@ def beam_topk_rows(logits: torch.Tensor, beam_scores: torch.Tensor, k: int, eos:
             r = torch.arange(R).view(-1, 1).expand_as(b)
             ok = b >= 0
             lp[r[ok], b[ok]] = float("-inf")
+        if ngram is not None:
+            seq, cur, n = ngram
+            br, bt = ngram_bans(seq[:, :cur].cpu().long(), int(n))
+            lp[br, bt] = float("-inf")
         lp = lp + beam_scores.float().view(-1, 1)
         sc, idx = torch.topk(lp, k, dim=-1)
         return sc, idx.to(torch.int32)
@@ -151,8 +182,14 @@ def beam_topk_rows(logits: torch.Tensor, beam_scores: torch.Tensor, k: int, eos:
               "bans must be contiguous int32 [R, n] on the logits' device")
     sc = torch.empty((R, k), dtype=torch.float32, device=logits.device)
     idx = torch.empty((R, k), dtype=torch.int32, device=logits.device)
+    seq_p, seq_stride, cur, n = 0, 0, 0, 0
+    if ngram is not None:
+        seq, cur, n = ngram
+        check(seq.dtype == torch.int32 and seq.is_contiguous() and seq.shape[0] == R and seq.device == logits.device
+              and 0 <= int(cur) <= seq.shape[1], "ngram: token history must be contiguous int32 [R, >= cur] on device")
+        seq_p, seq_stride, cur, n = ptr(seq), int(seq.shape[1]), int(cur), int(n)
     native().beam_topk_rows(ptr(logits), R, V, ptr(beam_scores), int(eos), int(mask_eos), int(k), ptr(sc), ptr(idx),
-                            stream_handle(), ptr(bans) if nbmax else 0, nbmax)
+                            stream_handle(), ptr(bans) if nbmax else 0, nbmax, seq_p, seq_stride, cur, n)
     return sc, idx
 
 

@@ -70,23 +70,7 @@ class GenConfig:
                          pick(self.forced_eos_id, "forced_eos_id", None), self.use_graph, self.device_select)
 
 
-def ngram_bans(seq: torch.Tensor, n: int) -> Tuple[torch.Tensor, torch.Tensor]:
-    """HF NoRepeatNGramLogitsProcessor for every row of ``seq`` [R, cur] at once.
-
-    Returns ``(rows, tokens)``: token t is banned for row r when the row's last
-    n-1 tokens followed by t already occur in the row.
-    """
-    R, cur = seq.shape
-    if n <= 0 or cur + 1 < n or cur < n:
-        return torch.empty(0, dtype=torch.long), torch.empty(0, dtype=torch.long)
-    if n == 1:
-        rows = torch.arange(R).repeat_interleave(cur)
-        return rows, seq.reshape(-1)
-    ng = seq.unfold(1, n, 1)  # [R, cur-n+1, n]
-    prefix = seq[:, cur - n + 1:]  # [R, n-1]
-    match = (ng[:, :, :n - 1] == prefix.unsqueeze(1)).all(-1)
-    r, c = match.nonzero(as_tuple=True)
-    return r, ng[r, c, n - 1]
+ngram_bans = ops.ngram_bans  # (re-exported: HF NoRepeatNGramLogitsProcessor, vectorised)
 
 
 @dataclass
@@ -98,12 +82,10 @@ class GenResult:
 
 
 def _select(logits: torch.Tensor, run_scores: torch.Tensor, K2: int, cfg, gen: GenConfig, cur: int, T: int,
-            run_seq: torch.Tensor, scores_dev: Optional[torch.Tensor] = None,
-            on_device: bool = False, bans_buf=None) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Per beam row: the top ``K2`` continuations ``(score [rows, K2], token [rows, K2])``
-    after log-softmax and the logits processors (min-length EOS mask, n-gram bans,
-    forced BOS/EOS), on the host; ``on_device``: left on the logits' device (fp32 /
-    int32, for :func:`ops.beam_select`), no D2H."""
+            run_seq: torch.Tensor, scores_dev: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Host selection path: per beam row, the top ``K2`` continuations ``(score [rows, K2],
+    token [rows, K2])`` after log-softmax and the logits processors (min-length EOS mask,
+    n-gram bans from the host sequences, forced BOS/EOS), returned on the host."""
     rows, V = logits.shape
     forced = None
     if gen.forced_bos_id is not None and cur == 1:
@@ -116,8 +98,6 @@ def _select(logits: torch.Tensor, run_scores: torch.Tensor, K2: int, cfg, gen: G
         tk = torch.arange(K2).view(1, -1).expand(rows, -1).clone()
         tk[:, 1:] += (tk[:, 1:] >= forced).long()  # placeholders distinct from the forced token
         tk[:, 0] = forced
-        if on_device:
-            return sc.to(logits.device), tk.to(device=logits.device, dtype=torch.int32)
         return sc, tk
     mask_eos = cur < gen.min_length
     br, bt = ngram_bans(run_seq.view(rows, -1)[:, :cur], gen.no_repeat_ngram_size)
@@ -128,27 +108,13 @@ def _select(logits: torch.Tensor, run_scores: torch.Tensor, K2: int, cfg, gen: G
     if logits.is_cuda and 0 < nban <= ops.MAX_BANS:
         # the kernel skips each row's banned tokens itself: exactly K2 per row come back
         starts = torch.cumsum(counts, 0) - counts
-        if bans_buf is not None:  # (pinned host, device) staging: async H2D, nothing waits for it
-            bh, bd = bans_buf
-            bans = bh[:rows * nban].view(rows, nban)
-            bans.fill_(-1)
-        else:
-            bans = torch.full((rows, nban), -1, dtype=torch.int32)
+        bans = torch.full((rows, nban), -1, dtype=torch.int32)
         bans[br, torch.arange(br.numel()) - starts[br]] = bt.to(torch.int32)
-        if bans_buf is not None:
-            bans_dev = bd[:rows * nban].view(rows, nban)
-            bans_dev.copy_(bans, non_blocking=True)
-        else:
-            bans_dev = bans.to(logits.device)
-        sc, tk = ops.beam_topk_rows(logits, scores_dev, K2, cfg.eos_id, mask_eos, bans=bans_dev)
-        if on_device:
-            return sc, tk
+        sc, tk = ops.beam_topk_rows(logits, scores_dev, K2, cfg.eos_id, mask_eos, bans=bans.to(logits.device))
         both = torch.cat([sc, tk.view(torch.float32)], 1).cpu()
         return both[:, :K2].contiguous(), both[:, K2:].contiguous().view(torch.int32).long()
     if K2 + nban <= 16:
         sc, tk = ops.beam_topk_rows(logits, scores_dev, K2 + nban, cfg.eos_id, mask_eos)
-        if on_device and nban == 0:
-            return sc, tk
         if sc.is_cuda:  # one D2H copy (one sync) for scores and token ids
             both = torch.cat([sc, tk.view(torch.float32)], 1).cpu()
             sc, tk = both[:, :K2 + nban].contiguous(), both[:, K2 + nban:].contiguous().view(torch.int32).long()
@@ -171,8 +137,6 @@ def _select(logits: torch.Tensor, run_scores: torch.Tensor, K2: int, cfg, gen: G
         lp[:, cfg.eos_id] = float("-inf")
     lp[br.to(lp.device), bt.to(lp.device)] = float("-inf")
     sc, tk = torch.topk(lp + scores_dev.view(-1, 1), K2, dim=-1)
-    if on_device:
-        return sc.contiguous(), tk.to(torch.int32).contiguous()
     return sc.cpu(), tk.cpu().long()
 
 
@@ -284,12 +248,16 @@ def _generate_iter(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
     # captured once and replayed: the host loop issues 1 launch per step.
     use_graph = gen.use_graph and dev.type == "cuda"
     graph, g_logits = None, None
+    seq_dev = seq_alt = None  # device token history (device selection with n-gram bans)
 
     def advance() -> torch.Tensor:
         """Histories follow their parent beams (backpointers, no KV copy), new tokens in,
         position + 1, decoder step -> logits. Static buffers only (graph-capturable)."""
         ops.beam_reorder_hist(hist, hist_alt, par_dev, step_dev)
         hist.copy_(hist_alt)  # keep the captured buffer address
+        if seq_dev is not None:  # token history for the in-kernel n-gram bans
+            ops.beam_reorder_hist(seq_dev, seq_alt, par_dev, step_dev, last=tok_dev, off=1)
+            seq_dev.copy_(seq_alt)
         tokens.copy_(tok_dev)
         step_dev.add_(1)
         return model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist)
@@ -359,52 +327,74 @@ def _generate_iter(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
     if pin and gen.device_select:
         yield  # let other runs start their encoders / first steps
         on_stream()
-        # Device selection: top-k -> beam_select -> next decoder step are enqueued back to
-        # back; the host folds step t's record into its state while the GPU runs step t+1
-        # (the sequences it needs for step t+1's n-gram bans are complete by then).
+        # Device selection: nothing the GPU needs for step t comes from the host (n-gram
+        # bans read the device token history, forced tokens the device beam scores), so
+        # top-k(t) -> beam_select(t) -> decoder step t+1 are enqueued FIRST and the host
+        # then folds step t-1's record into its state: the GPU always has a step queued
+        # behind the one it runs. Two pinned record slots alternate.
         rec_dev = torch.empty((B, 3 * K2 + nb), dtype=torch.int32, device=dev)
-        rec_host = torch.empty((B, 3 * K2 + nb), dtype=torch.int32, pin_memory=True)
-        rec_ev = torch.cuda.Event()
-        # n-gram ban staging (free again once the previous step's record event has passed)
-        bans_buf = ((torch.empty(rows * ops.MAX_BANS, dtype=torch.int32, pin_memory=True),
-                     torch.empty(rows * ops.MAX_BANS, dtype=torch.int32, device=dev))
-                    if gen.no_repeat_ngram_size else None)
-        pending = None
+        rec_host = [torch.empty((B, 3 * K2 + nb), dtype=torch.int32, pin_memory=True) for _ in range(2)]
+        rec_ev = [torch.cuda.Event(), torch.cuda.Event()]
+        forced_tk = {}
+        for fid in (gen.forced_bos_id, gen.forced_eos_id):
+            if fid is not None:
+                tk = torch.arange(K2).view(1, -1).expand(rows, -1).clone()
+                tk[:, 1:] += (tk[:, 1:] >= int(fid)).long()  # placeholders distinct from the forced token
+                tk[:, 0] = int(fid)
+                forced_tk[int(fid)] = tk.to(device=dev, dtype=torch.int32)
+
+        def select_dev(cur: int):
+            forced = None
+            if gen.forced_bos_id is not None and cur == 1:
+                forced = int(gen.forced_bos_id)
+            elif gen.forced_eos_id is not None and cur == T - 1:
+                forced = int(gen.forced_eos_id)
+            if forced is not None:  # the only allowed token gets log-prob 0
+                sc = torch.full((rows, K2), float("-inf"), device=dev)
+                sc[:, 0] = score_dev
+                return sc, forced_tk[forced]
+            ngram = (seq_dev, cur, gen.no_repeat_ngram_size) if seq_dev is not None else None
+            return ops.beam_topk_rows(logits, score_dev, K2, cfg.eos_id, cur < gen.min_length, ngram=ngram)
+
+        def record(slot: int):
+            r = rec_host[slot].numpy()
+            return (r[:, :K2].copy().view(np.float32), r[:, K2:2 * K2].astype(np.int64),
+                    r[:, 2 * K2:3 * K2].astype(np.int64), r[:, 3 * K2:].astype(np.int64))
+
+        if gen.no_repeat_ngram_size:
+            # running beams' tokens [rows, T], reordered by parents in advance() (graph)
+            seq_dev = torch.full((rows, T), cfg.pad_id, dtype=torch.int32, device=dev)
+            seq_dev[:, 0] = cfg.decoder_start_id
+            seq_alt = torch.zeros_like(seq_dev)
+        pending, slot = None, 0
         while True:
             tp0 = time.perf_counter()
-            if pending is not None:
-                yield  # other runs enqueue their next step while this one's selection lands
-                on_stream()
-                rec_ev.synchronize()
-                r = rec_host.numpy()
-                rs = (r[:, :K2].copy().view(np.float32), r[:, K2:2 * K2].astype(np.int64),
-                      r[:, 2 * K2:3 * K2].astype(np.int64), r[:, 3 * K2:].astype(np.int64))
-                steps += 1
-                if apply(pending, *rs):
-                    break
-            tp1 = time.perf_counter()
             with span("beam_select"):
-                sc_d, tk_d = _select(logits, torch.from_numpy(run_scores), K2, cfg, gen, cur, T,
-                                     torch.from_numpy(run_seq), scores_dev=score_dev, on_device=True,
-                                     bans_buf=bans_buf)
+                sc_d, tk_d = select_dev(cur)
                 ops.beam_select(sc_d, tk_d, nb, V, cfg.eos_id, cur + 1 >= T, NEG, stage_dev, rec_dev)
-                rec_host.copy_(rec_dev, non_blocking=True)
-                rec_ev.record()
-            pending = cur
+                rec_host[slot].copy_(rec_dev, non_blocking=True)
+                rec_ev[slot].record()
             if cur + 1 < T:
                 logits = launch_next()
+            tp1 = time.perf_counter()
+            if pending is not None:
+                yield  # other runs enqueue their steps while this one's record is folded in
+                on_stream()
+                rec_ev[pending[1]].synchronize()  # passed already: it precedes the running step
+                steps += 1
+                if apply(pending[0], *record(pending[1])):
+                    break
             tp2 = time.perf_counter()
             prof(tp0, tp1, tp2)
+            pending, slot = (cur, slot), slot ^ 1
             cur += 1
             if cur >= T:  # the last selection: fold it in and stop
-                rec_ev.synchronize()
-                r = rec_host.numpy()
+                rec_ev[pending[1]].synchronize()
                 steps += 1
-                apply(pending, r[:, :K2].copy().view(np.float32), r[:, K2:2 * K2].astype(np.int64),
-                      r[:, 2 * K2:3 * K2].astype(np.int64), r[:, 3 * K2:].astype(np.int64))
+                apply(pending[0], *record(pending[1]))
                 break
-        # an early stop leaves the speculatively launched step in flight: let it drain
-        # before its graph and buffers go out of scope
+        # an early stop leaves up to two speculatively launched steps in flight: let them
+        # drain before their graph and buffers go out of scope
         torch.cuda.current_stream(dev).synchronize()
     else:
         while True:

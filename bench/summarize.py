@@ -36,6 +36,7 @@ def main() -> int:
     ap.add_argument("--num-beams", type=int, default=4)
     ap.add_argument("--max-length", type=int, default=130)
     ap.add_argument("--min-length", type=int, default=30)
+    ap.add_argument("--no-repeat-ngram", type=int, default=None, help="override the model default (bart-large-cnn 3)")
     a = ap.parse_args()
 
     from agent_tpu_amd.runtime.summarize import GenConfig, SummarizeEngine, build_model, family_of
@@ -44,7 +45,8 @@ def main() -> int:
     dev = torch.device("cuda", 0)
     model, _ = build_model(a.model, device=dev, seed=0)
     eng = SummarizeEngine(model, max_source_len=a.src_len)
-    gen = GenConfig(num_beams=a.num_beams, max_length=a.max_length, min_length=a.min_length)
+    gen = GenConfig(num_beams=a.num_beams, max_length=a.max_length, min_length=a.min_length,
+                    no_repeat_ngram_size=a.no_repeat_ngram)
     docs = make_text_rows(a.docs * (a.warmup + a.steps), words_per_row=int(a.src_len * 0.8), seed=5)
 
     for w in range(a.warmup):

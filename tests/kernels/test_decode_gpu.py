@@ -141,6 +141,37 @@ def test_beam_topk_rows_ties(gpu, V, k):
         assert idx[r].tolist() == want.tolist(), r
 
 
+@pytest.mark.parametrize("n,cur", [(3, 40), (3, 2), (2, 17), (4, 64)])
+def test_beam_topk_rows_device_ngram(gpu, n, cur):
+    # n-gram bans computed in the kernel from the device token history == host processor;
+    # tokens drawn from a tiny alphabet so every row repeats its n-grams
+    R, V, T = 12, 4096, 70
+    logits = _r((R, V), gpu, 3.0, torch.float32, seed=51)
+    bs = _r((R,), gpu, 1.0, torch.float32, seed=52)
+    g = torch.Generator().manual_seed(53)
+    seq = torch.randint(0, 6, (R, T), generator=g, dtype=torch.int32)
+    logits[:, :6] += 20.0  # the banned candidates are the best raw ones
+    sc, idx = ops.beam_topk_rows(logits, bs, 8, eos=1, mask_eos=False, ngram=(seq.to(gpu), cur, n))
+    rsc, ridx = ops.beam_topk_rows(logits.cpu(), bs.cpu(), 8, eos=1, mask_eos=False, ngram=(seq, cur, n))
+    torch.testing.assert_close(sc.cpu(), rsc, atol=2e-4, rtol=1e-5)
+    assert torch.equal(idx.cpu(), ridx)
+
+
+def test_beam_reorder_token_history(gpu):
+    R, T = 10, 16
+    g = torch.Generator().manual_seed(3)
+    src = torch.randint(0, 100, (R, T), generator=g, dtype=torch.int32)
+    parent = torch.randint(0, R, (R,), generator=g, dtype=torch.int32)
+    tok = torch.randint(0, 100, (R,), generator=g, dtype=torch.int32)
+    for step in (0, 5, T - 2, T - 1):
+        st = torch.tensor([step], dtype=torch.int32)
+        want = torch.full((R, T), -7, dtype=torch.int32)
+        ops.beam_reorder_hist(src, want, parent, st, last=tok, off=1)
+        got = torch.full((R, T), -7, dtype=torch.int32, device=gpu)
+        ops.beam_reorder_hist(src.to(gpu), got, parent.to(gpu), st.to(gpu), last=tok.to(gpu), off=1)
+        assert torch.equal(got.cpu(), want), step
+
+
 @pytest.mark.parametrize("V,k,nb", [(50264, 8, 12), (32128, 8, 1), (4096, 3, 300)])
 def test_beam_topk_rows_bans(gpu, V, k, nb):
     # per-row banned tokens filtered inside the kernel: equal to the CPU path, and the

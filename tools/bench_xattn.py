@@ -26,3 +26,10 @@ lens = torch.full((a.docs,), S, dtype=torch.int32, device=dev)
 fn = lambda: ops.decode_attention(q, kv[:, :H * 64], kv[:, H * 64:], H, S, nb, lens=lens)  # noqa: E731
 t = statistics.median([timeit(fn, 20) for _ in range(5)])
 print(f"xattn docs={a.docs} beams={nb} S={S} H={H}: {t * 1e3:.1f} us ({kv.numel() * 2 / (t * 1e-3) / 1e12:.2f} TB/s)", flush=True)
+if os.getenv("XATTN_REF"):
+    red = lambda: kv.view(torch.int32).bitwise_xor_(torch.zeros(1, dtype=torch.int32, device=dev))  # noqa: E731
+    t2 = statistics.median([timeit(red, 20) for _ in range(5)])
+    s = lambda: torch.amax(kv, dim=0)  # noqa: E731
+    t3 = statistics.median([timeit(s, 20) for _ in range(5)])
+    print(f"ref: in-place xor (read+write) {kv.numel() * 4 / (t2 * 1e-3) / 1e12:.2f} TB/s, amax read "
+          f"{kv.numel() * 2 / (t3 * 1e-3) / 1e12:.2f} TB/s", flush=True)
