@@ -16,12 +16,14 @@
 //    into the cache at step t (t read from device memory -> graph friendly).
 //  * beam_reorder_hist: hist'[r][j] = hist[parent[r]][j] (j < t), hist'[r][t]
 //    = parent[r]; the O(rows*T) int gather replaces an O(rows*T*L*2d) copy.
+//    The same kernel keeps the running beams' token history (n-gram bans).
 //  * gather_rows: explicit cache reorder (kept for callers without hist).
 //  * beam_topk_rows: per beam row, ONE pass over the logits computes the
-//    online max / sum-exp (log-softmax normaliser) and a per-thread top-K
-//    (register lists with compile-time indexing only -> no scratch), then
-//    wave-level argmax rounds merge them; the union over an item's beams
-//    contains the item's global top-k (merged on the host).
+//    online max / sum-exp (log-softmax normaliser) and each wave's exact top-K
+//    (candidates >= a rising threshold kept in LDS, cut back when full), then
+//    wave-level argmax rounds merge the waves; the union over an item's beams
+//    contains the item's global top-k (beam_select).
+//  * beam_select: per item, the global top-2nb and the next running beams.
 #include "atpu/common.h"
 #include "atpu/kernels.h"
 
