@@ -586,9 +586,23 @@ __global__ __launch_bounds__(kTopkThreads) void beam_topk_kernel(const float* __
         lm[u] = fmaxf(fmaxf(v[u].x, v[u].y), fmaxf(v[u].z, v[u].w));
       }
     }
-    // first chunk: no candidates yet; K lanes hold values >= the K-th largest lane
-    // maximum (banned tokens would not count: rows with bans start from -FLT_MAX)
-    if (!BANS && jb == 0) thr = kth_lane_max(fmaxf(fmaxf(lm[0], lm[1]), fmaxf(lm[2], lm[3])));
+    // first chunk: no candidates yet; K lanes hold allowed values >= the K-th largest
+    // lane maximum (banned values are dropped from this chunk's selection first)
+    if (jb == 0) {
+      if (BANS) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i = 4 * (jb + tid + u * kTopkThreads);
+          auto banned = [&](int t) { return t < V && ((ban_bits[t >> 5] >> (t & 31)) & 1u); };
+          if (banned(i)) v[u].x = -FLT_MAX;
+          if (banned(i + 1)) v[u].y = -FLT_MAX;
+          if (banned(i + 2)) v[u].z = -FLT_MAX;
+          if (banned(i + 3)) v[u].w = -FLT_MAX;
+          lm[u] = fmaxf(fmaxf(v[u].x, v[u].y), fmaxf(v[u].z, v[u].w));
+        }
+      }
+      thr = kth_lane_max(fmaxf(fmaxf(lm[0], lm[1]), fmaxf(lm[2], lm[3])));
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       // a float4 of the wave enters the per-value path only if one of its values can
