@@ -32,6 +32,15 @@ enum GemmEpilogue : int {
   kEpiRowRms = 512,    // A rows are raw RMSNorm inputs (gamma folded into Bt): the kernel sums A^2
                        //   over its K loop, C = rsqrt(mean_k A^2 + rms_eps) * (A . Bt^T) ... (128x128 and
                        //   skinny "dec" kernels, no split-K; T5 decoder steps)
+  // LayerNorm folding for decode steps (post-LN decoders, BART; 128x128 and "dec" kernels,
+  // no split-K). Row statistics travel as partial (sum, sumsq) per 32-column slab:
+  kEpiRowLn = 2048,     // A rows are raw LN inputs, gamma folded into Bt, beta into bias:
+                        //   C = rstd*acc - rstd*mu*colsum + bias, (mu, rstd) of A's rows from in_part
+                        //   [K/32][M][2] (eps in rms_eps)
+  kEpiResLn = 4096,     // R rows are raw LN inputs (beta folded into bias), stats from res_part
+                        //   [N/32][M][2]: C = ... + (R*rstd - rstd*mu) * gamma
+  kEpiRowStats = 8192,  // also write part_out [N/32][M][2]: (sum, sumsq) of the bf16-rounded C
+                        //   values of each row's 32-column slabs
 };
 
 struct GemmArgs {
@@ -55,6 +64,8 @@ struct GemmArgs {
   const float* res_fin = nullptr;  // ResNorm: [M][2] (rstd, rstd*mu) of R's rows
   const float* gamma = nullptr;    // ResNorm: [N] LN gamma of R
   float* part_out = nullptr;       // StatsOut: [N/256][M][2] partial (sum, sumsq) of C's rows (fp32 values)
+  const float* in_part = nullptr;   // RowLn: [K/32][M][2] (sum, sumsq) partials of A's rows (+ colsum)
+  const float* res_part = nullptr;  // ResLn: [N/32][M][2] partials of R's rows (+ gamma); RowStats: part_out
   float rms_eps = 0.f;             // RowRms
   bf16* kv_cache = nullptr;        // KvScatter: cache [rows * kv_T, kv_ld]
   int kv_ld = 0, kv_T = 0, kv_col0 = 0;

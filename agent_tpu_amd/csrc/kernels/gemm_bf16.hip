@@ -68,11 +68,56 @@ __device__ __forceinline__ float sumsq_bf16x8(bf16x8 a, float acc) {
   return acc;
 }
 
+// Decode LayerNorm folding (kEpiRowLn / kEpiResLn / kEpiRowStats; GemmArgs fields of the
+// same names). A row's statistics travel as partial (sum, sumsq) per 32-column slab, written
+// by the epilogue of the GEMM that produced the row (RowStats) and summed by its consumers:
+// no K-loop VALU work in the consumers, no LayerNorm pass between them.
+struct LnDec {
+  const float* colsum = nullptr;    // RowLn: [N] column sums of the gamma-folded weights
+  const float* in_part = nullptr;   // RowLn: [K/32][M][2] partials of A's rows
+  const float* res_part = nullptr;  // ResLn: [N/32][M][2] partials of R's rows
+  const float* gamma = nullptr;     // ResLn: [N] LN gamma of R
+  float* part_out = nullptr;        // RowStats: [N/32][M][2] partials of C's rows (bf16-rounded values)
+};
+
+// Row partials of a width <= 1024 row (<= 32 slots): the 4 lanes of the row (fchunk 0-3)
+// take slots fchunk, fchunk + 4, ... Loaded at kernel start (every load in flight at once,
+// landing under the K loop), reduced in the epilogue.
+constexpr int kPartPerLane = 8;
+__device__ __forceinline__ void part_prefetch(float2 (&v)[kPartPerLane], const float* part, int slots, int M, int m,
+                                              int fchunk) {
+  // unconditional loads (a clamped slot; part_ln drops the extras): a conditional load per
+  // slot became a branch per slot and hipcc drained vmcnt at the joins
+  const size_t mc = min(m, M - 1);
+#pragma unroll
+  for (int t = 0; t < kPartPerLane; ++t) {
+    const int k = min(fchunk + 4 * t, slots - 1);
+    v[t] = *reinterpret_cast<const float2*>(part + 2 * ((size_t)k * M + mc));
+  }
+}
+// (rstd, rstd*mu) of the row from its prefetched partials; every lane of the row gets it.
+// Variance as E[x^2] - mu^2 in fp32, clamped at 0. Call with all 4 lanes of the row active.
+__device__ __forceinline__ float2 part_ln(const float2 (&v)[kPartPerLane], int slots, int fchunk, float eps) {
+  float s = 0.f, q = 0.f;
+#pragma unroll
+  for (int t = 0; t < kPartPerLane; ++t) {
+    const bool in = fchunk + 4 * t < slots;
+    s += in ? v[t].x : 0.f;
+    q += in ? v[t].y : 0.f;
+  }
+  const float inv = 1.f / (32 * slots);
+  const float mu = lane_rows_sum(s) * inv;
+  const float var = fmaxf(lane_rows_sum(q) * inv - mu * mu, 0.f);
+  const float rs = __builtin_amdgcn_rsqf(var + eps);
+  return float2{rs, rs * mu};
+}
+
 template <int BM, int BN, int WM, int WN, int EPI, int SPLIT = 0>
 __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
     const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C, int ldc,
     const float* __restrict__ bias, const bf16* __restrict__ R, int ldr, int M, int N, int K,
-    float* __restrict__ ws = nullptr, float rms_eps = 0.f, KvOut kvo = {}) {
+    float* __restrict__ ws = nullptr, float rms_eps = 0.f, KvOut kvo = {}, LnDec ln = {}) {
+  static_assert(!(SPLIT && (EPI & (kEpiRowRms | kEpiRowLn | kEpiResLn))), "row statistics need the whole K loop");
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 16;
   constexpr int TN = BN / WN / 16;
@@ -132,6 +177,15 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int frow = lane & 15, fchunk = lane >> 4;
+  // RowLn / ResLn: the rows' partials, loaded before the K loop
+  constexpr bool kPart = EPI & (kEpiRowLn | kEpiResLn);
+  float2 pv[kPart ? TM : 1][kPartPerLane];
+  const int pslots = (EPI & kEpiRowLn) ? K / 32 : N / 32;
+  if constexpr (kPart) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+      part_prefetch(pv[i], (EPI & kEpiRowLn) ? ln.in_part : ln.res_part, pslots, M, m0 + arow0 + i * 16 + frow, fchunk);
+  }
   float ssq[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) ssq[i] = 0.f;
@@ -187,20 +241,39 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
 
   // ---- epilogue: lane owns C[m][n..n+3] for each (i, j) fragment ----
   const int kv_pos = (EPI & kEpiKvScatter) ? max(*kvo.step, 0) : 0;
-  float rstd[TM];
+  float rstd[TM], rmu[TM];
+  float2 rfs[TM];
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int i = 0; i < TM; ++i) {
     rstd[i] = (EPI & kEpiRowRms) ? __builtin_amdgcn_rsqf(lane_rows_sum(ssq[i]) * (1.f / K) + rms_eps) : 1.f;
+    rmu[i] = 0.f;
+    rfs[i] = float2{1.f, 0.f};
+    if constexpr (EPI & kEpiRowLn) {
+      const float2 st = part_ln(pv[i], pslots, fchunk, rms_eps);
+      rstd[i] = st.x;
+      rmu[i] = st.y;
+    }
+    if constexpr (EPI & kEpiResLn) rfs[i] = part_ln(pv[i], pslots, fchunk, rms_eps);
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = m0 + arow0 + i * 16 + frow;
     if (m >= M) continue;
+    const float2 rf = rfs[i];
+    float ps[(TN + 1) / 2], pss[(TN + 1) / 2];  // RowStats: this lane's share of each 32-column slab
+#pragma unroll
+    for (int h = 0; h < (TN + 1) / 2; ++h) ps[h] = pss[h] = 0.f;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = n0 + brow0 + j * 16 + fchunk * 4;
       if (n >= N) continue;
       f32x4 v = acc[i][j];
       if constexpr (EPI & kEpiRowRms) v *= rstd[i];
+      if constexpr (EPI & kEpiRowLn) {
+        const f32x4 cs = *reinterpret_cast<const f32x4*>(ln.colsum + n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaf(v[e], rstd[i], -rmu[i] * cs[e]);
+      }
       if constexpr (EPI & kEpiBias) {
         const f32x4 b = *reinterpret_cast<const f32x4*>(bias + n);
         v += b;
@@ -219,8 +292,14 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
       }
       if constexpr (EPI & kEpiResidual) {
         const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + n);
+        if constexpr (EPI & kEpiResLn) {
+          const f32x4 g = *reinterpret_cast<const f32x4*>(ln.gamma + n);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += bf2f(r[e]);
+          for (int e = 0; e < 4; ++e) v[e] = fmaf(fmaf(bf2f(r[e]), rf.x, -rf.y), g[e], v[e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += bf2f(r[e]);
+        }
       }
       if constexpr (EPI & kEpiOutF32) {
         *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + (size_t)m * ldc + n) = v;
@@ -238,6 +317,22 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
         } else {
           *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
         }
+        if constexpr (EPI & kEpiRowStats) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float f = bf2f(o[e]);
+            ps[j / 2] += f;
+            pss[j / 2] = fmaf(f, f, pss[j / 2]);
+          }
+        }
+      }
+    }
+    if constexpr (EPI & kEpiRowStats) {
+#pragma unroll
+      for (int h = 0; h < (TN + 1) / 2; ++h) {
+        const float S = lane_rows_sum(ps[h]), Q = lane_rows_sum(pss[h]);
+        const int col = n0 + brow0 + h * 32;
+        if (fchunk == 0 && col < N) *reinterpret_cast<float2*>(ln.part_out + 2 * ((size_t)(col / 32) * M + m)) = float2{S, Q};
       }
     }
   }
@@ -1569,8 +1664,8 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
                                                           int ldc, const float* __restrict__ bias,
                                                           const bf16* __restrict__ R, int ldr, int M, int N, int K,
                                                           float* __restrict__ ws, float rms_eps = 0.f,
-                                                          KvOut kvo = {}) {
-  static_assert(!(SPLIT && (EPI & kEpiRowRms)), "RowRms needs the whole K loop in one block");
+                                                          KvOut kvo = {}, LnDec ln = {}) {
+  static_assert(!(SPLIT && (EPI & (kEpiRowRms | kEpiRowLn | kEpiResLn))), "row statistics need the whole K loop");
   constexpr int BM = 64, BN = 64;
   constexpr int STAGE = (BM + BN) * kRowBytes;  // 16 KiB: A rows 0-63, B rows 64-127
   constexpr int LPS = (BM + BN) / 8 / 4;        // DMA instructions per wave per stage (4)
@@ -1608,6 +1703,15 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
 
   const int wm = wave >> 1, wn = wave & 1;
   const int frow = lane & 15, fchunk = lane >> 4;
+  // RowLn / ResLn: the rows' partials, loaded before the K loop
+  constexpr bool kPart = EPI & (kEpiRowLn | kEpiResLn);
+  float2 pv[kPart ? 2 : 1][kPartPerLane];
+  const int pslots = (EPI & kEpiRowLn) ? K / 32 : N / 32;
+  if constexpr (kPart) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      part_prefetch(pv[i], (EPI & kEpiRowLn) ? ln.in_part : ln.res_part, pslots, M, m0 + wm * 32 + i * 16 + frow, fchunk);
+  }
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -1671,20 +1775,37 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
     return;
   }
   const int kv_pos = (EPI & kEpiKvScatter) ? max(*kvo.step, 0) : 0;
-  float rstd[2];
+  float rstd[2], rmu[2];
+  float2 rfs[2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 2; ++i) {
     rstd[i] = (EPI & kEpiRowRms) ? __builtin_amdgcn_rsqf(lane_rows_sum(ssq[i]) * (1.f / K) + rms_eps) : 1.f;
+    rmu[i] = 0.f;
+    rfs[i] = float2{1.f, 0.f};
+    if constexpr (EPI & kEpiRowLn) {
+      const float2 st = part_ln(pv[i], pslots, fchunk, rms_eps);
+      rstd[i] = st.x;
+      rmu[i] = st.y;
+    }
+    if constexpr (EPI & kEpiResLn) rfs[i] = part_ln(pv[i], pslots, fchunk, rms_eps);
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int m = m0 + wm * 32 + i * 16 + frow;
     if (m >= M) continue;
+    const float2 rf = rfs[i];
+    float ps = 0.f, pss = 0.f;  // RowStats: this lane's share of the wave's 32-column slab
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int n = n0 + wn * 32 + j * 16 + fchunk * 4;
       if (n >= N) continue;
       f32x4 v = acc[i][j];
       if constexpr (EPI & kEpiRowRms) v *= rstd[i];
+      if constexpr (EPI & kEpiRowLn) {
+        const f32x4 cs = *reinterpret_cast<const f32x4*>(ln.colsum + n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaf(v[e], rstd[i], -rmu[i] * cs[e]);
+      }
       if constexpr (EPI & kEpiBias) v += *reinterpret_cast<const f32x4*>(bias + n);
       if constexpr (EPI & kEpiGelu) {
 #pragma unroll
@@ -1700,8 +1821,14 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
       }
       if constexpr (EPI & kEpiResidual) {
         const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + n);
+        if constexpr (EPI & kEpiResLn) {
+          const f32x4 g = *reinterpret_cast<const f32x4*>(ln.gamma + n);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += bf2f(r[e]);
+          for (int e = 0; e < 4; ++e) v[e] = fmaf(fmaf(bf2f(r[e]), rf.x, -rf.y), g[e], v[e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += bf2f(r[e]);
+        }
       }
       if constexpr (EPI & kEpiOutF32) {
         *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + (size_t)m * ldc + n) = v;
@@ -1719,7 +1846,20 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
         } else {
           *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
         }
+        if constexpr (EPI & kEpiRowStats) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float f = bf2f(o[e]);
+            ps += f;
+            pss = fmaf(f, f, pss);
+          }
+        }
       }
+    }
+    if constexpr (EPI & kEpiRowStats) {
+      const float S = lane_rows_sum(ps), Q = lane_rows_sum(pss);
+      const int col = n0 + wn * 32;
+      if (fchunk == 0 && col < N) *reinterpret_cast<float2*>(ln.part_out + 2 * ((size_t)(col / 32) * M + m)) = float2{S, Q};
     }
   }
 }
@@ -1735,9 +1875,16 @@ void launch_dec(const GemmArgs& g, hipStream_t s) {
   case E:                                                                                                      \
     hipLaunchKernelGGL((gemm_dec_kernel<E, kDecStages, 0>), grid, block, 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, \
                        g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, nullptr, g.rms_eps,                          \
-                       KvOut{g.kv_cache, g.kv_ld, g.kv_T, g.kv_col0, g.kv_step});                             \
+                       KvOut{g.kv_cache, g.kv_ld, g.kv_T, g.kv_col0, g.kv_step},                              \
+                       LnDec{g.colsum, g.in_part, g.res_part, g.gamma, g.part_out});                        \
     break;
   switch (g.epi) {
+    ATPU_DEC_CASE(kEpiRowLn | kEpiBias | kEpiKvScatter)
+    ATPU_DEC_CASE(kEpiRowLn | kEpiBias)
+    ATPU_DEC_CASE(kEpiRowLn | kEpiBias | kEpiGelu)
+    ATPU_DEC_CASE(kEpiBias | kEpiResidual | kEpiResLn | kEpiRowStats)
+    ATPU_DEC_CASE(kEpiBias | kEpiResidual | kEpiRowStats)
+    ATPU_DEC_CASE(kEpiBias | kEpiResidual | kEpiResLn)
     ATPU_DEC_CASE(kEpiRowRms | kEpiKvScatter)
     ATPU_DEC_CASE(kEpiBias | kEpiKvScatter)
     ATPU_DEC_CASE(kEpiRowRms)
@@ -1844,9 +1991,16 @@ void launch_tile(const GemmArgs& g, hipStream_t s) {
   case E:                                                                                             \
     hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, E>), grid, block, 0, s, g.A, g.lda, g.Bt, g.ldb, \
                        g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, nullptr, g.rms_eps,              \
-                       KvOut{g.kv_cache, g.kv_ld, g.kv_T, g.kv_col0, g.kv_step});                     \
+                       KvOut{g.kv_cache, g.kv_ld, g.kv_T, g.kv_col0, g.kv_step},                      \
+                       LnDec{g.colsum, g.in_part, g.res_part, g.gamma, g.part_out});                \
     break;
   switch (g.epi) {
+    ATPU_GEMM_CASE(kEpiRowLn | kEpiBias | kEpiKvScatter)
+    ATPU_GEMM_CASE(kEpiRowLn | kEpiBias)
+    ATPU_GEMM_CASE(kEpiRowLn | kEpiBias | kEpiGelu)
+    ATPU_GEMM_CASE(kEpiBias | kEpiResidual | kEpiResLn | kEpiRowStats)
+    ATPU_GEMM_CASE(kEpiBias | kEpiResidual | kEpiRowStats)
+    ATPU_GEMM_CASE(kEpiBias | kEpiResidual | kEpiResLn)
     ATPU_GEMM_CASE(kEpiRowRms | kEpiKvScatter)
     ATPU_GEMM_CASE(kEpiBias | kEpiKvScatter)
     ATPU_GEMM_CASE(kEpiRowRms)
@@ -1964,7 +2118,8 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
   // ATPU_GEMM_TILE=128|256 forces one (benchmarks/tests).
   const int forced = gemm_force_tile(-1);
   if (g.splits > 1) {
-    ATPU_CHECK(!(g.epi & (kEpiRowRms | kEpiKvScatter)), "gemm: RowRms / KvScatter cannot split K");
+    ATPU_CHECK(!(g.epi & (kEpiRowRms | kEpiKvScatter | kEpiRowLn | kEpiResLn | kEpiRowStats)),
+               "gemm: RowRms / RowLn / ResLn / KvScatter cannot split K");
     ATPU_CHECK(g.ws && (g.K / kBK) % g.splits == 0, "gemm: split-K needs a workspace and K/64 % splits == 0");
     launch_splitk(g, g.splits, gemm_dec_mode(-1) == 1 && skinny(g.M, g.N), stream);
     ATPU_HIP_CHECK(hipGetLastError());
@@ -1998,16 +2153,34 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
     // decode QKV straight into the KV cache (128x128 / dec kernels; every 64- and
     // 128-column tile must be all Q or all K|V)
     const int fe = g.epi & ~kEpiKvScatter;
-    ATPU_CHECK(fe == kEpiRowRms || fe == kEpiBias, "gemm: unsupported KvScatter epilogue " + std::to_string(g.epi));
+    ATPU_CHECK(fe == kEpiRowRms || fe == kEpiBias || fe == (kEpiRowLn | kEpiBias),
+               "gemm: unsupported KvScatter epilogue " + std::to_string(g.epi));
     ATPU_CHECK(g.kv_cache && g.kv_step && g.kv_T > 0 && g.kv_col0 % 128 == 0 && g.kv_col0 > 0 && g.kv_col0 < g.N &&
                    g.kv_ld >= g.N - g.kv_col0 && g.kv_ld % 4 == 0,
                "gemm: KvScatter needs a cache, a device step, kv_col0 % 128 == 0 and kv_ld >= N - kv_col0");
   }
-  if (g.epi & (kEpiRowRms | kEpiKvScatter)) {
-    // RMSNorm folded into the GEMM (T5 decoder steps): the 128x128 and skinny kernels
-    // sum the A rows' squares over their whole K loop (no split-K)
+  if (g.epi & (kEpiRowLn | kEpiResLn | kEpiRowStats)) {
+    // decode LayerNorm folding (BART decoder steps): producers write per-row partials
+    // (RowStats), RowLn consumers normalise their A rows and ResLn consumers their
+    // residual rows from those partials
+    const int fe = g.epi & ~kEpiKvScatter;
+    ATPU_CHECK(fe == (kEpiRowLn | kEpiBias) || fe == (kEpiRowLn | kEpiBias | kEpiGelu) ||
+                   (!(g.epi & kEpiKvScatter) && (fe == (kEpiBias | kEpiResidual | kEpiResLn | kEpiRowStats) ||
+                                                 fe == (kEpiBias | kEpiResidual | kEpiRowStats) ||
+                                                 fe == (kEpiBias | kEpiResidual | kEpiResLn))),
+               "gemm: unsupported decode LayerNorm-folding epilogue " + std::to_string(g.epi));
+    ATPU_CHECK(!(fe & kEpiRowLn) || (g.colsum && g.in_part && g.K <= 1024), "gemm: RowLn needs colsum, in_part, K <= 1024");
+    ATPU_CHECK(!(fe & kEpiResLn) || (g.res_part && g.gamma && g.N <= 1024 && g.N % 32 == 0),
+               "gemm: ResLn needs res_part, gamma, N <= 1024");
+    ATPU_CHECK(!(fe & (kEpiRowLn | kEpiResLn)) || g.rms_eps > 0.f, "gemm: RowLn / ResLn need eps > 0");
+    ATPU_CHECK(!(fe & kEpiRowStats) || (g.part_out && g.N % 32 == 0), "gemm: RowStats needs part_out and N % 32 == 0");
+  }
+  if (g.epi & (kEpiRowRms | kEpiKvScatter | kEpiRowLn | kEpiResLn | kEpiRowStats)) {
+    // RMSNorm / LayerNorm folded into the GEMM (T5 / BART decoder steps): the 128x128 and
+    // skinny kernels sum the A rows' statistics over their whole K loop (no split-K)
     const int fe = g.epi & ~(kEpiRowRms | kEpiKvScatter);
-    ATPU_CHECK(fe == 0 || fe == kEpiRelu || fe == kEpiOutF32 || fe == kEpiBias,
+    ATPU_CHECK(fe == 0 || fe == kEpiRelu || fe == kEpiOutF32 || fe == kEpiBias ||
+                   (g.epi & (kEpiRowLn | kEpiResLn | kEpiRowStats)),
                "gemm: unsupported RowRms / KvScatter epilogue " + std::to_string(g.epi));
     ATPU_CHECK(!(g.epi & kEpiRowRms) || g.rms_eps > 0.f, "gemm: RowRms needs rms_eps > 0");
     if (forced == 64 || (forced != 128 && gemm_dec_mode(-1) == 1 && skinny(g.M, g.N)))

@@ -23,12 +23,34 @@ _ACTS = {None: 0, "none": 0, "gelu": EPI_GELU, "tanh": EPI_TANH, "relu": EPI_REL
 
 EPI_ROW_RMS = 512
 EPI_KV_SCATTER = 1024
+EPI_ROW_LN, EPI_RES_LN, EPI_ROW_STATS = 2048, 4096, 8192
 
 
-def linear_ref(x, w, bias=None, act=None, residual=None, out_f32=False, rms_eps=None):
+def row_parts_ref(y: torch.Tensor) -> torch.Tensor:
+    """[N/32, M, 2] per-row (sum, sum of squares) of ``y`` over each 32-column slab (fp32)."""
+    M, N = y.shape
+    t = y.float().view(M, N // 32, 32).transpose(0, 1)
+    return torch.stack([t.sum(-1), (t * t).sum(-1)], -1).contiguous()
+
+
+def row_ln_from_parts_ref(part: torch.Tensor, eps: float) -> torch.Tensor:
+    """[M, 2] (rstd, rstd*mu) of rows of width 32 * slots from their partials (as the kernels)."""
+    s = part.float().sum(0)
+    K = 32 * part.shape[0]
+    mu = s[:, 0] / K
+    rs = torch.rsqrt((s[:, 1] / K - mu * mu).clamp_min(0.0) + eps)
+    return torch.stack([rs, rs * mu], -1)
+
+
+def linear_ref(x, w, bias=None, act=None, residual=None, out_f32=False, rms_eps=None, row_ln=None, res_ln=None,
+               stats_out=None):
     y = x.float() @ w.float().t()
     if rms_eps is not None:
         y = y * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + rms_eps)
+    if row_ln is not None:
+        eps, colsum, in_part = row_ln
+        st = row_ln_from_parts_ref(in_part, eps)
+        y = y * st[:, :1] - st[:, 1:] * colsum.float().unsqueeze(0)
     if bias is not None:
         y = y + bias.float()
     if act == "gelu":
@@ -38,8 +60,16 @@ def linear_ref(x, w, bias=None, act=None, residual=None, out_f32=False, rms_eps=
     elif act == "relu":
         y = torch.relu(y)
     if residual is not None:
-        y = y + residual.float()
-    return y if out_f32 else y.to(x.dtype)
+        r = residual.float()
+        if res_ln is not None:
+            eps, res_part, gamma = res_ln
+            st = row_ln_from_parts_ref(res_part, eps)
+            r = (r * st[:, :1] - st[:, 1:]) * gamma.float().unsqueeze(0)
+        y = y + r
+    y = y if out_f32 else y.to(x.dtype)
+    if stats_out is not None:
+        stats_out.copy_(row_parts_ref(y))
+    return y
 
 
 @functools.lru_cache(maxsize=4096)
@@ -49,7 +79,8 @@ def _splits(M: int, N: int, K: int) -> int:
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: Optional[str] = None,
            residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-           out_f32: bool = False, rms_eps: Optional[float] = None, kv_cache=None) -> torch.Tensor:
+           out_f32: bool = False, rms_eps: Optional[float] = None, kv_cache=None, row_ln=None,
+           res_ln=None, stats_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``act(x @ w.T + bias) + residual``; ``out_f32`` returns fp32 (LM-head logits).
 
     ``rms_eps``: ``x`` rows are raw RMSNorm inputs and ``w`` carries the norm's gamma
@@ -58,8 +89,44 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 
     ``kv_cache = (cache, T, step, col0)`` (decode QKV): output columns ``>= col0`` (K|V)
     are written to ``cache[m*T + step, :]`` (``step`` a 1-element int32 device tensor),
-    the Q columns to ``out [M, col0]``, which is returned (no kv_append pass)."""
+    the Q columns to ``out [M, col0]``, which is returned (no kv_append pass).
+
+    Decode LayerNorm folding (post-LN decoder steps; :func:`fold_ln_into_linear`). Row
+    statistics travel as partial (sum, sumsq) per 32-column slab, ``[width/32, M, 2]`` fp32:
+    ``stats_out``: write the partials of the (bf16-rounded) output rows;
+    ``row_ln = (eps, colsum, in_part)``: ``x`` rows are raw LN inputs with partials ``in_part``,
+    ``w``/``bias`` folded: ``y = rstd*(x @ w.T) - rstd*mu*colsum + bias``;
+    ``res_ln = (eps, res_part, gamma)``: ``residual`` rows are raw LN inputs with partials
+    ``res_part``, added as ``(r - mu)*rstd*gamma`` (beta folded into ``bias``)."""
     check(act in _ACTS, f"unknown activation {act!r}")
+    M0, N0 = x.shape[0], w.shape[0]
+
+    def parts(t, width, name):
+        check(t.dtype == torch.float32 and t.is_contiguous() and tuple(t.shape) == (width // 32, M0, 2),
+              f"linear: {name} must be contiguous fp32 [{width // 32}, {M0}, 2]")
+
+    if row_ln is not None:
+        eps, colsum, in_part = row_ln
+        check(rms_eps is None and residual is None and bias is not None and act in (None, "none", "gelu")
+              and not out_f32 and stats_out is None, "linear: row_ln takes a bias, no residual, at most a GELU")
+        check(eps > 0, "linear: row_ln eps must be > 0")
+        check(colsum.dtype == torch.float32 and colsum.is_contiguous() and colsum.numel() == N0,
+              "linear: row_ln colsum must be contiguous fp32 [N]")
+        parts(in_part, x.shape[1], "row_ln in_part")
+        check(x.shape[1] <= 1024, "linear: row_ln rows must be <= 1024 wide")
+    if res_ln is not None:
+        eps, res_part, gamma = res_ln
+        check(residual is not None and bias is not None and act in (None, "none") and kv_cache is None
+              and rms_eps is None and row_ln is None and not out_f32, "linear: res_ln takes a bias and a residual only")
+        check(eps > 0, "linear: res_ln eps must be > 0")
+        parts(res_part, N0, "res_ln res_part")
+        check(N0 <= 1024, "linear: res_ln rows must be <= 1024 wide")
+        check(gamma.dtype == torch.float32 and gamma.is_contiguous() and gamma.numel() == N0,
+              "linear: res_ln gamma must be contiguous fp32 [N]")
+    if stats_out is not None:
+        check(residual is not None and bias is not None and act in (None, "none") and kv_cache is None
+              and rms_eps is None and not out_f32 and N0 % 32 == 0, "linear: stats_out takes a bias and a residual only")
+        parts(stats_out, N0, "stats_out")
     if kv_cache is not None:
         cache, T, step, col0 = kv_cache
         N0 = w.shape[0]
@@ -68,7 +135,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         check(cache.dim() == 2 and cache.shape[1] >= N0 - col0 and cache.shape[0] == x.shape[0] * T
               and cache.dtype == torch.bfloat16, "linear: cache must be bf16 [M*T, >= N-col0]")
         if not x.is_cuda:
-            y = linear_ref(x, w, bias, act, None, False, rms_eps)
+            y = linear_ref(x, w, bias, act, None, False, rms_eps, row_ln)
             rows = torch.arange(x.shape[0]) * T + int(step.reshape(-1)[0])
             cache[rows, :N0 - col0] = y[:, col0:]
             q = y[:, :col0]
@@ -78,7 +145,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
               "linear: rms_eps takes no bias / residual and only a ReLU")
         check(rms_eps > 0, "linear: rms_eps must be > 0")
     if not x.is_cuda:
-        y = linear_ref(x, w, bias, act, residual, out_f32, rms_eps)
+        y = linear_ref(x, w, bias, act, residual, out_f32, rms_eps, row_ln, res_ln, stats_out)
         if out is not None:
             out.copy_(y)
             return out
@@ -115,15 +182,35 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         check(step.dtype == torch.int32, "linear: kv step must be an int32 device tensor")
         epi |= EPI_KV_SCATTER
         kv_args = (ptr(cache), row_stride(cache, "cache"), int(T), int(col0), ptr(step))
-    if rms_eps is not None or kv_cache is not None:
+    ln_args = [0, 0, 0, 0, 0]  # colsum, in_part, res_part, gamma, part_out
+    eps_arg = float(rms_eps or 0.0)
+    if row_ln is not None:
+        eps, colsum, in_part = row_ln
+        same_device(x, colsum, in_part)
+        epi |= EPI_ROW_LN
+        eps_arg = float(eps)
+        ln_args[0], ln_args[1] = ptr(colsum), ptr(in_part)
+    if res_ln is not None:
+        eps, res_part, gamma = res_ln
+        same_device(x, res_part, gamma)
+        epi |= EPI_RES_LN
+        eps_arg = float(eps)
+        ln_args[2], ln_args[3] = ptr(res_part), ptr(gamma)
+    if stats_out is not None:
+        same_device(x, stats_out)
+        epi |= EPI_ROW_STATS
+        ln_args[4] = ptr(stats_out)
+    if rms_eps is not None or kv_cache is not None or row_ln is not None or res_ln is not None or stats_out is not None:
         if rms_eps is not None:
             epi |= EPI_ROW_RMS
         splits = 1
     else:
         splits = _splits(M, N, K)
     ws = torch.empty(splits * M * N, dtype=torch.float32, device=x.device) if splits > 1 else None
+    if not kv_args:
+        kv_args = (0, 0, 0, 0, 0)
     native().gemm(ptr(x), lda, ptr(w), ldb, ptr(out), ldc, ptr(bias), ptr(residual), ldr, M, N, K, epi,
-                  stream_handle(), splits, ptr(ws), float(rms_eps or 0.0), *kv_args)
+                  stream_handle(), splits, ptr(ws), eps_arg, *kv_args, *ln_args)
     return out
 
 

@@ -79,3 +79,55 @@ def test_folded_encoder_equals_layernorm_encoder_fp32():
         ref = m.encode(ids, lens, cls_only_last=cls_only)
         got = m.encode_folded(ids, lens, cls_only_last=cls_only)
         torch.testing.assert_close(got, ref, rtol=2e-4, atol=2e-4)
+
+
+def test_decode_row_ln_and_res_ln_equal_ln_then_linear():
+    # decode LayerNorm folding (ops.linear stats_out / row_ln / res_ln, the BART decoder
+    # step): the producer writes per-32-column row partials, both consumers normalise from them
+    g = torch.Generator().manual_seed(7)
+    M, K, N = 12, 256, 96
+    ctx0, W0, b0 = torch.randn(M, 64, generator=g), torch.randn(K, 64, generator=g) * 0.05, torch.zeros(K)
+    res = torch.randn(M, K, generator=g) * 2 + 0.3
+    part = torch.empty(K // 32, M, 2)
+    x = ops.linear(ctx0, W0, b0, residual=res, stats_out=part)  # producer of the raw rows
+    torch.testing.assert_close(part.sum(0)[:, 0], x.sum(1), rtol=1e-5, atol=1e-4)
+    gam, bet = 1 + 0.3 * torch.randn(K, generator=g), 0.2 * torch.randn(K, generator=g)
+    w, b = torch.randn(N, K, generator=g) * 0.05, torch.randn(N, generator=g) * 0.1
+    wf, cs, bf = ops.fold_ln_into_linear(w, b, gam, bet)
+    y = ops.linear(x, wf, bf, act="gelu", row_ln=(1e-5, cs, part))
+    torch.testing.assert_close(y, F.gelu(_ln(x, gam, bet, 1e-5) @ w.t() + b), rtol=1e-4, atol=1e-4)
+    # residual consumer: ctx @ Wo.T + bo + LN(x), with beta in the bias
+    Wo, bo = torch.randn(K, 64, generator=g) * 0.05, torch.randn(K, generator=g) * 0.1
+    ctx = torch.randn(M, 64, generator=g)
+    z = ops.linear(ctx, Wo, bo + bet, residual=x, res_ln=(1e-5, part, gam))
+    torch.testing.assert_close(z, ctx @ Wo.t() + bo + _ln(x, gam, bet, 1e-5), rtol=1e-4, atol=1e-4)
+
+
+def test_bart_folded_decoder_step_equals_unfolded():
+    from agent_tpu_amd.models.bart import BartModel, config_for as bart_config, init_random as bart_init
+
+    cfg = bart_config("bart-tiny")
+    pack = bart_init(cfg, seed=2, std=0.1)
+    g = torch.Generator().manual_seed(4)
+    for n in pack.names():  # non-trivial LayerNorm gammas and betas
+        base = n.split(".")[-1]
+        if base.startswith("ln") and base.endswith("_g"):
+            pack[n].copy_(1 + 0.3 * torch.randn(pack[n].shape, generator=g))
+        elif base.startswith("ln") and base.endswith("_b"):
+            pack[n].copy_(0.2 * torch.randn(pack[n].shape, generator=g))
+    plain, fold = BartModel(cfg, pack, fp32=True), BartModel(cfg, pack, fp32=True)
+    fold.ln_fold = True
+    assert not plain.ln_fold
+    B, S, T = 3, 16, 8
+    ids = torch.randint(3, cfg.vocab_size, (B, S), generator=g, dtype=torch.int32)
+    lens = torch.tensor([16, 9, 12], dtype=torch.int32)
+    _, kv = plain.encode(ids, lens)
+    tok = torch.randint(3, cfg.vocab_size, (B,), generator=g, dtype=torch.int32)
+    step = torch.zeros(1, dtype=torch.int32)
+    c1, c2 = plain.new_cache(B, T), fold.new_cache(B, T)
+    for t in range(3):
+        step.fill_(t)
+        l1 = plain.step(tok, step, c1, T, kv, lens, S, 1)
+        l2 = fold.step(tok, step, c2, T, kv, lens, S, 1)
+        torch.testing.assert_close(l2, l1, rtol=1e-4, atol=1e-4)
+        tok = l1.argmax(-1).to(torch.int32)

@@ -375,6 +375,91 @@ def test_t5_step_rms_fold_matches_unfolded(gpu):
     assert _rel(lf, lp) < 3e-2
 
 
+@pytest.mark.parametrize("M,N,K,act,kv", [(1024, 1024, 1024, None, False), (1024, 4096, 1024, "gelu", False),
+                                          (4096, 1024, 1024, None, False), (2048, 4096, 1024, "gelu", False),
+                                          (1024, 3072, 1024, None, True), (4096, 3072, 1024, None, True),
+                                          (77, 192, 256, "gelu", False)])
+def test_gemm_row_ln_fold(gpu, M, N, K, act, kv):
+    # decode LayerNorm folding (dec and 128x128 kernels): a producer GEMM writes the row
+    # partials of its bf16 output (RowStats), a RowLn consumer and a ResLn consumer normalise
+    # from them; against the fp32 LayerNorm-then-linear reference
+    import torch.nn.functional as F
+
+    ctx0 = _r((M, 256), gpu, 1.0, seed=60)
+    w0 = _r((K, 256), gpu, 0.05, seed=59)
+    b0 = _r((K,), gpu, 0.1, torch.float32, seed=58)
+    res0 = _r((M, K), gpu, 2.0, seed=61) + 0.25
+    part = torch.full((K // 32, M, 2), float("nan"), dtype=torch.float32, device=gpu)
+    x = ops.linear(ctx0, w0, b0, residual=res0, stats_out=part)
+    torch.testing.assert_close(part.cpu(), ops.row_parts_ref(x.cpu()), rtol=1e-4, atol=1e-2)
+    w = _r((N, K), gpu, 0.05, seed=62)
+    b = _r((N,), gpu, 0.1, torch.float32, seed=63)
+    gam = 1 + _r((K,), gpu, 0.3, torch.float32, seed=64)
+    bet = _r((K,), gpu, 0.2, torch.float32, seed=65)
+    eps = 1e-5
+    wf, cs, bf = ops.fold_ln_into_linear(w, b, gam, bet)
+    xf = x.cpu().float()
+    xn = F.layer_norm(xf, (K,), gam.cpu(), bet.cpu(), eps)
+    ref = xn @ w.cpu().float().t() + b.cpu()
+    if act == "gelu":
+        ref = F.gelu(ref)
+    if kv:
+        d = N // 3
+        T, t = 5, 3
+        cache = torch.zeros((M * T, 2 * d), dtype=torch.bfloat16, device=gpu)
+        step = torch.tensor([t], dtype=torch.int32, device=gpu)
+        q = ops.linear(x, wf, bf, kv_cache=(cache, T, step, d), row_ln=(eps, cs, part))
+        assert _rel(q, ref[:, :d]) < 2e-2
+        assert _rel(cache.view(M, T, 2 * d)[:, t], ref[:, d:]) < 2e-2
+    else:
+        y = ops.linear(x, wf, bf, act=act, row_ln=(eps, cs, part))
+        assert _rel(y, ref) < 2e-2
+    # residual consumer (o-proj / FFN2 of the folded step): ctx @ Wo.T + (bo + beta) + LN(x)
+    ctx = _r((M, 256), gpu, 1.0, seed=66)
+    wo = _r((K, 256), gpu, 0.05, seed=67)
+    bo = _r((K,), gpu, 0.1, torch.float32, seed=68)
+    z = ops.linear(ctx, wo, (bo + bet).contiguous(), residual=x, res_ln=(eps, part, gam))
+    zref = ctx.cpu().float() @ wo.cpu().float().t() + bo.cpu() + xn
+    assert _rel(z, zref) < 2e-2
+
+
+def test_bart_step_ln_fold_matches_unfolded(gpu):
+    # non-trivial LayerNorm gammas / betas: the folded BART decoder step vs the layernorm +
+    # linear step (GPU) and the fp32 oracle
+    from agent_tpu_amd.models.bart import BartModel, config_for, init_random
+
+    cfg = config_for("bart-tiny")
+    pack = init_random(cfg, seed=2, std=0.1)
+    g = torch.Generator().manual_seed(4)
+    for n in pack.names():
+        base = n.split(".")[-1]
+        if base.startswith("ln") and base.endswith("_g"):
+            pack[n].copy_(1 + 0.3 * torch.randn(pack[n].shape, generator=g))
+        elif base.startswith("ln") and base.endswith("_b"):
+            pack[n].copy_(0.2 * torch.randn(pack[n].shape, generator=g))
+    cpu_m = BartModel(cfg, pack, fp32=True)
+    gp = pack.to(gpu)
+    fold_m, plain_m = BartModel(cfg, gp), BartModel(cfg, gp)
+    plain_m.ln_fold = False
+    assert fold_m.ln_fold
+    B, S, T = 3, 16, 8
+    ids = torch.randint(3, cfg.vocab_size, (B, S), generator=g, dtype=torch.int32)
+    lens = torch.tensor([16, 9, 12], dtype=torch.int32)
+    _, kc = cpu_m.encode(ids, lens)
+    _, kg = fold_m.encode(ids.to(gpu), lens.to(gpu))
+    tok = torch.randint(3, cfg.vocab_size, (B,), generator=g, dtype=torch.int32)
+    step = torch.zeros(1, dtype=torch.int32)
+    caches = [cpu_m.new_cache(B, T), fold_m.new_cache(B, T), plain_m.new_cache(B, T)]
+    for t in range(3):
+        step.fill_(t)
+        lc = cpu_m.step(tok, step, caches[0], T, kc, lens, S, 1)
+        lf = fold_m.step(tok.to(gpu), step.to(gpu), caches[1], T, kg, lens.to(gpu), S, 1)
+        lp = plain_m.step(tok.to(gpu), step.to(gpu), caches[2], T, kg, lens.to(gpu), S, 1)
+        assert _rel(lf, lc) < 5e-2 and _rel(lp, lc) < 5e-2, t
+        assert _rel(lf, lp) < 3e-2, t
+        tok = lc.argmax(-1).to(torch.int32)
+
+
 @pytest.mark.parametrize("M,d,rms", [(1024, 768, True), (256, 1024, False), (4096, 768, True), (77, 256, False)])
 def test_gemm_kv_scatter(gpu, M, d, rms):
     # decode QKV GEMM writing K|V into the cache row m*T + step and Q into out, vs the plain GEMM
