@@ -131,3 +131,22 @@ def test_bart_folded_decoder_step_equals_unfolded():
         l2 = fold.step(tok, step, c2, T, kv, lens, S, 1)
         torch.testing.assert_close(l2, l1, rtol=1e-4, atol=1e-4)
         tok = l1.argmax(-1).to(torch.int32)
+
+
+def test_decode_ln_fold_argument_checks():
+    import pytest
+
+    M, K = 4, 64
+    x, w, b = torch.randn(M, K), torch.randn(32, K), torch.zeros(32)
+    cs, part = torch.zeros(32), torch.zeros(K // 32, M, 2)
+    with pytest.raises(ValueError, match="row_ln in_part"):
+        ops.linear(x, w, b, row_ln=(1e-5, cs, torch.zeros(1, M, 2)))
+    with pytest.raises(ValueError, match="row_ln takes a bias"):
+        ops.linear(x, w, None, row_ln=(1e-5, cs, part))
+    with pytest.raises(ValueError, match="res_ln takes a bias and a residual"):
+        ops.linear(x, w, b, res_ln=(1e-5, torch.zeros(1, M, 2), torch.ones(32)))
+    with pytest.raises(ValueError, match="stats_out"):
+        ops.linear(x, w, b, residual=torch.zeros(M, 32), stats_out=torch.zeros(2, M, 2, dtype=torch.float64))
+    wide = torch.randn(M, 2048)
+    with pytest.raises(ValueError, match="<= 1024"):
+        ops.linear(wide, torch.randn(32, 2048), b, row_ln=(1e-5, cs, torch.zeros(64, M, 2)))
