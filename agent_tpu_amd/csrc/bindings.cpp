@@ -246,6 +246,25 @@ PYBIND11_MODULE(_atpu, m) {
         return py::make_tuple(ids, lens);
       },
       py::arg("text"), py::arg("offsets"), py::arg("seq_len"), py::arg("vocab"), py::arg("max_row_bytes"));
+  m.def(
+      "word_maps_host",
+      [](py::array_t<uint8_t, py::array::c_style> text, py::array_t<int64_t, py::array::c_style> offsets, int vocab,
+         int cap) {
+        const int B = static_cast<int>(offsets.size()) - 1;
+        ATPU_CHECK(B >= 0, "word_maps_host: offsets must have B+1 entries");
+        std::vector<int32_t> ids;
+        std::vector<int64_t> word_of, doc_off;
+        {
+          py::gil_scoped_release nogil;
+          word_maps_host(text.data(), offsets.data(), B, vocab, cap, ids, word_of, doc_off);
+        }
+        return py::make_tuple(py::array_t<int32_t>(ids.size(), ids.data()),
+                              py::array_t<int64_t>(word_of.size(), word_of.data()),
+                              py::array_t<int64_t>(doc_off.size(), doc_off.data()));
+      },
+      "per document (words joined by single spaces): distinct token ids ascending, first word index of each, "
+      "document offsets [B+1]",
+      py::arg("text"), py::arg("offsets"), py::arg("vocab"), py::arg("cap"));
 
   m.def("device_query", [] {
     py::list out;

@@ -19,6 +19,11 @@ namespace atpu {
 // Host twin of the K1 GPU tokenizer (identical output, see tokenize.hip).
 void tokenize_host(const uint8_t* text, const int32_t* offsets, int32_t* ids, int32_t* lens, int B, int S, int vocab,
                    int max_row_bytes);
+// Per document (words joined by single 0x20 bytes): its distinct hash-token ids, ascending,
+// and the index of the first word producing each (at most cap tokens per word); doc_off[B+1]
+// delimits each document's entries in ids / word_of (detokenization maps, runtime/summarize.py)
+void word_maps_host(const uint8_t* text, const int64_t* offsets, int B, int vocab, int cap,
+                    std::vector<int32_t>& ids, std::vector<int64_t>& word_of, std::vector<int64_t>& doc_off);
 
 struct DeviceInfo {
   int index;

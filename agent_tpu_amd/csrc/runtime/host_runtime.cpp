@@ -24,38 +24,78 @@ inline uint32_t step(uint32_t h, uint32_t c) {
 }
 }  // namespace
 
+namespace {
+// Hash tokens of bytes [p, p+n) (the tokenize_host rules), at most cap; emit(id) per token.
+template <typename Emit>
+int tokenize_bytes(const uint8_t* p, int n, int cap, uint32_t mod, Emit emit) {
+  const uint32_t cont = step(step(kBasis, '#'), '#');
+  int nt = 0;
+  for (int i = 0; i < n && nt < cap;) {
+    const int c = cls_of(p[i]);
+    if (c == 0) { ++i; continue; }
+    if (c == 1) {
+      emit(static_cast<int32_t>(1000u + step(kBasis, p[i]) % mod));
+      ++nt;
+      ++i;
+      continue;
+    }
+    int j = i;
+    while (j < n && cls_of(p[j]) == 2) ++j;
+    for (int b0 = i, piece = 0; b0 < j && nt < cap; b0 += kPieceBytes, ++piece) {
+      uint32_t h = piece == 0 ? kBasis : cont;
+      for (int k = b0; k < std::min(j, b0 + kPieceBytes); ++k) h = step(h, p[k]);
+      emit(static_cast<int32_t>(1000u + h % mod));
+      ++nt;
+    }
+    i = j;
+  }
+  return nt;
+}
+}  // namespace
+
 void tokenize_host(const uint8_t* text, const int32_t* offsets, int32_t* ids, int32_t* lens, int B, int S, int vocab,
                    int max_row_bytes) {
   if (S < 2 || vocab <= 1000) throw std::invalid_argument("tokenize_host: bad S/vocab");
   const uint32_t mod = static_cast<uint32_t>(vocab - 1000);
-  const uint32_t cont = step(step(kBasis, '#'), '#');
-  const int cap = S - 2;
   for (int r = 0; r < B; ++r) {
-    const uint8_t* p = text + offsets[r];
     const int n = std::min(offsets[r + 1] - offsets[r], max_row_bytes);
     int32_t* out = ids + static_cast<size_t>(r) * S;
-    int nt = 0;
-    for (int i = 0; i < n && nt < cap;) {
-      const int c = cls_of(p[i]);
-      if (c == 0) { ++i; continue; }
-      if (c == 1) {
-        out[1 + nt++] = static_cast<int32_t>(1000u + step(kBasis, p[i]) % mod);
-        ++i;
-        continue;
-      }
-      int j = i;
-      while (j < n && cls_of(p[j]) == 2) ++j;
-      for (int b0 = i, piece = 0; b0 < j && nt < cap; b0 += kPieceBytes, ++piece) {
-        uint32_t h = piece == 0 ? kBasis : cont;
-        for (int k = b0; k < std::min(j, b0 + kPieceBytes); ++k) h = step(h, p[k]);
-        out[1 + nt++] = static_cast<int32_t>(1000u + h % mod);
-      }
-      i = j;
-    }
+    int32_t* w = out + 1;
+    const int nt = tokenize_bytes(text + offsets[r], n, S - 2, mod, [&](int32_t id) { *w++ = id; });
     out[0] = 101;
     out[1 + nt] = 102;
     for (int j = nt + 2; j < S; ++j) out[j] = 0;
     lens[r] = nt + 2;
+  }
+}
+
+void word_maps_host(const uint8_t* text, const int64_t* offsets, int B, int vocab, int cap,
+                    std::vector<int32_t>& ids, std::vector<int64_t>& word_of, std::vector<int64_t>& doc_off) {
+  if (vocab <= 1000 || cap < 1) throw std::invalid_argument("word_maps_host: bad vocab/cap");
+  const uint32_t mod = static_cast<uint32_t>(vocab - 1000);
+  doc_off.assign(1, 0);
+  std::vector<std::pair<int32_t, int64_t>> v;  // (token id, word index), word-major
+  for (int r = 0; r < B; ++r) {
+    const uint8_t* p = text + offsets[r];
+    const int64_t n = offsets[r + 1] - offsets[r];
+    v.clear();
+    int64_t word = 0;
+    for (int64_t a = 0; a <= n;) {  // words are separated by exactly one 0x20 (the caller joins str.split())
+      int64_t b = a;
+      while (b < n && p[b] != 0x20) ++b;
+      if (b > a) {
+        tokenize_bytes(p + a, static_cast<int>(b - a), cap, mod, [&](int32_t id) { v.emplace_back(id, word); });
+        ++word;
+      }
+      a = b + 1;
+    }
+    std::stable_sort(v.begin(), v.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+    for (size_t k = 0; k < v.size(); ++k) {
+      if (k > 0 && v[k].first == v[k - 1].first) continue;  // first word producing the id
+      ids.push_back(v[k].first);
+      word_of.push_back(v[k].second);
+    }
+    doc_off.push_back(static_cast<int64_t>(ids.size()));
   }
 }
 
