@@ -128,3 +128,38 @@ def test_word_maps_match_python_oracle():
         want = " ".join(oracle.get(t, f"<{t}>") for t in seq if t != cfg.eos_id and t != cfg.pad_id)
         assert eng.detokenize(seq, wm) == want
     assert np.asarray(eng.word_maps([""])[0].ids).size == 0
+
+
+def test_encode_texts_wrapping_matches_python_reference():
+    """The array-op source wrapping equals per-row Python wrapping (T5: toks </s>; BART:
+    <s> toks </s>), with truncation to max_source_len, empty rows and S padded to % 8."""
+    import numpy as np
+    import torch
+
+    from agent_tpu_amd import tokenizer as T
+    from agent_tpu_amd.models import bart, t5
+    from agent_tpu_amd.runtime.summarize import SummarizeEngine
+
+    texts = ["The quick, brown fox; jumps over the lazy dog's back.", "", "naïve café " * 60, "a b c", "x" * 500]
+    for mod, name, pre in ((t5, "t5-tiny", False), (bart, "bart-tiny", True)):
+        cfg = mod.config_for(name)
+
+        class Stub:
+            def __init__(self):
+                self.cfg, self.device = cfg, torch.device("cpu")
+
+            def wrap_source(self, toks):
+                return ([cfg.bos_id] if pre else []) + list(toks) + [cfg.eos_id]
+
+        for max_src in (16, 64, 512):
+            eng = SummarizeEngine(Stub(), max_src)
+            ids, lens, _ = eng.encode_texts(texts, with_maps=False)
+            n_sp = 2 if pre else 1
+            rows = [Stub().wrap_source(T.token_ids(t.encode(), cfg.vocab_size, max_src - 1)[:max_src - n_sp])
+                    for t in texts]
+            S = max(8, (max(map(len, rows)) + 7) // 8 * 8)
+            want = np.full((len(rows), S), cfg.pad_id, dtype=np.int32)
+            for r, toks in enumerate(rows):
+                want[r, :len(toks)] = toks
+            assert np.array_equal(ids.numpy(), want), (name, max_src)
+            assert lens.tolist() == [len(r) for r in rows]
