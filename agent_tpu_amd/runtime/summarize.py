@@ -586,6 +586,26 @@ class SummarizeEngine:
 
     def summarize(self, texts: Sequence[str], gen: GenConfig) -> Tuple[List[str], GenResult]:
         ids, lens, _ = self.encode_texts(texts, with_maps=False)
-        res = self.run(ids, lens, gen)
-        maps = self.word_maps(texts)
+        if self.device.type == "cuda" and os.getenv("ATPU_SUMM_MAPS_OVERLAP", "1") not in ("0", "false", "no"):
+            # the detokenization maps are built on a worker thread while the GPU decodes
+            # (the native part releases the GIL; the decode loop mostly waits on events)
+            fut = _host_pool().submit(self.word_maps, texts)
+            res = self.run(ids, lens, gen)
+            maps = fut.result()
+        else:
+            res = self.run(ids, lens, gen)
+            maps = self.word_maps(texts)
         return [self.detokenize(s, m) for s, m in zip(res.sequences, maps)], res
+
+
+_POOL = None
+
+
+def _host_pool():
+    """One long-lived worker thread for host work overlapped with GPU decoding."""
+    global _POOL
+    if _POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+
+        _POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix="atpu-summ-host")
+    return _POOL
