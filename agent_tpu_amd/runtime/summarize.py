@@ -557,14 +557,16 @@ class SummarizeEngine:
 
     def run(self, ids: torch.Tensor, lens: torch.Tensor, gen: GenConfig) -> GenResult:
         """Beam search over a tokenized batch. On a GPU with device selection the batch is
-        split into ``ATPU_SUMM_STREAMS`` (default 2) contiguous parts searched concurrently
+        split into ``ATPU_SUMM_STREAMS`` (default 3) contiguous parts searched concurrently
         on their own streams (:func:`generate_concurrent`), each part >= ``ATPU_SUMM_PART_MIN``
-        (default 512) documents. One host thread runs every part's bookkeeping, so the
+        (default 300). Two parts ran bimodally (T5, 1024 docs: 708 / 989 / 987 and 575 / 645 docs/s in
+        separate processes), three held 980-990 (tools/gpu_summ_streams.sh).
+        One host thread runs every part's bookkeeping, so the
         split only pays once a part's GPU step outlasts the other parts' host work
         (T5-base, MI355X: 1024 docs 819 -> 845 docs/s; 256 docs as 2x128: 668 -> 654)."""
-        n = int(os.getenv("ATPU_SUMM_STREAMS", "2"))
+        n = int(os.getenv("ATPU_SUMM_STREAMS", "3"))
         B = int(ids.shape[0])
-        n = max(1, min(n, B // max(1, int(os.getenv("ATPU_SUMM_PART_MIN", "512")))))
+        n = max(1, min(n, B // max(1, int(os.getenv("ATPU_SUMM_PART_MIN", "300")))))
         if n < 2 or self.device.type != "cuda" or not gen.device_select:
             return generate(self.model, ids, lens, gen)
         cuts = [B * i // n for i in range(n + 1)]
