@@ -381,6 +381,11 @@ def summarize_task(payload: Dict[str, Any]) -> Any:
     gen = ms._gen_config(payload)
     err, steps = "", 0
     seqs = torch.full((0, gen.max_length), -1, dtype=torch.int32)
+    maps = None
+    if rank == 0 and eng.device.type == "cuda":  # detokenization maps built while the GPUs decode
+        from ..runtime.summarize import _host_pool
+
+        maps = _host_pool().submit(eng.word_maps, texts)
     try:
         s_r, n_r = split_range(0, len(texts), ws, rank)
         maybe_inject_fault("summarize")
@@ -401,6 +406,9 @@ def summarize_task(payload: Dict[str, Any]) -> Any:
     if rank != 0:
         return None
     rows = [[int(t) for t in r if t >= 0] for r in seqs.cpu().tolist()]
-    summaries = eng.detokenize_all(texts, rows)
+    if maps is not None:
+        summaries = [eng.detokenize(s, m) for s, m in zip(rows, maps.result())]
+    else:
+        summaries = eng.detokenize_all(texts, rows)
     return ms.result(bool(payload.get("texts_mode", True)), summaries, steps, timing,
                      float(payload.get("t0", time.time())), dp_world_size=ws)
