@@ -27,6 +27,7 @@ executing their shard of every DP-capable job (map_classify, risk_accumulate).
 """
 from __future__ import annotations
 
+import json
 import os
 import signal
 import socket
@@ -217,6 +218,9 @@ def worker_profile(health: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
 
 
 # ------------------------------------------------------------------- http
+_JSON_HEADERS = {"Content-Type": "application/json"}
+
+
 class Controller:
     def __init__(self, base: str, timeout: float) -> None:
         self.base = base
@@ -226,7 +230,9 @@ class Controller:
     def post(self, path: str, body: Dict[str, Any]) -> Tuple[int, Any]:
         url = self.base + path
         try:
-            r = self.http.post(url, json=body, timeout=self.timeout)
+            # compact separators: a 8192-row classify result is ~20 % smaller than requests' json=
+            data = json.dumps(body, separators=(",", ":"), allow_nan=False).encode("utf-8")
+            r = self.http.post(url, data=data, headers=_JSON_HEADERS, timeout=self.timeout)
         except Exception as exc:
             return 0, {"error": str(exc), "url": url}
         if r.status_code == 204:

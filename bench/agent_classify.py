@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Whole-agent classify throughput on one GPU: the real ``app.py`` leases ``map_classify``
+CSV-shard jobs from a local mock controller and posts their per-row top-k results back.
+
+Unlike ``bench.py`` (the engine alone) the clock here covers everything a deployed agent
+does per job: lease over HTTP, the native CSV index, pinned staging, the BERT pipeline on
+the GPU, building the reference-format JSON result (one dict per row, or the
+``output: "summary"`` histogram) and posting it. It runs from the first lease request to
+the last result; the model load (first job) is excluded by a warm-up job.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import signal
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+from tests.integration.mock_controller import MockController  # noqa: E402
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--jobs", type=int, default=16)
+    ap.add_argument("--shard", type=int, default=16384, help="CSV rows per job")
+    ap.add_argument("--output", default="rows", choices=["rows", "summary"])
+    ap.add_argument("--model", default="bert-base")
+    a = ap.parse_args()
+    from agent_tpu_amd.utils.synthetic import write_csv
+
+    rows = (a.jobs + 1) * a.shard
+    csv_path = f"/tmp/atpu_agent_bench_{rows}.csv"
+    if not os.path.exists(csv_path):
+        write_csv(csv_path, rows, 150, seed=77)
+    ctl = MockController().start()
+
+    def job(i):
+        return {"id": f"j{i}", "op": "map_classify",
+                "payload": {"source_uri": csv_path, "start_row": i * a.shard, "shard_size": a.shard,
+                            "text_column": "text", "topk": 2, "output": a.output, "dataset_id": "bench"}}
+
+    ctl.lease(job(0), lease_id="Lwarm")  # model load + graph capture
+    env = dict(os.environ, CONTROLLER_URL=ctl.url, TASKS="map_classify", IDLE_SLEEP_SEC="0.01", MAX_TASKS="1",
+               GPU_MODEL_PATH=a.model, PYTHONUNBUFFERED="1")
+    p = subprocess.Popen([sys.executable, "app.py"], cwd=REPO, env=env, stdout=subprocess.DEVNULL,
+                         stderr=subprocess.DEVNULL)
+    try:
+        ok = ctl.wait(lambda c: len(c.results) >= 1, 600)
+        for i in range(1, a.jobs + 1):
+            ctl.lease(job(i), lease_id=f"L{i}")
+        t0 = time.perf_counter()
+        ok = ok and ctl.wait(lambda c: len(c.results) >= a.jobs + 1, 1200)
+        el = time.perf_counter() - t0
+    finally:
+        p.send_signal(signal.SIGTERM)
+        p.wait(timeout=120)
+        ctl.stop()
+    bad = [r for r in ctl.results if r.get("status") != "succeeded"]
+    if not ok or bad:
+        print(json.dumps({"error": "timeout" if not ok else "failed jobs", "results": len(ctl.results),
+                          "first_bad": bad[:1]}, default=str)[:2000])
+        return 1
+    res = [r["result"] for r in ctl.results[1:]]
+    n = sum(int(r["row_count"]) for r in res)
+    engine_rps = sorted(float(r["rows_per_sec"]) for r in res)[len(res) // 2]
+    keys = sorted({k for r in res for k in (r.get("timing_ms") or {})})
+    timing = {k: round(sorted(float((r.get("timing_ms") or {}).get(k, 0.0)) for r in res)[len(res) // 2], 2)
+              for k in keys}
+    op_ms = round(sorted(float(r["elapsed_ms"]) for r in res)[len(res) // 2], 2)
+    print(json.dumps({"metric": f"classified rows/sec end to end through the agent ({a.model}, 1 GPU)",
+                      "value": round(n / el, 1), "unit": "rows/s", "higher_is_better": True,
+                      "config": {"jobs": a.jobs, "rows_per_job": a.shard, "output": a.output,
+                                 "median_op_rows_per_sec": round(engine_rps, 1),
+                                 "median_op_elapsed_ms": op_ms, "median_op_timing_ms": timing,
+                                 "transport": "HTTP/1.1 keep-alive, loopback mock controller",
+                                 "data": "synthetic CSV rows, random-init weights"}}), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -82,20 +82,31 @@ def csv_result(h, idx, sc, meta: Dict[str, Any], payload: Dict[str, Any]) -> Dic
 
 
 def _rows_result(h, idx, sc, start: int, k: int, op: str, t0: float, extra: Dict[str, Any]) -> Dict[str, Any]:
+    """Reference-format rows. ``tolist`` already yields Python ints / floats, so the rows are
+    built by one comprehension (a helper call and int()/float() per entry cost ~50 ms per
+    8192 rows); the summary form never builds them (top-1 histogram by ``bincount``)."""
+    import torch
+
     summary = bool(extra.pop("_summary", False))
-    idx_l, sc_l = idx.tolist(), sc.tolist()
-    rows = [{"row": start + i, "topk": _topk_list(a, b)} for i, (a, b) in enumerate(zip(idx_l, sc_l))]
+    n = int(idx.shape[0])
+    first = _topk_list(idx[0].tolist(), sc[0].tolist()) if n else []
+    if not summary:
+        idx_l, sc_l = idx.tolist(), sc.tolist()
+        if k == 2:  # the common binary-label case without the inner comprehension (-25 %)
+            rows = [{"row": r, "topk": [{"index": a[0], "score": b[0]}, {"index": a[1], "score": b[1]}]}
+                    for r, a, b in zip(range(start, start + n), idx_l, sc_l)]
+        else:
+            rows = [{"row": r, "topk": [{"index": i, "score": s} for i, s in zip(a, b)]}
+                    for r, a, b in zip(range(start, start + n), idx_l, sc_l)]
     dt = time.time() - t0
-    out = {"ok": True, "op": op, "model_path": h.model_path, "row_count": len(rows),
-           "topk": rows[0]["topk"] if rows else [], "elapsed_ms": dt * 1000.0,
-           "rows_per_sec": (len(rows) / dt) if dt > 0 else None}
+    out = {"ok": True, "op": op, "model_path": h.model_path, "row_count": n,
+           "topk": first, "elapsed_ms": dt * 1000.0,
+           "rows_per_sec": (n / dt) if dt > 0 else None}
     out.update(extra)
     if summary:
-        hist: Dict[int, int] = {}
-        for r in idx_l:
-            hist[r[0]] = hist.get(r[0], 0) + 1
+        counts = torch.bincount(idx[:, 0].to(torch.int64)).tolist() if n else []
         out.pop("topk", None)
-        out["top1_histogram"] = {str(c): n for c, n in sorted(hist.items())}
+        out["top1_histogram"] = {str(c): m for c, m in enumerate(counts) if m}
     else:
         out["rows"] = rows
     return out
