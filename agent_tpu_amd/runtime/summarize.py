@@ -504,7 +504,7 @@ class SummarizeEngine:
         ntok = np.minimum(lens.astype(np.int64) - 2, self.max_src - len(pre) - len(post))
         L = P + ntok + len(post)
         B = len(texts)
-        S = max(8, (int(L.max()) + 7) // 8 * 8)
+        S = max(8, (int(L.max()) + 7) // 8 * 8) if B else 8
         arr = np.full((B, S), self.cfg.pad_id, dtype=np.int32)
         arr[:, :P] = pre
         cols = np.arange(S)[None, :]
