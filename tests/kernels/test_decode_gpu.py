@@ -535,8 +535,9 @@ def test_generate_concurrent_matches_serial(gpu, family):
             assert r.sequences == o.sequences and r.scores == o.scores and r.steps == o.steps, (cuts, ml)
 
 
-def test_engine_stream_split_matches_single(gpu, monkeypatch):
-    # SummarizeEngine.run split over two streams: same output as one search
+@pytest.mark.parametrize("streams", [2, 3])
+def test_engine_stream_split_matches_single(gpu, monkeypatch, streams):
+    # SummarizeEngine.run split over two / three streams (3 is the default): same output as one search
     from agent_tpu_amd.runtime.summarize import GenConfig, SummarizeEngine, build_model
 
     model, _ = build_model("t5-tiny", device=gpu, seed=2)
@@ -548,7 +549,7 @@ def test_engine_stream_split_matches_single(gpu, monkeypatch):
     gen = GenConfig(num_beams=4, max_length=16, min_length=2)
     monkeypatch.setenv("ATPU_SUMM_STREAMS", "1")
     a = eng.run(ids, lens, gen)
-    monkeypatch.setenv("ATPU_SUMM_STREAMS", "2")
-    monkeypatch.setenv("ATPU_SUMM_PART_MIN", "32")
+    monkeypatch.setenv("ATPU_SUMM_STREAMS", str(streams))
+    monkeypatch.setenv("ATPU_SUMM_PART_MIN", "20")
     b = eng.run(ids, lens, gen)
     assert a.sequences == b.sequences and a.scores == b.scores
