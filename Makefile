@@ -20,7 +20,7 @@ test-gpu-serial: build  ## same, every launch synchronous + serialized (localise
 	HIP_LAUNCH_BLOCKING=1 AMD_SERIALIZE_KERNEL=3 AMD_SERIALIZE_COPY=3 $(PY) -m pytest tests -m gpu -q -x
 
 test-dist:
-	$(PY) -m pytest tests/dist -q
+	$(PY) -m pytest tests/distributed -q
 
 sanitize:         ## host C++ (CSV index, tokenizer) under ASan + UBSan
 	$(PY) -m pytest tests/contract/test_host_sanitizers.py -q

@@ -72,5 +72,29 @@ def stream_handle(stream: Optional["torch.cuda.Stream"] = None) -> int:
     return int(s.cuda_stream)
 
 
+class DeviceMismatch(ValueError):
+    pass
+
+
+def check_launch_device(operand_dev: "torch.device", current_index: int) -> None:
+    """Kernels take raw pointers and launch on the CURRENT device's stream, so
+    operands on another GPU would be dereferenced by the wrong device (a memory
+    access fault without peer access). Refuse it instead."""
+    if operand_dev.type != "cuda":
+        raise DeviceMismatch(f"kernel operand on {operand_dev}, expected a ROCm device tensor")
+    idx = operand_dev.index if operand_dev.index is not None else current_index
+    if idx != current_index:
+        raise DeviceMismatch(f"kernel operands are on cuda:{idx} but the current device (launch stream) is "
+                             f"cuda:{current_index}; wrap the call in torch.cuda.device({idx})")
+
+
+def launch_stream(t: torch.Tensor) -> int:
+    """The hipStream_t a kernel over ``t`` is launched on: the current stream of
+    ``t``'s device, which must be the current device (:func:`check_launch_device`)."""
+    cur = torch.cuda.current_device()
+    check_launch_device(t.device, cur)
+    return int(torch.cuda.current_stream(cur).cuda_stream)
+
+
 def ptr(t: Optional[torch.Tensor]) -> int:
     return 0 if t is None else int(t.data_ptr())

@@ -266,16 +266,22 @@ PYBIND11_MODULE(_atpu, m) {
       "document offsets [B+1]",
       py::arg("text"), py::arg("offsets"), py::arg("vocab"), py::arg("cap"));
 
-  m.def("device_query", [] {
+  m.def("device_query", [](int mem_of) {
+    if (mem_of < 0) {
+      int cur = 0;
+      (void)hipGetDevice(&cur);
+      mem_of = cur;
+    }
     py::list out;
-    for (const auto& d : device_query()) {
+    for (const auto& d : device_query(mem_of)) {
       py::dict x;
       x["index"] = d.index; x["name"] = d.name; x["arch"] = d.arch; x["total_memory_bytes"] = d.total_bytes;
       x["free_memory_bytes"] = d.free_bytes; x["compute_units"] = d.cus; x["clock_khz"] = d.clock_khz;
+      x["free_memory_known"] = d.index == mem_of;
       out.append(x);
     }
     return out;
-  });
+  }, "every visible device; free HBM only for device mem_of (-1: current)", py::arg("mem_of") = -1);
 
   py::class_<CsvTable, std::shared_ptr<CsvTable>>(m, "CsvTable")
       .def(py::init([](const std::string& path) {

@@ -34,7 +34,9 @@ struct DeviceInfo {
   int cus;
   int clock_khz;
 };
-std::vector<DeviceInfo> device_query();
+// Properties of every visible device; free HBM only for device ``mem_of`` (-1: the
+// current device), so a DP rank never creates contexts on its peers' GPUs.
+std::vector<DeviceInfo> device_query(int mem_of = -1);
 
 // Double-buffered CSV column -> pinned host -> device pipeline.
 //  submit(slot, ...)  : background thread extracts rows into slot's pinned

@@ -100,7 +100,7 @@ void word_maps_host(const uint8_t* text, const int64_t* offsets, int B, int voca
 }
 
 // -------------------------------------------------------------- device query
-std::vector<DeviceInfo> device_query() {
+std::vector<DeviceInfo> device_query(int mem_of) {
   std::vector<DeviceInfo> out;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) {
@@ -109,6 +109,7 @@ std::vector<DeviceInfo> device_query() {
   }
   int cur = 0;
   (void)hipGetDevice(&cur);
+  if (mem_of < 0) mem_of = cur;
   for (int i = 0; i < n; ++i) {
     hipDeviceProp_t prop{};
     if (hipGetDeviceProperties(&prop, i) != hipSuccess) continue;
@@ -120,7 +121,8 @@ std::vector<DeviceInfo> device_query() {
     d.cus = prop.multiProcessorCount;
     d.clock_khz = prop.clockRate;
     size_t fr = 0, tot = 0;
-    if (hipSetDevice(i) == hipSuccess && hipMemGetInfo(&fr, &tot) == hipSuccess) d.free_bytes = fr;
+    d.free_bytes = 0;
+    if (i == mem_of && hipSetDevice(i) == hipSuccess && hipMemGetInfo(&fr, &tot) == hipSuccess) d.free_bytes = fr;
     out.push_back(d);
   }
   (void)hipSetDevice(cur);

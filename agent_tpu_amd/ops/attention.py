@@ -11,7 +11,7 @@ from typing import Optional
 
 import torch
 
-from .._native import native, ptr, stream_handle
+from .._native import native, ptr, launch_stream
 from ._util import check, check_bf16_dev, row_stride
 
 HEAD_DIM = 64
@@ -58,7 +58,7 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, lens: torch.Ten
         out = torch.empty((B * Sq, H * HEAD_DIM), dtype=torch.bfloat16, device=q.device)
     native().attention_strided(ptr(q), row_stride(q, "q"), ptr(k), row_stride(k, "k"), ptr(v), row_stride(v, "v"),
                                ptr(out), row_stride(out, "out"), ptr(lens), ptr(bias), B, Sq, Skv, H, HEAD_DIM,
-                               scale, int(causal), stream_handle())
+                               scale, int(causal), launch_stream(q))
     return out
 
 

@@ -19,7 +19,7 @@ import numpy as np
 
 import torch
 
-from .._native import native, ptr, stream_handle
+from .._native import native, ptr, launch_stream
 from ._util import check, check_bf16_dev, row_stride, same_device
 
 HEAD_DIM = 64
@@ -50,7 +50,7 @@ def decode_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, H: int, 
     native().decode_attention(ptr(q), row_stride(q, "q"), ptr(k), ptr(v), row_stride(k, "k"), seq_stride, group,
                               ptr(lens), ptr(step), ptr(hist), 0 if hist is None else hist.shape[1], ptr(bias_dist),
                               0 if bias_dist is None else bias_dist.shape[1], ptr(out), row_stride(out, "out"), R, H,
-                              float(scale), stream_handle())
+                              float(scale), launch_stream(q))
     return out
 
 
@@ -89,7 +89,7 @@ def kv_append(src: torch.Tensor, col0: int, ncols: int, cache: torch.Tensor, seq
         cache.view(R, seq_stride, -1)[:, t, :ncols] = src[:, col0:col0 + ncols]
         return
     native().kv_append(ptr(src), row_stride(src, "src"), col0, ncols, ptr(cache), seq_stride,
-                       row_stride(cache, "cache"), ptr(step), R, stream_handle())
+                       row_stride(cache, "cache"), ptr(step), R, launch_stream(src))
 
 
 def beam_reorder_hist(src: torch.Tensor, dst: torch.Tensor, parent: torch.Tensor, step: torch.Tensor,
@@ -108,7 +108,7 @@ def beam_reorder_hist(src: torch.Tensor, dst: torch.Tensor, parent: torch.Tensor
           "hist/parent must be int32")
     check(src.is_contiguous() and dst.is_contiguous() and tuple(dst.shape) == (R, T), "hist must be contiguous [R, T]")
     check(last is None or (last.dtype == torch.int32 and last.is_cuda and last.numel() >= R), "last: int32 [R] on device")
-    native().beam_reorder_hist(ptr(src), ptr(dst), ptr(parent), R, T, ptr(step), stream_handle(),
+    native().beam_reorder_hist(ptr(src), ptr(dst), ptr(parent), R, T, ptr(step), launch_stream(src),
                                ptr(last) if last is not None else 0, int(off))
 
 
@@ -123,7 +123,7 @@ def gather_rows(src: torch.Tensor, dst: torch.Tensor, parent: torch.Tensor, nrow
     check(parent.dtype == torch.int32 and parent.is_cuda, "parent must be int32 on device")
     C = src.shape[-1]
     native().gather_rows(ptr(src), ptr(dst), ptr(parent), nrows, seq_stride, C, ptr(step), slabs,
-                         nrows * seq_stride * C, stream_handle())
+                         nrows * seq_stride * C, launch_stream(src))
 
 
 MAX_BANS = 512  # banned tokens per row the kernel filters (decode.hip kMaxBans)
@@ -189,7 +189,7 @@ def beam_topk_rows(logits: torch.Tensor, beam_scores: torch.Tensor, k: int, eos:
               and 0 <= int(cur) <= seq.shape[1], "ngram: token history must be contiguous int32 [R, >= cur] on device")
         seq_p, seq_stride, cur, n = ptr(seq), int(seq.shape[1]), int(cur), int(n)
     native().beam_topk_rows(ptr(logits), R, V, ptr(beam_scores), int(eos), int(mask_eos), int(k), ptr(sc), ptr(idx),
-                            stream_handle(), ptr(bans) if nbmax else 0, nbmax, seq_p, seq_stride, cur, n)
+                            launch_stream(logits), ptr(bans) if nbmax else 0, nbmax, seq_p, seq_stride, cur, n)
     return sc, idx
 
 
@@ -246,4 +246,4 @@ def beam_select(sc: torch.Tensor, tk: torch.Tensor, nb: int, V: int, eos: int, h
           "beam_select: sc fp32 / tk int32, contiguous")
     same_device(sc, tk, stage, rec)
     native().beam_select(ptr(sc), ptr(tk), B, nb, K2, int(V), int(eos), int(bool(hit_all)), float(neg), ptr(stage),
-                         ptr(rec), stream_handle())
+                         ptr(rec), launch_stream(sc))

@@ -10,7 +10,7 @@ from typing import Optional, Tuple
 
 import torch
 
-from .._native import native, ptr, stream_handle
+from .._native import native, ptr, launch_stream
 from ._util import check, check_bf16_dev, row_stride
 
 
@@ -40,5 +40,5 @@ def classify_head_topk(pooled: torch.Tensor, Wc: torch.Tensor, bc: Optional[torc
     idx = torch.empty((B, k), dtype=torch.int32, device=dev) if idx is None else idx
     score = torch.empty((B, k), dtype=torch.float32, device=dev) if score is None else score
     native().head_topk(ptr(pooled), row_stride(pooled, "pooled"), ptr(Wc), ptr(bc), ptr(logits), ptr(idx), ptr(score),
-                       B, N, C, k, stream_handle())
+                       B, N, C, k, launch_stream(pooled))
     return logits, idx, score

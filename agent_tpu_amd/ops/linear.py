@@ -14,7 +14,7 @@ from typing import Optional
 import torch
 import torch.nn.functional as F
 
-from .._native import native, ptr, stream_handle
+from .._native import native, ptr, launch_stream
 from ._util import check, check_bf16_dev, row_stride, same_device
 
 EPI_BIAS, EPI_GELU, EPI_TANH, EPI_RESIDUAL, EPI_RELU, EPI_OUT_F32 = 1, 2, 4, 8, 16, 32
@@ -210,7 +210,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     if not kv_args:
         kv_args = (0, 0, 0, 0, 0)
     native().gemm(ptr(x), lda, ptr(w), ldb, ptr(out), ldc, ptr(bias), ptr(residual), ldr, M, N, K, epi,
-                  stream_handle(), splits, ptr(ws), eps_arg, *kv_args, *ln_args)
+                  launch_stream(x), splits, ptr(ws), eps_arg, *kv_args, *ln_args)
     return out
 
 
@@ -252,7 +252,7 @@ def ln_finalize(part: torch.Tensor, K: int, eps: float, out: Optional[torch.Tens
         rs = torch.rsqrt((s[:, 1] * (1.0 / K) - mu * mu).clamp_min(0.0) + eps)
         return out.copy_(torch.stack([rs, rs * mu], -1))
     same_device(part, out)
-    native().ln_stats_finalize(ptr(part), slots, M, int(K), float(eps), ptr(out), stream_handle())
+    native().ln_stats_finalize(ptr(part), slots, M, int(K), float(eps), ptr(out), launch_stream(part))
     return out
 
 
@@ -348,5 +348,5 @@ def linear_ln(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, *, act: Opti
     check(tuple(out.shape) == (M, N) and out.dtype == torch.bfloat16, "out must be bf16 [M, N]")
     native().gemm_ln(ptr(x), row_stride(x, "x"), ptr(w), row_stride(w, "w"), ptr(out), row_stride(out, "out"),
                      ptr(bias), ptr(residual), ldr, M, N, K, epi, ptr(in_fin), ptr(colsum), ptr(res_fin),
-                     ptr(res_gamma), ptr(part_out), stream_handle())
+                     ptr(res_gamma), ptr(part_out), launch_stream(x))
     return out

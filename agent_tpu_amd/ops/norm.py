@@ -10,7 +10,7 @@ from typing import Optional
 import torch
 import torch.nn.functional as F
 
-from .._native import native, ptr, stream_handle
+from .._native import native, ptr, launch_stream
 from ._util import check, check_bf16_dev
 
 
@@ -43,7 +43,7 @@ def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: flo
         out = torch.empty_like(x)
     else:
         _check_out(out, x.shape, x)
-    native().layernorm(ptr(x), ptr(residual), ptr(gamma), ptr(beta), ptr(out), rows, N, float(eps), stream_handle())
+    native().layernorm(ptr(x), ptr(residual), ptr(gamma), ptr(beta), ptr(out), rows, N, float(eps), launch_stream(x))
     return out
 
 
@@ -60,7 +60,7 @@ def rmsnorm(x: torch.Tensor, gamma: torch.Tensor, eps: float = 1e-6, out: Option
         out = torch.empty_like(x)
     else:
         _check_out(out, x.shape, x)
-    native().rmsnorm(ptr(x), ptr(gamma), ptr(out), rows, N, float(eps), stream_handle())
+    native().rmsnorm(ptr(x), ptr(gamma), ptr(out), rows, N, float(eps), launch_stream(x))
     return out
 
 
@@ -91,7 +91,7 @@ def embed_layernorm(ids: torch.Tensor, word: torch.Tensor, pos: torch.Tensor, ty
     else:
         _check_out(out, (B * S, N), word)
     native().embed_layernorm(ptr(ids), ptr(type_ids), ptr(word), ptr(pos), ptr(type_), ptr(gamma), ptr(beta),
-                             ptr(out), B, S, N, V, type_.shape[0], float(eps), stream_handle())
+                             ptr(out), B, S, N, V, type_.shape[0], float(eps), launch_stream(ids))
     return out
 
 
@@ -107,5 +107,5 @@ def embed_gather(ids: torch.Tensor, table: torch.Tensor, out: Optional[torch.Ten
         out = torch.empty((flat.numel(), N), dtype=torch.bfloat16, device=ids.device)
     else:
         _check_out(out, (flat.numel(), N), table)
-    native().embed_gather(ptr(flat), ptr(table), ptr(out), flat.numel(), N, V, stream_handle())
+    native().embed_gather(ptr(flat), ptr(table), ptr(out), flat.numel(), N, V, launch_stream(table))
     return out

@@ -9,7 +9,7 @@ from typing import Dict, List, Sequence, Union
 
 import torch
 
-from .._native import native, ptr, stream_handle
+from .._native import native, ptr, launch_stream
 from ._util import check
 
 
@@ -27,7 +27,7 @@ def reduce_stats_tensor(x: torch.Tensor) -> torch.Tensor:
     blocks = nat.reduce_stats_blocks(n)
     partial = torch.empty(4 * blocks, dtype=torch.float64, device=x.device)
     out = torch.empty(4, dtype=torch.float64, device=x.device)
-    s = stream_handle()
+    s = launch_stream(x)
     if x.dtype == torch.float64:
         nat.reduce_stats_f64(ptr(x), n, ptr(partial), blocks, s)
     else:

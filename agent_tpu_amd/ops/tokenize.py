@@ -9,7 +9,7 @@ from typing import Optional, Tuple
 import numpy as np
 import torch
 
-from .._native import native, ptr, stream_handle
+from .._native import native, ptr, launch_stream
 from .. import tokenizer as _tok
 from ._util import check
 
@@ -35,5 +35,5 @@ def tokenize(text: torch.Tensor, offsets: torch.Tensor, seq_len: int, vocab: int
         lens = torch.empty((B,), dtype=torch.int32, device=text.device)
     check(ids.shape[1] == seq_len and ids.shape[0] >= B and lens.numel() >= B, "ids/lens too small")
     native().tokenize(ptr(text), ptr(offsets), ptr(ids), ptr(lens), B, seq_len, vocab, max_row_bytes,
-                      stream_handle(), int(text.numel()))
+                      launch_stream(text), int(text.numel()))
     return ids, lens

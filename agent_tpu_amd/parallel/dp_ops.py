@@ -231,6 +231,26 @@ def shutdown_workers() -> None:
         broadcast_task({"op": _SHUTDOWN})
 
 
+# ------------------------------------------------------------ health
+@dp_task("health_check")
+def health_task(payload: Dict[str, Any]) -> Any:
+    """Every rank probes ONLY its own GPU (no HIP context on a peer's device);
+    rank 0 merges the per-rank answers into the node view it advertises."""
+    from ..runtime import health
+
+    if torch.cuda.is_available():
+        res = health.check(probe=bool(payload.get("probe", True)), only=[torch.cuda.current_device()])
+    else:
+        res = {"ok": False, "devices": [], "healthy": [], "unhealthy": {}, "error": "no ROCm device visible"}
+    parts = [res]
+    if is_dist():
+        parts = [None] * world()[1]
+        dist.all_gather_object(parts, res, group=dp.group())
+    if world()[0] != 0:
+        return None
+    return health.set_last(health.merge(parts))
+
+
 # ------------------------------------------------------------ map_classify
 def _open_table(path: str):
     from ..io.csv import open_csv

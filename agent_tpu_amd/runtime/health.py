@@ -29,7 +29,9 @@ def _probe(index: int) -> Optional[str]:
         g = torch.Generator().manual_seed(index)
         a = torch.randn(64, 128, generator=g).to(torch.bfloat16)
         w = torch.randn(256, 128, generator=g).to(torch.bfloat16)
-        y = ops.linear(a.to(dev), w.to(dev)).float().cpu()
+        # the kernel launches on the CURRENT device's stream: make device ``index`` current
+        with torch.cuda.device(dev):
+            y = ops.linear(a.to(dev), w.to(dev)).float().cpu()
         ref = a.float() @ w.float().t()
         err = ((y - ref).abs().max() / ref.abs().max()).item()
         if not err < 2e-2:
@@ -39,8 +41,12 @@ def _probe(index: int) -> Optional[str]:
         return f"{type(exc).__name__}: {exc}"
 
 
-def check(probe: bool = True) -> Dict[str, Any]:
-    """``{ok, devices:[...], healthy:[idx], unhealthy:{idx: reason}}``; never raises."""
+def check(probe: bool = True, only: Optional[List[int]] = None) -> Dict[str, Any]:
+    """``{ok, devices:[...], healthy:[idx], unhealthy:{idx: reason}}``; never raises.
+
+    ``only``: the device indices this process may touch (MFMA probe, free-HBM
+    query). A DP rank passes its own device so it never creates a HIP context on
+    a peer's GPU; :func:`check_dp` gathers the ranks' answers. ``None`` = all."""
     global _last
     out: Dict[str, Any] = {"ok": False, "devices": [], "healthy": [], "unhealthy": {}}
     try:
@@ -52,16 +58,20 @@ def check(probe: bool = True) -> Dict[str, Any]:
             return out
         from .._native import native
 
-        devs = native().device_query()
+        mem_of = only[0] if only else -1
+        devs = native().device_query(mem_of)
     except Exception as exc:
         out["error"] = f"{type(exc).__name__}: {exc}"
         _last = out
         return out
     for d in devs:
         idx = int(d["index"])
+        if only is not None and idx not in only:
+            continue
         info = {k: d[k] for k in ("index", "name", "arch", "compute_units", "clock_khz")}
         info["hbm_total_gb"] = round(d["total_memory_bytes"] / 2**30, 2)
-        info["hbm_free_gb"] = round(d["free_memory_bytes"] / 2**30, 2)
+        if d.get("free_memory_known", True):
+            info["hbm_free_gb"] = round(d["free_memory_bytes"] / 2**30, 2)
         out["devices"].append(info)
         reason = None
         if not str(d["arch"]).startswith(EXPECTED_ARCH):
@@ -77,6 +87,36 @@ def check(probe: bool = True) -> Dict[str, Any]:
     out["ok"] = bool(out["healthy"])
     _last = out
     return out
+
+
+def merge(parts: List[Dict[str, Any]]) -> Dict[str, Any]:
+    """One node view from per-rank :func:`check` results (each covering its own device)."""
+    out: Dict[str, Any] = {"ok": False, "devices": [], "healthy": [], "unhealthy": {}}
+    errs = []
+    for p in parts:
+        out["devices"] += p.get("devices", [])
+        out["healthy"] += p.get("healthy", [])
+        out["unhealthy"].update(p.get("unhealthy", {}))
+        if p.get("error"):
+            errs.append(p["error"])
+    out["devices"].sort(key=lambda d: d["index"])
+    out["healthy"] = sorted(set(out["healthy"]) - set(out["unhealthy"]))
+    out["ok"] = bool(out["healthy"])
+    if errs:
+        out["error"] = "; ".join(errs)
+    return out
+
+
+def set_last(res: Dict[str, Any]) -> Dict[str, Any]:
+    global _last
+    with _lock:
+        for idx, reason in _unhealthy.items():
+            res["unhealthy"].setdefault(idx, reason)
+            if idx in res["healthy"]:
+                res["healthy"].remove(idx)
+        res["ok"] = bool(res["healthy"])
+        _last = res
+    return res
 
 
 def mark_unhealthy(index: int, reason: str) -> None:

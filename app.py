@@ -148,8 +148,9 @@ class Metrics:
 
 
 def gpu_metrics() -> Dict[str, Any]:
-    """``gpu_util[]`` from amdgpu sysfs; HBM use per device only if this process
-    already initialised the GPU."""
+    """``gpu_util[]`` and ``hbm_used_gb[]``/``hbm_total_gb[]`` from amdgpu sysfs for
+    every GPU of the node. Without sysfs, HBM of this process's
+    own device only, and only if it already initialised it."""
     out: Dict[str, Any] = {}
     try:
         from worker_sizing import probe_gpu_busy
@@ -160,16 +161,22 @@ def gpu_metrics() -> Dict[str, Any]:
     except Exception:
         pass
     try:
+        from worker_sizing import probe_vram
+
+        vram = probe_vram()
+        if vram:  # node-wide, from sysfs: no HIP context on any device
+            out.update({"hbm_used_gb": [round(u / 2**30, 2) for u, _ in vram],
+                        "hbm_total_gb": [round(t / 2**30, 2) for _, t in vram]})
+            return out
         import torch
 
         if not torch.cuda.is_available() or not torch.cuda.is_initialized():
             return out
-        used, total = [], []
-        for i in range(torch.cuda.device_count()):
-            free_b, tot_b = torch.cuda.mem_get_info(i)
-            used.append(round((tot_b - free_b) / 2**30, 2))
-            total.append(round(tot_b / 2**30, 2))
-        out.update({"hbm_used_gb": used, "hbm_total_gb": total})
+        # no sysfs: this process's OWN device only (never a peer rank's GPU)
+        i = torch.cuda.current_device()
+        free_b, tot_b = torch.cuda.mem_get_info(i)
+        out.update({"hbm_used_gb": [round((tot_b - free_b) / 2**30, 2)], "hbm_total_gb": [round(tot_b / 2**30, 2)],
+                    "hbm_device": i})
     except Exception:
         pass
     return out
@@ -195,6 +202,11 @@ def gpu_health(caps: List[str]) -> Optional[Dict[str, Any]]:
             return {"ok": False, "error": "no ROCm device visible"}
         from agent_tpu_amd.runtime import health
 
+        if int(os.getenv("WORLD_SIZE", "1")) > 1:
+            # DP: each rank probes its own GPU; rank 0 never touches a peer's device
+            from agent_tpu_amd.parallel.dp_ops import dispatch
+
+            return dispatch("health_check", {})
         return health.check()
     except Exception as exc:
         return {"ok": False, "error": f"{type(exc).__name__}: {exc}"}

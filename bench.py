@@ -55,20 +55,56 @@ def parse():
     return ap.parse_args()
 
 
+def launch_ranks(a) -> int:
+    """Bare ``bench.py --gpus N`` (N > 1): start N ranks as a child torch.distributed.run.
+
+    Nothing here touches the GPU (``device_count`` does not create a context on
+    this image), and the ranks run in a child process, never an exec."""
+    from agent_tpu_amd.parallel.launch import self_launch, visible_device_count
+
+    if a.dist_backend == "nccl":
+        n = visible_device_count()
+        if n < a.gpus:
+            print(f"[bench] --gpus {a.gpus} but only {n} visible GPU(s): RCCL needs one GPU per rank "
+                  f"(use --dist-backend gloo to rehearse on fewer)", file=sys.stderr, flush=True)
+            return 3
+    rc, objs = self_launch(os.path.abspath(__file__), sys.argv[1:], a.gpus)
+    if rc != 0 or not objs:
+        print(f"[bench] ranks exited with {rc} ({len(objs)} result lines)", file=sys.stderr, flush=True)
+        return rc or 4
+    out = objs[-1]
+    out.setdefault("config", {})["launcher"] = "self (bench.py -> child torch.distributed.run)"
+    print(json.dumps(out), flush=True)
+    return 0
+
+
 def main() -> int:
     a = parse()
+    from agent_tpu_amd.parallel.launch import LaunchError, bind_local_device, emit_result, launched, verify_ranks
+
+    if a.gpus > 1 and not launched():
+        return launch_ranks(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus and rank == 0:
-        print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
-    torch.cuda.set_device(dev)
+    if world != a.gpus:
+        print(f"[bench] rank {rank}: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr, flush=True)
+        return 5
+    try:
+        dev = bind_local_device(a.dist_backend)
+    except LaunchError as exc:
+        print(f"[bench] rank {rank}: {exc}", file=sys.stderr, flush=True)
+        return 5
     if world > 1:
         if a.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(a.dist_backend)
+    try:
+        rank_table = verify_ranks(a.gpus, a.dist_backend if world > 1 else "nccl", dev)
+    except LaunchError as exc:
+        print(f"[bench] rank {rank}: {exc}", file=sys.stderr, flush=True)
+        return 5
+    rccl_world = dist.get_world_size() if world > 1 else 1
 
     from agent_tpu_amd._native import native
     from agent_tpu_amd.models.bert import config_for, init_random
@@ -145,6 +181,10 @@ def main() -> int:
                 "seq_len": a.seq_len,
                 "parallelism": f"dp{world}",
                 "dist_backend": a.dist_backend if world > 1 else None,
+                "rccl_world_size": rccl_world if a.dist_backend == "nccl" or world == 1 else None,
+                "pg_world_size": rccl_world,
+                "rank_devices": [t["device"] for t in rank_table],
+                "distinct_devices": len({t["device_id"] for t in rank_table}) == len(rank_table),
                 "rows_per_gpu_per_step": B,
                 "num_labels": cfg.num_labels,
                 "topk": min(a.topk, cfg.num_labels),
@@ -157,7 +197,7 @@ def main() -> int:
                                                          / world / 1e12, 1),
             },
         }
-        print(json.dumps(out), flush=True)
+        emit_result(out)
     if world > 1:
         dist.destroy_process_group()
     return 0

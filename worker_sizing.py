@@ -24,7 +24,7 @@ import json
 import math
 import os
 import subprocess
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List, Optional, Tuple
 
 try:
     import psutil
@@ -164,6 +164,32 @@ def probe_gpu_busy(root: Optional[str] = None) -> List[float]:
                 out.append(round(int(f.read().strip()) / 100.0, 3))
         except (OSError, ValueError):
             continue
+    return out
+
+
+def probe_vram(root: Optional[str] = None) -> List[Tuple[int, int]]:
+    """(used, total) VRAM bytes of every AMD GPU from amdgpu's sysfs
+    ``mem_info_vram_used/total``, in card order — node-wide HBM use without a HIP
+    context on any device (rank 0 must not open contexts on its peers' GPUs)."""
+    root = root or os.getenv("ATPU_DRM_ROOT", DRM_ROOT)
+    try:
+        cards = [c for c in os.listdir(root) if c.startswith("card") and c[4:].isdigit()]
+    except OSError:
+        return []
+    out: List[Tuple[int, int]] = []
+    for c in sorted(cards, key=lambda c: int(c[4:])):
+        dev = os.path.join(root, c, "device")
+        try:
+            with open(os.path.join(dev, "vendor")) as f:
+                if f.read().strip().lower() != "0x1002":
+                    continue
+            with open(os.path.join(dev, "mem_info_vram_used")) as f:
+                used = int(f.read().strip())
+            with open(os.path.join(dev, "mem_info_vram_total")) as f:
+                total = int(f.read().strip())
+        except (OSError, ValueError):
+            continue
+        out.append((used, total))
     return out
 
 
