@@ -12,7 +12,7 @@ tests. Collectives issued by a DP classify task:
 * C2 :func:`all_gather_rows` — per-rank top-k rows, padded to the largest
   shard, gathered with one ``all_gather_into_tensor`` per tensor; counts are
   gathered first (4 B/rank) so ragged shards reassemble exactly.
-* C3 (risk) lives in :mod:`agent_tpu_amd.parallel.risk`.
+* C3 (risk) is the all-reduce in :func:`agent_tpu_amd.parallel.dp_ops.risk_task`.
 
 Shard planning is contiguous and balanced (:func:`split_range`), so results
 concatenate in rank order into the original row order.
@@ -29,6 +29,8 @@ from typing import Any, Iterable, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
+
+from . import watchdog
 
 
 def is_dist() -> bool:
@@ -112,7 +114,8 @@ def broadcast_pack(pack, cfg, device: torch.device, src: int = 0, builder=None):
     if is_dist():
         cdev = comm_device(device)
         buf = out.buffer if out.buffer.device == cdev else out.buffer.to(cdev)
-        dist.broadcast(buf, src=src, group=_GROUP)
+        with watchdog.collective("weight broadcast"):
+            dist.broadcast(buf, src=src, group=_GROUP)
         if buf is not out.buffer:
             out.buffer.copy_(buf)
     return out
@@ -123,7 +126,8 @@ def broadcast_task(obj: Any, src: int = 0) -> Any:
     if not is_dist():
         return obj
     box = [obj]
-    dist.broadcast_object_list(box, src=src, group=_GROUP)
+    with watchdog.collective("task broadcast"):
+        dist.broadcast_object_list(box, src=src, group=_GROUP)
     return box[0]
 
 
@@ -140,7 +144,8 @@ def all_gather_rows(*tensors: torch.Tensor) -> Tuple[torch.Tensor, ...]:
     cdev = comm_device(dev)
     cnt = torch.tensor([tensors[0].shape[0]], dtype=torch.int64, device=cdev)
     counts = torch.empty(ws, dtype=torch.int64, device=cdev)
-    dist.all_gather_into_tensor(counts, cnt, group=_GROUP)
+    with watchdog.collective("row-count gather"):
+        dist.all_gather_into_tensor(counts, cnt, group=_GROUP)
     counts_l: List[int] = counts.tolist()
     mx = max(counts_l) if counts_l else 0
     outs = []
@@ -151,7 +156,8 @@ def all_gather_rows(*tensors: torch.Tensor) -> Tuple[torch.Tensor, ...]:
             t = torch.cat([t, pad], 0)
         t = t.contiguous()
         g = torch.empty((ws * mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=cdev)
-        dist.all_gather_into_tensor(g, t, group=_GROUP)
+        with watchdog.collective("row all-gather"):
+            dist.all_gather_into_tensor(g, t, group=_GROUP)
         if all(c == mx for c in counts_l):
             outs.append(g.to(dev))
         else:

@@ -28,7 +28,7 @@ import torch
 import torch.distributed as dist
 
 from ..utils.trace import span
-from . import dp
+from . import dp, watchdog
 from .dp import all_gather_rows, broadcast_task, comm_device, is_dist, members, split_range, world
 
 _TASKS: Dict[str, Callable[[Dict[str, Any]], Any]] = {}
@@ -44,17 +44,22 @@ def dp_task(name: str):
 
 
 def init_from_env() -> None:
-    """Join the node's process group (RCCL on GPUs, gloo otherwise)."""
+    """Join the node's process group (RCCL on GPUs, gloo otherwise) with a bounded
+    collective timeout (``DP_COLLECTIVE_TIMEOUT`` s), and start this rank's heartbeat."""
     if is_dist():
         return
+    from datetime import timedelta
+
     local = int(os.getenv("LOCAL_RANK", "0"))
+    timeout = timedelta(seconds=watchdog.collective_timeout())
     if torch.cuda.is_available() and os.getenv("ATPU_DP_BACKEND", "nccl") == "nccl":
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
     else:
         if torch.cuda.is_available():  # gloo rehearsal: ranks may share a GPU
             torch.cuda.set_device(local % torch.cuda.device_count())
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=timeout)
+    watchdog.start(dist.get_rank())
 
 
 _FAULT_HITS: Dict[str, int] = {}
@@ -97,8 +102,15 @@ def maybe_inject_fault(stage: str) -> None:
         if n >= int(parts[3]):
             return
         _FAULT_HITS[stage] = n + 1
-    if len(parts) >= 5 and parts[4] == "device":
+    kind = parts[4] if len(parts) >= 5 else ""
+    if kind == "device":
         raise RuntimeError(f"hipErrorLaunchFailure: injected device fault ({spec}) at {stage}")
+    if kind == "kill":  # the process dies mid-job (OOM killer, abort, SIGKILL)
+        import signal
+
+        os.kill(os.getpid(), signal.SIGKILL)
+    if kind == "hang":  # a wedged rank: alive, heartbeat running, never reaches the next collective
+        time.sleep(1e6)
     raise RuntimeError(f"injected fault ({spec}) at {stage}")
 
 
@@ -119,7 +131,8 @@ def _check_errors(err: str) -> None:
         return
     rank, ws = world()
     errs = [None] * ws
-    dist.all_gather_object(errs, err, group=dp.group())
+    with watchdog.collective("error exchange"):
+        dist.all_gather_object(errs, err, group=dp.group())
     glob = members()  # group index -> global rank (errors name global ranks)
     bad = [(glob[r], e) for r, e in enumerate(errs) if e]
     if not bad:
@@ -153,10 +166,12 @@ def in_task() -> bool:
 def run_collective(name: str, payload: Dict[str, Any]) -> Any:
     fn = _TASKS[name]
     _CTX.depth = getattr(_CTX, "depth", 0) + 1
+    watchdog.progress(f"run {name}")
     try:
         return fn(payload)
     finally:
         _CTX.depth -= 1
+        watchdog.progress("idle")
 
 
 def load_collectively(local: Callable[[], Any], collective: Callable[[Any], Any],
@@ -199,9 +214,37 @@ def load_collectively(local: Callable[[], Any], collective: Callable[[Any], Any]
     return res
 
 
+def _announce() -> None:
+    """Rank 0: flag task ``seq`` in the store; idle workers wait on that key, not in a
+    collective, so an idle gap between jobs never trips the collective timeout."""
+    seq = watchdog.next_task()
+    st = watchdog._get_store()
+    if st is not None:
+        st.set(f"task/{seq}", "1")
+
+
+def _await_task() -> bool:
+    """Worker: block until rank 0 announces the next task; False if rank 0 is gone."""
+    from datetime import timedelta
+
+    seq = watchdog.next_task()
+    st = watchdog._get_store()
+    if st is None:
+        return True
+    while True:
+        try:
+            st.wait([f"task/{seq}"], timedelta(seconds=5))
+            return True
+        except Exception:
+            pid = watchdog._get("pid/0")
+            if pid is not None and not watchdog._pid_alive(int(pid)):
+                return False
+
+
 def dispatch(name: str, payload: Dict[str, Any]) -> Any:
     """Rank 0: broadcast ``(name, payload)`` then execute it with every rank."""
     if is_dist():
+        _announce()
         broadcast_task({"op": name, "payload": payload})
     return run_collective(name, payload)
 
@@ -211,6 +254,9 @@ def worker_loop() -> int:
     rank, _ = world()
     print(f"[agent-mi355x] dp worker rank={rank} ready", flush=True)
     while True:
+        if not _await_task():
+            print(f"[agent-mi355x] dp worker rank={rank}: rank 0 is gone; exiting", flush=True)
+            return watchdog.EXIT_RANK_LOST
         desc = broadcast_task(None)
         if not isinstance(desc, dict) or desc.get("op") == _SHUTDOWN:
             break
@@ -228,6 +274,7 @@ def worker_loop() -> int:
 
 def shutdown_workers() -> None:
     if is_dist() and world()[0] == 0:
+        _announce()
         broadcast_task({"op": _SHUTDOWN})
 
 
@@ -245,7 +292,8 @@ def health_task(payload: Dict[str, Any]) -> Any:
     parts = [res]
     if is_dist():
         parts = [None] * world()[1]
-        dist.all_gather_object(parts, res, group=dp.group())
+        with watchdog.collective("health gather"):
+            dist.all_gather_object(parts, res, group=dp.group())
     if world()[0] != 0:
         return None
     return health.set_last(health.merge(parts))
@@ -329,6 +377,19 @@ def classify_rows_task(payload: Dict[str, Any]) -> Any:
     return mc.texts_result(h, idx.cpu(), sc.cpu(), payload, ws)
 
 
+@dp_task("map_classify_batch")
+def classify_batch_task(payload: Dict[str, Any]) -> Any:
+    """Several ``input``/``texts`` jobs of one lease (same model): one collective model
+    load, then :func:`ops.map_classify.classify_batch` on every rank."""
+    from ops import map_classify as mc
+    from ops._gpu_runtime import get_gpu_handle, get_model_path
+
+    rank, ws = world()
+    payloads = payload["payloads"]
+    h = get_gpu_handle(get_model_path(payloads[0].get("model_path")))
+    return mc.classify_batch(h, payloads, rank, ws)
+
+
 # ---------------------------------------------------------- risk_accumulate
 def _local_values(payload: Dict[str, Any], rank: int, ws: int) -> Tuple[torch.Tensor, int]:
     """This rank's slice of the values, as fp64."""
@@ -371,8 +432,9 @@ def risk_task(payload: Dict[str, Any]) -> Any:
         s = stats.to(cdev)
         sums = s[:2].clone()
         ext = torch.stack([s[3], -s[2]])  # max, -min -> one MAX all-reduce
-        dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=dp.group())
-        dist.all_reduce(ext, op=dist.ReduceOp.MAX, group=dp.group())
+        with watchdog.collective("risk all-reduce"):
+            dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=dp.group())
+            dist.all_reduce(ext, op=dist.ReduceOp.MAX, group=dp.group())
         stats = torch.stack([sums[0], sums[1], -ext[1], ext[0]]).cpu()
     else:
         stats = stats.cpu()

@@ -63,10 +63,15 @@ TASKS_RAW = os.getenv("TASKS", "echo,map_classify_tpu")
 AGENT_LABELS_RAW = os.getenv("AGENT_LABELS", "")
 # new knobs
 RESULT_RETRIES = int(os.getenv("RESULT_RETRIES", "2"))
+# same-op jobs of one lease run as ONE device batch (map_summarize docs, map_classify rows)
+LEASE_BATCH = os.getenv("LEASE_BATCH", "1").strip().lower() not in ("0", "false", "no", "off")
+# lease size this agent can batch well; advertised in worker_profile.limits (MAX_TASKS stays the request)
+MAX_BATCH_TASKS = int(os.getenv("MAX_BATCH_TASKS", "256"))
 FAIL_ON_NOT_OK = os.getenv("FAIL_ON_NOT_OK", "0").strip().lower() in ("1", "true", "yes")
 
 _running = True
 _last_log: Dict[str, float] = {}
+EXIT_RANK_LOST = 3  # a DP rank died or hung: restart the group (torchrun --max-restarts)
 
 
 def parse_labels(raw: str) -> Dict[str, Any]:
@@ -187,6 +192,7 @@ METRICS = Metrics()
 
 # --------------------------------------------------------------- profile
 GPU_OPS = {"map_classify", "map_classify_tpu", "map_summarize", "risk_accumulate"}
+BATCH_OPS = {"map_classify", "map_classify_tpu", "map_summarize"}
 
 
 def gpu_health(caps: List[str]) -> Optional[Dict[str, Any]]:
@@ -212,7 +218,7 @@ def gpu_health(caps: List[str]) -> Optional[Dict[str, Any]]:
         return {"ok": False, "error": f"{type(exc).__name__}: {exc}"}
 
 
-def worker_profile(health: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
+def worker_profile(health: Optional[Dict[str, Any]] = None, caps: Optional[List[str]] = None) -> Dict[str, Any]:
     from worker_sizing import build_worker_profile
 
     prof = build_worker_profile()
@@ -226,6 +232,11 @@ def worker_profile(health: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
     prof["tier"] = "mi355x" if prof.get("gpu", {}).get("gpu_present") else "cpu"
     prof["limits"] = {"max_payload_bytes": int(os.getenv("MAX_PAYLOAD_BYTES", "262144")),
                       "max_tokens": int(os.getenv("MAX_TOKENS", "2048"))}
+    batchable = sorted(BATCH_OPS & set(caps or ()))
+    if LEASE_BATCH and batchable:
+        # a controller may lease up to this many same-op jobs at once: they run as one GPU batch
+        prof.setdefault("workers", {})["max_batch_tasks"] = MAX_BATCH_TASKS
+        prof["workers"]["batch_ops"] = batchable
     return prof
 
 
@@ -331,14 +342,50 @@ class Agent:
         if self.health is not None:
             print(f"{LOG} gpu health ok={self.health.get('ok')} healthy={self.health.get('healthy')} "
                   f"unhealthy={self.health.get('unhealthy', {})} {self.health.get('error', '')}", flush=True)
-        self.profile = worker_profile(self.health)
+        self.profile = worker_profile(self.health, self.caps)
+        self.exit_code = 0
+        self._inflight: Dict[str, Tuple[str, Any, str]] = {}  # job_id -> (lease_id, epoch, op)
+        self._inflight_lock = threading.Lock()
+
+    # ---------------------------------------------------- lost-rank handling
+    def _begin(self, lease_id: str, jobs: List[Tuple[str, str, Dict[str, Any], Any]]) -> None:
+        with self._inflight_lock:
+            for job_id, op, _, epoch in jobs:
+                self._inflight[job_id] = (lease_id, epoch, op)
+
+    def _claim(self, job_id: str) -> bool:
+        """True once per job: whoever claims it (main loop or DP watchdog) posts its result."""
+        with self._inflight_lock:
+            return self._inflight.pop(job_id, None) is not None
+
+    def on_rank_lost(self, msg: str) -> None:
+        """DP watchdog (rank 0): a rank died or hung. Fail every in-flight job naming it,
+        then exit non-zero so the launcher restarts the group in fresh processes (the
+        main thread may be blocked in a collective that will never complete)."""
+        print(f"{LOG} {msg}; failing in-flight jobs and exiting for a restart", flush=True)
+        with self._inflight_lock:
+            jobs, self._inflight = dict(self._inflight), {}
+        err = {"type": "RankLost", "message": msg, "trace": ""}
+        for job_id, (lease_id, epoch, op) in jobs.items():
+            try:
+                self.ctl.result(lease_id, job_id, epoch, "failed", None, err)
+            except Exception as exc:
+                print(f"{LOG} post result error: {exc}", flush=True)
+            log_every("exec", f"{LOG} FAIL job={job_id} op={op} err={err}")
+        sys.stdout.flush()
+        os._exit(EXIT_RANK_LOST)
 
     def run_task(self, lease_id: str, task: Any) -> None:
         try:
-            job_id, op, payload, epoch = extract_task(task)
+            job = extract_task(task)
         except Exception as exc:
             log_every("task:bad", f"{LOG} bad task: {exc} task={repr(task)[:300]}")
             return
+        self._run_one(lease_id, job)
+
+    def _run_one(self, lease_id: str, job: Tuple[str, str, Dict[str, Any], Any]) -> None:
+        job_id, op, payload, epoch = job
+        self._begin(lease_id, [job])
         t0 = time.time()
         out, err = None, None
         try:
@@ -352,8 +399,14 @@ class Agent:
         except Exception as exc:
             err = {"type": type(exc).__name__, "message": str(exc), "trace": traceback.format_exc(limit=12)}
             self._note_device_fault(str(exc))
+            self._note_rank_lost(exc)
+        self._finish(lease_id, job_id, op, epoch, out, err, (time.time() - t0) * 1000.0)
+
+    def _finish(self, lease_id: str, job_id: str, op: str, epoch: Any, out: Any, err: Optional[Dict[str, Any]],
+                ms: float) -> None:
+        if not self._claim(job_id):
+            return  # already failed by the DP watchdog
         ok = err is None
-        ms = (time.time() - t0) * 1000.0
         METRICS.job_done(ok, out)
         try:
             self.ctl.result(lease_id, job_id, epoch, "succeeded" if ok else "failed",
@@ -364,6 +417,78 @@ class Agent:
             print(f"{LOG} ok job={job_id} op={op} ms={ms:.1f}", flush=True)
         else:
             log_every("exec", f"{LOG} FAIL job={job_id} op={op} ms={ms:.1f} err={err}")
+
+    def _run_batch(self, lease_id: str, jobs: List[Tuple[str, str, Dict[str, Any], Any]]) -> None:
+        """Same-op jobs of one lease as ONE device batch. Each job
+        still gets its own result with its own ``job_epoch``; a bad payload fails
+        (or soft-fails) only its own result, exactly as the single-job handler would."""
+        from ops import get_batch_op
+
+        op = jobs[0][1]
+        fn = get_batch_op(op)
+        self._begin(lease_id, jobs)
+        t0 = time.time()
+        try:
+            with _op_span(f"{op}[x{len(jobs)}]"):
+                outs = fn([p for _, _, p, _ in jobs])
+            if len(outs) != len(jobs):
+                raise RuntimeError(f"batch handler of {op} returned {len(outs)} results for {len(jobs)} jobs")
+        except Exception as exc:  # the batch as a whole failed (e.g. a device fault): every job fails
+            tr = traceback.format_exc(limit=12)
+            self._note_device_fault(str(exc))
+            self._note_rank_lost(exc)
+            outs = [("err", exc, tr)] * len(jobs)
+        ms = (time.time() - t0) * 1000.0
+        for (job_id, _, _, epoch), res in zip(jobs, outs):
+            out, err = None, None
+            if res[0] == "ok":
+                out = res[1]
+                if FAIL_ON_NOT_OK and isinstance(out, dict) and out.get("ok") is False:
+                    out, err = None, {"type": "RuntimeError", "message": str(out.get("error", "op returned ok=false")),
+                                      "trace": ""}
+            else:
+                exc = res[1]
+                tr = res[2] if len(res) > 2 else "".join(
+                    traceback.format_exception(type(exc), exc, exc.__traceback__, limit=12))
+                err = {"type": type(exc).__name__, "message": str(exc), "trace": tr}
+            self._finish(lease_id, job_id, op, epoch, out, err, ms)
+
+    def run_tasks(self, lease_id: str, tasks: List[Any]) -> None:
+        """Every task of the lease, in order; with LEASE_BATCH, same-op jobs of a
+        batchable op run together at the position of the first of them."""
+        from ops import get_batch_op
+
+        jobs: List[Tuple[str, str, Dict[str, Any], Any]] = []
+        for task in tasks:
+            try:
+                jobs.append(extract_task(task))
+            except Exception as exc:
+                log_every("task:bad", f"{LOG} bad task: {exc} task={repr(task)[:300]}")
+        groups: Dict[str, List[Tuple[str, str, Dict[str, Any], Any]]] = {}
+        if LEASE_BATCH and len(jobs) > 1:
+            for j in jobs:
+                if j[1] in self.handlers and get_batch_op(j[1]) is not None:
+                    groups.setdefault(j[1], []).append(j)
+            groups = {op: js for op, js in groups.items() if len(js) > 1}
+        done: set = set()
+        for j in jobs:
+            op = j[1]
+            if op in groups:
+                if op not in done:
+                    done.add(op)
+                    self._run_batch(lease_id, groups[op])
+                continue
+            self._run_one(lease_id, j)
+
+    def _note_rank_lost(self, exc: BaseException) -> None:
+        """A job that lost a DP rank ends the loop after its result: exit non-zero."""
+        from agent_tpu_amd.parallel.watchdog import RankLost
+
+        global _running
+        if isinstance(exc, RankLost):
+            print(f"{LOG} {exc}; exiting for a restart", flush=True)
+            self.exit_code = EXIT_RANK_LOST
+            _running = False
 
     def _note_device_fault(self, msg: str) -> None:
         """A HIP fault marks the device unhealthy and re-advertises the profile.
@@ -389,7 +514,7 @@ class Agent:
             print(f"{LOG} device {dev} marked unhealthy: {m[:200]}", flush=True)
         if hit:
             self.health = health.last()
-            self.profile = worker_profile(self.health)
+            self.profile = worker_profile(self.health, self.caps)
 
     def loop(self) -> None:
         while _running:
@@ -403,8 +528,7 @@ class Agent:
                 time.sleep(IDLE_SLEEP_SEC)
                 continue
             lease_id, tasks = leased
-            for task in tasks:
-                self.run_task(lease_id, task)
+            self.run_tasks(lease_id, tasks)
 
 
 def _on_signal(signum: int, _frame: Any) -> None:
@@ -432,16 +556,22 @@ def main() -> int:
             return dp_ops.worker_loop()
 
     agent = Agent()
+    if world > 1:
+        from agent_tpu_amd.parallel.watchdog import Watchdog
+
+        Watchdog(agent.on_rank_lost).start()
     print(f"{LOG} starting name={AGENT_NAME} controller={CONTROLLER_URL} ops={agent.caps}", flush=True)
     try:
         agent.loop()
     finally:
         if world > 1:
-            from agent_tpu_amd.parallel import dp_ops
+            from agent_tpu_amd.parallel import dp_ops, watchdog
 
-            dp_ops.shutdown_workers()
+            watchdog.stop()  # workers exiting on shutdown are not "lost"
+            if agent.exit_code == 0:
+                dp_ops.shutdown_workers()
     print(f"{LOG} stopped", flush=True)
-    return 0
+    return agent.exit_code
 
 
 if __name__ == "__main__":

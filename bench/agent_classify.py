@@ -30,7 +30,13 @@ def main() -> int:
     ap.add_argument("--shard", type=int, default=16384, help="CSV rows per job")
     ap.add_argument("--output", default="rows", choices=["rows", "summary"])
     ap.add_argument("--model", default="bert-base")
+    ap.add_argument("--form", default="csv", choices=["csv", "input"],
+                    help="csv: CSV-shard jobs; input: the reference job shape, one pre-tokenized row per job")
+    ap.add_argument("--max-tasks", type=int, default=1, help="MAX_TASKS (input form: jobs per lease, batched)")
+    ap.add_argument("--batch", default="1", help="LEASE_BATCH")
     a = ap.parse_args()
+    if a.form == "input":
+        return input_form(a)
     from agent_tpu_amd.utils.synthetic import write_csv
 
     rows = (a.jobs + 1) * a.shard
@@ -79,6 +85,56 @@ def main() -> int:
                                  "median_op_elapsed_ms": op_ms, "median_op_timing_ms": timing,
                                  "transport": "HTTP/1.1 keep-alive, loopback mock controller",
                                  "data": "synthetic CSV rows, random-init weights"}}), flush=True)
+    return 0
+
+
+def input_form(a) -> int:
+    """Reference-shaped jobs (``{"input": [128 token ids]}``, one row each; ref
+    ``ops/map_classify_tpu.py:52-75``), MAX_TASKS per lease, batched on the GPU."""
+    import numpy as np
+
+    rng = np.random.default_rng(3)
+    S = 128
+
+    def ids(i):
+        n = int(rng.integers(16, S - 2))
+        return [101] + [int(x) for x in rng.integers(1000, 30000, n)] + [102] + [0] * (S - n - 2)
+
+    ctl = MockController().start()
+
+    def job(i):
+        return {"id": f"j{i}", "op": "map_classify", "job_epoch": i,
+                "payload": {"input": ids(i), "topk": 2, "model_path": a.model}}
+
+    ctl.lease(*[job(-1 - i) for i in range(a.max_tasks)], lease_id="Lwarm")
+    nwarm = a.max_tasks
+    env = dict(os.environ, CONTROLLER_URL=ctl.url, TASKS="map_classify", IDLE_SLEEP_SEC="0.01",
+               MAX_TASKS=str(a.max_tasks), LEASE_BATCH=a.batch, PYTHONUNBUFFERED="1")
+    p = subprocess.Popen([sys.executable, "app.py"], cwd=REPO, env=env, stdout=subprocess.DEVNULL,
+                         stderr=subprocess.DEVNULL)
+    try:
+        ok = ctl.wait(lambda c: len(c.results) >= nwarm, 600)
+        for b0 in range(0, a.jobs, a.max_tasks):
+            ctl.lease(*[job(i) for i in range(b0, min(a.jobs, b0 + a.max_tasks))], lease_id=f"L{b0}")
+        t0 = time.perf_counter()
+        ok = ok and ctl.wait(lambda c: len(c.results) >= nwarm + a.jobs, 1200)
+        el = time.perf_counter() - t0
+    finally:
+        p.send_signal(signal.SIGTERM)
+        p.wait(timeout=120)
+        ctl.stop()
+    res = ctl.results[nwarm:]
+    bad = [r for r in res if r.get("status") != "succeeded" or "fallback" in (r.get("result") or {})]
+    if not ok or bad:
+        print(json.dumps({"error": "timeout" if not ok else "failed jobs", "results": len(res),
+                          "first_bad": bad[:1]}, default=str)[:2000])
+        return 1
+    print(json.dumps({"metric": f"classified rows/sec end to end through the agent, 1-row input jobs ({a.model}, 1 GPU)",
+                      "value": round(a.jobs / el, 1), "unit": "rows/s", "higher_is_better": True,
+                      "config": {"jobs": a.jobs, "max_tasks": a.max_tasks, "lease_batch": a.batch, "seq_len": S,
+                                 "result_keys": sorted(res[0]["result"]),
+                                 "transport": "HTTP/1.1 keep-alive, loopback mock controller",
+                                 "data": "synthetic token ids, random-init weights"}}), flush=True)
     return 0
 
 

@@ -34,6 +34,9 @@ from typing import Any, Callable, Dict, FrozenSet, List, Optional, Set, Tuple
 OpFn = Callable[..., Any]
 
 OPS_REGISTRY: Dict[str, OpFn] = {}
+#: op name -> handler over a LIST of payloads (same-op jobs of one lease, run as
+#: one device batch); returns one ``("ok", result)`` / ``("err", exception)`` per payload
+BATCH_REGISTRY: Dict[str, OpFn] = {}
 OPS_LOAD_ERRORS: List[Tuple[str, str]] = []  # (module, "Type: message")
 
 #: op name -> module file under ``ops/`` (every entry exists in this tree)
@@ -73,6 +76,23 @@ def register_op(name: str) -> Callable[[OpFn], OpFn]:
         return fn
 
     return _wrap
+
+
+def register_batch_op(name: str) -> Callable[[OpFn], OpFn]:
+    """Decorator: ``fn(payloads) -> [("ok", result) | ("err", exc), ...]`` runs several
+    jobs of op ``name`` as one batch. Every entry must equal what the single-job
+    handler would return (or raise) for that payload; only the throughput differs."""
+
+    def _wrap(fn: OpFn) -> OpFn:
+        BATCH_REGISTRY[name] = fn
+        return fn
+
+    return _wrap
+
+
+def get_batch_op(name: str) -> Optional[OpFn]:
+    """The batch handler of an op already resolved by :func:`get_op` (or None)."""
+    return BATCH_REGISTRY.get(name)
 
 
 def _enabled_set() -> Optional[Set[str]]:
@@ -154,7 +174,10 @@ __all__ = [
     "OPS_LOAD_ERRORS",
     "OP_TO_MODULE",
     "OPT_IN_OPS",
+    "BATCH_REGISTRY",
     "register_op",
+    "register_batch_op",
+    "get_batch_op",
     "list_ops",
     "get_op",
 ]

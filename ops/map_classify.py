@@ -20,9 +20,9 @@ quantized outputs cast to float; see CONTRACT "Notes").
 from __future__ import annotations
 
 import time
-from typing import Any, Dict, List
+from typing import Any, Dict, List, Optional
 
-from . import register_op
+from . import register_batch_op, register_op
 
 OP_NAME = "map_classify_tpu"
 
@@ -55,6 +55,89 @@ def classify_ids(h, payload: Dict[str, Any], op: str, t0: float) -> Dict[str, An
                                          torch.tensor([max(1, n)], dtype=torch.int32, device=dev), k)
     return {"op": op, "model_path": h.model_path, "topk": _topk_list(idx[0].tolist(), sc[0].tolist()),
             "elapsed_ms": (time.time() - t0) * 1000.0}
+
+
+def _input_row(h, payload: Dict[str, Any]):
+    """Validate one reference-form row -> (ids int32 [S], n_tokens, k); raises like :func:`classify_ids`."""
+    import torch
+
+    k = max(1, min(int(payload.get("topk", 5)), h.cfg.num_labels))
+    S = h.engine.S
+    ids = torch.tensor(payload["input"], dtype=torch.int64)
+    if ids.numel() != S:
+        raise ValueError(f"Input size mismatch. Got {ids.numel()}, expected {S} for shape (1, {S}).")
+    if int(ids.min()) < 0 or int(ids.max()) >= h.cfg.vocab_size:
+        raise ValueError(f"token id out of range [0, {h.cfg.vocab_size})")
+    nz = (ids != 0).nonzero()
+    n = int(nz[-1]) + 1 if nz.numel() else 1
+    return ids.to(torch.int32), max(1, n), k
+
+
+def classify_batch(h, payloads: List[Dict[str, Any]], rank: int, ws: int) -> Optional[List[Any]]:
+    """Several ``input``/``texts`` jobs of one lease as one device batch (every rank calls it).
+
+    ``input`` rows (one pre-tokenized row per job, the reference job shape) are stacked
+    into ``[n, S]`` and run through the encoder in chunks of the engine batch on rank 0;
+    ``texts`` jobs are concatenated, split over the DP ranks and all-gathered (C2). Each
+    job gets exactly its single-job result; a bad payload gets its own error entry."""
+    import torch
+
+    from agent_tpu_amd.parallel.dp import all_gather_rows, split_range
+    from agent_tpu_amd.parallel.dp_ops import _check_errors, _err_str
+
+    out: List[Any] = [None] * len(payloads)
+    # ---- input form: rank 0 only (as the single-job path) ----
+    rows = []
+    if rank == 0:
+        for i, p in enumerate(payloads):
+            if "input" in p:
+                try:
+                    rows.append((i,) + _input_row(h, p))
+                except Exception as exc:
+                    out[i] = ("err", exc)
+        if rows:
+            dev, B, S = h.engine.device, h.engine.B, h.engine.S
+            kmax = max(r[3] for r in rows)
+            ids = torch.stack([r[1] for r in rows]).to(dev)
+            lens = torch.tensor([r[2] for r in rows], dtype=torch.int32).to(dev)
+            idx_l, sc_l = [], []
+            for b0 in range(0, len(rows), B):
+                _, idx, sc = h.engine.model.forward(ids[b0:b0 + B], lens[b0:b0 + B], kmax)
+                idx_l.append(idx[:, :kmax].cpu())
+                sc_l.append(sc[:, :kmax].cpu())
+            idx_all, sc_all = torch.cat(idx_l).tolist(), torch.cat(sc_l).tolist()
+            for (i, _, _, k), ir, sr in zip(rows, idx_all, sc_all):
+                p = payloads[i]
+                out[i] = ("ok", {"op": p.get("_op", OP_NAME), "model_path": h.model_path,
+                                 "topk": _topk_list(ir[:k], sr[:k]),
+                                 "elapsed_ms": (time.time() - float(p.get("_t0", time.time()))) * 1000.0})
+    # ---- texts form: every rank (same payloads everywhere -> same validation outcome) ----
+    tjobs = []
+    for i, p in enumerate(payloads):
+        if "input" not in p and "texts" in p:
+            try:
+                tjobs.append((i, check_texts(p), max(1, min(int(p.get("topk", 5)), h.cfg.num_labels))))
+            except Exception as exc:
+                out[i] = ("err", exc)
+    if tjobs:
+        texts = [t for _, ts, _ in tjobs for t in ts]
+        kmax = max(k for _, _, k in tjobs)
+        err, idx, sc = "", None, None
+        try:
+            s_r, n_r = split_range(0, len(texts), ws, rank)
+            res = h.engine.classify_texts(texts[s_r:s_r + n_r], kmax)
+            idx, sc = res.idx[:, :kmax].contiguous(), res.score[:, :kmax].contiguous()
+        except Exception as exc:
+            err = _err_str(exc)
+        _check_errors(err)
+        idx, sc = all_gather_rows(idx, sc)
+        if rank == 0:
+            idx, sc, pos = idx.cpu(), sc.cpu(), 0
+            for i, ts, k in tjobs:
+                n = len(ts)
+                out[i] = ("ok", texts_result(h, idx[pos:pos + n], sc[pos:pos + n], payloads[i], ws))
+                pos += n
+    return out if rank == 0 else None
 
 
 def check_texts(payload: Dict[str, Any]) -> List[str]:
@@ -112,13 +195,62 @@ def _rows_result(h, idx, sc, start: int, k: int, op: str, t0: float, extra: Dict
     return out
 
 
+def run_batch(payloads: List[Dict[str, Any]], op: str) -> List[Any]:
+    """Batch handler: ``input``/``texts`` jobs of one lease go to the device together
+    (one collective model load, one stacked forward); CSV-shard jobs (already large)
+    and malformed payloads run through the single-job path. Per-job errors follow the
+    single-job contract: the fallback stub when ``allow_fallback`` (default), else raised."""
+    from agent_tpu_amd.parallel.dp_ops import dispatch
+
+    t0 = time.time()
+    out: List[Any] = [None] * len(payloads)
+    groups: Dict[Any, List[int]] = {}
+    for i, p in enumerate(payloads):
+        p = p or {}
+        if ("input" in p or "texts" in p) and not ("source_uri" in p and "input" not in p):
+            groups.setdefault(p.get("model_path"), []).append(i)
+            continue
+        try:
+            out[i] = ("ok", run(p, op=op))
+        except Exception as exc:
+            out[i] = ("err", exc)
+
+    def settle(i: int, entry: Any) -> Any:
+        p = payloads[i] or {}
+        if entry[0] == "err" and p.get("allow_fallback", True) and not hard_failure(entry[1]):
+            return ("ok", _fallback(p, str(entry[1]), t0, op))
+        return entry
+
+    for idxs in groups.values():
+        descs = [dict(payloads[i], _op=op, _t0=t0) for i in idxs]
+        try:
+            res = dispatch("map_classify_batch", {"payloads": descs})
+        except Exception as exc:
+            res = [("err", exc)] * len(idxs)
+        for i, entry in zip(idxs, res):
+            out[i] = settle(i, entry)
+    return out
+
+
+@register_batch_op("map_classify_tpu")
+def map_classify_tpu_batch(payloads: List[Dict[str, Any]]) -> List[Any]:
+    return run_batch(payloads, "map_classify_tpu")
+
+
+@register_batch_op("map_classify")
+def map_classify_batch(payloads: List[Dict[str, Any]]) -> List[Any]:
+    return run_batch(payloads, "map_classify")
+
+
 def hard_failure(exc: BaseException) -> bool:
     """Failures the fallback stub must not hide: a HIP device fault (the agent
-    marks the device unhealthy from the raised error) and any DP job failure
-    (it names the ranks; a faulted rank has already left the DP group)."""
+    marks the device unhealthy from the raised error), any DP job failure
+    (it names the ranks; a faulted rank has already left the DP group) and a
+    lost rank (dead or hung process; the agent exits for a restart)."""
     from agent_tpu_amd.parallel.dp_ops import DPError, is_device_fault
+    from agent_tpu_amd.parallel.watchdog import RankLost
 
-    return isinstance(exc, DPError) or is_device_fault(str(exc))
+    return isinstance(exc, (DPError, RankLost)) or is_device_fault(str(exc))
 
 
 def run(payload: Dict[str, Any], ctx: Dict[str, Any] = None, op: str = OP_NAME) -> Dict[str, Any]:

@@ -29,7 +29,7 @@ import threading
 import time
 from typing import Any, Dict, List, Optional
 
-from . import register_op
+from . import register_batch_op, register_op
 
 
 
@@ -115,24 +115,10 @@ def _gen_config(payload: Dict[str, Any]):
 
 @register_op("map_summarize")
 def handle(payload: Optional[Dict[str, Any]]) -> Dict[str, Any]:
-    if not payload:
-        return {"ok": False, "error": "empty payload"}
-    texts: Optional[List[str]] = None
-    if "texts" in payload:
-        raw = payload.get("texts")
-        if not isinstance(raw, list) or not raw or not all(isinstance(t, str) and t.strip() for t in raw):
-            return {"ok": False, "error": "payload.texts must be a non-empty list of non-empty strings"}
-        texts = [t.strip() for t in raw]
-    else:
-        text = payload.get("text", "")
-        text = text.strip() if isinstance(text, str) else ""
-        if not text:
-            return {"ok": False, "error": "no text provided"}
-        texts = [text]
-    try:
-        gen = _gen_config(payload)
-    except (TypeError, ValueError) as exc:
-        return {"ok": False, "error": f"bad generation parameter: {exc}"}
+    v = _validate_one(payload)
+    if isinstance(v, dict):
+        return v
+    texts, _, gen = v
     t0 = time.time()
     if _dp_world() > 1:
         from agent_tpu_amd.parallel.dp_ops import dispatch
@@ -143,3 +129,74 @@ def handle(payload: Optional[Dict[str, Any]]) -> Dict[str, Any]:
     eng = _init_engine()
     summaries, res = eng.summarize(texts, gen)
     return result("texts" in payload, summaries, res.steps, res.timing_ms, t0)
+
+
+def _validate_one(payload: Any):
+    """-> (texts, texts_mode, gen) or an ``{"ok": False, ...}`` soft-error result (as :func:`handle`)."""
+    if not payload or not isinstance(payload, dict):
+        return {"ok": False, "error": "empty payload"}
+    if "texts" in payload:
+        raw = payload.get("texts")
+        if not isinstance(raw, list) or not raw or not all(isinstance(t, str) and t.strip() for t in raw):
+            return {"ok": False, "error": "payload.texts must be a non-empty list of non-empty strings"}
+        texts, mode = [t.strip() for t in raw], True
+    else:
+        text = payload.get("text", "")
+        text = text.strip() if isinstance(text, str) else ""
+        if not text:
+            return {"ok": False, "error": "no text provided"}
+        texts, mode = [text], False
+    try:
+        gen = _gen_config(payload)
+    except (TypeError, ValueError) as exc:
+        return {"ok": False, "error": f"bad generation parameter: {exc}"}
+    return texts, mode, gen
+
+
+@register_batch_op("map_summarize")
+def handle_batch(payloads: List[Dict[str, Any]]) -> List[Any]:
+    """Several leased ``map_summarize`` jobs as ONE beam-search batch.
+
+    The reference job stream is one document per task (ref ``ops/map_summarize.py:39-49``)
+    decoded at batch 1; here the documents of every job of a lease that share the
+    generation settings are decoded together (one encoder pass, one batched beam search)
+    and split back per job. Beam search is per document, so each job's summary equals
+    its single-job result. Invalid payloads get their own soft error."""
+    out: List[Any] = [None] * len(payloads)
+    groups: Dict[tuple, List[tuple]] = {}
+    for i, p in enumerate(payloads):
+        v = _validate_one(p)
+        if isinstance(v, dict):
+            out[i] = ("ok", v)
+            continue
+        texts, mode, gen = v
+        key = (gen.num_beams, gen.max_length, gen.min_length, gen.length_penalty, gen.no_repeat_ngram_size)
+        groups.setdefault(key, []).append((i, texts, mode, gen, p))
+    for members in groups.values():
+        t0 = time.time()
+        all_texts = [t for _, texts, _, _, _ in members for t in texts]
+        gen = members[0][3]
+        try:
+            if _dp_world() > 1:
+                from agent_tpu_amd.parallel.dp_ops import dispatch
+
+                desc = {k: members[0][4][k] for k in _GEN_KEYS if k in members[0][4]}
+                desc.update(texts=all_texts, texts_mode=True, t0=t0)
+                res = dispatch("map_summarize", desc)
+                summaries, steps, timing = res["summaries"], res["decode_steps"], res.get("timing_ms", {})
+                extra = {"dp_world_size": res.get("dp_world_size", _dp_world())}
+            else:
+                eng = _init_engine()
+                summaries, r = eng.summarize(all_texts, gen)
+                steps, timing, extra = r.steps, r.timing_ms, {}
+        except Exception as exc:
+            for i, *_ in members:
+                out[i] = ("err", exc)
+            continue
+        pos = 0
+        for i, texts, mode, _, _ in members:
+            mine = summaries[pos:pos + len(texts)]
+            pos += len(texts)
+            out[i] = ("ok", result(mode, mine, steps, timing, t0, batched_docs=len(all_texts),
+                                   batched_jobs=len(members), **extra))
+    return out

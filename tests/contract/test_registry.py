@@ -105,8 +105,8 @@ def test_device_fault_marks_the_faulting_ranks_device(monkeypatch):
 
     monkeypatch.setattr(health, "_unhealthy", {})
     monkeypatch.setattr(health, "_last", {"ok": True, "devices": [], "healthy": [0, 1, 2, 3], "unhealthy": {}})
-    monkeypatch.setattr(app, "worker_profile", lambda h: {"health": h})
-    me = types.SimpleNamespace(health=health.last(), profile=None)
+    monkeypatch.setattr(app, "worker_profile", lambda h, caps=None: {"health": h})
+    me = types.SimpleNamespace(health=health.last(), profile=None, caps=["map_classify"])
     app.Agent._note_device_fault(me, "rank 1: ValueError: bad; rank 2: RuntimeError: hipErrorLaunchFailure: boom")
     assert sorted(health._unhealthy) == [2] and health.last()["healthy"] == [0, 1, 3]
     assert me.profile == {"health": health.last()}

@@ -122,3 +122,56 @@ def test_dp_agent_classify_input_first_and_device_fault(ctl):
     assert tx2["status"] == "succeeded" and tx2["result"]["row_count"] == 2, tx2
     assert res["e"]["result"] == {"ok": True, "echo": {"k": 2}}
     assert p.returncode == 0, out[-3000:]
+
+
+def _run_lost_rank(ctl, fault, extra_env=None, wait_s=90):
+    """torchrun 2 ranks of app.py; rank 1 is SIGKILLed / hangs mid-job per ``fault``."""
+    model = "bert-tiny?labels=3&batch=4&seq=32"
+    ctl.lease({"id": "tx", "op": "map_classify", "job_epoch": 11,
+               "payload": {"texts": ["d e f", "g", "h i"], "model_path": model}})
+    env = dict(os.environ, CONTROLLER_URL=ctl.url, TASKS="echo,map_classify", IDLE_SLEEP_SEC="0.02",
+               ERROR_LOG_EVERY_SEC="0", ATPU_DP_BACKEND="gloo", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="",
+               GPU_DISABLED="1", OMP_NUM_THREADS="1", PYTHONUNBUFFERED="1", CLASSIFY_DEVICE="cpu",
+               MI355X_FAULT=fault, DP_COLLECTIVE_TIMEOUT="8", DP_HEARTBEAT_TIMEOUT="30")
+    env.update(extra_env or {})
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", "app.py"]
+    t0 = time.time()
+    p = subprocess.Popen(cmd, cwd=REPO, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    try:
+        got = ctl.wait(lambda c: "tx" in {r["job_id"] for r in c.results}, wait_s)
+        t_res = time.time() - t0
+        out, _ = p.communicate(timeout=90)
+    finally:
+        if p.poll() is None:
+            for r in psutil.Process(p.pid).children(recursive=True):
+                try:
+                    r.kill()
+                except psutil.NoSuchProcess:
+                    pass
+            p.kill()
+            p.communicate(timeout=30)
+    assert got, ctl.results
+    return {r["job_id"]: r for r in ctl.results}, p.returncode, out, t_res
+
+
+def test_dp_rank_killed_mid_job_fails_job_naming_rank(ctl):
+    """SIGKILL rank 1 inside a classify job -> rank 0 posts ``failed`` naming
+    rank 1 (not a hang until a backend timeout), then the agent exits non-zero for a restart."""
+    res, rc, out, t_res = _run_lost_rank(ctl, "rank:1:classify:1:kill")
+    tx = res["tx"]
+    assert tx["status"] == "failed" and tx["job_epoch"] == 11, tx
+    assert "rank 1: process died" in tx["error"]["message"], tx["error"]
+    assert t_res < 60
+    assert rc != 0, out[-2000:]
+
+
+def test_dp_rank_hung_mid_job_fails_job_naming_rank(ctl):
+    """A wedged rank (alive, heartbeat running, never reaches the next collective): rank 0's
+    watchdog names it after 0.8 x DP_COLLECTIVE_TIMEOUT and fails the in-flight job."""
+    res, rc, out, t_res = _run_lost_rank(ctl, "rank:1:classify:1:hang")
+    tx = res["tx"]
+    assert tx["status"] == "failed" and tx["error"]["type"] == "RankLost", tx
+    assert "rank 1: hung" in tx["error"]["message"], tx["error"]
+    assert t_res < 60
+    assert rc != 0, out[-2000:]
