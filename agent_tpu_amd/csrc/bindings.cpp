@@ -185,10 +185,15 @@ PYBIND11_MODULE(_atpu, m) {
   });
   m.def("attention_strided", [](uintptr_t q, int ldq, uintptr_t k, int ldk, uintptr_t v, int ldv, uintptr_t out,
                                 int ldo, uintptr_t lens, uintptr_t bias, int B, int Sq, int Skv, int H, int D,
-                                float scale, int causal, uintptr_t stream) {
+                                float scale, int causal, uintptr_t stream, uintptr_t bias_dist) {
     attention_fwd_strided(P<const bf16>(q), ldq, P<const bf16>(k), ldk, P<const bf16>(v), ldv, P<bf16>(out), ldo,
-                          P<const int32_t>(lens), P<const float>(bias), B, Sq, Skv, H, D, scale, causal, S(stream));
-  });
+                          P<const int32_t>(lens), P<const float>(bias), B, Sq, Skv, H, D, scale, causal, S(stream),
+                          P<const float>(bias_dist));
+  }, py::arg("q"), py::arg("ldq"), py::arg("k"), py::arg("ldk"), py::arg("v"), py::arg("ldv"), py::arg("out"),
+     py::arg("ldo"), py::arg("lens"), py::arg("bias"), py::arg("B"), py::arg("Sq"), py::arg("Skv"), py::arg("H"),
+     py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("stream"), py::arg("bias_dist") = 0);
+  m.def("attention_flash_mode", &attention_flash_mode, py::arg("set") = -1,
+        "long-sequence encoder attention: 1 = double-buffered flash kernel (default), 0 = per-chunk kernel");
   m.def("layernorm", [](uintptr_t x, uintptr_t res, uintptr_t g, uintptr_t b, uintptr_t out, int rows, int N,
                         float eps, uintptr_t stream) {
     layernorm_bf16(P<const bf16>(x), P<const bf16>(res), P<const float>(g), P<const float>(b), P<bf16>(out), rows, N,

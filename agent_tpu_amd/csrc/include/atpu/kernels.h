@@ -166,8 +166,12 @@ void reduce_stats_finalize(const double* partial, int blocks, double* out, hipSt
 
 namespace atpu {
 // General strided form (T5 cross/causal attention): q rows b*Sq+t, k/v rows
-// b*Skv+t; head h at column h*D of each row.
+// b*Skv+t; head h at column h*D of each row. ``bias`` is a dense fp32 [H, Sq, Skv]
+// additive bias; ``bias_dist`` (exclusive with it) a bias by key-query distance,
+// fp32 [H, Sq+Skv-1] with entry k - q + Sq - 1 (T5's relative position bias).
 void attention_fwd_strided(const bf16* q, int ldq, const bf16* k, int ldk, const bf16* v, int ldv, bf16* out,
                            int ldo, const int32_t* lens, const float* bias, int B, int Sq, int Skv, int H, int D,
-                           float scale, int causal, hipStream_t stream);
+                           float scale, int causal, hipStream_t stream, const float* bias_dist = nullptr);
+// 1 = long-sequence encoder attention on the double-buffered flash kernel (default), 0 = per-chunk kernel
+int attention_flash_mode(int set);
 }  // namespace atpu

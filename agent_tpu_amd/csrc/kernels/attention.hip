@@ -219,6 +219,192 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(HAS_BI
 
 
 // ============================================================================
+// Long-sequence encoder attention (SURVEY.md §2.6 K4/K8 at S = 512 / 1024: the
+// summarizer's encoder, the reference truncating at 1024 tokens, ref
+// ops/map_summarize.py:49). Same 8-wave x 16-query tile and MFMA / transposed-V
+// math as attention_fwd_kernel, restructured for many key chunks per query block:
+//  * K/V chunks double-buffered by LDS-DMA: chunk c+1 is in flight while chunk c
+//    is computed (counted vmcnt(4): every wave issues exactly 4 LDS-DMA pieces
+//    per chunk), instead of a full HBM round trip per chunk;
+//  * T5 relative-position bias by DISTANCE: bias[h,q,k] depends only on k - q,
+//    so the head's [Sq + Skv - 1] row is staged in LDS once (pre-scaled by
+//    log2 e) instead of streaming a dense [H, S, S] fp32 tensor from L2/HBM
+//    (4 B per score: at S = 1024 that was 12.9 GB per call);
+//  * softmax in the exp2 domain with scale*log2(e) folded into one multiply;
+//    the key-length mask is applied only in the last (partial) chunk;
+//  * XCD-aware block order: the query blocks of one (batch, head) run on one XCD,
+//    so its K/V chunks are fetched into that XCD's L2 once, not once per XCD.
+// ============================================================================
+constexpr int kFlashTab = 4096;  // Sq + Skv - 1 <= 4096 distance-bias entries (16 KiB)
+constexpr float kLog2e = 1.4426950408889634f;
+
+template <bool DIST>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void attention_flash_kernel(
+    const bf16* __restrict__ Q, int ldq, const bf16* __restrict__ Kp, int ldk, const bf16* __restrict__ V, int ldv,
+    bf16* __restrict__ O, int ldo, const int32_t* __restrict__ lens, const float* __restrict__ bias_dist, int Sq,
+    int Skv, int H, float scale_log2, int nq, int nblocks) {
+  constexpr int kTab = DIST ? kFlashTab * 4 : 16;
+  __shared__ __attribute__((aligned(16))) char lds[2 * (kLdsK + kLdsV) + kTab];
+  float* tab = reinterpret_cast<float*>(lds + 2 * (kLdsK + kLdsV));
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int t = xcd_remap(blockIdx.x, nblocks);
+  const int qblk = t % nq, bh = t / nq, h = bh % H, b = bh / H;
+  const int len = lens ? min(lens[b], Skv) : Skv;
+  const int fr = lane & 15, fg = lane >> 4;
+
+  const bf16* Qb = Q + (size_t)b * Sq * ldq + h * kD;
+  const bf16* Kb = Kp + (size_t)b * Skv * ldk + h * kD;
+  const bf16* Vb = V + (size_t)b * Skv * ldv + h * kD;
+
+  const int qw = qblk * kQB + wave * 16;
+  bf16x8 qf[2];
+  {
+    const int q = min(qw + fr, Sq - 1);
+#pragma unroll
+    for (int ds = 0; ds < 2; ++ds) qf[ds] = *reinterpret_cast<const bf16x8*>(Qb + (size_t)q * ldq + ds * 32 + fg * 8);
+  }
+  const int ntab = Sq + Skv - 1;
+  if constexpr (DIST) {
+    const float* row = bias_dist + (size_t)h * ntab;
+    for (int j = tid; j < ntab; j += kThreads) tab[j] = row[j] * kLog2e;
+  }
+
+  // 4 LDS-DMA pieces per wave per chunk: 2 for K, 2 for V
+  auto stage = [&](int kc, int buf) {
+    char* lk = lds + buf * (kLdsK + kLdsV);
+    char* lv = lk + kLdsK;
+    const int srow = lane >> 3, spos = lane & 7;
+#pragma unroll
+    for (int i = 0; i < 16 / kWaves; ++i) {
+      const int r = (i * kWaves + wave) * 8 + srow;
+      const int key = min(kc + r, Skv - 1);
+      glds16(Kb + (size_t)key * ldk + kswz(r, spos) * 8, lk + (i * kWaves + wave) * 8 * kKRowB);
+    }
+#pragma unroll
+    for (int i = 0; i < 16 / kWaves; ++i) {
+      const int r = (i * kWaves + wave) * 8 + srow;
+      const int key = min(kc + r, Skv - 1);
+      glds16(Vb + (size_t)key * ldv + vswz(r, spos) * 8, lv + (i * kWaves + wave) * 8 * kVRowB);
+    }
+  };
+
+  const int nch = (len + kKC - 1) / kKC;
+  if (nch > 0) stage(0, 0);
+  wait_vmcnt0();
+  __syncthreads();  // Q fragments, distance table and chunk 0 are in place
+
+  float m_run = -1e30f, l_run = 0.f;
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int q = qw + fr;
+  const int qc = min(q, Sq - 1);
+
+  for (int c = 0; c < nch; ++c) {
+    const int kc = c * kKC;
+    const int buf = c & 1;
+    if (c + 1 < nch) {
+      stage(kc + kKC, buf ^ 1);  // buffer buf^1 was released by the barrier closing chunk c-1
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      wait_vmcnt0();
+    }
+    __syncthreads();  // chunk c landed for every wave
+    const char* ldsK = lds + buf * (kLdsK + kLdsV);
+    const char* ldsV = ldsK + kLdsK;
+
+    f32x4 s[8];
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ds = 0; ds < 2; ++ds) {
+        const int r = kt * 16 + fr;
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ldsK + r * kKRowB + kswz(r, ds * 4 + fg) * 16);
+        s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ds], s[kt], 0, 0, 0);
+      }
+    }
+
+    const bool tail = kc + kKC > len;
+    float cmax = -1e30f;
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      const int key0 = kc + kt * 16 + fg * 4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float x = s[kt][r] * scale_log2;
+        if constexpr (DIST) x += tab[min(key0 + r - qc + Sq - 1, ntab - 1)];
+        if (tail) x = key0 + r >= len ? -1e30f : x;
+        s[kt][r] = x;
+        cmax = fmaxf(cmax, x);
+      }
+    }
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+    const float m_new = fmaxf(m_run, cmax);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+    float psum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float x = s[kt][r];
+        float p = __builtin_amdgcn_exp2f(x - m_new);
+        if (tail) p = x <= -1e29f ? 0.f : p;
+        s[kt][r] = p;
+        psum += p;
+      }
+    psum += __shfl_xor(psum, 16, 64);
+    psum += __shfl_xor(psum, 32, 64);
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      bf16x8 pf;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        pf[e] = f2bf(s[2 * ks][e]);
+        pf[4 + e] = f2bf(s[2 * ks + 1][e]);
+      }
+      const int tq = fr >> 2, tp = fr & 3;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int klo = ks * 32 + fg * 4 + tq, khi = klo + 16;
+        const int cc = dt * 2 + (tp >> 1);
+        const bf16x4 lo = lds_read_tr16(ldsV + klo * kVRowB + vswz(klo, cc) * 16 + (tp & 1) * 8);
+        const bf16x4 hi = lds_read_tr16(ldsV + khi * kVRowB + vswz(khi, cc) * 16 + (tp & 1) * 8);
+        bf16x8 vf;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          vf[e] = lo[e];
+          vf[4 + e] = hi[e];
+        }
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[dt], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // every wave is done with buffer buf before chunk c+2 is staged into it
+  }
+
+  if (q < Sq) {
+    const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+    bf16* orow = O + ((size_t)b * Sq + q) * ldo + h * kD;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      bf16x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = f2bf(o[dt][e] * inv);
+      *reinterpret_cast<bf16x4*>(orow + dt * 16 + fg * 4) = v;
+    }
+  }
+}
+
+
+// ============================================================================
 // Persistent packed-QKV attention (BERT encoder: no bias, not causal, S <= 128,
 // so one key chunk per (batch, head) item). The one-item-per-workgroup kernel
 // above waits a full HBM round trip for K/V/Q before every item and only
@@ -483,10 +669,24 @@ int attention_persist_mode(int set) {
   return v;
 }
 
+int attention_flash_mode(int set) {
+  // encoder attention with many key chunks: 1 = double-buffered flash kernel (default), 0 = attention_fwd_kernel
+  static int v = [] {
+    const char* f = std::getenv("ATPU_ATTN_FLASH");
+    return (f && f[0] == '0') ? 0 : 1;
+  }();
+  if (set >= 0) v = set;
+  return v;
+}
+
 void attention_fwd_strided(const bf16* q, int ldq, const bf16* k, int ldk, const bf16* v, int ldv, bf16* out,
                            int ldo, const int32_t* lens, const float* bias, int B, int Sq, int Skv, int H, int D,
-                           float scale, int causal, hipStream_t stream) {
+                           float scale, int causal, hipStream_t stream, const float* bias_dist) {
   ATPU_CHECK(D == kD, "attention: head dim must be 64");
+  ATPU_CHECK(!(bias && bias_dist), "attention: dense bias and distance bias are exclusive");
+  if (bias_dist) {
+    ATPU_CHECK(!causal && Sq + Skv - 1 <= kFlashTab, "attention: distance bias needs !causal and Sq + Skv <= 4097");
+  }
   ATPU_CHECK(B > 0 && Sq > 0 && Skv > 0 && H > 0, "attention: empty problem");
   ATPU_CHECK(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0, "attention: row strides must be 16-B");
   ATPU_CHECK(!bias || Skv % 4 == 0, "attention: bias path needs Skv % 4 == 0");
@@ -521,6 +721,21 @@ void attention_fwd_strided(const bf16* q, int ldq, const bf16* k, int ldk, const
     else
       hipLaunchKernelGGL(attention_packed_persist_kernel<0>, dim3(std::min(items, nb)), dim3(kThreads), 0, stream, q,
                          ldq, out, ldo, lens, Sq, H, items, scale);
+    ATPU_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  if (bias_dist || (!bias && !causal && Skv > kKC && attention_flash_mode(-1) == 1)) {
+    ATPU_CHECK(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0, "attention: 16-B rows required");
+    const int nq = (Sq + kQB - 1) / kQB;
+    const long long nb = (long long)nq * H * B;
+    ATPU_CHECK(nb < (1LL << 31), "attention: grid too large");
+    const float sl2 = scale * kLog2e;
+    if (bias_dist)
+      hipLaunchKernelGGL(attention_flash_kernel<true>, dim3((unsigned)nb), dim3(kThreads), 0, stream, q, ldq, k, ldk,
+                         v, ldv, out, ldo, lens, bias_dist, Sq, Skv, H, sl2, nq, (int)nb);
+    else
+      hipLaunchKernelGGL(attention_flash_kernel<false>, dim3((unsigned)nb), dim3(kThreads), 0, stream, q, ldq, k, ldk,
+                         v, ldv, out, ldo, lens, nullptr, Sq, Skv, H, sl2, nq, (int)nb);
     ATPU_HIP_CHECK(hipGetLastError());
     return;
   }

@@ -225,19 +225,22 @@ class T5Model:
     def prepare_decode(self, S: int, T: int) -> None:
         """Build the lazily cached tensors a search of source length S / length T reads, on
         the caller's stream (concurrent searches on other streams then only read them)."""
-        self.enc_bias(S)
+        self.enc_bias_dist(S)
         self.dec_bias(T)
         if self.rms_fold:
             self.rms_folded()
 
     # ------------------------------------------------------------- biases
-    def enc_bias(self, S: int) -> torch.Tensor:
-        if S not in self._enc_bias:
-            pos = torch.arange(S)
-            b = relative_bucket(pos.view(1, S) - pos.view(S, 1), True, self.cfg.buckets, self.cfg.max_distance)
+    def enc_bias_dist(self, S: int) -> torch.Tensor:
+        """Encoder relative-position bias by distance: [H, 2S-1], entry k - q + S - 1
+        (the attention kernel stages one head's row in LDS; no dense [H, S, S])."""
+        key = -S
+        if key not in self._enc_bias:
+            rel_pos = torch.arange(-(S - 1), S)
+            b = relative_bucket(rel_pos, True, self.cfg.buckets, self.cfg.max_distance)
             rel = self.p["enc.rel"].float().cpu()  # [buckets, H]
-            self._enc_bias[S] = rel[b].permute(2, 0, 1).contiguous().to(self.device)  # [H, S, S]
-        return self._enc_bias[S]
+            self._enc_bias[key] = rel[b].t().contiguous().to(self.device)  # [H, 2S-1]
+        return self._enc_bias[key]
 
     def dec_bias(self, T: int) -> torch.Tensor:
         if self._dec_bias is None or self._dec_bias.shape[1] < T:
@@ -253,7 +256,7 @@ class T5Model:
         cfg, p = self.cfg, self.p
         B, S = ids.shape
         d, H = cfg.d_model, cfg.heads
-        bias = self.enc_bias(S)
+        bias = self.enc_bias_dist(S)
         h = ops.embed_gather(ids, p["shared"])
         if h.dtype != p["enc.l0.qkv"].dtype:
             h = h.to(p["enc.l0.qkv"].dtype)
@@ -261,7 +264,8 @@ class T5Model:
             q = f"enc.l{i}."
             x = ops.rmsnorm(h, p[q + "ln1"], cfg.eps)
             qkv = ops.linear(x, p[q + "qkv"])
-            ctx = ops.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], lens, B, S, S, H, scale=1.0, bias=bias)
+            ctx = ops.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], lens, B, S, S, H, scale=1.0,
+                                bias_dist=bias)
             h = ops.linear(ctx, p[q + "o"], residual=h)
             x = ops.rmsnorm(h, p[q + "ln2"], cfg.eps)
             f = ops.linear(x, p[q + "wi"], act="relu")

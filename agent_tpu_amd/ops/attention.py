@@ -12,9 +12,15 @@ from typing import Optional
 import torch
 
 from .._native import native, ptr, launch_stream
-from ._util import check, check_bf16_dev, row_stride
+from ._util import check, check_bf16_dev, row_stride, same_device
 
 HEAD_DIM = 64
+
+
+def dist_to_dense(bias_dist: torch.Tensor, Sq: int, Skv: int) -> torch.Tensor:
+    """[H, Sq+Skv-1] bias by distance (entry k - q + Sq - 1) -> dense [H, Sq, Skv]."""
+    idx = torch.arange(Skv, device=bias_dist.device).view(1, Skv) - torch.arange(Sq, device=bias_dist.device).view(Sq, 1)
+    return bias_dist[:, idx + Sq - 1]
 
 
 def attention_ref(q, k, v, lens, B, Sq, Skv, H, scale, bias=None, causal=False):
@@ -38,9 +44,20 @@ def attention_ref(q, k, v, lens, B, Sq, Skv, H, scale, bias=None, causal=False):
 
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, lens: torch.Tensor, B: int, Sq: int, Skv: int,
               H: int, scale: Optional[float] = None, bias: Optional[torch.Tensor] = None, causal: bool = False,
-              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+              out: Optional[torch.Tensor] = None, bias_dist: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Masked multi-head attention (K4). ``bias``: dense fp32 [H, Sq, Skv]; ``bias_dist``:
+    fp32 [H, Sq+Skv-1] indexed by key - query + Sq - 1 (T5 relative positions), which the
+    kernel stages per head in LDS instead of streaming a dense S x S tensor."""
     scale = 1.0 / math.sqrt(HEAD_DIM) if scale is None else float(scale)
+    check(bias is None or bias_dist is None, "attention: bias and bias_dist are exclusive")
+    if bias_dist is not None:
+        check(not causal, "attention: bias_dist is for non-causal (encoder) attention")
+        check(bias_dist.dtype == torch.float32 and bias_dist.is_contiguous()
+              and tuple(bias_dist.shape) == (H, Sq + Skv - 1), "bias_dist must be fp32 [H, Sq+Skv-1]")
+        check(Sq + Skv - 1 <= 4096, "attention: bias_dist needs Sq + Skv - 1 <= 4096")
     if not q.is_cuda:
+        if bias_dist is not None:
+            bias = dist_to_dense(bias_dist.float(), Sq, Skv)
         o = attention_ref(q, k, v, lens, B, Sq, Skv, H, scale, bias, causal)
         if out is not None:
             out.copy_(o)
@@ -54,11 +71,13 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, lens: torch.Ten
     if bias is not None:
         check(bias.dtype == torch.float32 and bias.is_contiguous() and tuple(bias.shape) == (H, Sq, Skv),
               "bias must be fp32 [H, Sq, Skv]")
+    if bias_dist is not None:
+        same_device(q, bias_dist)
     if out is None:
         out = torch.empty((B * Sq, H * HEAD_DIM), dtype=torch.bfloat16, device=q.device)
     native().attention_strided(ptr(q), row_stride(q, "q"), ptr(k), row_stride(k, "k"), ptr(v), row_stride(v, "v"),
                                ptr(out), row_stride(out, "out"), ptr(lens), ptr(bias), B, Sq, Skv, H, HEAD_DIM,
-                               scale, int(causal), launch_stream(q))
+                               scale, int(causal), launch_stream(q), ptr(bias_dist))
     return out
 
 

@@ -30,7 +30,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="t5-base")
     ap.add_argument("--docs", type=int, default=256, help="documents per step (batch)")
-    ap.add_argument("--src-len", type=int, default=512)
+    ap.add_argument("--src-len", type=int, default=1024)  # ref truncation (ops/map_summarize.py:49)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--num-beams", type=int, default=4)

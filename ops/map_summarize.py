@@ -48,7 +48,7 @@ def _resolve_model() -> str:
 
 MODEL_NAME = _resolve_model()
 FORCE_CPU = os.getenv("SUMMARIZE_FORCE_CPU", "0").strip().lower() in ("1", "true", "yes")
-MAX_SOURCE_TOKENS = int(os.getenv("SUMMARIZE_MAX_SOURCE_TOKENS", "512"))
+MAX_SOURCE_TOKENS = int(os.getenv("SUMMARIZE_MAX_SOURCE_TOKENS", "1024"))  # ref ops/map_summarize.py:49
 
 _lock = threading.Lock()
 _engine = None

@@ -9,7 +9,7 @@
 #   bash tools/gpu.sh "pmc:ffn:SQ_WAVES SQ_BUSY_CYCLES:tools/bench_kernels.py --only gemm_ffn1"
 #
 # Stage forms:
-#   tests[:<pytest args>]  GPU tests (default: the whole -m gpu suite)
+#   tests[:<pytest args>]  GPU tests (default: the whole -m gpu suite); args are eval'd, so quote a -k expression
 #   smoke                  __graft_entry__.smoke()
 #   bench[:<args>]         bench.py (default --steps 20 --warmup 5)
 #   run:<name>:<cmd>       any command; its log is gpurun_out/<OUT>/<name>.log
@@ -39,8 +39,8 @@ for spec in "$@"; do
   echo "[gpu.sh] $(date +%T) stage $spec"
   case $kind in
     tests)
-      env $STAGE_ENV timeout -k 10 $T python -u -m pytest -x -v --timeout 120 --timeout-method thread \
-        ${rest:--m gpu tests} > "$O/tests.log" 2>&1
+      eval "env $STAGE_ENV timeout -k 10 $T python -u -m pytest -x -v --timeout 120 --timeout-method thread \
+        ${rest:--m gpu tests}" > "$O/tests.log" 2>&1
       rc=$?; grep -E "passed|failed|error" "$O/tests.log" | tail -3 ;;
     smoke)
       env $STAGE_ENV timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1
