@@ -113,6 +113,11 @@ PYBIND11_MODULE(_atpu, m) {
   m.def("gemm_force_tile", &gemm_force_tile, py::arg("set") = -1, "GEMM kernel family override: 0 auto, 64, 128, 256");
   m.def("gemm_dec_mode", &gemm_dec_mode, py::arg("set") = -1,
         "skinny-M GEMM path: 1 = 64x64 multi-stage dec kernel, 0 = 128x128 split-K; returns the current");
+#ifdef ATPU_DEV_BUILD
+  m.attr("DEV_BUILD") = true;
+#else
+  m.attr("DEV_BUILD") = false;
+#endif
   m.def("gemm_256_variant", &gemm_256_variant, py::arg("set") = -1,
         "256x256 GEMM schedule: 0 = 256b, 1 = 256p ping-pong, 2 = 256s persistent, 3 = 256l full-line "
         "epilogue, 4 = 256n full-line + nt stores (default); set >= 0 switches, returns the current");

@@ -6,7 +6,7 @@ Every ``kernels/*.hip`` and ``runtime/*.cpp`` translation unit plus
 rebuilt when its source or any header is newer). No hipify, no torch headers:
 kernels take raw device pointers and a hipStream_t from torch.
 
-Usage: ``python -m agent_tpu_amd.csrc.build [--force] [--debug] [--asan-host]``
+Usage: ``python -m agent_tpu_amd.csrc.build [--force] [--debug] [--asan-host] [--dev]``
 """
 from __future__ import annotations
 
@@ -68,11 +68,21 @@ def _compile(src: Path, flags: List[str], force: bool) -> Path:
     return obj
 
 
-def build(force: bool = False, debug: bool = False, asan_host: bool = False, jobs: int = 0, verbose: bool = False) -> Path:
+def build(force: bool = False, debug: bool = False, asan_host: bool = False, jobs: int = 0, verbose: bool = False,
+          dev: bool = False) -> Path:
+    """``dev`` (or ATPU_DEV_BUILD=1) compiles in the timing-only GEMM ablations and the
+    retired 256b / 256s schedules (tools/gemm_ablate.py, tools/bench_gelu.py,
+    tools/bench_fold.py); a release build has none of them. The objects of the two
+    flavours live in separate directories."""
+    dev = dev or os.environ.get("ATPU_DEV_BUILD", "0") == "1"
+    global BUILD
+    BUILD = REPO / "build" / ("obj_dev" if dev else "obj")
     BUILD.mkdir(parents=True, exist_ok=True)
     flags = [f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result",
              "-Wno-unused-function", "-fvisibility=hidden"]
     flags += ["-O0", "-g"] if debug else ["-O3", "-DNDEBUG"]
+    if dev:
+        flags += ["-DATPU_DEV_BUILD"]
     if asan_host:
         # host-only sanitizer: GPU ASan/xnack+ is not available on this pool
         flags += ["-Xarch_host", "-fsanitize=address", "-fno-omit-frame-pointer"]
@@ -83,7 +93,10 @@ def build(force: bool = False, debug: bool = False, asan_host: bool = False, job
         objs = list(ex.map(lambda s: _compile(s, flags, force), srcs))
     out = ext_path()
     newest = max(o.stat().st_mtime for o in objs)
-    if force or not out.exists() or out.stat().st_mtime < newest:
+    stamp = REPO / "build" / "linked_flavour"
+    flavour = ("dev" if dev else "release") + ("-debug" if debug else "") + ("-asan" if asan_host else "")
+    same = stamp.exists() and stamp.read_text() == flavour
+    if force or not same or not out.exists() or out.stat().st_mtime < newest:
         link = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", str(out) + ".tmp", "-lpthread"]
         if asan_host:
             link += ["-fsanitize=address"]
@@ -91,6 +104,7 @@ def build(force: bool = False, debug: bool = False, asan_host: bool = False, job
         if res.returncode != 0:
             raise RuntimeError(f"link failed:\n{res.stdout}\n{res.stderr}")
         os.replace(str(out) + ".tmp", out)
+        stamp.write_text(flavour)
     if verbose:
         print(f"[atpu-build] {out} ({len(objs)} objects, arch {ARCH})", flush=True)
     return out
@@ -101,9 +115,10 @@ def main(argv=None) -> int:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--asan-host", action="store_true")
+    ap.add_argument("--dev", action="store_true", help="compile in timing-only ablations / retired schedules")
     ap.add_argument("-j", "--jobs", type=int, default=0)
     a = ap.parse_args(argv)
-    build(force=a.force, debug=a.debug, asan_host=a.asan_host, jobs=a.jobs, verbose=True)
+    build(force=a.force, debug=a.debug, asan_host=a.asan_host, jobs=a.jobs, verbose=True, dev=a.dev)
     return 0
 
 

@@ -339,7 +339,8 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
 }
 
 // ============================================================================
-// 256x256 tile, 8 waves, FULL-LINE staging (kernel "256b").
+// 256x256 tile, 8 waves, FULL-LINE staging (kernel "256b"; retired: dev builds only,
+// python -m agent_tpu_amd.csrc.build --dev). Its staging constants (g2) are shared.
 //
 // The ablation of the ring kernel showed the LDS-DMA instructions themselves
 // costing ~40 % of the MFMA rate; its k-half chunks had 64-byte rows, so every
@@ -360,6 +361,8 @@ constexpr int kChunk = 16384;    // 128 rows x 128 B
 constexpr int kTile = 4 * kChunk;
 __device__ __forceinline__ int sw(int r, int c) { return c ^ ((r >> 1) & 7); }
 }  // namespace g2
+
+#ifdef ATPU_DEV_BUILD
 
 // DBG: timing-only ablation builds (results are WRONG): 1 = no vmcnt/barrier
 // waits, 2 = no global->LDS DMA. See docs/PERF_NOTES.md.
@@ -517,6 +520,7 @@ __global__ __launch_bounds__(512, 2) void gemm256b_kernel(
   }
 }
 
+#endif  // ATPU_DEV_BUILD (256b)
 
 // ============================================================================
 // 256x256 tile, 8 waves, PING-PONG schedule (kernel "256p").
@@ -802,15 +806,13 @@ __global__ __launch_bounds__(512, 1) void gemm256p_kernel(
 
 void launch_256p(const GemmArgs& g, hipStream_t s) {
   const int nb = ((g.M + 255) / 256) * (g.N / 256);
-  static const int ablate = [] {
-    const char* f = std::getenv("ATPU_GEMM_ABLATE");
-    return f ? std::atoi(f) : 0;
-  }();
-  if (ablate == 4) {  // no epilogue (timing only)
+#ifdef ATPU_DEV_BUILD
+  if (gemm_ablate(-1) == 4) {  // no epilogue (timing only, results wrong)
     hipLaunchKernelGGL((gemm256p_kernel<kEpiBias, 1>), dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C,
                        g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K);
     return;
   }
+#endif
 #define ATPU_G256P(E)                                                                                     \
   case E:                                                                                                 \
     hipLaunchKernelGGL((gemm256p_kernel<E>), dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, \
@@ -1507,13 +1509,20 @@ int64_t make_cu_mask_stream(int first_bit, int nbits) {
 }
 
 int gemm_ablate(int set) {
-  // timing-only ablations of the persistent kernel (results WRONG): ATPU_GEMM_ABLATE=4|5|6|7
+#ifdef ATPU_DEV_BUILD
+  // timing-only ablations of the persistent kernel (results WRONG): ATPU_GEMM_ABLATE=4|5|6|7,
+  // and A/B schedules 8-11. Compiled into dev builds only.
   static int v = [] {
     const char* f = std::getenv("ATPU_GEMM_ABLATE");
     return f ? std::atoi(f) : 0;
   }();
   if (set >= 0) v = set;
   return v;
+#else
+  // release build: no ablation exists; ATPU_GEMM_ABLATE and set() are ignored
+  (void)set;
+  return 0;
+#endif
 }
 
 namespace {
@@ -1524,8 +1533,9 @@ void launch_256s(const GemmArgs& g, hipStream_t s) {
   // one workgroup per CU; a multiple of 8 so v % 8 keeps naming the XCD
   int nb = std::min(tiles, num_cus());
   if (nb >= 8) nb &= ~7;
-  const int ablate = gemm_ablate(-1);
   const LnFold lf{g.in_fin, g.colsum, g.res_fin, g.gamma, g.part_out};
+#ifdef ATPU_DEV_BUILD
+  const int ablate = gemm_ablate(-1);
   if (ablate == 4 || ablate == 5 || ablate == 6) {  // timing only: no epilogue / no stores / no VALU
     auto k = ablate == 4 ? gemm256s_kernel<kEpiBias, 1> : ablate == 5 ? gemm256s_kernel<kEpiBias, 2>
                                                                        : gemm256s_kernel<kEpiBias, 4>;
@@ -1533,12 +1543,14 @@ void launch_256s(const GemmArgs& g, hipStream_t s) {
                        g.N, g.K, lf);
     return;
   }
+#endif
 #define ATPU_G256S(E)                                                                                          \
   case E:                                                                                                      \
     hipLaunchKernelGGL((gemm256s_kernel<E, 0, NT, LINE>), dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, \
                        g.bias, g.R, g.ldr, g.M, g.N, g.K, lf);                                                 \
     break;
   if constexpr (LINE) {
+#ifdef ATPU_DEV_BUILD
     if (ablate == 8 && (g.epi & kEpiInNorm)) {  // A/B: InNorm with the accumulators started at -mu*colsum
       if (g.epi & kEpiGelu)
         hipLaunchKernelGGL((gemm256s_kernel<kEpiBias | kEpiInNorm | kEpiGelu, 16, NT, LINE>), dim3(nb), dim3(512), 0, s,
@@ -1573,6 +1585,7 @@ void launch_256s(const GemmArgs& g, hipStream_t s) {
       }
 #undef ATPU_G256S_A
     }
+#endif  // ATPU_DEV_BUILD
     switch (g.epi) {
       ATPU_G256S(kEpiBias | kEpiInNorm)
       ATPU_G256S(kEpiBias | kEpiInNorm | kEpiGelu)
@@ -1598,6 +1611,7 @@ void launch_256s(const GemmArgs& g, hipStream_t s) {
 #undef ATPU_G256S
 }
 
+#ifdef ATPU_DEV_BUILD
 void launch_256b(const GemmArgs& g, hipStream_t s) {
   const int nb = ((g.M + 255) / 256) * (g.N / 256);
   static const int ablate = [] {
@@ -1635,6 +1649,7 @@ void launch_256b(const GemmArgs& g, hipStream_t s) {
   }
 #undef ATPU_G256B
 }
+#endif  // ATPU_DEV_BUILD
 
 
 
@@ -2030,18 +2045,26 @@ int gemm_256_variant(int set) {
   //   2 "256s" persistent ping-pong, permlane epilogue
   //   3 "256l" persistent, full-line LDS-transposed epilogue
   //   4 "256n" = 256l with non-temporal stores (default; docs/PERF_NOTES.md)
+  //   0 and 2 are retired schedules, compiled into dev builds only
   static int v = [] {
     const char* f = std::getenv("ATPU_GEMM_256");
     if (!f) return 4;
     switch (f[0]) {
+#ifdef ATPU_DEV_BUILD
       case 'b': return 0;
-      case 'p': return 1;
       case 's': return 2;
+#endif
+      case 'p': return 1;
       case 'l': return 3;
       default: return 4;
     }
   }();
-  if (set >= 0) v = set;
+  if (set >= 0) {
+#ifndef ATPU_DEV_BUILD
+    ATPU_CHECK(set == 1 || set == 3 || set == 4, "gemm_256_variant: schedules 0 (256b) and 2 (256s) need a dev build");
+#endif
+    v = set;
+  }
   return v;
 }
 
@@ -2195,13 +2218,18 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
   // 256s counts its epilogue's stores in the next tile's waits: whole row tiles only
   const bool persistent_ok = g.M % 256 == 0;
   if (use_big && persistent_ok && kernel256 >= 2) {
+#ifdef ATPU_DEV_BUILD
     if (kernel256 == 2) launch_256s<false, false>(g, stream);
-    else if (kernel256 == 3) launch_256s<false, true>(g, stream);
+    else
+#endif
+    if (kernel256 == 3) launch_256s<false, true>(g, stream);
     else launch_256s<true, true>(g, stream);
-  } else if (use_big && kernel256 >= 1)
-    launch_256p(g, stream);
+  } else if (use_big && kernel256 != 0)
+    launch_256p(g, stream);  // M % 256 != 0 (or the per-tile schedule forced)
+#ifdef ATPU_DEV_BUILD
   else if (use_big)
     launch_256b(g, stream);
+#endif
   else if ((forced == 64 || (!forced && gemm_dec_mode(-1) == 1 && skinny(g.M, g.N))))
     launch_dec(g, stream);
   else

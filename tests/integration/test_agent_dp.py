@@ -151,7 +151,7 @@ def _run_lost_rank(ctl, fault, extra_env=None, wait_s=90):
                     pass
             p.kill()
             p.communicate(timeout=30)
-    assert got, ctl.results
+    assert got, (ctl.results, out[-3000:] if p.poll() is not None else "")
     return {r["job_id"]: r for r in ctl.results}, p.returncode, out, t_res
 
 
@@ -160,9 +160,9 @@ def test_dp_rank_killed_mid_job_fails_job_naming_rank(ctl):
     rank 1 (not a hang until a backend timeout), then the agent exits non-zero for a restart."""
     res, rc, out, t_res = _run_lost_rank(ctl, "rank:1:classify:1:kill")
     tx = res["tx"]
-    assert tx["status"] == "failed" and tx["job_epoch"] == 11, tx
-    assert "rank 1: process died" in tx["error"]["message"], tx["error"]
-    assert t_res < 60
+    assert tx["status"] == "failed" and tx["job_epoch"] == 11, (tx, out[-3000:])
+    assert "rank 1: process died" in tx["error"]["message"], (tx["error"], out[-3000:])
+    assert t_res < 120, out[-3000:]
     assert rc != 0, out[-2000:]
 
 
@@ -172,6 +172,6 @@ def test_dp_rank_hung_mid_job_fails_job_naming_rank(ctl):
     res, rc, out, t_res = _run_lost_rank(ctl, "rank:1:classify:1:hang")
     tx = res["tx"]
     assert tx["status"] == "failed" and tx["error"]["type"] == "RankLost", tx
-    assert "rank 1: hung" in tx["error"]["message"], tx["error"]
-    assert t_res < 60
+    assert "rank 1: hung" in tx["error"]["message"], (tx["error"], out[-3000:])
+    assert t_res < 120, out[-3000:]
     assert rc != 0, out[-2000:]

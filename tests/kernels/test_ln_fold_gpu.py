@@ -46,6 +46,8 @@ def test_input_norm_epilogue(gpu, M, K, N, act):
     # the alternative schedule (accumulators started at -mu*colsum, gemm_ablate(8)) agrees to rounding
     from agent_tpu_amd._native import native
     nat = native()
+    if not nat.DEV_BUILD:  # A/B schedules exist in dev builds only
+        return
     prev = nat.gemm_ablate(-1)
     try:
         nat.gemm_ablate(8)

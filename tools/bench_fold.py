@@ -31,6 +31,7 @@ def main():
     from agent_tpu_amd._native import native
 
     nat = native()
+    assert nat.DEV_BUILD, "needs the dev extension: python -m agent_tpu_amd.csrc.build --dev (ablation schedules)"
     dev = torch.device("cuda", 0)
     M, H, I = a.rows * 128, 768, 3072
     g = torch.Generator(device=dev).manual_seed(0)

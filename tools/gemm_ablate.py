@@ -12,6 +12,10 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from agent_tpu_amd import ops  # noqa: E402
+from agent_tpu_amd._native import native  # noqa: E402
+
+if os.getenv("ATPU_GEMM_ABLATE", "0") != "0":
+    assert native().DEV_BUILD, "ATPU_GEMM_ABLATE needs the dev extension: python -m agent_tpu_amd.csrc.build --dev"
 
 
 def t(fn, iters=30):
