@@ -276,6 +276,24 @@ PYBIND11_MODULE(_atpu, m) {
       "document offsets [B+1]",
       py::arg("text"), py::arg("offsets"), py::arg("vocab"), py::arg("cap"));
 
+  m.def("topk_json",
+        [](int64_t start_row, py::array_t<int32_t, py::array::c_style | py::array::forcecast> idx,
+           py::array_t<float, py::array::c_style | py::array::forcecast> score, int mode) {
+          if (idx.ndim() != 2 || score.ndim() != 2 || idx.shape(0) != score.shape(0) || idx.shape(1) != score.shape(1))
+            throw std::invalid_argument("topk_json: idx and score must be [n, k]");
+          std::string s;
+          const int32_t* ip = idx.data();
+          const float* sp = score.data();
+          const int64_t n = idx.shape(0);
+          const int k = static_cast<int>(idx.shape(1));
+          {
+            py::gil_scoped_release nogil;
+            s = topk_json(start_row, ip, sp, n, k, mode);
+          }
+          return py::bytes(s);
+        },
+        "top-k [n,k] -> JSON bytes (0 rows, 1 index columns, 2 score columns)", py::arg("start_row"),
+        py::arg("idx"), py::arg("score"), py::arg("mode") = 0);
   m.def("device_query", [](int mem_of) {
     if (mem_of < 0) {
       int cur = 0;
@@ -379,6 +397,12 @@ PYBIND11_MODULE(_atpu, m) {
              return s.wait(slot);
            })
       .def("release", [](HostStager& s, int slot, uintptr_t stream) { s.release(slot, S(stream)); })
+      .def("take_h2d_ms",
+           [](HostStager& s) {
+             py::gil_scoped_release nogil;
+             return s.take_h2d_ms();
+           },
+           "(device ms of the H2D copies since the last call, number of uploads)")
       .def_property_readonly("slots", &HostStager::slots)
       .def_property_readonly("text_capacity", &HostStager::text_capacity);
 }

@@ -38,6 +38,11 @@ struct DeviceInfo {
 // current device), so a DP rank never creates contexts on its peers' GPUs.
 std::vector<DeviceInfo> device_query(int mem_of = -1);
 
+// Classify top-k [n, k] -> JSON text. mode 0: reference-style rows
+// [{"row":start+r,"topk":[{"index":i,"score":s},...]},...]; 1: [[index,...],...];
+// 2: [[score,...],...]. Floats in the shortest round-trip form.
+std::string topk_json(int64_t start_row, const int32_t* idx, const float* score, int64_t n, int k, int mode);
+
 // Double-buffered CSV column -> pinned host -> device pipeline.
 //  submit(slot, ...)  : background thread extracts rows into slot's pinned
 //                       buffer (after the slot's previous H2D has finished).
@@ -59,6 +64,10 @@ class HostStager {
   std::pair<int64_t, int64_t> upload(int slot, void* dev_text, size_t dev_text_cap, void* dev_offsets,
                                      hipStream_t copy_stream, hipStream_t compute_stream);
   void release(int slot, hipStream_t compute_stream);
+  // Device time of the H2D copies (hipEvent pairs around each upload's memcpys, after its
+  // wait for the slot's previous consumer), summed since the last call. Synchronizes on
+  // the outstanding pairs. {milliseconds, copies}.
+  std::pair<double, int64_t> take_h2d_ms();
   int slots() const { return static_cast<int>(slots_.size()); }
   size_t text_capacity() const { return text_cap_; }
   // host view of a slot's staged data (valid after upload/wait)
@@ -72,6 +81,8 @@ class HostStager {
     int32_t* offsets = nullptr;
     hipEvent_t copied = nullptr;    // H2D done -> pinned buffer reusable
     hipEvent_t consumed = nullptr;  // compute done with device buffers
+    hipEvent_t t0 = nullptr, t1 = nullptr;  // timing pair around the last upload's copies
+    bool has_t = false;
     bool has_copy = false;
     bool has_consume = false;
     int64_t rows = 0, bytes = 0;
@@ -80,7 +91,10 @@ class HostStager {
   };
   void worker();
 
+  void settle_timing(Slot& s);
   std::vector<Slot> slots_;
+  double h2d_ms_ = 0.0;
+  int64_t h2d_n_ = 0;
   size_t text_cap_;
   int max_rows_;
   std::mutex mu_;

@@ -139,6 +139,8 @@ HostStager::HostStager(int slots, size_t text_capacity, int max_rows)
                                  hipHostMallocDefault));
     ATPU_HIP_CHECK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
     ATPU_HIP_CHECK(hipEventCreateWithFlags(&s.consumed, hipEventDisableTiming));
+    ATPU_HIP_CHECK(hipEventCreate(&s.t0));
+    ATPU_HIP_CHECK(hipEventCreate(&s.t1));
   }
   thread_ = std::thread([this] { worker(); });
 }
@@ -153,6 +155,9 @@ HostStager::~HostStager() {
   for (auto& s : slots_) {
     if (s.copied) (void)hipEventSynchronize(s.copied), (void)hipEventDestroy(s.copied);
     if (s.consumed) (void)hipEventDestroy(s.consumed);
+    if (s.t1) (void)hipEventSynchronize(s.t1);
+    if (s.t0) (void)hipEventDestroy(s.t0);
+    if (s.t1) (void)hipEventDestroy(s.t1);
     if (s.text) (void)hipHostFree(s.text);
     if (s.offsets) (void)hipHostFree(s.offsets);
   }
@@ -220,13 +225,35 @@ std::pair<int64_t, int64_t> HostStager::upload(int slot, void* dev_text, size_t 
   Slot& s = slots_[slot];
   ATPU_CHECK(static_cast<size_t>(bytes) <= dev_text_cap, "stager: device text buffer too small");
   if (s.has_consume) ATPU_HIP_CHECK(hipStreamWaitEvent(copy_stream, s.consumed, 0));
+  settle_timing(s);  // the previous pair of this slot completed before its pinned buffer was refilled
+  ATPU_HIP_CHECK(hipEventRecord(s.t0, copy_stream));  // after the wait: times the copies only
   if (bytes > 0) ATPU_HIP_CHECK(hipMemcpyAsync(dev_text, s.text, bytes, hipMemcpyHostToDevice, copy_stream));
   ATPU_HIP_CHECK(
       hipMemcpyAsync(dev_offsets, s.offsets, sizeof(int32_t) * (rows + 1), hipMemcpyHostToDevice, copy_stream));
+  ATPU_HIP_CHECK(hipEventRecord(s.t1, copy_stream));
+  s.has_t = true;
   ATPU_HIP_CHECK(hipEventRecord(s.copied, copy_stream));
   s.has_copy = true;
   if (compute_stream != copy_stream) ATPU_HIP_CHECK(hipStreamWaitEvent(compute_stream, s.copied, 0));
   return {rows, bytes};
+}
+
+void HostStager::settle_timing(Slot& s) {
+  if (!s.has_t) return;
+  ATPU_HIP_CHECK(hipEventSynchronize(s.t1));
+  float ms = 0.f;
+  ATPU_HIP_CHECK(hipEventElapsedTime(&ms, s.t0, s.t1));
+  h2d_ms_ += ms;
+  h2d_n_ += 1;
+  s.has_t = false;
+}
+
+std::pair<double, int64_t> HostStager::take_h2d_ms() {
+  for (auto& s : slots_) settle_timing(s);
+  std::pair<double, int64_t> out{h2d_ms_, h2d_n_};
+  h2d_ms_ = 0.0;
+  h2d_n_ = 0;
+  return out;
 }
 
 void HostStager::release(int slot, hipStream_t compute_stream) {

@@ -314,10 +314,18 @@ class BertClassifier:
         cls_rows = h if h.shape[0] == B else h.view(B, S, self.cfg.hidden)[:, 0, :]  # strided: row stride S*H
         return ops.linear(cls_rows, self.p["pool_w"], self.p["pool_b"], act="tanh")
 
+    def encoder(self, ids: torch.Tensor, lens: torch.Tensor,
+                type_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """The encoder stage of :meth:`forward` ([CLS] states when the last layer is pruned)."""
+        return self.encode(ids, lens, type_ids, cls_only_last=self.cls_only_last and ids.shape[1] > 1)
+
+    def head(self, h: torch.Tensor, B: int, S: int, k: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """Pooler + classifier + softmax/top-k (K7) over encoder states ``h``."""
+        pooled = self.pooled(h, B, S)
+        return ops.classify_head_topk(pooled, self.p["cls_w"], self.p["cls_b"], k)
+
     def forward(self, ids: torch.Tensor, lens: torch.Tensor, k: int = 5,
                 type_ids: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
         """Returns ``(logits[B,C] fp32, topk_idx[B,k] int32, topk_prob[B,k] fp32)``."""
         B, S = ids.shape
-        h = self.encode(ids, lens, type_ids, cls_only_last=self.cls_only_last and S > 1)
-        pooled = self.pooled(h, B, S)
-        return ops.classify_head_topk(pooled, self.p["cls_w"], self.p["cls_b"], k)
+        return self.head(self.encoder(ids, lens, type_ids), B, S, k)

@@ -27,7 +27,7 @@ from typing import Any, Callable, Dict, Optional, Tuple
 import torch
 import torch.distributed as dist
 
-from ..utils.trace import span
+from ..utils.trace import DeviceStages, span
 from . import dp, watchdog
 from .dp import all_gather_rows, broadcast_task, comm_device, is_dist, members, split_range, world
 
@@ -329,22 +329,34 @@ def classify_csv_task(payload: Dict[str, Any]) -> Any:
         s_r, n_r = split_range(start, total, ws, rank)
         maybe_inject_fault("classify")
         with span("classify_ms", timing):
-            idx, sc, st = h.engine.classify_table(table.native, s_r, n_r, col)
-        timing.update({f"{k}_ms": round(v, 3) for k, v in st.timing_ms.items()})
+            idx, sc, st = h.engine.classify_table(table.native, s_r, n_r, col,
+                                                  stage_timing=payload.get("timing", "device") != "host")
+        timing.update({k: (round(v, 3) if isinstance(v, float) else v) for k, v in st.timing_ms.items()})
         meta = {"start_row": start, "end_row": start + total, "world": ws}
     except Exception as exc:
         err = f"{type(exc).__name__}: {exc}"
         if os.getenv("ATPU_DEBUG"):
             traceback.print_exc()
     _check_errors(err)
-    with span("allgather_ms", timing):
+    dev_t = idx is not None and idx.is_cuda
+    ev = DeviceStages.event if dev_t else (lambda *a: None)
+    g0 = ev()
+    with span("host_allgather_ms", timing):
         idx, sc = all_gather_rows(idx, sc)
+    g1 = ev()
     if rank != 0:
         return None
+    with span("host_d2h_ms", timing):
+        idx_h, sc_h = idx.cpu(), sc.cpu()
+    g2 = ev()
+    if dev_t:
+        g2.synchronize()
+        timing["device_allgather_ms"] = round(g0.elapsed_time(g1), 3)
+        timing["device_d2h_ms"] = round(g1.elapsed_time(g2), 3)
     meta["timing_ms"] = timing
     from ops.map_classify import csv_result
 
-    return csv_result(h, idx.cpu(), sc.cpu(), meta, payload)
+    return csv_result(h, idx_h, sc_h, meta, payload)
 
 
 @dp_task("map_classify_rows")

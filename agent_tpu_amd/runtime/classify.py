@@ -31,7 +31,7 @@ from .._native import native
 from ..models.bert import BertClassifier, BertConfig
 from ..models.params import ParamPack
 from ..tokenizer import DEFAULT_MAX_ROW_BYTES, pack_rows
-from ..utils.trace import span
+from ..utils.trace import DeviceStages, span
 
 
 @dataclass
@@ -96,7 +96,12 @@ class ClassifyEngine:
             self.compute_streams = [torch.cuda.ExternalStream(nat.make_cu_mask_stream(i * share, share), device=device)
                                     for i in range(slots)]
             nat.cu_budget(share)
+        if device.type == "cuda" and self.model.can_fold(self.B, self.S):
+            self.model.folded()  # build the LN-folded weights now, so memory_bytes() counts them
         self._graphs: Dict[int, Tuple["torch.cuda.CUDAGraph", Tuple[torch.Tensor, ...]]] = {}
+        # stage-timed replay: the same step as three graphs (tokenize | encoder | head) with
+        # hipEvents between them, so timing_ms carries device time per stage
+        self._staged: Dict[int, Tuple[Tuple["torch.cuda.CUDAGraph", ...], Tuple[torch.Tensor, ...]]] = {}
         self._stager = None
 
     # ------------------------------------------------------------ device step
@@ -121,10 +126,63 @@ class ClassifyEngine:
         g.replay()
         return outs
 
-    def run_slot(self, slot: int, rows: int):
+    def _stage_fns(self, slot: int, rows: int):
+        ids, lens = self.ids_s[slot], self.lens_s[slot]
+        box = {}
+
+        def tok():
+            ops.tokenize(self.text[slot], self.offs[slot], self.S, self.cfg.vocab_size, self.max_row_bytes,
+                         ids=ids, lens=lens, rows=rows)
+
+        def enc():
+            box["h"] = self.model.encoder(ids[:rows], lens[:rows])
+
+        def head():
+            box["out"] = self.model.head(box["h"], rows, self.S, self.k)
+            return box["out"]
+
+        return tok, enc, head
+
+    def _staged_graphs(self, slot: int):
+        if slot not in self._staged:
+            tok, enc, head = self._stage_fns(slot, self.B)
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):  # warm-up off-graph
+                tok(), enc(), head()
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            pool = torch.cuda.graph_pool_handle()
+            gs = []
+            outs = None
+            for fn in (tok, enc, head):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    r = fn()
+                gs.append(g)
+                outs = r if r is not None else outs
+            self._staged[slot] = (tuple(gs), outs)
+        return self._staged[slot]
+
+    def run_slot(self, slot: int, rows: int, stages: Optional[DeviceStages] = None, stream=None):
+        if stages is None:
+            if self.use_graph and rows == self.B:
+                return self._graph_step(slot)
+            return self._step(slot, rows)
+        ev = DeviceStages.event
         if self.use_graph and rows == self.B:
-            return self._graph_step(slot)
-        return self._step(slot, rows)
+            gs, outs = self._staged_graphs(slot)
+            fns = [g.replay for g in gs]
+        else:
+            fns, outs = list(self._stage_fns(slot, rows)), None
+        marks = [ev(stream)]
+        res = None
+        for fn in fns:
+            r = fn()
+            res = r if r is not None else res
+            marks.append(ev(stream))
+        for name, a, b in zip(("tokenize", "encoder", "head"), marks, marks[1:]):
+            stages.add(name, a, b)
+        return outs if outs is not None else res
 
     # -------------------------------------------------------------- host APIs
     def classify_texts(self, rows: Sequence, k: Optional[int] = None) -> BatchResult:
@@ -158,12 +216,18 @@ class ClassifyEngine:
         return self._stager
 
     def classify_table(self, table, start: int, n: int, col: int, host_threads: int = 8,
-                       out_idx: Optional[torch.Tensor] = None, out_score: Optional[torch.Tensor] = None
-                       ) -> Tuple[torch.Tensor, torch.Tensor, RunStats]:
+                       out_idx: Optional[torch.Tensor] = None, out_score: Optional[torch.Tensor] = None,
+                       stage_timing: bool = False) -> Tuple[torch.Tensor, torch.Tensor, RunStats]:
         """Pipelined classification of CSV rows ``[start, start+n)``.
 
         Returns device tensors ``idx[n,k]`` / ``score[n,k]`` (left on the GPU
         so a DP caller can all-gather them without a host round trip).
+        ``stats.timing_ms``: ``host_*_ms`` host-side spans (stager waits, launch
+        enqueue, the final drain); with ``stage_timing`` also ``device_*_ms``, GPU
+        time per stage from hipEvent pairs (h2d: the copies on the copy stream,
+        timed by the native stager after its wait for the slot's consumer;
+        tokenize / encoder / head replayed as three graphs; the top-k copy-out),
+        and ``device_span_ms`` (see :class:`DeviceStages`).
         """
         assert self.device.type == "cuda", "classify_table needs a ROCm device"
         n = max(0, min(int(n), table.num_rows - int(start)))
@@ -182,40 +246,54 @@ class ClassifyEngine:
         cs = int(self.copy_stream.cuda_stream)
         nb = (n + self.B - 1) // self.B
         t0 = time.perf_counter()
-        tm = stats.timing_ms  # host-side enqueue time per stage (+ roctx ranges under MI355X_TRACE=1)
-        with span("csv_stage", tm):
+        tm = stats.timing_ms  # host_* spans (+ roctx ranges under MI355X_TRACE=1); device_* from hipEvents
+        dst = DeviceStages() if stage_timing else None
+        ev = DeviceStages.event
+        with span("host_csv_stage_ms", tm):
             st.submit(0, table, start, min(self.B, n), col, self.max_row_bytes, host_threads)
         for i in range(nb):
             slot = i % self.n_slots
             if i + 1 < nb:
                 b1 = start + (i + 1) * self.B
-                with span("csv_stage", tm):
+                with span("host_csv_stage_ms", tm):
                     st.submit((i + 1) % self.n_slots, table, b1, min(self.B, start + n - b1), col,
                               self.max_row_bytes, host_threads)
             stream = streams[slot]
             ks = int(stream.cuda_stream)
             with torch.cuda.stream(stream):
-                with span("h2d_upload", tm):
+                with span("host_stager_wait_ms", tm):
                     rows, _ = st.upload(slot, self.text[slot].data_ptr(), self.text[slot].numel(),
                                         self.offs[slot].data_ptr(), cs, ks)
-                with span("encoder_launch", tm):
-                    _, idx, sc = self.run_slot(slot, int(rows))
+                with span("host_launch_ms", tm):
+                    _, idx, sc = self.run_slot(slot, int(rows), dst, stream)
                 st.release(slot, ks)
                 r0 = i * self.B
+                c0 = ev(stream) if dst else None
                 out_idx[r0:r0 + rows].copy_(idx[:rows], non_blocking=True)
                 out_score[r0:r0 + rows].copy_(sc[:rows], non_blocking=True)
+                if dst:
+                    dst.add("copy_out", c0, ev(stream))
             stats.batches += 1
         for s in streams:
             if s is not caller:
                 caller.wait_stream(s)
-        with span("device_drain", tm):
+        with span("host_drain_ms", tm):
             torch.cuda.synchronize(dev)
+        h2d_ms, _ = st.take_h2d_ms()  # hipEvent pairs around the copies (native stager)
+        if dst:
+            dst.resolve(tm)
+            tm["device_h2d_ms"] = round(h2d_ms, 3)
         stats.rows = n
         stats.wall_s = time.perf_counter() - t0
         return out_idx, out_score, stats
 
     def memory_bytes(self) -> int:
-        return self.pack.nbytes + sum(t.numel() for t in self.text) + self.ids.numel() * 8
+        """Resident device bytes: weights, the LayerNorm-folded weight copies once built
+        (they are ~45 % of the encoder weights), staging and token buffers."""
+        folded = getattr(self.model, "_folded", None) or {}
+        extra = sum(t.numel() * t.element_size() for t in folded.values())
+        return (self.pack.nbytes + extra + sum(t.numel() for t in self.text)
+                + sum(t.numel() * 4 for t in self.ids_s) + sum(t.numel() * 4 for t in self.offs))
 
 
 def activation_bytes_per_row(cfg: BertConfig, seq_len: int) -> int:

@@ -53,3 +53,45 @@ def span(name: str, timings: Optional[Dict[str, float]] = None, sync: bool = Fal
 def mark(name: str) -> None:
     if _ENABLED:
         _native().trace_mark(name)
+
+
+class DeviceStages:
+    """Device-side stage timing: hipEvent pairs recorded on the
+    streams that run each stage, resolved after the caller's synchronize.
+
+    ``timing_ms`` then carries ``device_<stage>_ms`` (sum of that stage's event
+    pairs, GPU time) and ``device_span_ms`` (first start to last end on the
+    device timeline). With one compute stream the compute stages add up to the
+    span minus the gaps; with concurrent slots they overlap and their sum
+    exceeds it (``device_overlap`` = sum / span)."""
+
+    def __init__(self) -> None:
+        self.pairs = []  # (stage, start, end)
+
+    @staticmethod
+    def event(stream=None):
+        import torch
+
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(stream)
+        return e
+
+    def add(self, stage: str, start, end) -> None:
+        self.pairs.append((stage, start, end))
+
+    def resolve(self, out: Dict[str, float]) -> Dict[str, float]:
+        if not self.pairs:
+            return out
+        ref = self.pairs[0][1]
+        lo, hi, busy = 0.0, 0.0, 0.0
+        for stage, a, b in self.pairs:
+            ms = a.elapsed_time(b)
+            key = f"device_{stage}_ms"
+            out[key] = round(out.get(key, 0.0) + ms, 3)
+            lo = min(lo, ref.elapsed_time(a))
+            hi = max(hi, ref.elapsed_time(b))
+            busy += ms
+        out["device_span_ms"] = round(hi - lo, 3)
+        out["device_overlap"] = round(busy / (hi - lo), 3) if hi > lo else 1.0
+        self.pairs = []
+        return out

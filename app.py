@@ -244,6 +244,14 @@ def worker_profile(health: Optional[Dict[str, Any]] = None, caps: Optional[List[
 _JSON_HEADERS = {"Content-Type": "application/json"}
 
 
+def _dumps(body: Dict[str, Any]) -> bytes:
+    try:
+        from agent_tpu_amd.utils.rawjson import dumps
+    except Exception:  # pragma: no cover - package not importable: plain encoder
+        return json.dumps(body, separators=(",", ":"), allow_nan=False).encode("utf-8")
+    return dumps(body)
+
+
 class Controller:
     def __init__(self, base: str, timeout: float) -> None:
         self.base = base
@@ -253,8 +261,9 @@ class Controller:
     def post(self, path: str, body: Dict[str, Any]) -> Tuple[int, Any]:
         url = self.base + path
         try:
-            # compact separators: a 8192-row classify result is ~20 % smaller than requests' json=
-            data = json.dumps(body, separators=(",", ":"), allow_nan=False).encode("utf-8")
+            # compact separators (a 8192-row classify result is ~20 % smaller than requests' json=);
+            # natively pre-encoded values (RawJSON: classify rows / columns) are spliced in verbatim
+            data = _dumps(body)
             r = self.http.post(url, data=data, headers=_JSON_HEADERS, timeout=self.timeout)
         except Exception as exc:
             return 0, {"error": str(exc), "url": url}

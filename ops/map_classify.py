@@ -147,9 +147,17 @@ def check_texts(payload: Dict[str, Any]) -> List[str]:
     return ["" if t is None else str(t) for t in texts]
 
 
+def _output_form(payload: Dict[str, Any]) -> str:
+    form = payload.get("output", "rows")
+    if form not in ("rows", "columns", "summary"):
+        raise ValueError("payload.output must be 'rows', 'columns' or 'summary'")
+    return form
+
+
 def texts_result(h, idx, sc, payload: Dict[str, Any], dp_world: int) -> Dict[str, Any]:
     k = max(1, min(int(payload.get("topk", 5)), h.cfg.num_labels))
     extra = {"dp_world_size": dp_world} if dp_world > 1 else {}
+    extra["_output"] = _output_form(payload)
     return _rows_result(h, idx[:, :k], sc[:, :k], 0, k, payload.get("_op", OP_NAME),
                         float(payload.get("_t0", time.time())), extra)
 
@@ -161,37 +169,41 @@ def csv_result(h, idx, sc, meta: Dict[str, Any], payload: Dict[str, Any]) -> Dic
                         {"dataset_id": payload.get("dataset_id", "unknown_dataset"),
                          "start_row": meta["start_row"], "end_row": meta["end_row"],
                          "dp_world_size": meta["world"], "timing_ms": meta["timing_ms"],
-                         "_summary": payload.get("output", "rows") == "summary"})
+                         "_output": _output_form(payload)})
 
 
 def _rows_result(h, idx, sc, start: int, k: int, op: str, t0: float, extra: Dict[str, Any]) -> Dict[str, Any]:
-    """Reference-format rows. ``tolist`` already yields Python ints / floats, so the rows are
-    built by one comprehension (a helper call and int()/float() per entry cost ~50 ms per
-    8192 rows); the summary form never builds them (top-1 histogram by ``bincount``)."""
+    """Result of a multi-row job. ``output``: ``rows`` (default; the reference's top-k
+    dicts per row), ``columns`` (``index``/``score`` as [n, k] arrays) or ``summary``
+    (top-1 histogram). rows / columns are JSON-encoded natively from the top-k arrays
+    (``_atpu.topk_json``) and carried as :class:`RawJSON`: no per-row Python objects."""
     import torch
 
-    summary = bool(extra.pop("_summary", False))
+    from agent_tpu_amd._native import native
+    from agent_tpu_amd.utils.rawjson import RawJSON
+
+    form = extra.pop("_output", "rows")
     n = int(idx.shape[0])
     first = _topk_list(idx[0].tolist(), sc[0].tolist()) if n else []
-    if not summary:
-        idx_l, sc_l = idx.tolist(), sc.tolist()
-        if k == 2:  # the common binary-label case without the inner comprehension (-25 %)
-            rows = [{"row": r, "topk": [{"index": a[0], "score": b[0]}, {"index": a[1], "score": b[1]}]}
-                    for r, a, b in zip(range(start, start + n), idx_l, sc_l)]
-        else:
-            rows = [{"row": r, "topk": [{"index": i, "score": s} for i, s in zip(a, b)]}
-                    for r, a, b in zip(range(start, start + n), idx_l, sc_l)]
     dt = time.time() - t0
     out = {"ok": True, "op": op, "model_path": h.model_path, "row_count": n,
            "topk": first, "elapsed_ms": dt * 1000.0,
            "rows_per_sec": (n / dt) if dt > 0 else None}
     out.update(extra)
-    if summary:
+    if form == "summary":
         counts = torch.bincount(idx[:, 0].to(torch.int64)).tolist() if n else []
         out.pop("topk", None)
         out["top1_histogram"] = {str(c): m for c, m in enumerate(counts) if m}
+        return out
+    ia = idx.to(torch.int32).contiguous().numpy()
+    sa = sc.to(torch.float32).contiguous().numpy()
+    nat = native()
+    if form == "columns":
+        out["k"] = k
+        out["index"] = RawJSON(nat.topk_json(start, ia, sa, 1))
+        out["score"] = RawJSON(nat.topk_json(start, ia, sa, 2))
     else:
-        out["rows"] = rows
+        out["rows"] = RawJSON(nat.topk_json(start, ia, sa, 0))
     return out
 
 
@@ -263,6 +275,7 @@ def run(payload: Dict[str, Any], ctx: Dict[str, Any] = None, op: str = OP_NAME) 
         # same order and the C1 weight broadcast always has every rank in it.
         from agent_tpu_amd.parallel.dp_ops import dispatch
 
+        _output_form(payload)  # validated before any device work
         if "source_uri" in payload and "input" not in payload:
             return dispatch("map_classify_csv", dict(payload, _op=op, _t0=t0))
         if "input" not in payload and "texts" not in payload:

@@ -50,7 +50,43 @@ def test_map_classify_op_forms(gpu, tmp_path, monkeypatch):
         assert abs(a["topk"][0]["score"] - b["topk"][0]["score"]) < 1e-3
     summ = mc.map_classify({"source_uri": path, "start_row": 0, "shard_size": 300, "output": "summary"})
     assert sum(summ["top1_histogram"].values()) == 300 and "rows" not in summ
-    assert "classify_ms" in csv["timing_ms"] and "h2d_upload_ms" in csv["timing_ms"]
+    tm = csv["timing_ms"]
+    assert "classify_ms" in tm and "host_stager_wait_ms" in tm and "host_drain_ms" in tm
+    # device time per stage from hipEvent pairs
+    for k in ("device_h2d_ms", "device_tokenize_ms", "device_encoder_ms", "device_head_ms", "device_copy_out_ms",
+              "device_span_ms", "device_allgather_ms", "device_d2h_ms"):
+        assert k in tm and tm[k] >= 0.0, (k, tm)
+    assert tm["device_encoder_ms"] > tm["device_tokenize_ms"] and tm["device_encoder_ms"] > tm["device_head_ms"]
+    # the device timeline fits inside the classify wall span
+    assert tm["device_span_ms"] <= tm["classify_ms"] + 1.0, tm
+    compute = tm["device_tokenize_ms"] + tm["device_encoder_ms"] + tm["device_head_ms"]
+    assert compute <= tm["device_span_ms"] * tm["device_overlap"] + 1.0, tm
+
+
+def test_stage_timed_classify_matches_fused_graph(gpu):
+    """The stage-timed replay (tokenize | encoder | head graphs with hipEvents between)
+    computes exactly what the single fused graph does; serial slots: stages add up."""
+    from agent_tpu_amd.models.bert import config_for, init_random
+    from agent_tpu_amd.runtime.classify import ClassifyEngine
+    from agent_tpu_amd.utils.synthetic import write_csv
+    from agent_tpu_amd._native import native
+
+    cfg = config_for("bert-base", num_labels=2)
+    dev = torch.device("cuda", 0)
+    eng = ClassifyEngine(cfg, init_random(cfg, seed=0), dev, batch_rows=256, seq_len=128, topk=2, concurrent=False)
+    import tempfile, os
+    path = os.path.join(tempfile.mkdtemp(), "t.csv")
+    write_csv(path, 1100, 60)
+    tab = native().CsvTable(path)
+    col = tab.column_index("text")
+    i1, s1, st1 = eng.classify_table(tab, 0, 1100, col)
+    i2, s2, st2 = eng.classify_table(tab, 0, 1100, col, stage_timing=True)
+    assert torch.equal(i1, i2) and torch.equal(s1, s2)
+    tm = st2.timing_ms
+    stages = sum(tm[f"device_{k}_ms"] for k in ("tokenize", "encoder", "head", "copy_out"))
+    assert stages <= tm["device_span_ms"] + 0.5, tm
+    assert stages >= 0.5 * tm["device_span_ms"], tm  # one compute stream: the stages fill most of the span
+    assert "device_h2d_ms" not in st1.timing_ms
 
 
 def test_risk_gpu_path_matches_cpu(gpu, monkeypatch):
