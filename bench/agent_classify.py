@@ -28,7 +28,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=16)
     ap.add_argument("--shard", type=int, default=16384, help="CSV rows per job")
-    ap.add_argument("--output", default="rows", choices=["rows", "summary"])
+    ap.add_argument("--output", default="rows", choices=["rows", "columns", "summary"])
     ap.add_argument("--model", default="bert-base")
     ap.add_argument("--form", default="csv", choices=["csv", "input"],
                     help="csv: CSV-shard jobs; input: the reference job shape, one pre-tokenized row per job")

@@ -156,3 +156,19 @@ def test_unavailable_op_not_advertised(ctl):
         code, out = stop_agent(p)
     assert ctl.lease_requests[0]["capabilities"]["ops"] == ["echo"]
     assert "op unavailable: definitely_not_an_op" in out
+
+
+def test_async_result_poster_keeps_every_result(ctl):
+    """RESULT_POST_ASYNC=1: results go out from a background thread, in order, each with
+    its job_epoch, and SIGTERM flushes the queue before exit."""
+    for i in range(12):
+        ctl.lease({"id": f"a{i}", "op": "echo", "payload": {"i": i}, "job_epoch": i})
+    ctl.result_codes["a3"] = [500, 200]  # retried by the poster, still delivered
+    p = start_agent(ctl, tasks="echo", RESULT_POST_ASYNC="1")
+    try:
+        assert ctl.wait(lambda c: len(c.results) >= 12, 60), ctl.results
+    finally:
+        code, out = stop_agent(p)
+    assert code == 0, out
+    got = [(r["job_id"], r["job_epoch"], r["result"]["echo"]["i"]) for r in ctl.results]
+    assert got == [(f"a{i}", i, i) for i in range(12)]
