@@ -276,6 +276,22 @@ PYBIND11_MODULE(_atpu, m) {
       "document offsets [B+1]",
       py::arg("text"), py::arg("offsets"), py::arg("vocab"), py::arg("cap"));
 
+  m.def("risk_stats_list",
+        [](py::list values, int mode, py::object field, bool keep) -> py::object {
+          RiskStats st{};
+          std::vector<double> vals;
+          if (!risk_stats_pylist(values.ptr(), mode, field.ptr(), &st, keep ? &vals : nullptr))
+            throw py::error_already_set();
+          py::object arr = py::none();
+          if (keep) {
+            py::array_t<double> a(static_cast<py::ssize_t>(vals.size()));
+            std::memcpy(a.mutable_data(), vals.data(), vals.size() * sizeof(double));
+            arr = a;
+          }
+          return py::make_tuple(st.count, st.sum, st.min, st.max, arr);
+        },
+        "risk_accumulate over a JSON list: (count, sum, min, max, values f64 | None); mode 0 values, 1 items[field]",
+        py::arg("values"), py::arg("mode") = 0, py::arg("field") = py::str("risk"), py::arg("keep") = false);
   m.def("topk_json",
         [](int64_t start_row, py::array_t<int32_t, py::array::c_style | py::array::forcecast> idx,
            py::array_t<float, py::array::c_style | py::array::forcecast> score, int mode) {

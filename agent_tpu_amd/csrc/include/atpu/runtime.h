@@ -41,6 +41,15 @@ std::vector<DeviceInfo> device_query(int mem_of = -1);
 // Classify top-k [n, k] -> JSON text. mode 0: reference-style rows
 // [{"row":start+r,"topk":[{"index":i,"score":s},...]},...]; 1: [[index,...],...];
 // 2: [[score,...],...]. Floats in the shortest round-trip form.
+struct RiskStats {
+  int64_t count;
+  double sum, min, max;
+};
+// risk_accumulate over a Python list (see runtime/risk_parse.cpp); needs the GIL.
+// mode 0 values, 1 items[field]. False = Python exception set.
+bool risk_stats_pylist(struct _object* list, int mode, struct _object* field, RiskStats* st,
+                       std::vector<double>* out);
+
 std::string topk_json(int64_t start_row, const int32_t* idx, const float* score, int64_t n, int k, int mode);
 
 // Double-buffered CSV column -> pinned host -> device pipeline.

@@ -414,11 +414,11 @@ def _local_values(payload: Dict[str, Any], rank: int, ws: int) -> Tuple[torch.Te
         total = max(0, min(int(payload.get("shard_size", table.num_rows)), table.num_rows - start))
         s_r, n_r = split_range(start, total, ws, rank)
         return torch.from_numpy(table.native.float_column(s_r, n_r, col)), total
-    from ops.risk_accumulate import _gather  # same validation/messages as the CPU op
+    from ops.risk_accumulate import gather_array  # same validation/messages as the CPU op (native parse)
 
-    vals = _gather(payload)
+    vals = gather_array(payload)
     s_r, n_r = split_range(0, len(vals), ws, rank)
-    return torch.tensor(vals[s_r:s_r + n_r], dtype=torch.float64), len(vals)
+    return torch.from_numpy(vals[s_r:s_r + n_r].copy()), len(vals)
 
 
 @dp_task("risk_accumulate")

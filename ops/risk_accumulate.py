@@ -12,7 +12,10 @@ partials are combined with RCCL all-reduces
 Sums are taken with ``math.fsum``-free sequential float64 addition on the CPU
 path so that results are bit-identical to the reference's ``sum()``; the GPU
 path accumulates in fp64 per lane and is exact to rounding order (documented in
-risk_accumulate.CONTRACT.md).
+risk_accumulate.CONTRACT.md). JSON lists (``values`` / ``items``) are converted
+and reduced in ONE native pass (``_atpu.risk_stats_list``: the reference's
+conversion rules via the CPython API, same sequential sum), instead of a Python
+loop; ``RISK_DEVICE=gpu`` sends them through the K12 kernel instead.
 """
 from __future__ import annotations
 
@@ -31,6 +34,43 @@ def to_float(value: Any) -> float:
     if isinstance(value, str):
         return float(value.strip())
     raise ValueError("value must be numeric")
+
+
+def _native():
+    if os.getenv("RISK_NATIVE", "1").strip().lower() in ("0", "false", "no"):
+        return None
+    try:
+        from agent_tpu_amd._native import native
+
+        return native()
+    except Exception:
+        return None
+
+
+def _source(payload: Dict[str, Any]):
+    """(list, mode, field) after the reference's payload checks (ref :34-53)."""
+    if "values" in payload:
+        raw = payload.get("values")
+        if not isinstance(raw, list):
+            raise ValueError("payload.values must be a list")
+        return raw, 0, None
+    if "items" in payload:
+        items = payload.get("items")
+        if not isinstance(items, list):
+            raise ValueError("payload.items must be a list")
+        return items, 1, payload.get("field", "risk")
+    raise ValueError("payload must include either 'values' or 'items'")
+
+
+def gather_array(payload: Dict[str, Any]):
+    """The payload's values as a float64 numpy array (native conversion when available)."""
+    import numpy as np
+
+    nat = _native()
+    lst, mode, field = _source(payload)
+    if nat is not None and (mode == 0 or isinstance(field, str)):
+        return nat.risk_stats_list(lst, mode, field if mode else "risk", True)[4]
+    return np.asarray(_gather(payload), dtype=np.float64)
 
 
 def _gather(payload: Dict[str, Any]) -> List[float]:
@@ -118,6 +158,19 @@ def risk_accumulate(payload: Dict[str, Any]) -> Dict[str, Any]:
             stats["device"] = "gpu"
         stats["compute_time_ms"] = (time.time() - t0) * 1000.0
         return stats
+    nat = _native()
+    mode_env = os.getenv("RISK_DEVICE", "auto").strip().lower()
+    if nat is not None and mode_env != "gpu":
+        # one native pass over the JSON list: the reference's conversions, sequential float64
+        # sum and comparisons (bit-identical results), no per-element Python
+        lst, mode, field = _source(payload)
+        if mode == 0 or isinstance(field, str):
+            cnt, total, lo, hi, _ = nat.risk_stats_list(lst, mode, field if mode else "risk", False)
+            if cnt == 0:
+                return {"count": 0, "sum": 0.0, "mean": 0.0, "min": None, "max": None,
+                        "compute_time_ms": (time.time() - t0) * 1000.0}
+            return {"count": cnt, "sum": total, "mean": total / cnt, "min": lo, "max": hi,
+                    "compute_time_ms": (time.time() - t0) * 1000.0}
     values = _gather(payload)
     if not values:
         return {"count": 0, "sum": 0.0, "mean": 0.0, "min": None, "max": None,
