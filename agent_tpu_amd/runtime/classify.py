@@ -32,6 +32,7 @@ from ..models.bert import BertClassifier, BertConfig
 from ..models.params import ParamPack
 from ..tokenizer import DEFAULT_MAX_ROW_BYTES, pack_rows
 from ..utils.trace import DeviceStages, span
+from .graphs import capture_graph
 
 
 @dataclass
@@ -118,9 +119,7 @@ class ClassifyEngine:
             with torch.cuda.stream(s):  # warm up allocator + code objects off-graph
                 self._step(slot, self.B)
             torch.cuda.current_stream(self.device).wait_stream(s)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                outs = self._step(slot, self.B)
+            g, outs = capture_graph(lambda: self._step(slot, self.B))
             self._graphs[slot] = (g, outs)
         g, outs = self._graphs[slot]
         g.replay()
@@ -155,9 +154,7 @@ class ClassifyEngine:
             gs = []
             outs = None
             for fn in (tok, enc, head):
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool):
-                    r = fn()
+                g, r = capture_graph(fn, pool=pool)
                 gs.append(g)
                 outs = r if r is not None else outs
             self._staged[slot] = (tuple(gs), outs)

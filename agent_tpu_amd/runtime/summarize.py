@@ -269,10 +269,12 @@ def _generate_iter(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
             return g_logits
         out = advance()
         if use_graph:
-            # capture records without executing: the state stays at the eager step's
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                g_logits = advance()
+            # capture records without executing: the state stays at the eager step's.
+            # capture_graph skips torch.cuda.graph's device-wide synchronize + empty_cache,
+            # which stalled the sibling searches' streams
+            from .graphs import capture_graph
+
+            graph, g_logits = capture_graph(advance)
         return out
 
     def apply(cur: int, top_sc, top_tok, top_beam, nxt) -> bool:
@@ -397,6 +399,7 @@ def _generate_iter(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
         # drain before their graph and buffers go out of scope
         torch.cuda.current_stream(dev).synchronize()
     else:
+        stage_ev = None  # stage_host is rewritten only after its last H2D retired
         while True:
             tp0 = time.perf_counter()
             with span("beam_select"):
@@ -411,11 +414,16 @@ def _generate_iter(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
                 # step synchronised past its previous H2D)
                 hits = (top_tok == cfg.eos_id) | (cur + 1 >= T)
                 run_cand = np.where(hits, top_sc + neg, top_sc)
+                if stage_ev is not None:
+                    stage_ev.synchronize()  # the previous step's async H2D has read stage_host
                 st = stage_host.numpy()
                 st[:rows] = (rowsB * nb + top_beam[rowsB, nxt]).reshape(-1)
                 st[rows:2 * rows] = top_tok[rowsB, nxt].reshape(-1)
                 st[2 * rows:] = run_cand[rowsB, nxt].reshape(-1).view(np.int32)
                 stage_dev.copy_(stage_host, non_blocking=True)
+                if pin:
+                    stage_ev = torch.cuda.Event()
+                    stage_ev.record()
                 logits = launch_next()
             tp2 = time.perf_counter()
             stop = apply(cur, top_sc, top_tok, top_beam, nxt)  # under the GPU step
