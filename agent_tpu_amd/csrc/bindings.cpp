@@ -14,6 +14,7 @@
 #include <string>
 #include <vector>
 
+#include "atpu/comm.h"
 #include "atpu/common.h"
 #include "atpu/csv.h"
 #include "atpu/kernels.h"
@@ -394,6 +395,39 @@ PYBIND11_MODULE(_atpu, m) {
              return py::make_tuple(text, offs);
            },
            py::arg("start"), py::arg("n"), py::arg("col"), py::arg("max_bytes"), py::arg("threads") = 8);
+
+  py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
+      .def(py::init([](int world, int rank, py::bytes uid, int device) {
+             std::string u = uid;
+             py::gil_scoped_release nogil;  // ncclCommInitRank blocks until every rank joined
+             return std::make_shared<RcclComm>(world, rank, u, device);
+           }),
+           py::arg("world"), py::arg("rank"), py::arg("uid"), py::arg("device"))
+      .def_static("unique_id", [] { return py::bytes(RcclComm::unique_id()); })
+      .def_static("init_all", &RcclComm::init_all, py::arg("devices"))
+      .def("broadcast",
+           [](RcclComm& c, uintptr_t buf, size_t count, int dtype, int root, uintptr_t stream) {
+             py::gil_scoped_release nogil;
+             c.broadcast(P<void>(buf), count, dtype, root, S(stream));
+           })
+      .def("all_gather",
+           [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, uintptr_t stream) {
+             py::gil_scoped_release nogil;
+             c.all_gather(P<const void>(send), P<void>(recv), count, dtype, S(stream));
+           })
+      .def("all_reduce",
+           [](RcclComm& c, uintptr_t buf, size_t count, int dtype, int op, uintptr_t stream) {
+             py::gil_scoped_release nogil;
+             c.all_reduce(P<void>(buf), count, dtype, op, S(stream));
+           })
+      .def("async_error", &RcclComm::async_error)
+      .def("abort", &RcclComm::abort)
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("world", &RcclComm::world)
+      .def_property_readonly("device", &RcclComm::device);
+  m.def("rccl_group_start", &rccl_group_start);
+  m.def("rccl_group_end", &rccl_group_end);
+  m.def("rccl_version", &rccl_version);
 
   py::class_<HostStager>(m, "HostStager")
       .def(py::init<int, size_t, int>(), py::arg("slots"), py::arg("text_capacity"), py::arg("max_rows"))

@@ -1,6 +1,6 @@
 """Build the native `_atpu` extension in-tree with hipcc for gfx950.
 
-Every ``kernels/*.hip`` and ``runtime/*.cpp`` translation unit plus
+Every ``kernels/*.hip``, ``runtime/*.cpp`` and ``comm/*.cpp`` translation unit plus
 ``bindings.cpp`` is compiled to ``build/obj`` in parallel and linked into
 ``agent_tpu_amd/_atpu<EXT_SUFFIX>``. Compilation is incremental (an object is
 rebuilt when its source or any header is newer). No hipify, no torch headers:
@@ -34,6 +34,10 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found (expected /opt/rocm/bin/hipcc)")
 
 
+def _rocm() -> str:
+    return os.environ.get("ROCM_PATH", "/opt/rocm")
+
+
 def _includes() -> List[str]:
     import pybind11
 
@@ -45,7 +49,8 @@ def _includes() -> List[str]:
 
 
 def sources() -> List[Path]:
-    srcs = sorted((HERE / "kernels").glob("*.hip")) + sorted((HERE / "runtime").glob("*.cpp"))
+    srcs = (sorted((HERE / "kernels").glob("*.hip")) + sorted((HERE / "runtime").glob("*.cpp"))
+            + sorted((HERE / "comm").glob("*.cpp")))
     return srcs + [HERE / "bindings.cpp"]
 
 
@@ -97,7 +102,9 @@ def build(force: bool = False, debug: bool = False, asan_host: bool = False, job
     flavour = ("dev" if dev else "release") + ("-debug" if debug else "") + ("-asan" if asan_host else "")
     same = stamp.exists() and stamp.read_text() == flavour
     if force or not same or not out.exists() or out.stat().st_mtime < newest:
-        link = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", str(out) + ".tmp", "-lpthread"]
+        # librccl.so.1: at run time the copy torch already loaded (same SONAME) serves it
+        link = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", str(out) + ".tmp", "-lpthread",
+                f"-L{_rocm()}/lib", "-lrccl"]
         if asan_host:
             link += ["-fsanitize=address"]
         res = subprocess.run([str(x) for x in link], capture_output=True, text=True)

@@ -12,6 +12,10 @@ tests. Collectives issued by a DP classify task:
 * C2 :func:`all_gather_rows` — per-rank top-k rows, padded to the largest
   shard, gathered with one ``all_gather_into_tensor`` per tensor; counts are
   gathered first (4 B/rank) so ragged shards reassemble exactly.
+
+With ``ATPU_COMM=native`` (RCCL backend) the tensor collectives run on the
+native communicator of :mod:`agent_tpu_amd.parallel.rccl` (csrc/comm/rccl_comm.cpp)
+instead of ProcessGroupNCCL; objects and the task descriptor stay on torch.distributed.
 * C3 (risk) is the all-reduce in :func:`agent_tpu_amd.parallel.dp_ops.risk_task`.
 
 Shard planning is contiguous and balanced (:func:`split_range`), so results
@@ -38,6 +42,7 @@ def is_dist() -> bool:
 
 
 _GROUP = None  # active DP group after a shrink (None = the default group)
+_NATIVE = None  # ATPU_COMM=native: RCCL communicator over the active group (rebuilt on shrink)
 _MEMBERS: Optional[List[int]] = None  # its global ranks, ascending
 _LOST: List[int] = []
 
@@ -79,9 +84,27 @@ def shrink(lost: Iterable[int]) -> bool:
     keep = [r for r in cur if r not in gone]
     _LOST.extend(sorted(gone))
     _MEMBERS = keep
+    global _NATIVE
+    if _NATIVE is not None:
+        _NATIVE.comm.abort()  # its peers include the lost ranks; rebuilt lazily over the survivors
+        _NATIVE = None
     if dist.get_rank() in keep:
         _GROUP = dist.new_group(ranks=keep, use_local_synchronization=True)
     return True
+
+
+def native_comm(dev: torch.device):
+    """The native RCCL communicator of the active DP group (``ATPU_COMM=native``, RCCL
+    backend, device tensors), created collectively on first use; None otherwise."""
+    global _NATIVE
+    from . import rccl
+
+    if not (rccl.enabled() and is_dist() and dist.get_backend() == "nccl" and dev.type == "cuda"):
+        return None
+    if _NATIVE is None:
+        with watchdog.collective("rccl communicator init"):
+            _NATIVE = rccl.NativeComm.from_group(dev, group=_GROUP, ranks=members())
+    return _NATIVE
 
 
 def split_range(start: int, n: int, world_size: int, rank: int) -> Tuple[int, int]:
@@ -114,8 +137,12 @@ def broadcast_pack(pack, cfg, device: torch.device, src: int = 0, builder=None):
     if is_dist():
         cdev = comm_device(device)
         buf = out.buffer if out.buffer.device == cdev else out.buffer.to(cdev)
+        nc = native_comm(cdev)
         with watchdog.collective("weight broadcast"):
-            dist.broadcast(buf, src=src, group=_GROUP)
+            if nc is not None:  # C1 on the native communicator (group rank of the source)
+                nc.broadcast(buf, root=members().index(src))
+            else:
+                dist.broadcast(buf, src=src, group=_GROUP)
         if buf is not out.buffer:
             out.buffer.copy_(buf)
     return out
@@ -144,8 +171,12 @@ def all_gather_rows(*tensors: torch.Tensor) -> Tuple[torch.Tensor, ...]:
     cdev = comm_device(dev)
     cnt = torch.tensor([tensors[0].shape[0]], dtype=torch.int64, device=cdev)
     counts = torch.empty(ws, dtype=torch.int64, device=cdev)
+    nc = native_comm(cdev)
     with watchdog.collective("row-count gather"):
-        dist.all_gather_into_tensor(counts, cnt, group=_GROUP)
+        if nc is not None:
+            nc.all_gather_into(counts, cnt)
+        else:
+            dist.all_gather_into_tensor(counts, cnt, group=_GROUP)
     counts_l: List[int] = counts.tolist()
     mx = max(counts_l) if counts_l else 0
     outs = []
@@ -157,7 +188,10 @@ def all_gather_rows(*tensors: torch.Tensor) -> Tuple[torch.Tensor, ...]:
         t = t.contiguous()
         g = torch.empty((ws * mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=cdev)
         with watchdog.collective("row all-gather"):
-            dist.all_gather_into_tensor(g, t, group=_GROUP)
+            if nc is not None:
+                nc.all_gather_into(g, t)
+            else:
+                dist.all_gather_into_tensor(g, t, group=_GROUP)
         if all(c == mx for c in counts_l):
             outs.append(g.to(dev))
         else:

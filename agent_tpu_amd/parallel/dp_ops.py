@@ -444,9 +444,14 @@ def risk_task(payload: Dict[str, Any]) -> Any:
         s = stats.to(cdev)
         sums = s[:2].clone()
         ext = torch.stack([s[3], -s[2]])  # max, -min -> one MAX all-reduce
+        nc = dp.native_comm(cdev)
         with watchdog.collective("risk all-reduce"):
-            dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=dp.group())
-            dist.all_reduce(ext, op=dist.ReduceOp.MAX, group=dp.group())
+            if nc is not None:
+                nc.all_reduce(sums, "sum")
+                nc.all_reduce(ext, "max")
+            else:
+                dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=dp.group())
+                dist.all_reduce(ext, op=dist.ReduceOp.MAX, group=dp.group())
         stats = torch.stack([sums[0], sums[1], -ext[1], ext[0]]).cpu()
     else:
         stats = stats.cpu()

@@ -52,7 +52,11 @@ def parse():
     ap.add_argument("--csv", default="")
     # rehearsal only: "gloo" lets >1 ranks share one GPU (RCCL refuses duplicate devices)
     ap.add_argument("--dist-backend", default=os.environ.get("BENCH_DIST_BACKEND", "nccl"))
-    return ap.parse_args()
+    ap.add_argument("--comm", default=os.environ.get("ATPU_COMM", "torch"), choices=["torch", "native"],
+                    help="data-plane collectives: torch.distributed (ProcessGroupNCCL) or the native RcclComm")
+    a = ap.parse_args()
+    os.environ["ATPU_COMM"] = a.comm
+    return a
 
 
 def launch_ranks(a) -> int:
@@ -181,6 +185,7 @@ def main() -> int:
                 "seq_len": a.seq_len,
                 "parallelism": f"dp{world}",
                 "dist_backend": a.dist_backend if world > 1 else None,
+                "comm": a.comm if world > 1 else None,
                 "rccl_world_size": rccl_world if a.dist_backend == "nccl" or world == 1 else None,
                 "pg_world_size": rccl_world,
                 "rank_devices": [t["device"] for t in rank_table],

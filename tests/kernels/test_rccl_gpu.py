@@ -34,23 +34,48 @@ out["desc"] = dp.broadcast_task({"op": "x"}) == {"op": "x"}
 vals = [float(i) / 7 for i in range(1000)]
 r = dp_ops.dispatch("risk_accumulate", {"values": vals})
 out["risk"] = r["count"] == 1000 and abs(r["sum"] - sum(vals)) < 1e-9 and r["dp_world_size"] == 1
+from agent_tpu_amd.parallel import rccl
+out["native"] = rccl.enabled() == (os.environ.get("ATPU_COMM") == "native") and (
+    dp.native_comm(dev) is not None) == rccl.enabled()
+if rccl.enabled():
+    nc = dp.native_comm(dev)
+    t = torch.arange(10, dtype=torch.float64, device=dev)
+    nc.all_reduce(t, "max")
+    b = torch.full((5,), 3, dtype=torch.bfloat16, device=dev)
+    nc.broadcast(b, 0)
+    o = torch.empty(5, dtype=torch.bfloat16, device=dev)
+    nc.all_gather_into(o, b)
+    out["native_ops"] = torch.equal(t.cpu(), torch.arange(10, dtype=torch.float64)) and torch.equal(o.cpu(), b.cpu()) and nc.healthy()
+    # single-process form over the local GPU(s) (ncclCommInitAll)
+    cs = rccl.local_comms([0])
+    x = torch.ones(4, device=dev)
+    with rccl.group():
+        cs[0].all_reduce(x, "sum")
+    torch.cuda.synchronize()
+    out["init_all"] = cs[0].world == 1 and torch.equal(x.cpu(), torch.ones(4))
 dist.barrier()
 dist.destroy_process_group()
 print("RESULT " + json.dumps(out))
 '''
 
 
-def test_rccl_world1_collectives(gpu):
+@pytest.mark.parametrize("comm", ["torch", "native"])
+def test_rccl_world1_collectives(gpu, comm):
+    """Same collectives through ProcessGroupNCCL and through the native RcclComm
+    (ATPU_COMM=native: csrc/comm/rccl_comm.cpp)."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
-               LOCAL_RANK="0", REPO=REPO, HSA_ENABLE_IPC_MODE_LEGACY="0")
+               LOCAL_RANK="0", REPO=REPO, HSA_ENABLE_IPC_MODE_LEGACY="0", ATPU_COMM=comm)
     p = subprocess.run([sys.executable, "-c", SCRIPT], env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")][-1]
     import json
 
     res = json.loads(line[7:])
-    assert res == {"pack_on_gpu": True, "gather": True, "desc": True, "risk": True}, res
+    want = {"pack_on_gpu": True, "gather": True, "desc": True, "risk": True, "native": True}
+    if comm == "native":
+        want.update(native_ops=True, init_all=True)
+    assert res == want, res
