@@ -182,6 +182,86 @@ class ClassifyEngine:
         return outs if outs is not None else res
 
     # -------------------------------------------------------------- host APIs
+    # ------------------------------------------------- small jobs (texts / input)
+    # The per-job forms (the reference's one-row ``input`` job, short ``texts`` lists)
+    # replay a captured graph too: rows are padded up to a power-of-two bucket (8 .. B),
+    # so a job costs one H2D from pinned staging, one graph launch and one D2H instead
+    # of ~100 eager launches (padding rows are empty and their results dropped).
+    def _bucket(self, n: int) -> int:
+        b = 8
+        while b < n:
+            b *= 2
+        return min(b, self.B)
+
+    def _pinned(self):
+        if getattr(self, "_pin", None) is None:
+            self._pin = {
+                "ids": torch.zeros((self.B, self.S), dtype=torch.int32, pin_memory=True),
+                "lens": torch.ones(self.B, dtype=torch.int32, pin_memory=True),
+                "text": torch.zeros(self.B * self.max_row_bytes, dtype=torch.uint8, pin_memory=True),
+                "offs": torch.zeros(self.B + 1, dtype=torch.int32, pin_memory=True),
+            }
+            self._bpool = torch.cuda.graph_pool_handle()
+            self._bgraphs = {}
+        return self._pin
+
+    def _bucket_graph(self, kind: str, bucket: int):
+        key = (kind, bucket)
+        if key not in self._bgraphs:
+            ids, lens = self.ids_s[0][:bucket], self.lens_s[0][:bucket]
+
+            def fn():
+                if kind == "text":
+                    ops.tokenize(self.text[0], self.offs[0], self.S, self.cfg.vocab_size, self.max_row_bytes,
+                                 ids=self.ids_s[0], lens=self.lens_s[0], rows=bucket)
+                return self.model.forward(ids, lens, self.k)
+
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):  # warm-up off-graph
+                fn()
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self._bgraphs[key] = capture_graph(fn, pool=self._bpool)
+        return self._bgraphs[key]
+
+    def _run_bucket(self, kind: str, m: int, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        bk = self._bucket(m)
+        if self.use_graph:
+            g, (_, idx, sc) = self._bucket_graph(kind, bk)
+            g.replay()
+        else:
+            if kind == "text":
+                ops.tokenize(self.text[0], self.offs[0], self.S, self.cfg.vocab_size, self.max_row_bytes,
+                             ids=self.ids_s[0], lens=self.lens_s[0], rows=bk)
+            _, idx, sc = self.model.forward(self.ids_s[0][:bk], self.lens_s[0][:bk], self.k)
+        both = torch.cat([idx[:m, :k].view(torch.float32), sc[:m, :k]], 1).cpu()  # one D2H, one sync
+        return both[:, :k].contiguous().view(torch.int32), both[:, k:].contiguous()
+
+    def classify_ids(self, ids: torch.Tensor, lens: torch.Tensor, k: Optional[int] = None) -> BatchResult:
+        """Pre-tokenized rows ``ids [n, S]`` / ``lens [n]`` (host tensors) -> top-k on the host."""
+        k = self.k if k is None else max(1, min(int(k), self.k))
+        n = int(ids.shape[0])
+        if self.device.type != "cuda":
+            _, idx, sc = self.model.forward(ids.to(torch.int32), lens.to(torch.int32), k)
+            return BatchResult(n, idx[:, :k].cpu(), sc[:, :k].cpu())
+        pin = self._pinned()
+        idx_all, sc_all = [], []
+        for c0 in range(0, n, self.B):
+            m = min(self.B, n - c0)
+            bk = self._bucket(m)
+            pin["ids"][:m].copy_(ids[c0:c0 + m])
+            pin["ids"][m:bk].zero_()
+            pin["lens"][:m].copy_(lens[c0:c0 + m])
+            pin["lens"][m:bk].fill_(1)
+            self.ids_s[0][:bk].copy_(pin["ids"][:bk], non_blocking=True)
+            self.lens_s[0][:bk].copy_(pin["lens"][:bk], non_blocking=True)
+            i, s_ = self._run_bucket("ids", m, k)  # its D2H synchronizes: the pinned rows are free again
+            idx_all.append(i)
+            sc_all.append(s_)
+        if not idx_all:
+            return BatchResult(0, torch.zeros((0, k), dtype=torch.int32), torch.zeros((0, k)))
+        return BatchResult(n, torch.cat(idx_all), torch.cat(sc_all))
+
     def classify_texts(self, rows: Sequence, k: Optional[int] = None) -> BatchResult:
         """Classify an in-memory list of strings (small jobs; no CSV)."""
         k = self.k if k is None else max(1, min(int(k), self.cfg.num_labels))
@@ -192,17 +272,23 @@ class ClassifyEngine:
                                    r.encode("utf-8")[:self.max_row_bytes] for r in chunk)
             n = len(chunk)
             if self.device.type == "cuda":
-                self.text[0][:text.size].copy_(torch.from_numpy(text), non_blocking=False)
-                self.offs[0][:n + 1].copy_(torch.from_numpy(offs))
-                ids, lens = ops.tokenize(self.text[0], self.offs[0], self.S, self.cfg.vocab_size,
-                                         self.max_row_bytes, ids=self.ids, lens=self.lens, rows=n)
-                logits, idx, sc = self.model.forward(ids[:n], lens[:n], k)
+                pin = self._pinned()
+                bk = self._bucket(n)
+                pin["text"][:text.size].copy_(torch.from_numpy(text))
+                pin["offs"][:n + 1].copy_(torch.from_numpy(offs))
+                pin["offs"][n + 1:bk + 1].fill_(int(offs[-1]))  # padding rows: empty strings
+                if text.size:
+                    self.text[0][:text.size].copy_(pin["text"][:text.size], non_blocking=True)
+                self.offs[0][:bk + 1].copy_(pin["offs"][:bk + 1], non_blocking=True)
+                i, s_ = self._run_bucket("text", n, min(k, self.k))
+                idx_all.append(i)
+                sc_all.append(s_)
             else:
                 ids, lens = ops.tokenize(torch.from_numpy(text), torch.from_numpy(offs), self.S,
                                          self.cfg.vocab_size, self.max_row_bytes)
                 logits, idx, sc = self.model.forward(ids, lens, k)
-            idx_all.append(idx.cpu())
-            sc_all.append(sc.cpu())
+                idx_all.append(idx.cpu())
+                sc_all.append(sc.cpu())
         if not idx_all:
             return BatchResult(0, torch.zeros((0, k), dtype=torch.int32), torch.zeros((0, k)))
         return BatchResult(len(rows), torch.cat(idx_all), torch.cat(sc_all))

@@ -40,20 +40,9 @@ def classify_ids(h, payload: Dict[str, Any], op: str, t0: float) -> Dict[str, An
     """The reference form: one pre-tokenized row (``input``) -> reference keys."""
     import torch
 
-    k = max(1, min(int(payload.get("topk", 5)), h.cfg.num_labels))
-    S = h.engine.S
-    raw = payload["input"]
-    ids = torch.tensor(raw, dtype=torch.int64)
-    if ids.numel() != S:
-        raise ValueError(f"Input size mismatch. Got {ids.numel()}, expected {S} for shape (1, {S}).")
-    if int(ids.min()) < 0 or int(ids.max()) >= h.cfg.vocab_size:
-        raise ValueError(f"token id out of range [0, {h.cfg.vocab_size})")
-    nz = (ids != 0).nonzero()
-    n = int(nz[-1]) + 1 if nz.numel() else 1
-    dev = h.engine.device
-    _, idx, sc = h.engine.model.forward(ids.view(1, S).to(torch.int32).to(dev),
-                                         torch.tensor([max(1, n)], dtype=torch.int32, device=dev), k)
-    return {"op": op, "model_path": h.model_path, "topk": _topk_list(idx[0].tolist(), sc[0].tolist()),
+    ids, n, k = _input_row(h, payload)
+    res = h.engine.classify_ids(ids.view(1, -1), torch.tensor([n], dtype=torch.int32), k)
+    return {"op": op, "model_path": h.model_path, "topk": _topk_list(res.idx[0].tolist(), res.score[0].tolist()),
             "elapsed_ms": (time.time() - t0) * 1000.0}
 
 
@@ -96,16 +85,10 @@ def classify_batch(h, payloads: List[Dict[str, Any]], rank: int, ws: int) -> Opt
                 except Exception as exc:
                     out[i] = ("err", exc)
         if rows:
-            dev, B, S = h.engine.device, h.engine.B, h.engine.S
             kmax = max(r[3] for r in rows)
-            ids = torch.stack([r[1] for r in rows]).to(dev)
-            lens = torch.tensor([r[2] for r in rows], dtype=torch.int32).to(dev)
-            idx_l, sc_l = [], []
-            for b0 in range(0, len(rows), B):
-                _, idx, sc = h.engine.model.forward(ids[b0:b0 + B], lens[b0:b0 + B], kmax)
-                idx_l.append(idx[:, :kmax].cpu())
-                sc_l.append(sc[:, :kmax].cpu())
-            idx_all, sc_all = torch.cat(idx_l).tolist(), torch.cat(sc_l).tolist()
+            res = h.engine.classify_ids(torch.stack([r[1] for r in rows]),
+                                        torch.tensor([r[2] for r in rows], dtype=torch.int32), kmax)
+            idx_all, sc_all = res.idx.tolist(), res.score.tolist()
             for (i, _, _, k), ir, sr in zip(rows, idx_all, sc_all):
                 p = payloads[i]
                 out[i] = ("ok", {"op": p.get("_op", OP_NAME), "model_path": h.model_path,

@@ -118,3 +118,30 @@ def test_model_lru_hbm_budget(gpu, monkeypatch):
     assert rt.cache_info()["entries"] == ["bert-tiny?seed=1&batch=32", "bert-tiny?seed=3&batch=32"]
     with rt._lock:
         rt._cache.clear()
+
+
+@pytest.mark.parametrize("n", [1, 7, 9, 300])
+def test_small_job_bucket_graphs_match_eager(gpu, n):
+    """texts / input jobs replay bucketed graphs (rows padded to a power of two);
+    results equal the eager path row for row."""
+    from agent_tpu_amd.models.bert import config_for, init_random
+    from agent_tpu_amd.runtime.classify import ClassifyEngine
+    from agent_tpu_amd.utils.synthetic import make_text_rows
+
+    cfg = config_for("bert-base", num_labels=5)
+    pack = init_random(cfg, seed=2)
+    dev = torch.device("cuda", 0)
+    g_eng = ClassifyEngine(cfg, pack, dev, batch_rows=256, seq_len=128, topk=5)
+    e_eng = ClassifyEngine(cfg, pack, dev, batch_rows=256, seq_len=128, topk=5, use_graph=False)
+    texts = make_text_rows(n, words_per_row=40, seed=n)
+    a, b = g_eng.classify_texts(texts, 3), e_eng.classify_texts(texts, 3)
+    assert a.idx.shape == (n, 3) and torch.equal(a.idx, b.idx) and torch.allclose(a.score, b.score, atol=1e-6)
+    g = torch.Generator().manual_seed(n)
+    ids = torch.randint(1000, cfg.vocab_size, (n, 128), generator=g, dtype=torch.int32)
+    lens = torch.randint(2, 129, (n,), generator=g, dtype=torch.int32)
+    ids[torch.arange(128).view(1, -1) >= lens.view(-1, 1)] = 0
+    a, b = g_eng.classify_ids(ids, lens, 2), e_eng.classify_ids(ids, lens, 2)
+    assert torch.equal(a.idx, b.idx) and torch.allclose(a.score, b.score, atol=1e-6)
+    # and the same rows through the full fp32-free forward on the device, one call
+    _, ri, rs = e_eng.model.forward(ids.to(dev), lens.to(dev), 2)
+    assert torch.equal(a.idx, ri.cpu())
