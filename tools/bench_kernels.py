@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
+    ap.add_argument("--docs", type=int, default=256, help="long-sequence attention cases: documents")
+    ap.add_argument("--src", type=int, default=1024, help="long-sequence attention cases: tokens per document")
     ap.add_argument("--variants", default="",
                     help="comma list of extra 256x256 GEMM variants to time (0=256b, 2=256p+nt stores)")
     a = ap.parse_args()
@@ -75,6 +77,23 @@ def main():
     cases["attention"] = (lambda: ops.attention_packed(qkv, lens, a.rows, 128, 12),
                           lambda: torch.nn.functional.scaled_dot_product_attention(q4, k4, v4),
                           4 * a.rows * 12 * 128 * 128 * 64)
+    if any(k.startswith("attn_flash") for k in a.only.split(",")):
+        # summarizer encoder attention at the reference's source length (flash kernel): T5 with the
+        # relative-position bias by distance, BART without bias; library = torch SDPA (dense bias mask)
+        D_, S_ = a.docs, a.src
+        ql, kl, vl = r(D_ * S_, H), r(D_ * S_, H), r(D_ * S_, H)
+        lens_l = torch.full((D_,), S_, dtype=torch.int32, device=dev)
+        bd = r(12, 2 * S_ - 1, dtype=torch.float32)
+        from agent_tpu_amd.ops.attention import dist_to_dense
+
+        dense = dist_to_dense(bd, S_, S_).unsqueeze(0).bfloat16()
+        qs, ks, vs = (t.view(D_, S_, 12, 64).transpose(1, 2) for t in (ql, kl, vl))
+        fl_l = 4 * D_ * 12 * S_ * S_ * 64
+        cases["attn_flash_t5"] = (lambda: ops.attention(ql, kl, vl, lens_l, D_, S_, S_, 12, scale=1.0, bias_dist=bd),
+                                  lambda: torch.nn.functional.scaled_dot_product_attention(qs, ks, vs, attn_mask=dense,
+                                                                                           scale=1.0), fl_l)
+        cases["attn_flash_bart"] = (lambda: ops.attention(ql, kl, vl, lens_l, D_, S_, S_, 12),
+                                    lambda: torch.nn.functional.scaled_dot_product_attention(qs, ks, vs), fl_l)
     gam, bet = r(H, dtype=torch.float32), r(H, dtype=torch.float32)
     cases["layernorm"] = (lambda: ops.layernorm(x768, gam, bet, 1e-12),
                           lambda: torch.nn.functional.layer_norm(x768, (H,), gam.bfloat16(), bet.bfloat16(), 1e-12),
