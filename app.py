@@ -70,7 +70,7 @@ LEASE_BATCH = os.getenv("LEASE_BATCH", "1").strip().lower() not in ("0", "false"
 # strictly serial lease -> execute -> post order.
 RESULT_POST_ASYNC = os.getenv("RESULT_POST_ASYNC", "0").strip().lower() in ("1", "true", "yes", "on")
 # lease size this agent can batch well; advertised in worker_profile.limits (MAX_TASKS stays the request)
-MAX_BATCH_TASKS = int(os.getenv("MAX_BATCH_TASKS", "256"))
+MAX_BATCH_TASKS = int(os.getenv("MAX_BATCH_TASKS", "1024"))
 FAIL_ON_NOT_OK = os.getenv("FAIL_ON_NOT_OK", "0").strip().lower() in ("1", "true", "yes")
 
 _running = True

@@ -57,7 +57,7 @@ def test_classify_lease_batch_matches_single():
     batched, lease_req = _run(jobs, "echo,map_classify", "1")
     single, _ = _run(jobs, "echo,map_classify", "0")
     assert lease_req["max_tasks"] == len(jobs)
-    assert lease_req["worker_profile"]["workers"]["max_batch_tasks"] == 256
+    assert lease_req["worker_profile"]["workers"]["max_batch_tasks"] == 1024
     assert lease_req["worker_profile"]["workers"]["batch_ops"] == ["map_classify"]
     assert lease_req["worker_profile"]["limits"] == {"max_payload_bytes": 262144, "max_tokens": 2048}
     for jid in ("a", "b", "c"):
