@@ -98,7 +98,7 @@ def start(rank: int) -> None:
     if _get_store() is None or _hb_thread is not None:
         return
     _set(f"pid/{rank}", str(os.getpid()))
-    progress("init")
+    _set(f"prog/{rank}", "0:init")
 
     def beat():
         while not _stop.wait(HB_SEC):
@@ -119,7 +119,14 @@ def next_task() -> int:
     return _seq
 
 
+def active() -> bool:
+    """True once :func:`start` ran on this rank (the agent's DP process model)."""
+    return _hb_thread is not None
+
+
 def progress(stage: str) -> None:
+    if _hb_thread is None:  # not an agent rank (bench / tests): no store traffic
+        return
     _set(f"prog/{_rank}", f"{_seq}:{stage}")
 
 
@@ -127,6 +134,9 @@ def progress(stage: str) -> None:
 def collective(stage: str):
     """Bracket a collective: progress marker, rank-0 wait clock, named failure."""
     global _in_collective
+    if _hb_thread is None:  # watchdog not running on this rank: a plain collective
+        yield
+        return
     progress(f"enter {stage}")
     if _rank == 0:
         _in_collective = (time.monotonic(), stage)
