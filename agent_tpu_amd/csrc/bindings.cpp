@@ -183,6 +183,18 @@ PYBIND11_MODULE(_atpu, m) {
       py::arg("logits"), py::arg("rows"), py::arg("V"), py::arg("beam_scores"), py::arg("eos"), py::arg("mask_eos"),
       py::arg("K"), py::arg("out_score"), py::arg("out_token"), py::arg("stream"), py::arg("bans") = 0,
       py::arg("nbmax") = 0, py::arg("seq") = 0, py::arg("seq_stride") = 0, py::arg("cur") = 0, py::arg("ngram") = 0);
+  m.def("lm_head_ws_bytes", &lm_head_ws_bytes);
+  m.def("lm_head_stages", &lm_head_stages, py::arg("set") = -1);
+  m.def(
+      "lm_head_topk",
+      [](uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t bias, float rms_eps, int M, int V, int K, int topk,
+         uintptr_t beam_scores, int eos, int mask_eos, uintptr_t bans, int nbmax, uintptr_t seq, int seq_stride,
+         int cur, int ngram, uintptr_t ws, uintptr_t out_score, uintptr_t out_token, uintptr_t stream) {
+        lm_head_topk(P<const bf16>(A), lda, P<const bf16>(W), ldw, P<const float>(bias), rms_eps, M, V, K, topk,
+                     P<const float>(beam_scores), eos, mask_eos, P<const int32_t>(bans), nbmax, P<const int32_t>(seq),
+                     seq_stride, cur, ngram, reinterpret_cast<void*>(ws), P<float>(out_score), P<int32_t>(out_token),
+                     S(stream));
+      });
 
   m.def("attention", [](uintptr_t qkv, uintptr_t lens, uintptr_t bias, uintptr_t out, int B, int Sq, int H, int D,
                         float scale, uintptr_t stream) {

@@ -113,6 +113,16 @@ void beam_topk_rows(const float* logits, int rows, int V, const float* beam_scor
                     float* out_score, int32_t* out_token, hipStream_t stream,
                     const int32_t* bans = nullptr, int nbmax = 0, const int32_t* seq = nullptr, int seq_stride = 0,
                     int cur = 0, int ngram = 0);
+// Fused LM head + beam top-k (lm_head.hip): the result of beam_topk_rows over the logits
+// (A[M,K] . W[V,K]^T) * rstd(A rows, when rms_eps > 0) + bias (when given), without the
+// fp32 logits. topk <= 8. ws: lm_head_ws_bytes(M, V) bytes, 16-B aligned (per-tile partials
+// and the per-row ban bitmap).
+size_t lm_head_ws_bytes(int M, int V);
+int lm_head_stages(int set);  // tile / ring / wave-grid config 0-5 (dev builds; release: 0); -1 reads
+void lm_head_topk(const bf16* A, int lda, const bf16* W, int ldw, const float* bias, float rms_eps, int M, int V,
+                  int K, int topk, const float* beam_scores, int eos, int mask_eos, const int32_t* bans, int nbmax,
+                  const int32_t* seq, int seq_stride, int cur, int ngram, void* ws, float* out_score,
+                  int32_t* out_token, hipStream_t stream);
 
 // ------------------------------------------------------------- attention (K4)
 // qkv: [B*S, 3*H*D] packed per token as [q(H*D) | k(H*D) | v(H*D)];

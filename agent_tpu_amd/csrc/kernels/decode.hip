@@ -26,6 +26,7 @@
 //  * beam_select: per item, the global top-2nb and the next running beams.
 #include "atpu/common.h"
 #include "atpu/kernels.h"
+#include "atpu/topk.h"
 
 #include <cfloat>
 #include <cstdlib>
@@ -369,50 +370,6 @@ constexpr int kTopkThreads = 256;
 constexpr int kTopkWaves = kTopkThreads / 64;
 constexpr int kMaxBeamK = 16;
 constexpr int kMaxBans = 512;  // banned tokens per row (beam_topk_rows); more -> the caller's exact path
-
-// (value desc, index asc) ordering
-__device__ __forceinline__ bool better(float a, int ia, float b, int ib) { return a > b || (a == b && ia < ib); }
-
-// insert (val, id) into a sorted register list; compile-time indices only
-template <int KM>
-__device__ __forceinline__ void list_insert(float (&tv)[KM], int (&ti)[KM], float val, int id) {
-#pragma unroll
-  for (int r = 0; r < KM; ++r) {
-    const bool sw = better(val, id, tv[r], ti[r]);
-    const float ov = tv[r];
-    const int oi = ti[r];
-    tv[r] = sw ? val : ov;
-    ti[r] = sw ? id : oi;
-    val = sw ? ov : val;
-    id = sw ? oi : id;
-  }
-}
-
-// K rounds of wave argmax over the lanes' list heads; results in lane r (< K)
-template <int KM>
-__device__ __forceinline__ void wave_topk(float (&tv)[KM], int (&ti)[KM], float& res_v, int& res_i) {
-  const int lane = threadIdx.x & 63;
-  res_v = -FLT_MAX;
-  res_i = 0x7fffffff;
-#pragma unroll
-  for (int r = 0; r < KM; ++r) {
-    float bv = tv[0];
-    int bi = ti[0];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const float ov = __shfl_xor(bv, off);
-      const int oi = __shfl_xor(bi, off);
-      if (better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
-    }
-    if (lane == r) { res_v = bv; res_i = bi; }
-    if (ti[0] == bi && tv[0] == bv && bi != 0x7fffffff) {  // owner pops its head
-#pragma unroll
-      for (int x = 0; x + 1 < KM; ++x) { tv[x] = tv[x + 1]; ti[x] = ti[x + 1]; }
-      tv[KM - 1] = -FLT_MAX;
-      ti[KM - 1] = 0x7fffffff;
-    }
-  }
-}
 
 template <int K, bool BANS>
 __global__ __launch_bounds__(kTopkThreads) void beam_topk_kernel(const float* __restrict__ logits, int V,

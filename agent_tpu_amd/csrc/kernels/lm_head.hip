@@ -1,0 +1,440 @@
+// Fused decode LM head + beam top-k (replaces the fp32-logit
+// GEMM + beam_topk_rows pair of decode.hip for the device-selection decode loop).
+//
+// The LM head of a beam-search step is [rows, d] x [V, d]^T (rows = docs x beams,
+// V = 32128 / 50264): 50-105 GFLOP whose output only feeds a per-row log-softmax
+// normaliser and the row's top-2nb tokens. Writing the fp32 logits (206 MB per
+// BART step) and reading them back in a separate top-k pass cost 175 + 74 us.
+// Here the logits never leave the CU:
+//
+//  lm_head_topk_kernel  one 128x128 (rows x vocab) tile per workgroup, K in full:
+//    * 4 waves, each 32 rows x 128 vocab columns (2 x 8 MFMA 16x16x32 fragments),
+//      so all 128 values of a row sit in the 4 lanes l, l^16, l^32, l^48 of ONE
+//      wave: every row reduction is two register permlane swaps, no LDS;
+//    * NST-deep LDS ring fed by LDS-DMA (counted vmcnt, one raw barrier per K-tile),
+//      M-fastest tile order under the XCD remap: the M tiles of one vocab panel
+//      run on one XCD, so each weight panel comes from HBM once;
+//    * epilogue per (row, tile): max and sum exp(x - max) over every column (the
+//      log-softmax normaliser covers banned tokens, as HF applies the processors
+//      after log_softmax), then the candidate set: values >= L, where L is the
+//      8th largest of the 16 lane-local top-4 values (v_med3 insertion, 4 VALU
+//      per value, no indices). Any 8 values >= L prove that the tile's 8 best
+//      allowed values are >= L, so the set holds the tile's exact top 8
+//      (ties at L included). It has 8.1 values on average and more than 16 with
+//      probability < 1e-5 on Gaussian logits; then (or on massive ties) the
+//      wave falls back to 8 exact argmax rounds over (value desc, index asc).
+//      Banned tokens (a per-row bitmap, built once per step by ban_bitmap_kernel
+//      from the ban list and the device token history) and the min-length EOS
+//      mask only drop values from the candidate set.
+//    Output per (row, tile): {max, sumexp, count} + up to 16 (value, token) pairs.
+//  lm_head_merge_kernel  one workgroup per row: log-sum-exp over the tiles and
+//    the exact top-K (K <= 8) of the candidates, written exactly like
+//    beam_topk_rows (score = logit - lse + beam score), so beam_select consumes
+//    it unchanged.
+//
+// Measured (tools/bench_kernels.py --only lm_bart,lm_t5, 1024 rows): BART 50264 x 1024
+// 187 us against 223 us for the logits GEMM + beam_topk_rows pair (the GEMM alone
+// 170 us: the epilogue is nearly free, hidden by the second workgroup per CU); T5
+// 32128 x 768 110 vs 135 us. The mainloop is the limit (~0.6 PF): the persistent
+// 256x256 kernel reaches 1 PF on this shape with bf16 output, but with this epilogue
+// (~12 VALU per logit, barrier-locked with the ping-pong partner) it ran 267 us, and
+// 256-row tiles / deeper rings / 2x2 wave grids here were all slower (dev builds,
+// ATPU_LM_CFG 1-5; docs/PERF_NOTES.md).
+#include "atpu/common.h"
+#include "atpu/kernels.h"
+#include "atpu/topk.h"
+
+#include <cfloat>
+#include <cstdlib>
+
+namespace atpu {
+namespace {
+
+constexpr int kBN = 128, kBK = 64;          // vocab columns per tile (= per wave), K per stage
+constexpr int kRowB = kBK * 2;                // 128-B staged row
+constexpr float kLog2e = 1.4426950408889634f;
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <bool RMS, bool BIAS, bool BANS, int BM, int NST, int WN>
+__global__ __launch_bounds__(BM / 32 * 64, (BM + kBN) * kRowB * NST <= 80 * 1024 ? 2 : 1) void lm_head_topk_kernel(
+    const bf16* __restrict__ A, int lda, const bf16* __restrict__ W, int ldw, const float* __restrict__ bias,
+    float rms_eps, int M, int V, int K, const uint32_t* __restrict__ ban_bits, int ban_ld, int eos, int mask_eos,
+    float4* __restrict__ hdr, float2* __restrict__ cand) {
+  constexpr int NW = BM / 32;                 // waves
+  constexpr int WM = NW / WN;                 // wave grid WM x WN
+  constexpr int WR = BM / WM, WC = kBN / WN;  // rows x vocab columns per wave (= one partial slab)
+  constexpr int TM = WR / 16, TN = WC / 16;
+  constexpr int kStage = (BM + kBN) * kRowB;  // ring slot: A rows 0..BM-1, vocab rows BM..
+  constexpr int kLps = (BM + kBN) / 8 / NW;   // LDS-DMA instructions per wave per slot
+  static_assert((BM + kBN) % (8 * NW) == 0 && BM % (8 * NW) == 0 && NW % WN == 0, "stage split");
+  __shared__ __attribute__((aligned(16))) char lds[NST * kStage];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int ntm = (M + BM - 1) / BM;
+  const int ntn = (V + kBN - 1) / kBN;
+  const int nslab = (V + WC - 1) / WC;
+  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
+  const int m0 = (tile % ntm) * BM;
+  const int n0 = (tile / ntm) * kBN;
+
+  // staged rows 0..BM-1: A rows m0.., BM..BM+127: vocab rows n0.. (clamped; masked in the epilogue)
+  const int srow = lane >> 3, spos = lane & 7;
+  const bf16* src[kLps];
+#pragma unroll
+  for (int i = 0; i < kLps; ++i) {
+    const int r = (i * NW + wave) * 8 + srow;  // A rows for i < BM / (8 NW) (wave-uniform)
+    src[i] = r < BM ? A + (size_t)min(m0 + r, M - 1) * lda + swz(r, spos) * 8
+                    : W + (size_t)min(n0 + r - BM, V - 1) * ldw + swz(r, spos) * 8;
+  }
+  auto stage = [&](int kt, int slot) {
+    char* base = lds + slot * kStage;
+#pragma unroll
+    for (int i = 0; i < kLps; ++i) glds16(src[i] + kt * kBK, base + (i * NW + wave) * 8 * kRowB);
+  };
+
+  const int frow = lane & 15, fchunk = lane >> 4;
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ssq[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) ssq[i] = 0.f;
+  auto compute = [&](int slot) {
+    const char* base = lds + slot * kStage;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[TM], bw[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm * WR + i * 16 + frow;
+        af[i] = *reinterpret_cast<const bf16x8*>(base + r * kRowB + swz(r, ks * 4 + fchunk) * 16);
+        if constexpr (RMS) ssq[i] = sumsq_chunk(af[i], ssq[i]);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = BM + wn * WC + j * 16 + frow;
+        bw[j] = *reinterpret_cast<const bf16x8*>(base + r * kRowB + swz(r, ks * 4 + fchunk) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af[i], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  const int nk = K / kBK;
+#pragma unroll
+  for (int t = 0; t < NST - 1; ++t)
+    if (t < nk) stage(t, t);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + NST - 1 <= nk)
+      wait_vm<(NST - 2) * kLps>();
+    else
+      wait_vm<0>();
+    // raw barrier: __syncthreads() would add a vmcnt(0) and drain the ring. Every wave's
+    // DMA for slot kt has landed; slot (kt-1) % NST is free (its reads fed retired MFMAs).
+    asm volatile("s_barrier" ::: "memory");
+    if (kt + NST - 1 < nk) stage(kt + NST - 1, (kt + NST - 1) % NST);
+    compute(kt % NST);
+  }
+
+  // ------------------------------------------------------------------ epilogue
+  // lane (frow, fchunk) holds rows wm*WR + i*16 + frow, columns c0 + j*16 + fchunk*4 + e
+  const int c0 = n0 + wn * WC;  // this wave's slab
+  if (c0 >= V) return;          // wholly past the vocabulary (wave-uniform)
+  const int slab = c0 / WC;
+  const bool tail = c0 + WC > V;
+  const bool eos_here = mask_eos && eos >= c0 && eos < c0 + WC;
+  f32x4 bv[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = c0 + j * 16 + fchunk * 4;
+    bv[j] = (BIAS && n < V) ? *reinterpret_cast<const f32x4*>(bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * WR + i * 16 + frow;
+    const bool live = m < M;
+    const float rs = RMS ? __builtin_amdgcn_rsqf(lane_rows_sum(ssq[i]) * (1.f / K) + rms_eps) : 1.f;
+    float v[TN][4];
+    float mx = -FLT_MAX;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x = acc[i][j][e];
+        if constexpr (RMS) x *= rs;
+        if constexpr (BIAS) x += bv[j][e];
+        if (tail && c0 + j * 16 + fchunk * 4 + e >= V) x = -FLT_MAX;
+        v[j][e] = x;
+        mx = fmaxf(mx, x);
+      }
+    const float rmax = lane_rows_max(mx);
+    const float mb = rmax * kLog2e;
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s += __builtin_amdgcn_exp2f(fmaf(v[j][e], kLog2e, -mb));
+    s = lane_rows_sum(s);
+
+    // selection values: banned / masked EOS / past-V columns -> -FLT_MAX
+    if constexpr (BANS) {
+      // the slab's WC / 32 bitmap words of row m (16-B rows, 8-B aligned slabs)
+      uint32_t wd[WC / 32];
+      const uint32_t* bp = ban_bits + (size_t)min(m, M - 1) * ban_ld + c0 / 32;
+      if constexpr (WC == 128) {
+        const uint4 q = *reinterpret_cast<const uint4*>(bp);
+        wd[0] = q.x, wd[1] = q.y, wd[2] = q.z, wd[3] = q.w;
+      } else {
+        const uint2 q = *reinterpret_cast<const uint2*>(bp);
+        wd[0] = q.x, wd[1] = q.y;
+      }
+      uint32_t any = 0u;
+#pragma unroll
+      for (int w = 0; w < WC / 32; ++w) any |= wd[w];
+      if (__ballot(any != 0u)) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if ((wd[j >> 1] >> ((j & 1) * 16 + fchunk * 4 + e)) & 1u) v[j][e] = -FLT_MAX;
+      }
+    }
+    if (eos_here) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (c0 + j * 16 + fchunk * 4 + e == eos) v[j][e] = -FLT_MAX;
+    }
+    const size_t slot = (size_t)m * nslab + slab;
+    tile_row_emit<TN>(v, c0, fchunk, live, rmax, s, hdr + slot, cand + slot * kTileCand);
+  }
+}
+
+constexpr int kMergeThreads = 256;
+
+__global__ __launch_bounds__(kMergeThreads) void lm_head_merge_kernel(const float4* __restrict__ hdr,
+                                                                       const float2* __restrict__ cand, int ntn,
+                                                                       const float* __restrict__ beam_scores, int K,
+                                                                       float* __restrict__ out_score,
+                                                                       int32_t* __restrict__ out_token) {
+  constexpr int NW = kMergeThreads / 64;
+  __shared__ float wm[NW], wsum[NW];
+  __shared__ float cv[NW * kTileSel];
+  __shared__ int ci[NW * kTileSel];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float4* h = hdr + (size_t)row * ntn;
+  const float2* c = cand + (size_t)row * ntn * kTileCand;
+  float mx = -FLT_MAX, sm = 0.f;
+  float tv[kTileSel];
+  int ti[kTileSel];
+#pragma unroll
+  for (int r = 0; r < kTileSel; ++r) {
+    tv[r] = -FLT_MAX;
+    ti[r] = 0x7fffffff;
+  }
+  for (int t = tid; t < ntn; t += kMergeThreads) {
+    const float4 p = h[t];
+    if (p.x > mx) {
+      sm = sm * __expf(mx - p.x) + p.y;
+      mx = p.x;
+    } else {
+      sm += p.y * __expf(p.x - mx);
+    }
+    const int n = __float_as_int(p.z);
+    for (int q = 0; q < n; ++q) {
+      const float2 e = c[(size_t)t * kTileCand + q];
+      const int id = __float_as_int(e.y);
+      if (better(e.x, id, tv[kTileSel - 1], ti[kTileSel - 1])) list_insert<kTileSel>(tv, ti, e.x, id);
+    }
+  }
+  const float gm0 = wave_max(mx);
+  float sa = (mx == -FLT_MAX) ? 0.f : sm * __expf(mx - gm0);
+  sa = wave_sum(sa);
+  float rv;
+  int ri;
+  wave_topk<kTileSel>(tv, ti, rv, ri);
+  if (lane == 0) {
+    wm[w] = gm0;
+    wsum[w] = sa;
+  }
+  if (lane < kTileSel) {
+    cv[w * kTileSel + lane] = rv;
+    ci[w * kTileSel + lane] = ri;
+  }
+  __syncthreads();
+  if (w == 0) {
+    float gm = -FLT_MAX;
+#pragma unroll
+    for (int x = 0; x < NW; ++x) gm = fmaxf(gm, wm[x]);
+    float gs = 0.f;
+#pragma unroll
+    for (int x = 0; x < NW; ++x) gs += wsum[x] * __expf(wm[x] - gm);
+    const float shift = beam_scores[row] - gm - __logf(gs);
+#pragma unroll
+    for (int r = 0; r < kTileSel; ++r) {
+      tv[r] = -FLT_MAX;
+      ti[r] = 0x7fffffff;
+    }
+    if (lane < NW * kTileSel) list_insert<kTileSel>(tv, ti, cv[lane], ci[lane]);
+    wave_topk<kTileSel>(tv, ti, rv, ri);
+    if (lane < K) {
+      out_score[(size_t)row * K + lane] = rv == -FLT_MAX ? -FLT_MAX : rv + shift;
+      out_token[(size_t)row * K + lane] = ri;
+    }
+  }
+}
+
+// Per-row ban bitmap (bit t of row r set = token t banned): the explicit ban list
+// (-1 padded) and/or the no-repeat-n-gram bans of the device token history, built
+// in LDS and written out whole (rows of ban_ld words, zero past V).
+__global__ __launch_bounds__(256) void ban_bitmap_kernel(int V, int ban_ld, const int32_t* __restrict__ bans,
+                                                         int nbmax, const int32_t* __restrict__ seq, int seq_stride,
+                                                         int cur, int ngram, uint32_t* __restrict__ bits) {
+  extern __shared__ uint32_t bb[];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  for (int w = tid; w < ban_ld; w += 256) bb[w] = 0u;
+  __syncthreads();
+  for (int b = tid; b < nbmax; b += 256) {
+    const int t = bans[(size_t)row * nbmax + b];
+    if (t >= 0 && t < V) atomicOr(&bb[t >> 5], 1u << (t & 31));
+  }
+  if (ngram > 0 && cur >= ngram) {
+    const int32_t* sr = seq + (size_t)row * seq_stride;
+    for (int i = tid; i + ngram <= cur; i += 256) {
+      bool eq = true;
+      for (int e = 0; e + 1 < ngram; ++e) eq = eq && sr[i + e] == sr[cur - ngram + 1 + e];
+      const int t = sr[i + ngram - 1];
+      if (eq && t >= 0 && t < V) atomicOr(&bb[t >> 5], 1u << (t & 31));
+    }
+  }
+  __syncthreads();
+  uint4* dst = reinterpret_cast<uint4*>(bits + (size_t)row * ban_ld);
+  for (int w = tid; w < ban_ld / 4; w += 256) dst[w] = uint4{bb[4 * w], bb[4 * w + 1], bb[4 * w + 2], bb[4 * w + 3]};
+}
+
+int ban_ld_words(int V) { return ((V + 31) / 32 + 3) & ~3; }  // 16-B rows
+
+}  // namespace
+
+int lm_head_stages(int set) {
+  // fused LM head tile / LDS ring / wave grid (rows x vocab per workgroup). Release builds
+  // run config 0; dev builds (python -m agent_tpu_amd.csrc.build --dev) also the measured
+  // alternatives (ATPU_LM_CFG, tools/bench_kernels.py --only lm_bart,lm_t5; docs/PERF_NOTES.md):
+  //   0: 128x128, 2 slots (64 KiB, two workgroups per CU), 4 waves of 32 rows x 128 columns
+  //   1: 128x128, 4 slots (128 KiB)   2: 256x128, 2 slots (96 KiB)   3: 256x128, 3 slots (144 KiB)
+  //   4: as 0 with 2x2 waves of 64 x 64 (fewer LDS fragment reads per MFMA; 64-column slabs)
+  //   5: as 2 with 4x2 waves of 64 x 64
+#ifdef ATPU_DEV_BUILD
+  static int v = [] {
+    const char* f = std::getenv("ATPU_LM_CFG");
+    return (f && f[0] >= '0' && f[0] <= '5') ? f[0] - '0' : 0;
+  }();
+  if (set >= 0 && set <= 5) v = set;
+  return v;
+#else
+  (void)set;
+  return 0;
+#endif
+}
+
+// workspace: per-slab headers and candidates (slabs of 64 columns at the finest), the ban bitmap
+size_t lm_head_ws_bytes(int M, int V) {
+  const size_t slabs = (size_t)M * ((V + 63) / 64);
+  return slabs * sizeof(float4) + slabs * kTileCand * sizeof(float2) + (size_t)M * ban_ld_words(V) * 4;
+}
+
+void lm_head_topk(const bf16* A, int lda, const bf16* W, int ldw, const float* bias, float rms_eps, int M, int V,
+                  int K, int topk, const float* beam_scores, int eos, int mask_eos, const int32_t* bans, int nbmax,
+                  const int32_t* seq, int seq_stride, int cur, int ngram, void* ws, float* out_score,
+                  int32_t* out_token, hipStream_t stream) {
+  ATPU_CHECK(M > 0 && V > 0 && K > 0 && K % kBK == 0, "lm_head_topk: K must be a positive multiple of 64");
+  ATPU_CHECK(V % 4 == 0, "lm_head_topk: V must be a multiple of 4");
+  ATPU_CHECK(topk >= 1 && topk <= kTileSel && topk <= V, "lm_head_topk: 1 <= k <= 8");
+  ATPU_CHECK(lda % 8 == 0 && ldw % 8 == 0 && lda >= K && ldw >= K, "lm_head_topk: 16-B rows of at least K");
+  ATPU_CHECK((reinterpret_cast<uintptr_t>(A) & 15) == 0 && (reinterpret_cast<uintptr_t>(W) & 15) == 0 &&
+                 (reinterpret_cast<uintptr_t>(bias) & 15) == 0 && (reinterpret_cast<uintptr_t>(ws) & 15) == 0,
+             "lm_head_topk: A, W, bias and the workspace must be 16-byte aligned");
+  ATPU_CHECK(ws && beam_scores && out_score && out_token, "lm_head_topk: null buffer");
+  ATPU_CHECK(nbmax >= 0 && (nbmax == 0 || bans), "lm_head_topk: ban list");
+  ATPU_CHECK(ngram <= 0 || (seq && cur <= seq_stride), "lm_head_topk: n-gram bans need the token history [rows, >= cur]");
+  const int cfg = lm_head_stages(-1);
+  const int wc = (cfg >= 4) ? 64 : 128;  // vocabulary columns per partial slab (the wave's columns)
+  const int nslab = (V + wc - 1) / wc;
+  const int ntn = (V + kBN - 1) / kBN;
+  ATPU_CHECK((long long)((M + 127) / 128) * ntn < (1ll << 31), "lm_head_topk: grid too large");
+  if (ngram > 0 && cur < ngram) ngram = 0;
+  const bool any_bans = nbmax > 0 || ngram > 0;
+  const int ld = ban_ld_words(V);
+  const size_t slabs = (size_t)M * ((V + 63) / 64);
+  float4* hdr = reinterpret_cast<float4*>(ws);
+  float2* cand = reinterpret_cast<float2*>(hdr + slabs);
+  uint32_t* bits = reinterpret_cast<uint32_t*>(cand + slabs * kTileCand);
+  if (any_bans) {
+    ATPU_CHECK((size_t)ld * 4 <= 64 * 1024, "lm_head_topk: vocabulary too large for the ban bitmap");
+    hipLaunchKernelGGL(ban_bitmap_kernel, dim3(M), dim3(256), (size_t)ld * 4, stream, V, ld, bans, nbmax, seq,
+                       seq_stride, cur, ngram, bits);
+  }
+  const bool rms = rms_eps > 0.f, has_bias = bias != nullptr;
+  ATPU_CHECK(!(rms && has_bias), "lm_head_topk: RMSNorm folding and a bias together are not instantiated");
+#define ATPU_LM(R, B, X, BM, N, WN)                                                                              \
+  hipLaunchKernelGGL((lm_head_topk_kernel<R, B, X, BM, N, WN>), dim3(((M + BM - 1) / BM) * ntn), dim3(BM / 32 * 64), \
+                     0, stream, A, lda, W, ldw, bias, rms_eps, M, V, K, bits, ld, eos, mask_eos, hdr, cand)
+#ifdef ATPU_DEV_BUILD
+#define ATPU_LM_CFG(R, B, X)          \
+  switch (cfg) {                      \
+    case 1:                           \
+      ATPU_LM(R, B, X, 128, 4, 1);    \
+      break;                          \
+    case 2:                           \
+      ATPU_LM(R, B, X, 256, 2, 1);    \
+      break;                          \
+    case 3:                           \
+      ATPU_LM(R, B, X, 256, 3, 1);    \
+      break;                          \
+    case 4:                           \
+      ATPU_LM(R, B, X, 128, 2, 2);    \
+      break;                          \
+    case 5:                           \
+      ATPU_LM(R, B, X, 256, 2, 2);    \
+      break;                          \
+    default:                          \
+      ATPU_LM(R, B, X, 128, 2, 1);    \
+  }
+#else
+#define ATPU_LM_CFG(R, B, X) ATPU_LM(R, B, X, 128, 2, 1);
+#endif
+#define ATPU_LM_BANS(R, B)    \
+  if (any_bans) {             \
+    ATPU_LM_CFG(R, B, true)   \
+  } else {                    \
+    ATPU_LM_CFG(R, B, false)  \
+  }
+  if (rms) {
+    ATPU_LM_BANS(true, false)
+  } else if (has_bias) {
+    ATPU_LM_BANS(false, true)
+  } else {
+    ATPU_LM_BANS(false, false)
+  }
+#undef ATPU_LM_BANS
+#undef ATPU_LM_CFG
+#undef ATPU_LM
+  hipLaunchKernelGGL(lm_head_merge_kernel, dim3(M), dim3(kMergeThreads), 0, stream, hdr, cand, nslab, beam_scores,
+                     topk, out_score, out_token);
+  ATPU_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace atpu

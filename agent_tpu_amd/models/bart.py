@@ -254,7 +254,7 @@ class BartModel:
         return torch.zeros((self.cfg.dec_layers, rows * T, 2 * self.cfg.d_model), dtype=dt, device=self.device)
 
     def step(self, tokens: torch.Tensor, step: torch.Tensor, cache: torch.Tensor, T: int, ckv: torch.Tensor,
-             src_lens: torch.Tensor, S: int, group: int, hist: Optional[torch.Tensor] = None) -> torch.Tensor:
+             src_lens: torch.Tensor, S: int, group: int, hist: Optional[torch.Tensor] = None, logits: bool = True):
         """One decoder position for ``rows`` sequences -> fp32 logits [rows, V] (see T5Model.step)."""
         cfg, p = self.cfg, self.p
         d, H = cfg.d_model, cfg.heads
@@ -264,7 +264,7 @@ class BartModel:
         x = ops.layernorm(x, p["dec.ln_emb_g"], p["dec.ln_emb_b"], cfg.eps,
                           residual=pos.expand(x.shape[0], d).contiguous())
         if self.ln_fold:
-            return self._step_folded(x, step, cache, T, ckv, src_lens, S, group, hist)
+            return self._step_folded(x, step, cache, T, ckv, src_lens, S, group, hist, logits)
         for i in range(cfg.dec_layers):
             q = f"dec.l{i}."
             c = cache[i]
@@ -285,9 +285,9 @@ class BartModel:
             f = ops.linear(x, p[q + "f1_w"], p[q + "f1_b"], act="gelu")
             x = ops.layernorm(ops.linear(f, p[q + "f2_w"], p[q + "f2_b"], residual=x), p[q + "ln2_g"],
                               p[q + "ln2_b"], cfg.eps)
-        return ops.linear(x, p["shared"], p["final_logits_bias"], out_f32=True)
+        return ops.lm_head(x, p["shared"], p["final_logits_bias"], 0.0, logits)
 
-    def _step_folded(self, x, step, cache, T, ckv, src_lens, S, group, hist) -> torch.Tensor:
+    def _step_folded(self, x, step, cache, T, ckv, src_lens, S, group, hist, logits=True):
         """:meth:`step` with the decoder LayerNorms folded into the GEMMs (only the last one
         runs as a pass). The GEMM producing a pre-LN row writes its partial (sum, sumsq) per
         32-column slab; the GEMM reading LN(x) as input and the one adding LN(x) as its
@@ -325,4 +325,4 @@ class BartModel:
             x = ops.linear(h, p[q + "f2_w"], f[q + "f2_b"], residual=x2, res_ln=(eps, p2, p[q + "lnc_g"]),
                            stats_out=px)
         x = ops.layernorm(x, p[f"dec.l{L - 1}.ln2_g"], p[f"dec.l{L - 1}.ln2_b"], eps)
-        return ops.linear(x, p["shared"], p["final_logits_bias"], out_f32=True)
+        return ops.lm_head(x, p["shared"], p["final_logits_bias"], 0.0, logits)

@@ -280,8 +280,9 @@ class T5Model:
         return torch.zeros((self.cfg.dec_layers, rows * T, 2 * self.cfg.d_model), dtype=dt, device=self.device)
 
     def step(self, tokens: torch.Tensor, step: torch.Tensor, cache: torch.Tensor, T: int, ckv: torch.Tensor,
-             src_lens: torch.Tensor, S: int, group: int, hist: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """One decoder position for ``rows`` sequences -> fp32 logits [rows, V].
+             src_lens: torch.Tensor, S: int, group: int, hist: Optional[torch.Tensor] = None, logits: bool = True):
+        """One decoder position for ``rows`` sequences -> fp32 logits [rows, V]
+        (``logits=False``: the :class:`ops.LmHead` input for the fused LM head + top-k).
 
         ``step`` is a 1-element int32 device tensor (position of ``tokens``);
         cache rows of sequence r are r*T .. r*T+T-1; encoder rows of batch item
@@ -296,7 +297,7 @@ class T5Model:
         if x.dtype != p["dec.l0.qkv"].dtype:
             x = x.to(p["dec.l0.qkv"].dtype)
         if self.rms_fold:
-            return self._step_folded(x, step, cache, T, ckv, src_lens, S, group, hist, dbias)
+            return self._step_folded(x, step, cache, T, ckv, src_lens, S, group, hist, dbias, logits)
         for i in range(cfg.dec_layers):
             q = f"dec.l{i}."
             c = cache[i]
@@ -314,9 +315,9 @@ class T5Model:
             f = ops.linear(y, p[q + "wi"], act="relu")
             x = ops.linear(f, p[q + "wo"], residual=x)
         y = ops.rmsnorm(x, p["dec.ln_f"], cfg.eps)
-        return ops.linear(y, p["lm"], out_f32=True)
+        return ops.lm_head(y, p["lm"], None, 0.0, logits)
 
-    def _step_folded(self, x, step, cache, T, ckv, src_lens, S, group, hist, dbias) -> torch.Tensor:
+    def _step_folded(self, x, step, cache, T, ckv, src_lens, S, group, hist, dbias, logits=True):
         """:meth:`step` with each RMSNorm folded into its consumer GEMM (37 fewer launches
         per step, no normalised copy of x); logits equal the unfolded step to bf16 rounding."""
         cfg, p, f = self.cfg, self.p, self.rms_folded()
@@ -338,4 +339,4 @@ class T5Model:
             x = ops.linear(ctx, p[q + "co"], residual=x)
             h = ops.linear(x, f[q + "wi"], act="relu", rms_eps=eps)
             x = ops.linear(h, p[q + "wo"], residual=x)
-        return ops.linear(x, f["lm"], out_f32=True, rms_eps=eps)
+        return ops.lm_head(x, f["lm"], None, eps, logits)

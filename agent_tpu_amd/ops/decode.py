@@ -9,11 +9,13 @@
 * :func:`beam_reorder_hist` — beam reorder of the backpointer table.
 * :func:`gather_rows` — explicit beam reorder of cache slabs.
 * :func:`beam_topk_rows` — log-softmax + beam score (+ EOS mask) + top-k per row.
+* :func:`lm_head_topk` — the LM-head GEMM fused with :func:`beam_topk_rows`
+  (``csrc/kernels/lm_head.hip``): no fp32 logits in HBM.
 """
 from __future__ import annotations
 
 import math
-from typing import Optional, Tuple
+from typing import NamedTuple, Optional, Tuple
 
 import numpy as np
 
@@ -190,6 +192,87 @@ def beam_topk_rows(logits: torch.Tensor, beam_scores: torch.Tensor, k: int, eos:
         seq_p, seq_stride, cur, n = ptr(seq), int(seq.shape[1]), int(cur), int(n)
     native().beam_topk_rows(ptr(logits), R, V, ptr(beam_scores), int(eos), int(mask_eos), int(k), ptr(sc), ptr(idx),
                             launch_stream(logits), ptr(bans) if nbmax else 0, nbmax, seq_p, seq_stride, cur, n)
+    return sc, idx
+
+
+LM_HEAD_MAX_K = 8  # lm_head.hip / topk.h kTileSel
+
+
+class LmHead(NamedTuple):
+    """A decoder step's LM-head input (``model.step(..., logits=False)``): the rows ``x``,
+    the vocabulary weights ``w`` [V, d], the logit bias and the folded RMSNorm eps."""
+    x: torch.Tensor
+    w: torch.Tensor
+    bias: Optional[torch.Tensor]
+    rms_eps: float
+
+    def logits(self) -> torch.Tensor:
+        from .linear import linear
+
+        if self.rms_eps > 0:
+            return linear(self.x, self.w, self.bias, out_f32=True, rms_eps=self.rms_eps)
+        return linear(self.x, self.w, self.bias, out_f32=True)
+
+    def topk(self, beam_scores: torch.Tensor, k: int, eos: int, mask_eos: bool,
+             ngram: Optional[Tuple[torch.Tensor, int, int]] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        return lm_head_topk(self.x, self.w, beam_scores, k, eos, mask_eos, bias=self.bias, rms_eps=self.rms_eps,
+                            ngram=ngram)
+
+
+def lm_head(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], rms_eps: float, logits: bool):
+    """End of a decoder step: fp32 logits, or the :class:`LmHead` for :func:`lm_head_topk`."""
+    head = LmHead(x, w, bias, float(rms_eps))
+    return head.logits() if logits else head
+
+
+def lm_head_topk(x: torch.Tensor, w: torch.Tensor, beam_scores: torch.Tensor, k: int, eos: int, mask_eos: bool,
+                 bias: Optional[torch.Tensor] = None, rms_eps: float = 0.0, bans: Optional[torch.Tensor] = None,
+                 ngram: Optional[Tuple[torch.Tensor, int, int]] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Fused decode LM head + beam top-k (``csrc/kernels/lm_head.hip``, K10).
+
+    The result of :func:`beam_topk_rows` over ``logits = (x @ w.T) * rstd(x) + bias``
+    (``rstd`` = RMSNorm of the rows of ``x`` when ``rms_eps > 0``, its gamma folded
+    into ``w``), computed without writing the fp32 logits: the GEMM's epilogue
+    reduces every 128-token tile of a row to its log-softmax partials and exact
+    top-8 candidates, a merge kernel finishes each row. ``k <= 8``."""
+    R, Kd = x.shape
+    V = int(w.shape[0])
+    if not x.is_cuda:
+        xf = x.float()
+        if rms_eps > 0:
+            xf = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + rms_eps)
+        logits = xf @ w.float().t()
+        if bias is not None:
+            logits = logits + bias.float().view(1, -1)
+        return beam_topk_rows(logits, beam_scores, k, eos, mask_eos, bans=bans, ngram=ngram)
+    check_bf16_dev(x, "x")
+    check_bf16_dev(w, "w")
+    same_device(x, w, beam_scores)
+    check(1 <= k <= LM_HEAD_MAX_K, f"lm_head_topk: 1 <= k <= {LM_HEAD_MAX_K}")
+    check(w.shape[1] == Kd and x.stride(1) == 1 and w.stride(1) == 1, "lm_head_topk: x [R, d], w [V, d], unit column stride")
+    check(not (bias is not None and rms_eps > 0), "lm_head_topk: bias and RMSNorm folding together are not supported")
+    if bias is not None:
+        check(bias.dtype == torch.float32 and bias.is_contiguous() and bias.numel() == V and bias.device == x.device,
+              "lm_head_topk: bias must be contiguous fp32 [V] on the device")
+    check(beam_scores.dtype == torch.float32 and beam_scores.is_contiguous() and beam_scores.numel() == R,
+          "lm_head_topk: beam_scores must be contiguous fp32 [R]")
+    nbmax = 0 if bans is None else int(bans.shape[1])
+    if nbmax:
+        check(bans.dtype == torch.int32 and bans.is_contiguous() and bans.shape[0] == R and bans.device == x.device,
+              "bans must be contiguous int32 [R, n] on the device")
+    seq_p, seq_stride, cur, n = 0, 0, 0, 0
+    if ngram is not None:
+        seq, cur, n = ngram
+        check(seq.dtype == torch.int32 and seq.is_contiguous() and seq.shape[0] == R and seq.device == x.device
+              and 0 <= int(cur) <= seq.shape[1], "ngram: token history must be contiguous int32 [R, >= cur] on device")
+        seq_p, seq_stride, cur, n = ptr(seq), int(seq.shape[1]), int(cur), int(n)
+    nat = native()
+    ws = torch.empty(int(nat.lm_head_ws_bytes(R, V)), dtype=torch.uint8, device=x.device)
+    sc = torch.empty((R, k), dtype=torch.float32, device=x.device)
+    idx = torch.empty((R, k), dtype=torch.int32, device=x.device)
+    nat.lm_head_topk(ptr(x), row_stride(x, "x"), ptr(w), row_stride(w, "w"), ptr(bias), float(rms_eps), R, V, Kd,
+                     int(k), ptr(beam_scores), int(eos), int(bool(mask_eos)), ptr(bans) if nbmax else 0, nbmax, seq_p,
+                     seq_stride, cur, n, ptr(ws), ptr(sc), ptr(idx), launch_stream(x))
     return sc, idx
 
 

@@ -22,7 +22,9 @@ min_length=30, early_stopping=True)`` (``/root/reference/ops/map_summarize.py:53
   gets log-prob 0), ``length_penalty`` 2.0.
 
 Device work per step: the decoder step (L layers of GEMMs, KV-cache appends,
-single-query attention), the LM-head GEMM and K10. Host work: bookkeeping on
+single-query attention), then the LM head fused with K10 (``ops.lm_head_topk``: per
+128-token tile log-softmax partials and exact top-8 candidates in the GEMM epilogue,
+no fp32 logits) or, on the host-selection path, the LM-head GEMM and K10. Host work: bookkeeping on
 ``[B, 2*num_beams]`` tensors. Beam reorder never copies the KV cache: each
 row's history is a backpointer table ``hist[row, pos]`` (physical cache row of
 position ``pos``) and only that int table is gathered by parent beam (K11).
@@ -44,6 +46,9 @@ from ..utils.trace import span
 NEG = -1.0e9
 # host-side step timing (tools/host_prof_summ.py): a dict to accumulate into, or None
 HOST_PROF: Optional[Dict[str, float]] = None
+# device selection runs the fused LM head + top-k (ops.lm_head_topk, csrc/kernels/lm_head.hip)
+# instead of the fp32-logit GEMM + beam_topk_rows pair; ATPU_LM_FUSED=0 restores the pair
+LM_FUSED = os.getenv("ATPU_LM_FUSED", "1").strip().lower() not in ("0", "false", "no")
 
 
 @dataclass
@@ -248,6 +253,9 @@ def _generate_iter(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
     # captured once and replayed: the host loop issues 1 launch per step.
     use_graph = gen.use_graph and dev.type == "cuda"
     graph, g_logits = None, None
+    # device selection with the fused LM head (lm_head.hip): the step ends at the LM-head
+    # input and lm_head_topk produces the per-row top-K2 without fp32 logits
+    fused = pin and gen.device_select and K2 <= ops.LM_HEAD_MAX_K and LM_FUSED
     seq_dev = seq_alt = None  # device token history (device selection with n-gram bans)
 
     def advance() -> torch.Tensor:
@@ -260,7 +268,7 @@ def _generate_iter(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
             seq_dev.copy_(seq_alt)
         tokens.copy_(tok_dev)
         step_dev.add_(1)
-        return model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist)
+        return model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist, logits=not fused)
 
     def launch_next() -> torch.Tensor:
         nonlocal graph, g_logits
@@ -325,7 +333,7 @@ def _generate_iter(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
     cur = 1  # sequence length so far (decoder start token included)
     steps = 0
     step_dev.fill_(0)
-    logits = model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist)
+    logits = model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist, logits=not fused)
     if pin and gen.device_select:
         yield  # let other runs start their encoders / first steps
         on_stream()
@@ -356,6 +364,8 @@ def _generate_iter(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
                 sc[:, 0] = score_dev
                 return sc, forced_tk[forced]
             ngram = (seq_dev, cur, gen.no_repeat_ngram_size) if seq_dev is not None else None
+            if fused:  # logits is the step's ops.LmHead
+                return logits.topk(score_dev, K2, cfg.eos_id, cur < gen.min_length, ngram=ngram)
             return ops.beam_topk_rows(logits, score_dev, K2, cfg.eos_id, cur < gen.min_length, ngram=ngram)
 
         def record(slot: int):

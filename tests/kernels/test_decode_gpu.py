@@ -192,6 +192,92 @@ def test_beam_topk_rows_bans(gpu, V, k, nb):
         assert not set(idx[r].tolist()) & set(b for b in bans[r].tolist() if b >= 0)
 
 
+def _lm_case(R, V, d, rms, bias, gpu, seed, scale=1.0):
+    x = _r((R, d), gpu, 1.0, seed=seed)
+    w = _r((V, d), gpu, scale / d ** 0.5, seed=seed + 1)
+    b = _r((V,), gpu, 0.5, torch.float32, seed=seed + 2) if bias else None
+    bs = _r((R,), gpu, 1.0, torch.float32, seed=seed + 3)
+    return ops.LmHead(x, w, b, 1e-6 if rms else 0.0), bs
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5])  # release builds run 0 whatever is set
+@pytest.mark.parametrize("R,V,d,rms,bias,k,mask", [(12, 32128, 768, True, False, 8, True), (300, 50264, 1024, False, True, 8, False),
+                                                   (4, 1000, 64, False, False, 2, True), (1024, 32128, 768, True, False, 8, False),
+                                                   (130, 4100, 128, False, True, 5, True), (512, 50264, 1024, False, True, 8, True),
+                                                   (256, 1000, 128, True, False, 8, False)])
+def test_lm_head_topk_matches_logits_path(gpu, cfg, R, V, d, rms, bias, k, mask):
+    # fused LM head + top-k == fp32-logit GEMM + beam_topk_rows: the same MFMA accumulation
+    # order gives bit-identical logits, so the tokens match exactly; the normaliser is summed
+    # in another order (scores to ~1e-6)
+    nat = __import__("agent_tpu_amd._native", fromlist=["native"]).native()
+    prev = nat.lm_head_stages(-1)
+    nat.lm_head_stages(cfg)
+    try:
+        head, bs = _lm_case(R, V, d, rms, bias, gpu, seed=R + V)
+        sc, idx = head.topk(bs, k, eos=1, mask_eos=mask)
+        rsc, ridx = ops.beam_topk_rows(head.logits(), bs, k, eos=1, mask_eos=mask)
+    finally:
+        nat.lm_head_stages(prev)
+    assert torch.equal(idx.cpu(), ridx.cpu())
+    torch.testing.assert_close(sc.cpu(), rsc.cpu(), atol=1e-4, rtol=1e-5)
+    if mask:
+        assert not (idx == 1).any()
+
+
+def test_lm_head_topk_matches_cpu(gpu):
+    head, bs = _lm_case(8, 2000, 256, False, True, gpu, seed=5)
+    sc, idx = head.topk(bs, 8, eos=1, mask_eos=True)
+    cpu = ops.LmHead(head.x.cpu(), head.w.cpu(), head.bias.cpu(), 0.0)
+    rsc, ridx = cpu.topk(bs.cpu(), 8, eos=1, mask_eos=True)
+    assert torch.equal(idx.cpu(), ridx)
+    torch.testing.assert_close(sc.cpu(), rsc, atol=1e-3, rtol=1e-4)
+
+
+@pytest.mark.parametrize("V,k,R", [(32128, 8, 20), (1000, 3, 20), (32128, 8, 256), (1000, 8, 512)])
+def test_lm_head_topk_ties_take_the_exact_path(gpu, V, k, R):
+    # identical vocabulary rows: every logit of a row ties, every tile overflows its 16
+    # candidate slots and falls back to the exact argmax rounds -> lowest token ids first
+    # (R % 256 == 0: the persistent 256x256 path)
+    d = 128
+    x = _r((R, d), gpu, 1.0, seed=3)
+    w = _r((1, d), gpu, 0.1, seed=4).expand(V, d).contiguous()
+    w[V // 2:V // 2 + 3] *= 2  # a few distinct values inside the ties
+    bs = _r((R,), gpu, 1.0, torch.float32, seed=5)
+    head = ops.LmHead(x, w, None, 0.0)
+    sc, idx = head.topk(bs, k, eos=1, mask_eos=True)
+    rsc, ridx = ops.beam_topk_rows(head.logits(), bs, k, eos=1, mask_eos=True)
+    assert torch.equal(idx.cpu(), ridx.cpu())
+    torch.testing.assert_close(sc.cpu(), rsc.cpu(), atol=1e-4, rtol=1e-5)
+
+
+@pytest.mark.parametrize("n,cur,R", [(3, 40, 12), (3, 2, 12), (2, 17, 12), (3, 40, 256)])
+def test_lm_head_topk_device_ngram(gpu, n, cur, R):
+    V, d, T = 4096, 128, 70
+    head, bs = _lm_case(R, V, d, False, True, gpu, seed=60)
+    g = torch.Generator().manual_seed(61)
+    seq = torch.randint(0, 6, (R, T), generator=g, dtype=torch.int32).to(gpu)
+    head.bias[:6] += 20.0  # the banned candidates are the best raw ones
+    sc, idx = head.topk(bs, 8, eos=1, mask_eos=False, ngram=(seq, cur, n))
+    rsc, ridx = ops.beam_topk_rows(head.logits(), bs, 8, eos=1, mask_eos=False, ngram=(seq, cur, n))
+    assert torch.equal(idx.cpu(), ridx.cpu())
+    torch.testing.assert_close(sc.cpu(), rsc.cpu(), atol=1e-4, rtol=1e-5)
+
+
+@pytest.mark.parametrize("R", [16, 256])
+def test_lm_head_topk_ban_list(gpu, R):
+    V, d, nb = 50264, 256, 12
+    head, bs = _lm_case(R, V, d, False, True, gpu, seed=70)
+    logits = head.logits()
+    g = torch.Generator().manual_seed(71)
+    bans = torch.randint(0, V, (R, nb), generator=g, dtype=torch.int32)
+    bans[:, :4] = torch.topk(logits.cpu(), 4, dim=-1).indices.to(torch.int32)
+    bans[::3, -1] = -1
+    sc, idx = ops.lm_head_topk(head.x, head.w, bs, 8, 1, True, bias=head.bias, bans=bans.to(gpu))
+    rsc, ridx = ops.beam_topk_rows(logits, bs, 8, eos=1, mask_eos=True, bans=bans.to(gpu))
+    assert torch.equal(idx.cpu(), ridx.cpu())
+    torch.testing.assert_close(sc.cpu(), rsc.cpu(), atol=1e-4, rtol=1e-5)
+
+
 @pytest.mark.parametrize("M,N,K,act,res,bias", [(256, 768, 3072, None, True, False), (256, 3072, 768, "relu", False, False),
                                                 (256, 2304, 768, None, False, True), (96, 768, 768, "gelu", False, True),
                                                 (512, 768, 768, None, True, False)])
@@ -540,7 +626,27 @@ def test_generate_device_select_matches_host(gpu, family):
         a = generate(model, ids.to(gpu), lens.to(gpu), GenConfig(num_beams=nbm, max_length=ml, min_length=mn))
         b = generate(model, ids.to(gpu), lens.to(gpu),
                      GenConfig(num_beams=nbm, max_length=ml, min_length=mn, device_select=False))
-        assert a.sequences == b.sequences and a.scores == b.scores and a.steps == b.steps, (ml, nbm)
+        # device selection runs the fused LM head: same tokens, the log-softmax normaliser
+        # summed in another order (scores to float rounding)
+        assert a.sequences == b.sequences and a.steps == b.steps, (ml, nbm)
+        np.testing.assert_allclose(a.scores, b.scores, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("family", ["t5-tiny", "bart-tiny"])
+def test_generate_device_select_unfused_is_exact(gpu, family, monkeypatch):
+    # ATPU_LM_FUSED=0: the device loop consumes the same logits + top-k kernels as the host loop
+    from agent_tpu_amd.runtime import summarize
+    from agent_tpu_amd.runtime.summarize import GenConfig, build_model, generate
+
+    monkeypatch.setattr(summarize, "LM_FUSED", False)
+    model, _ = build_model(family, device=gpu, seed=3)
+    g = torch.Generator().manual_seed(7)
+    ids = torch.randint(5, model.cfg.vocab_size, (5, 32), generator=g, dtype=torch.int32)
+    lens = torch.tensor([32, 20, 31, 9, 27], dtype=torch.int32)
+    gen = dict(num_beams=4, max_length=24, min_length=5)
+    a = generate(model, ids.to(gpu), lens.to(gpu), GenConfig(**gen))
+    b = generate(model, ids.to(gpu), lens.to(gpu), GenConfig(**gen, device_select=False))
+    assert a.sequences == b.sequences and a.scores == b.scores and a.steps == b.steps
 
 
 @pytest.mark.parametrize("family", ["t5-tiny", "bart-tiny"])

@@ -69,6 +69,7 @@ def main():
         "gemm_ffn2_res": (lambda: ops.linear(x3072, w2, b2, residual=res),
                           lambda: torch.addmm(b2.bfloat16(), x3072, w2.t()).add_(res), 2 * M * I * H),
     }
+    extra = {}  # per case: name -> extra timed callable
     qkv = r(M, 3 * H)
     lens = torch.full((a.rows,), 128, dtype=torch.int32, device=dev)
     q4 = qkv[:, :H].view(a.rows, 128, 12, 64).transpose(1, 2)
@@ -94,13 +95,25 @@ def main():
                                                                                            scale=1.0), fl_l)
         cases["attn_flash_bart"] = (lambda: ops.attention(ql, kl, vl, lens_l, D_, S_, S_, 12),
                                     lambda: torch.nn.functional.scaled_dot_product_attention(qs, ks, vs), fl_l)
+    if any(k.startswith("lm_") for k in a.only.split(",")):
+        # decode LM head at --docs x 4 beam rows: fused GEMM + top-k (lm_head.hip) against the
+        # fp32-logit GEMM + beam_topk_rows pair it replaces ("lib" here = that pair)
+        for name, V_, d_, rms in (("lm_bart", 50264, 1024, False), ("lm_t5", 32128, 768, True)):
+            R_ = a.docs * 4
+            head = ops.LmHead(r(R_, d_), r(V_, d_, scale=d_ ** -0.5),
+                              None if rms else r(V_, scale=0.5, dtype=torch.float32), 1e-6 if rms else 0.0)
+            bsc = torch.zeros(R_, device=dev)
+            cases[name] = (lambda h=head, b=bsc: h.topk(b, 8, 2, False),
+                           lambda h=head, b=bsc: ops.beam_topk_rows(h.logits(), b, 8, 2, False), 2 * R_ * V_ * d_)
+            extra[name] = {"gemm_only": lambda h=head: h.logits()}
     gam, bet = r(H, dtype=torch.float32), r(H, dtype=torch.float32)
     cases["layernorm"] = (lambda: ops.layernorm(x768, gam, bet, 1e-12),
                           lambda: torch.nn.functional.layer_norm(x768, (H,), gam.bfloat16(), bet.bfloat16(), 1e-12),
                           0)
     sel = [k for k in cases if not a.only or k in a.only.split(",")]
     variants = [int(v) for v in a.variants.split(",") if v]
-    times = {k: {"ours": [], "lib": [], "p16": [], **{f"v{v}": [] for v in variants}} for k in sel}
+    times = {k: {"ours": [], "lib": [], "p16": [], **{f"cfg{c}": [] for c in range(6)}, **{f"v{v}": [] for v in variants},
+                 **{e: [] for e in extra.get(k, {})}} for k in sel}
     prev_var = nat.gemm_256_variant(-1)
     for rd in range(a.rounds):
         for k in (sel if rd % 2 == 0 else list(reversed(sel))):
@@ -112,6 +125,14 @@ def main():
                     nat.gemm_256_variant(v)
                     times[k][f"v{v}"].append(timeit(ours, a.iters))
                     nat.gemm_256_variant(prev_var)
+            for e, fn in extra.get(k, {}).items():
+                times[k][e].append(timeit(fn, a.iters))
+            if k.startswith("lm_"):  # A/B: tile / LDS ring / wave-grid configs (lm_head.hip; dev build)
+                prev = nat.lm_head_stages(-1)
+                for c in range(6):
+                    nat.lm_head_stages(c)
+                    times[k][f"cfg{c}"].append(timeit(ours, a.iters))
+                nat.lm_head_stages(prev)
             if k == "attention":  # A/B: the 16-query persistent kernel (mode 1)
                 prev = nat.attention_persist_mode(-1)
                 nat.attention_persist_mode(1)
@@ -124,6 +145,9 @@ def main():
         if fl:
             out[k]["ours_tflops"] = round(fl / o / 1e9, 1)
             out[k]["lib_tflops"] = round(fl / l / 1e9, 1)
+        for e in [f"cfg{c}" for c in range(6)] + list(extra.get(k, {})):
+            if times[k][e]:
+                out[k][f"{e}_ms"] = round(statistics.median(times[k][e]), 4)
         if times[k]["p16"]:
             out[k]["p16_ms"] = round(statistics.median(times[k]["p16"]), 4)
         for v in variants:
