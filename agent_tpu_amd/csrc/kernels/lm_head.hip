@@ -231,6 +231,7 @@ __global__ __launch_bounds__(kMergeThreads) void lm_head_merge_kernel(const floa
                                                                        float* __restrict__ out_score,
                                                                        int32_t* __restrict__ out_token) {
   constexpr int NW = kMergeThreads / 64;
+  static_assert(NW * kTileSel <= 64, "wave 0 merges every wave's top kTileSel in one pass");
   __shared__ float wm[NW], wsum[NW];
   __shared__ float cv[NW * kTileSel];
   __shared__ int ci[NW * kTileSel];
@@ -245,19 +246,54 @@ __global__ __launch_bounds__(kMergeThreads) void lm_head_merge_kernel(const floa
     tv[r] = -FLT_MAX;
     ti[r] = 0x7fffffff;
   }
-  for (int t = tid; t < ntn; t += kMergeThreads) {
-    const float4 p = h[t];
-    if (p.x > mx) {
-      sm = sm * __expf(mx - p.x) + p.y;
-      mx = p.x;
-    } else {
-      sm += p.y * __expf(p.x - mx);
+  // two tiles per thread per round, every load of a round in flight at once: both headers
+  // and all 16 candidate slots of each tile (16-B loads). A per-candidate load loop
+  // serialised one memory latency per candidate (43 us per BART step).
+  const float4* c4 = reinterpret_cast<const float4*>(c);
+  for (int t0 = tid; t0 < ntn; t0 += 2 * kMergeThreads) {
+    const int t1 = t0 + kMergeThreads;
+    const float4 p0 = h[t0];
+    const float4 p1 = t1 < ntn ? h[t1] : float4{-FLT_MAX, 0.f, 0.f, 0.f};
+    const int n0 = __float_as_int(p0.z), n1 = __float_as_int(p1.z);
+    float4 e0[kTileCand / 2], e1[kTileCand / 2];
+    // slots 0-7 unconditionally (slots past the count hold stale data, masked below), 8-15
+    // in one block only when a tile has more than 8 (~9 % of tiles): a load under `2q < n`
+    // per slot became a branch with a vmcnt(0) at each join (39 us per step)
+    const size_t b0 = (size_t)t0 * (kTileCand / 2), b1 = (size_t)min(t1, ntn - 1) * (kTileCand / 2);
+#pragma unroll
+    for (int q = 0; q < kTileCand / 4; ++q) {
+      e0[q] = c4[b0 + q];
+      e1[q] = c4[b1 + q];
     }
-    const int n = __float_as_int(p.z);
-    for (int q = 0; q < n; ++q) {
-      const float2 e = c[(size_t)t * kTileCand + q];
-      const int id = __float_as_int(e.y);
-      if (better(e.x, id, tv[kTileSel - 1], ti[kTileSel - 1])) list_insert<kTileSel>(tv, ti, e.x, id);
+#pragma unroll
+    for (int q = kTileCand / 4; q < kTileCand / 2; ++q) e0[q] = e1[q] = float4{-FLT_MAX, 0.f, -FLT_MAX, 0.f};
+    if (n0 > kTileCand / 2 || n1 > kTileCand / 2) {
+#pragma unroll
+      for (int q = kTileCand / 4; q < kTileCand / 2; ++q) {
+        e0[q] = c4[b0 + q];
+        e1[q] = c4[b1 + q];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const float4 p = u ? p1 : p0;
+      if (p.x > mx) {
+        sm = sm * __expf(mx - p.x) + p.y;
+        mx = p.x;
+      } else if (p.x > -FLT_MAX) {
+        sm += p.y * __expf(p.x - mx);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kTileCand; ++q) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const float4 e = u ? e1[q / 2] : e0[q / 2];
+        const int n = u ? n1 : n0;
+        const float x = (q & 1) ? e.z : e.x;
+        const int id = __float_as_int((q & 1) ? e.w : e.y);
+        if (q < n && better(x, id, tv[kTileSel - 1], ti[kTileSel - 1])) list_insert<kTileSel>(tv, ti, x, id);
+      }
     }
   }
   const float gm0 = wave_max(mx);
