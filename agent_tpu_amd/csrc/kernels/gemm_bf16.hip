@@ -33,6 +33,10 @@
 #include <string>
 #include <type_traits>
 
+#ifndef ATPU_GEMM_SYNC_EPI
+#define ATPU_GEMM_SYNC_EPI 0
+#endif
+
 namespace atpu {
 namespace {
 
@@ -1152,6 +1156,9 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
   // base, which the DMA takes in its saddr form: 8 VGPRs instead of 16 live over
   // the whole tile loop (host: A and Bt each < 4 GiB)
   constexpr bool kFold = kIn || kRes || kSt;
+  // epilogues of the two wave groups side by side (see the end of the K loop);
+  // ATPU_GEMM_SYNC_EPI=0 builds the staggered form
+  constexpr bool kSyncEpi = ATPU_GEMM_SYNC_EPI && !(DBG & 128);
   // InNorm: statistics and colsum staged at K-tile 1 (peeled), the epilogue applies
   // rstd*acc - rstd*mu*colsum + bias (two packed FMAs per value pair). DBG & 16 (A/B
   // variant, gemm_ablate(8)): statistics staged ahead of the tile and the accumulators
@@ -1438,6 +1445,17 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
       for (int t = 0; t + 1 < nk; ++t) kstep(t, std::false_type{}, std::integral_constant<int, -2>{});
       kstep(nk - 1, std::true_type{}, std::integral_constant<int, -2>{});
     }
+    // Both wave groups run the epilogue TOGETHER: group 0 waits one barrier (group 1's
+    // last MMA phase) before it, group 1 takes one after it, so the stagger resumes at
+    // the next tile with equal barrier counts. A wave alone issues VALU at half the
+    // SIMD's rate and sits out its LDS / store latencies; two epilogues side by side
+    // fill each other's gaps, where the staggered form ran them back to back (each
+    // beside only one 16-MFMA phase of the partner).
+    if constexpr (kSyncEpi) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (wm == 0) __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if constexpr (DBG & 1) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -1458,6 +1476,10 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
       else
         epilogue_256<EPI, true, (DBG >> 1), NT>(acc, cm0, cn0, wm, wn, lane, C, ldc, bias, R, ldr, M,
                                             reinterpret_cast<const float*>(lds + kBiasOff) + tile_par * 256);
+    }
+    if constexpr (kSyncEpi) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (wm == 1) __builtin_amdgcn_s_barrier();
     }
     pm0 = cm0;
     pn0 = cn0;

@@ -229,8 +229,9 @@ class BartModel:
         return [self.cfg.bos_id] + list(toks) + [self.cfg.eos_id]
 
     # ------------------------------------------------------------- encoder
-    def encode(self, ids: torch.Tensor, lens: torch.Tensor):
-        """ids [B, S] int32, lens [B] -> (enc [B*S, d], cross K|V [B*S, L*2d])."""
+    def encode(self, ids: torch.Tensor, lens: torch.Tensor, ckv_out: Optional[torch.Tensor] = None):
+        """ids [B, S] int32, lens [B] -> (enc [B*S, d], cross K|V [B*S, L*2d]);
+        ``ckv_out``: a [B*S, L*2d] buffer the cross K|V is written into (cached decode graphs)."""
         cfg, p = self.cfg, self.p
         B, S = ids.shape
         H = cfg.heads
@@ -245,7 +246,7 @@ class BartModel:
             f = ops.linear(h1, p[q + "f1_w"], p[q + "f1_b"], act="gelu")
             h2 = ops.linear(f, p[q + "f2_w"], p[q + "f2_b"], residual=h1)
             h = ops.layernorm(h2, p[q + "ln2_g"], p[q + "ln2_b"], cfg.eps)
-        return h, ops.linear(h, p["dec.ckv_w"], p["dec.ckv_b"])
+        return h, ops.linear(h, p["dec.ckv_w"], p["dec.ckv_b"], out=ckv_out)
 
     # ------------------------------------------------------------- decoder
     def new_cache(self, rows: int, T: int) -> torch.Tensor:

@@ -251,8 +251,9 @@ class T5Model:
         return self._dec_bias
 
     # ------------------------------------------------------------- encoder
-    def encode(self, ids: torch.Tensor, lens: torch.Tensor):
-        """ids [B, S] int32 (S % 4 == 0), lens [B] -> (enc [B*S, d], cross K|V [B*S, L*2d])."""
+    def encode(self, ids: torch.Tensor, lens: torch.Tensor, ckv_out: Optional[torch.Tensor] = None):
+        """ids [B, S] int32 (S % 4 == 0), lens [B] -> (enc [B*S, d], cross K|V [B*S, L*2d]);
+        ``ckv_out``: a [B*S, L*2d] buffer the cross K|V is written into (cached decode graphs)."""
         cfg, p = self.cfg, self.p
         B, S = ids.shape
         d, H = cfg.d_model, cfg.heads
@@ -271,7 +272,7 @@ class T5Model:
             f = ops.linear(x, p[q + "wi"], act="relu")
             h = ops.linear(f, p[q + "wo"], residual=h)
         enc = ops.rmsnorm(h, p["enc.ln_f"], cfg.eps)
-        return enc, ops.linear(enc, p["dec.ckv"])
+        return enc, ops.linear(enc, p["dec.ckv"], out=ckv_out)
 
     # ------------------------------------------------------------- decoder
     def new_cache(self, rows: int, T: int) -> torch.Tensor:

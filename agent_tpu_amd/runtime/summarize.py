@@ -49,6 +49,93 @@ HOST_PROF: Optional[Dict[str, float]] = None
 # device selection runs the fused LM head + top-k (ops.lm_head_topk, csrc/kernels/lm_head.hip)
 # instead of the fp32-logit GEMM + beam_topk_rows pair; ATPU_LM_FUSED=0 restores the pair
 LM_FUSED = os.getenv("ATPU_LM_FUSED", "1").strip().lower() not in ("0", "false", "no")
+# decoder-step hipGraphs (and the buffers they were captured on) kept across calls of the
+# same shape (ATPU_SUMM_GRAPH_CACHE=1; default: capture per call); see _SlotCache
+GRAPH_CACHE = os.getenv("ATPU_SUMM_GRAPH_CACHE", "0").strip().lower() in ("1", "true", "yes")
+# source length buckets of a cached graph: ids are padded up to a multiple of this
+# (masked by src_lens in the encoder and the cross attention: the outputs do not change)
+SRC_BUCKET = 128
+
+
+class _Slot:
+    """One captured decoder step and every device buffer it reads or writes.
+
+    The graph replays on fixed addresses, so a later search of the same shape reuses the
+    buffers: the encoder writes its cross K/V into ``ckv``, the call's source lengths are
+    copied into ``lens``, the per-search state (histories, tokens, step, staging) is
+    reset. ``keep`` pins the model's lazily built tensors the graph read (a regrown
+    decoder bias must not free the memory a replay reads). ``ev``: recorded on the
+    search's stream when it releases the slot, waited for by the next user's stream."""
+
+    def __init__(self, key):
+        self.key = key
+        self.bufs: Dict[str, torch.Tensor] = {}
+        self.graph = None
+        self.out = None
+        self.keep: List[torch.Tensor] = []
+        self.busy = False
+        self.ev = None
+        self.last = 0.0
+
+    def nbytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in self.bufs.values())
+
+
+class _SlotCache:
+    """Per-model LRU of :class:`_Slot` (a model attribute: dropping the model drops them).
+
+    At most ``ATPU_SUMM_GRAPH_SLOTS`` (default 6) slots and ``ATPU_SUMM_GRAPH_CACHE_GB``
+    (default 48) GiB of buffers; an acquire that would exceed them evicts idle slots in
+    LRU order, and runs uncached if that is not enough. Capturing + instantiating a step
+    graph cost 3.1 / 5.8 ms per T5 / BART call (docs/PERF_NOTES.md)."""
+
+    def __init__(self):
+        self.slots: List[_Slot] = []
+        self.max_slots = int(os.getenv("ATPU_SUMM_GRAPH_SLOTS", "6"))
+        self.max_bytes = int(float(os.getenv("ATPU_SUMM_GRAPH_CACHE_GB", "48")) * (1 << 30))
+        self.hits = 0
+        self.misses = 0
+
+    def acquire(self, key) -> Optional[_Slot]:
+        for sl in self.slots:
+            if sl.key == key and not sl.busy and sl.graph is not None:
+                sl.busy, sl.last = True, time.perf_counter()
+                self.hits += 1
+                if sl.ev is not None:
+                    torch.cuda.current_stream().wait_event(sl.ev)
+                return sl
+        self.misses += 1
+        return None
+
+    def admit(self, sl: _Slot) -> bool:
+        """Keep a newly captured slot if it fits (evicting idle LRU slots)."""
+        need = sl.nbytes()
+        if need > self.max_bytes:
+            return False
+        idle = sorted((s for s in self.slots if not s.busy), key=lambda s: s.last)
+        while idle and (len(self.slots) >= self.max_slots or self.nbytes() + need > self.max_bytes):
+            self.slots.remove(idle.pop(0))
+        if len(self.slots) >= self.max_slots or self.nbytes() + need > self.max_bytes:
+            return False
+        sl.busy, sl.last = True, time.perf_counter()
+        self.slots.append(sl)
+        return True
+
+    def release(self, sl: _Slot) -> None:
+        ev = torch.cuda.Event()
+        ev.record()
+        sl.ev, sl.busy, sl.last = ev, False, time.perf_counter()
+
+    def nbytes(self) -> int:
+        return sum(s.nbytes() for s in self.slots)
+
+
+def slot_cache(model) -> _SlotCache:
+    sc = getattr(model, "_atpu_graph_slots", None)
+    if sc is None:
+        sc = _SlotCache()
+        model._atpu_graph_slots = sc
+    return sc
 
 
 @dataclass
@@ -191,7 +278,17 @@ def _drive(iters) -> List[GenResult]:
 
 def _generate_iter(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfig, stream=None):
     """:func:`generate` as a generator: yields where it would wait for its device step
-    (device selection only), returns the GenResult. ``stream``: the HIP stream to run on."""
+    (device selection only), returns the GenResult. ``stream``: the HIP stream to run on.
+    A cached decoder-step graph (:class:`_SlotCache`) is released when the search ends."""
+    held: List[_Slot] = []
+    try:
+        return (yield from _generate_body(model, src_ids, src_lens, gen, stream, held))
+    finally:
+        for sl in held:
+            slot_cache(model).release(sl)
+
+
+def _generate_body(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: GenConfig, stream, held: List[_Slot]):
     def on_stream():
         if stream is not None:
             torch.cuda.set_stream(stream)
@@ -206,15 +303,54 @@ def _generate_iter(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
     V = cfg.vocab_size
     T = int(gen.max_length)
     rows = B * nb
+    pin = dev.type == "cuda"
+    # Every step input is a static device buffer (tokens, step, cache, hist), so
+    # after one eager step the whole decoder step (~13 launches x L layers) is
+    # captured once and replayed: the host loop issues 1 launch per step.
+    use_graph = gen.use_graph and pin
+    # device selection with the fused LM head (lm_head.hip): the step ends at the LM-head
+    # input and lm_head_topk produces the per-row top-K2 without fp32 logits
+    fused = pin and gen.device_select and K2 <= ops.LM_HEAD_MAX_K and LM_FUSED
+    ngram_dev = pin and bool(gen.device_select) and bool(gen.no_repeat_ngram_size)
     t0 = time.perf_counter()
 
+    # graph cache: the source is padded to a length bucket (keys past src_lens are masked
+    # in the encoder and the cross attention), the buffers of a previous search of this
+    # shape are reused, and its captured step replays from the first launch
+    slot, new_slot = None, None
+    if use_graph and GRAPH_CACHE:
+        Sb = -(-S // SRC_BUCKET) * SRC_BUCKET
+        if Sb != S:
+            src_ids = torch.nn.functional.pad(src_ids, (0, Sb - S), value=int(cfg.pad_id))
+            S = Sb
+        key = (B, S, T, nb, fused, ngram_dev, bool(gen.device_select))
+        slot = slot_cache(model).acquire(key)
+        if slot is not None:
+            held.append(slot)
+            slot.bufs["lens"].copy_(src_lens)
+        else:
+            new_slot = _Slot(key)
+            new_slot.bufs["lens"] = src_lens.to(torch.int32).clone()
+        src_lens = (slot or new_slot).bufs["lens"]
+
     with span("encode"):
-        _, ckv = model.encode(src_ids, src_lens)
+        if slot is not None:
+            _, ckv = model.encode(src_ids, src_lens, ckv_out=slot.bufs["ckv"])
+        else:
+            _, ckv = model.encode(src_ids, src_lens)
     t_enc = time.perf_counter()
-    cache = model.new_cache(rows, T)
-    hist = torch.zeros((rows, T), dtype=torch.int32, device=dev)
-    hist_alt = torch.zeros_like(hist)
-    step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+    if slot is not None:
+        b = slot.bufs
+        cache, hist, hist_alt, step_dev = b["cache"], b["hist"], b["hist_alt"], b["step"]
+        hist.zero_()
+        hist_alt.zero_()
+    else:
+        cache = model.new_cache(rows, T)
+        hist = torch.zeros((rows, T), dtype=torch.int32, device=dev)
+        hist_alt = torch.zeros_like(hist)
+        step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+        if new_slot is not None:
+            new_slot.bufs.update(ckv=ckv, cache=cache, hist=hist, hist_alt=hist_alt, step=step_dev)
 
     # Host beam state lives in numpy: the per-step bookkeeping is ~40 tiny
     # array ops, ~4x cheaper than torch CPU ops, and everything that is not
@@ -236,27 +372,32 @@ def _generate_iter(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
     top_mask = np.arange(K2) < nb
     rowsB = np.arange(B)[:, None]
     neg = np.float32(NEG)
-    tokens = torch.full((rows,), cfg.decoder_start_id, dtype=torch.int32, device=dev)
-    pin = dev.type == "cuda"
     # one pinned staging row per step: [parent rows | new tokens | running beam scores]
     # -> ONE async H2D; everything after it (history reorder, token copy, step advance,
     # decoder step) is a single graph replay, and the next top-k finds the beam scores
     # already on the device (no synchronous pageable copy in front of it)
     stage_host = torch.empty(3 * rows, dtype=torch.int32, pin_memory=pin)
-    stage_dev = torch.zeros(3 * rows, dtype=torch.int32, device=dev)
+    seq_dev = seq_alt = None  # device token history (device selection with n-gram bans)
+    if slot is not None:
+        tokens, stage_dev = slot.bufs["tokens"], slot.bufs["stage"]
+        tokens.fill_(cfg.decoder_start_id)
+        if ngram_dev:
+            seq_dev, seq_alt = slot.bufs["seq"], slot.bufs["seq_alt"]
+    else:
+        tokens = torch.full((rows,), cfg.decoder_start_id, dtype=torch.int32, device=dev)
+        stage_dev = torch.zeros(3 * rows, dtype=torch.int32, device=dev)
+        if ngram_dev:
+            seq_dev = torch.empty((rows, T), dtype=torch.int32, device=dev)
+            seq_alt = torch.zeros_like(seq_dev)
+        if new_slot is not None:
+            new_slot.bufs.update(tokens=tokens, stage=stage_dev)
+            if ngram_dev:
+                new_slot.bufs.update(seq=seq_dev, seq_alt=seq_alt)
     par_dev, tok_dev = stage_dev[:rows], stage_dev[rows:2 * rows]
     score_dev = stage_dev[2 * rows:].view(torch.float32)
     score_dev.copy_(torch.from_numpy(run_scores.reshape(-1)).to(dev))
     lp = float(gen.length_penalty)
-    # Every step input is a static device buffer (tokens, step, cache, hist), so
-    # after one eager step the whole decoder step (~13 launches x L layers) is
-    # captured once and replayed: the host loop issues 1 launch per step.
-    use_graph = gen.use_graph and dev.type == "cuda"
-    graph, g_logits = None, None
-    # device selection with the fused LM head (lm_head.hip): the step ends at the LM-head
-    # input and lm_head_topk produces the per-row top-K2 without fp32 logits
-    fused = pin and gen.device_select and K2 <= ops.LM_HEAD_MAX_K and LM_FUSED
-    seq_dev = seq_alt = None  # device token history (device selection with n-gram bans)
+    graph, g_logits = (slot.graph, slot.out) if slot is not None else (None, None)
 
     def advance() -> torch.Tensor:
         """Histories follow their parent beams (backpointers, no KV copy), new tokens in,
@@ -283,6 +424,12 @@ def _generate_iter(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
             from .graphs import capture_graph
 
             graph, g_logits = capture_graph(advance)
+            if new_slot is not None:
+                new_slot.graph, new_slot.out = graph, g_logits
+                # the lazily built model tensors the step read (a regrown one must not be freed)
+                new_slot.keep = [t for t in (getattr(model, "_dec_bias", None),) if t is not None]
+                if slot_cache(model).admit(new_slot):
+                    held.append(new_slot)
         return out
 
     def apply(cur: int, top_sc, top_tok, top_beam, nxt) -> bool:
@@ -373,11 +520,11 @@ def _generate_iter(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
             return (r[:, :K2].copy().view(np.float32), r[:, K2:2 * K2].astype(np.int64),
                     r[:, 2 * K2:3 * K2].astype(np.int64), r[:, 3 * K2:].astype(np.int64))
 
-        if gen.no_repeat_ngram_size:
+        if seq_dev is not None:
             # running beams' tokens [rows, T], reordered by parents in advance() (graph)
-            seq_dev = torch.full((rows, T), cfg.pad_id, dtype=torch.int32, device=dev)
+            seq_dev.fill_(cfg.pad_id)
             seq_dev[:, 0] = cfg.decoder_start_id
-            seq_alt = torch.zeros_like(seq_dev)
+            seq_alt.zero_()
         pending, slot = None, 0
         while True:
             tp0 = time.perf_counter()

@@ -687,3 +687,58 @@ def test_engine_stream_split_matches_single(gpu, monkeypatch, streams):
     monkeypatch.setenv("ATPU_SUMM_PART_MIN", "20")
     b = eng.run(ids, lens, gen)
     assert a.sequences == b.sequences and a.scores == b.scores
+
+
+@pytest.mark.parametrize("family", ["t5-tiny", "bart-tiny"])
+def test_decoder_graph_cache_reuse_is_exact(gpu, family, monkeypatch):
+    # a second search of the same shape replays the first one's captured decoder step on the
+    # same buffers (cross K/V, cache, histories reset): bit-identical to capturing per call
+    from agent_tpu_amd.runtime import summarize
+    from agent_tpu_amd.runtime.summarize import GenConfig, build_model, generate, slot_cache
+
+    model, _ = build_model(family, device=gpu, seed=3)
+    g = torch.Generator().manual_seed(9)
+    B = 5
+    gen = GenConfig(num_beams=4, max_length=20, min_length=3)
+    inputs = []
+    for S, lens in ((128, [128, 90, 31, 9, 127]), (100, [100, 12, 77, 64, 5]), (120, [3, 120, 40, 41, 99])):
+        ids = torch.randint(5, model.cfg.vocab_size, (B, S), generator=g, dtype=torch.int32)
+        inputs.append((ids, torch.tensor(lens, dtype=torch.int32)))
+    monkeypatch.setattr(summarize, "GRAPH_CACHE", False)
+    ref = []
+    for ids, lens in inputs:  # uncached, source padded to the bucket by hand
+        pad = torch.full((B, 128 - ids.shape[1]), model.cfg.pad_id, dtype=torch.int32)
+        ref.append(generate(model, torch.cat([ids, pad], 1).to(gpu), lens.to(gpu), gen))
+    monkeypatch.setattr(summarize, "GRAPH_CACHE", True)
+    sc = slot_cache(model)
+    for rnd in range(2):
+        for (ids, lens), r in zip(inputs, ref):
+            o = generate(model, ids.to(gpu), lens.to(gpu), gen)
+            assert o.sequences == r.sequences and o.scores == r.scores and o.steps == r.steps
+    assert sc.misses == 1 and sc.hits == 5 and len(sc.slots) == 1 and not sc.slots[0].busy
+    # another shape (max_length) is another slot; a full cache evicts the idle LRU slot
+    monkeypatch.setattr(sc, "max_slots", 1)
+    generate(model, inputs[0][0].to(gpu), inputs[0][1].to(gpu), GenConfig(num_beams=4, max_length=12, min_length=3))
+    assert len(sc.slots) == 1 and sc.slots[0].key[2] == 12
+
+
+def test_decoder_graph_cache_concurrent_parts(gpu, monkeypatch):
+    # three equal parts on three streams take three slots of one key; the next call reuses them
+    from agent_tpu_amd.runtime import summarize
+    from agent_tpu_amd.runtime.summarize import GenConfig, build_model, generate, generate_concurrent, slot_cache
+
+    monkeypatch.setattr(summarize, "GRAPH_CACHE", True)
+    model, _ = build_model("t5-tiny", device=gpu, seed=5)
+    g = torch.Generator().manual_seed(12)
+    ids = torch.randint(5, model.cfg.vocab_size, (9, 40), generator=g, dtype=torch.int32).to(gpu)
+    lens = torch.tensor([40, 12, 33, 9, 27, 40, 3, 18, 25], dtype=torch.int32).to(gpu)
+    gen = GenConfig(num_beams=4, max_length=16, min_length=2)
+    parts = [(ids[a:a + 3], lens[a:a + 3]) for a in (0, 3, 6)]
+    ref = [generate(model, i, l, gen) for i, l in parts]
+    sc = slot_cache(model)
+    h0 = sc.hits
+    for _ in range(2):
+        got = generate_concurrent(model, parts, gen)
+        for r, o in zip(ref, got):
+            assert r.sequences == o.sequences and r.scores == o.scores and r.steps == o.steps
+    assert len(sc.slots) == 3 and sc.hits - h0 >= 3 and not any(s.busy for s in sc.slots)
