@@ -901,7 +901,8 @@ struct LnLds {
 
 // IN_ACC (InNorm): the caller started the accumulators at -mu*colsum (else the
 // epilogue applies -rstd*mu*colsum itself, from LDS colsum)
-template <int EPI, bool NT, bool IN_ACC = true, int GM = 0>
+// NOST (timing-only ablation, results WRONG): the output values are computed but not stored
+template <int EPI, bool NT, bool IN_ACC = true, int GM = 0, bool NOST = false>
 __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int m0, int n0, int wm, int wn, int lane,
                                                   bf16* __restrict__ C, int ldc, const bf16* __restrict__ R, int ldr,
                                                   const float* lds_bias, char* scratch,
@@ -1048,7 +1049,9 @@ __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int 
     const u32x4 o1 = *reinterpret_cast<const u32x4*>(scratch + line_off1);
     u32x4* cp = reinterpret_cast<u32x4*>(C + (row0 + i * 16 + lr) * ldc + col);
     u32x4* cp1 = reinterpret_cast<u32x4*>(C + (row0 + i * 16 + lr + 8) * ldc + col);
-    if constexpr (NT) {
+    if constexpr (NOST) {
+      asm volatile("" ::"v"(o0), "v"(o1), "v"(cp), "v"(cp1));
+    } else if constexpr (NT) {
       __builtin_nontemporal_store(o0, cp);
       __builtin_nontemporal_store(o1, cp1);
     } else {
@@ -1467,7 +1470,7 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
       constexpr int kEpiRun0 = kBiasAcc ? (EPI & ~kEpiBias) : EPI;
       constexpr int kEpiRun = (DBG & 8) ? (kEpiRun0 & ~(kEpiInNorm | kEpiResNorm | kEpiStatsOut)) : kEpiRun0;
       if constexpr (LINE)
-        epilogue_256_line<kEpiRun, NT, kInAcc, ((DBG >> 5) & 3)>(acc, cm0, cn0, wm, wn, (kIn || kRes || kSt) ? opaque_lane() : lane, C, ldc, R, ldr,
+        epilogue_256_line<kEpiRun, NT, kInAcc, ((DBG >> 5) & 3), bool(DBG & 256)>(acc, cm0, cn0, wm, wn, (kIn || kRes || kSt) ? opaque_lane() : lane, C, ldc, R, ldr,
                                    reinterpret_cast<const float*>(lds + kBiasOff) + tile_par * 256,
                                    lds + kEpiOff + wave * 2048, pre,
                                    LnLds{reinterpret_cast<const float*>(lds + kFinOff + (kInAcc ? tile_par * 2048 : 0)),
@@ -1590,6 +1593,24 @@ void launch_256s(const GemmArgs& g, hipStream_t s) {
       hipLaunchKernelGGL(k, dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M,
                          g.N, g.K, lf);
       return;
+    }
+    if (ablate == 12 || ablate == 13) {
+      // timing only: 12 = the LN-folding epilogues without their global stores, 13 = no epilogue
+#define ATPU_G256S_N(E)                                                                                        \
+  case E:                                                                                                      \
+    hipLaunchKernelGGL((ablate == 12 ? gemm256s_kernel<E, 256, NT, LINE> : gemm256s_kernel<E, 1, NT, LINE>),   \
+                       dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, \
+                       g.K, lf);                                                                               \
+    return;
+      switch (g.epi) {
+        ATPU_G256S_N(kEpiBias | kEpiInNorm)
+        ATPU_G256S_N(kEpiBias | kEpiInNorm | kEpiGelu)
+        ATPU_G256S_N(kEpiBias | kEpiResidual | kEpiStatsOut)
+        ATPU_G256S_N(kEpiBias | kEpiResidual | kEpiResNorm | kEpiStatsOut)
+        default:
+          break;
+      }
+#undef ATPU_G256S_N
     }
     if (ablate == 7) {  // timing only: LN-folding structure without its epilogue math
 #define ATPU_G256S_A(E)                                                                                        \

@@ -7,7 +7,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd "$R"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-O=$R/gpurun_out/ab
+O=$R/gpurun_out/ab${ABN:-}
 mkdir -p "$O"
 for r in $(seq 1 ${ROUNDS:-2}); do
   for side in A B; do
