@@ -97,7 +97,11 @@ int64_t make_cu_mask_stream(int first_bit, int nbits);  // hipStream_t over CU-m
 void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int ldkv, int seq_stride, int group,
                       const int32_t* lens, const int32_t* step_dev, const int32_t* hist, int hist_stride,
                       const float* bias_dist, int bias_stride, bf16* out, int ldo, int rows, int H, float scale,
-                      hipStream_t stream);
+                      hipStream_t stream, float* ws = nullptr);
+// Cross attention (lens) over a grid of few items splits the keys into 64-key chunks
+// (flash decoding) when given a workspace of this many floats (0: no split for the shape).
+int decode_attention_splits(int rows, int group, int H, int seq_stride, bool cross);
+size_t decode_attention_ws_floats(int rows, int group, int H, int seq_stride, bool cross);
 // dst[r][j] = src[parent[r]][j] (j < t), dst[r][t] = last ? last[r] : parent[r]; t = *step_dev + off
 // device beam selection (runtime/summarize.py): item top-K2 over its beams' candidates, hits,
 // next running beams -> stage [parents | tokens | score bits] and a host record per item

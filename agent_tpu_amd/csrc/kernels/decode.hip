@@ -250,7 +250,9 @@ __global__ __launch_bounds__(NW * 64) void decode_self_attention_kernel(
   __syncthreads();
   auto at = [&](int r, int j, int h) -> size_t { return ((size_t)r * seq_stride + j) * ldkv + h * kD; };
   const int ksub = lane >> 3, dc = (lane & 7) * 8;
-  for (int h = w; h < H; h += NW) {
+  // gridDim.y > 1 (few rows: a grid of `rows` workgroups leaves the chip idle): workgroup y
+  // takes heads y*NW + w, y*NW + w + NW*gridDim.y, ... (every workgroup resolves prow itself)
+  for (int h = blockIdx.y * NW + w; h < H; h += NW * gridDim.y) {
     bf16x8 qq[8];  // the head's query, identical in every lane
     const bf16* qr = q + (size_t)seq * ldq + h * kD;
 #pragma unroll
@@ -314,6 +316,148 @@ __global__ __launch_bounds__(NW * 64) void decode_self_attention_kernel(
     }
     if (ksub == 0) *reinterpret_cast<bf16x8*>(out + (size_t)seq * ldo + h * kD + dc) = ov;
   }
+}
+
+// ----------------------------------------------------------------------------
+// Cross attention with the keys split over workgroups ("flash decoding"), for grids
+// the per-(item, head) kernel leaves idle: 1 document x 12 heads is 12 workgroups on
+// 256 CUs, each walking 1024 keys through dependent load rounds (23 us per call where
+// the K/V bytes take < 1 us). Here one wave per (item, head, 64-key chunk):
+//   scores : lane = key, its 128-B K row in 8 x 16-B loads, v_dot2 with each of the
+//            item's G beam queries (registers), wave max / sum per query;
+//   P.V    : lane = (key sub 0..7, 8 dims), all 8 V slabs' loads in flight at once,
+//            probabilities through LDS, xor-reduce over the key subs;
+//   output : per (row, head, chunk) {max, sum, o[64]} (o unnormalised) into ws.
+// decode_attn_combine_kernel rescales the chunks to the global max and divides.
+// ----------------------------------------------------------------------------
+constexpr int kSplitKeys = 64;
+constexpr int kSplitRec = 2 + kD;  // floats per (row, head, chunk): max, sum, o[64]
+
+template <int GM>
+__global__ __launch_bounds__(64) void decode_cross_split_kernel(
+    const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k, const bf16* __restrict__ v, int ldkv,
+    int seq_stride, int group, int nrows, const int32_t* __restrict__ lens, const float* __restrict__ bias_dist,
+    int bias_stride, float* __restrict__ ws, int H, float scale) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  __shared__ float pl[GM][kSplitKeys];
+  const int seq = blockIdx.x, h = blockIdx.y, c = blockIdx.z, NS = gridDim.z;
+  const int lane = threadIdx.x;
+  const int G = min(group, nrows - seq * group);
+  const int len = min(lens[seq], seq_stride);
+  const int jb = c * kSplitKeys, n = max(0, min(kSplitKeys, len - jb));
+  auto at = [&](int j) -> size_t { return ((size_t)seq * seq_stride + j) * ldkv + h * kD; };
+  auto rec = [&](int g) { return ws + (((size_t)(seq * group + g) * H + h) * NS + c) * kSplitRec; };
+  if (n == 0) {  // a chunk past this item's source length contributes nothing
+    for (int i = lane; i < G * kSplitRec; i += 64) {
+      const int g = i / kSplitRec, e = i % kSplitRec;
+      rec(g)[e] = e == 0 ? -FLT_MAX : 0.f;
+    }
+    return;
+  }
+  // every load before any use: the beams' queries (lane = (beam, 16-B chunk); through
+  // LDS, as per-beam scalar loads they cost one round trip per beam), the bias, the K
+  // row of key jb + lane and the V slabs of P.V
+  __shared__ bf16x8 qsh[GM][8];
+  const int qg = lane >> 3, qe = lane & 7;
+  bf16x8 qv;
+  if (qg < G) qv = *reinterpret_cast<const bf16x8*>(q + (size_t)(seq * group + qg) * ldq + h * kD + qe * 8);
+  const int jk = jb + min(lane, n - 1);
+  const float bj = bias_dist ? bias_dist[h * bias_stride + (len - 1 - jk)] : 0.f;
+  bf16x8 kk[8];
+  const bf16* kr = k + at(jk);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) kk[e] = *reinterpret_cast<const bf16x8*>(kr + e * 8);
+  const int ksub = lane >> 3, dc = (lane & 7) * 8;
+  bf16x8 vv[kSplitKeys / 8];
+#pragma unroll
+  for (int u = 0; u < kSplitKeys / 8; ++u)
+    vv[u] = *reinterpret_cast<const bf16x8*>(v + at(jb + min(u * 8 + ksub, n - 1)) + dc);
+  if (qg < G) qsh[qg][qe] = qv;
+  __syncthreads();
+  float mxg[GM], smg[GM];
+#pragma unroll
+  for (int g = 0; g < GM; ++g) {
+    if (g < G) {  // G is uniform: no divergence
+      float d[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bf16x8 qq = qsh[g][e];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          d[t] = __builtin_amdgcn_fdot2_f32_bf16(bf16x2_t{kk[e][2 * t], kk[e][2 * t + 1]},
+                                                 bf16x2_t{qq[2 * t], qq[2 * t + 1]}, d[t], false);
+      }
+      const float sj = lane < n ? ((d[0] + d[1]) + (d[2] + d[3])) * scale + bj : -FLT_MAX;
+      const float m = wave_max(sj);
+      const float p = lane < n ? __expf(sj - m) : 0.f;
+      pl[g][lane] = p;
+      mxg[g] = m;
+      smg[g] = wave_sum(p);
+    }
+  }
+  __syncthreads();
+  float o[GM][8];
+#pragma unroll
+  for (int g = 0; g < GM; ++g)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[g][e] = 0.f;
+#pragma unroll
+  for (int u = 0; u < kSplitKeys / 8; ++u) {
+    const int jl = u * 8 + ksub;
+#pragma unroll
+    for (int g = 0; g < GM; ++g) {
+      if (g < G) {
+        const float pj = jl < n ? pl[g][jl] : 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[g][e] += pj * bf2f(vv[u][e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < GM; ++g) {
+    if (g < G) {
+      float* r = rec(g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = o[g][e];
+        x += __shfl_xor(x, 8);
+        x += __shfl_xor(x, 16);
+        x += __shfl_xor(x, 32);
+        o[g][e] = x;
+      }
+      if (ksub == 0) {
+        *reinterpret_cast<float4*>(r + 2 + dc) = make_float4(o[g][0], o[g][1], o[g][2], o[g][3]);
+        *reinterpret_cast<float4*>(r + 2 + dc + 4) = make_float4(o[g][4], o[g][5], o[g][6], o[g][7]);
+      }
+      if (lane == 0) {
+        r[0] = mxg[g];
+        r[1] = smg[g];
+      }
+    }
+  }
+}
+
+// out[row][h*64 + d] = sum_c o_c[d] e^(m_c - M) / sum_c l_c e^(m_c - M), M = max_c m_c
+// (one wave per (row, head)): lane c < NS loads chunk c's (max, sum) and the weights are
+// reduced across lanes; then lane = dimension sums the chunks' o with every load issued
+// before the first add (a loop of dependent rounds took 8 us per call)
+constexpr int kMaxSplits = kMaxKeys / kSplitKeys;
+__global__ __launch_bounds__(64) void decode_attn_combine_kernel(const float* __restrict__ ws, int NS, int H,
+                                                                 bf16* __restrict__ out, int ldo) {
+  const int row = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
+  const float* r = ws + ((size_t)row * H + h) * NS * kSplitRec;
+  float ov[kMaxSplits];
+#pragma unroll
+  for (int c = 0; c < kMaxSplits; ++c) ov[c] = r[min(c, NS - 1) * kSplitRec + 2 + lane];
+  const float m = lane < NS ? r[lane * kSplitRec] : -FLT_MAX;
+  const float l = lane < NS ? r[lane * kSplitRec + 1] : 0.f;
+  const float M = wave_max(m);
+  const float w = lane < NS ? __expf(m - M) : 0.f;  // 0 for an empty chunk (max -FLT_MAX)
+  const float L = wave_sum(w * l);
+  float o = 0.f;
+#pragma unroll
+  for (int c = 0; c < kMaxSplits; ++c) o += (c < NS ? __shfl(w, c) : 0.f) * ov[c];
+  out[(size_t)row * ldo + h * kD + lane] = f2bf(L > 0.f ? o / L : 0.f);
 }
 
 // hist'[r][j] = hist[parent[r]][j] for j < t; hist'[r][t] = last ? last[r] : parent[r],
@@ -700,10 +844,24 @@ __global__ __launch_bounds__(kSelMax) void beam_select_kernel(const float* __res
 
 }  // namespace
 
+int decode_attention_splits(int rows, int group, int H, int seq_stride, bool cross) {
+  // key chunks of the split cross attention, 0 = the per-(item, head) kernel: split while
+  // the unsplit grid (items x heads) cannot cover the chip twice
+  if (!cross || group < 1 || group > 8 || seq_stride < 2 * kSplitKeys) return 0;
+  const int nseq = (rows + group - 1) / group;
+  if (nseq * H >= 512) return 0;
+  return (seq_stride + kSplitKeys - 1) / kSplitKeys;
+}
+
+size_t decode_attention_ws_floats(int rows, int group, int H, int seq_stride, bool cross) {
+  const int ns = decode_attention_splits(rows, group, H, seq_stride, cross);
+  return ns ? (size_t)rows * H * ns * kSplitRec : 0;
+}
+
 void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int ldkv, int seq_stride, int group,
                       const int32_t* lens, const int32_t* step_dev, const int32_t* hist, int hist_stride,
                       const float* bias_dist, int bias_stride, bf16* out, int ldo, int rows, int H, float scale,
-                      hipStream_t stream) {
+                      hipStream_t stream, float* ws) {
   ATPU_CHECK(rows > 0 && H > 0 && group >= 1, "decode_attention: bad shape");
   ATPU_CHECK(lens || step_dev, "decode_attention: need lens or a device step");
   ATPU_CHECK(!hist || (step_dev && group == 1), "decode_attention: hist is for self attention (group 1)");
@@ -721,13 +879,35 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
                "decode_attention: q / out need 16-B rows");
     constexpr int NW = 4;
     const size_t smem = (size_t)((seq_stride + 3) & ~3) * 4 * (1 + NW);
-    hipLaunchKernelGGL((decode_self_attention_kernel<NW>), dim3(rows), dim3(NW * 64), smem, stream, q, ldq, k, v, ldkv,
+    // few rows: head groups over grid.y (one head per wave) so the launch covers more CUs
+    const int hg = rows < 128 ? (H + NW - 1) / NW : 1;
+    hipLaunchKernelGGL((decode_self_attention_kernel<NW>), dim3(rows, hg), dim3(NW * 64), smem, stream, q, ldq, k, v, ldkv,
                        seq_stride, step_dev, hist, hist_stride, bias_dist, bias_stride, out, ldo, H, scale);
     ATPU_HIP_CHECK(hipGetLastError());
     return;
   }
   ATPU_CHECK(seq_stride <= kMaxKeys, "decode_attention: cache length above 2048");
   const int nseq = (rows + group - 1) / group;
+  const int ns = decode_attention_splits(rows, group, H, seq_stride, lens != nullptr && !hist);
+  if (ns > 0 && ws) {
+    static_assert(kMaxSplits * kSplitKeys >= kMaxKeys, "combine kernel chunk count");
+    ATPU_CHECK(ldq % 8 == 0 && (reinterpret_cast<uintptr_t>(q) & 15) == 0, "decode_attention: q needs 16-B rows");
+    ATPU_CHECK((reinterpret_cast<uintptr_t>(ws) & 15) == 0, "decode_attention: ws must be 16-byte aligned");
+#define ATPU_DS(GM)                                                                                            \
+  hipLaunchKernelGGL((decode_cross_split_kernel<GM>), dim3(nseq, H, ns), dim3(64), 0, stream, q, ldq, k, v, ldkv, \
+                     seq_stride, group, rows, lens, bias_dist, bias_stride, ws, H, scale)
+    if (group == 1)
+      ATPU_DS(1);
+    else if (group <= 4)
+      ATPU_DS(4);
+    else
+      ATPU_DS(8);
+#undef ATPU_DS
+    ATPU_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(decode_attn_combine_kernel, dim3(rows, H), dim3(64), 0, stream, ws, ns, H, out, ldo);
+    ATPU_HIP_CHECK(hipGetLastError());
+    return;
+  }
 #define ATPU_DA(GM, NW)                                                                                          \
   hipLaunchKernelGGL((decode_attention_kernel<GM, NW>), dim3(nseq, H), dim3(NW * 64),                           \
                      (size_t)GM * ((seq_stride + 3) & ~3) * sizeof(float), stream, q, ldq, k, v, ldkv,          \

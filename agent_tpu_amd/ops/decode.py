@@ -49,10 +49,15 @@ def decode_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, H: int, 
         check(lens is None and group == 1, "hist is for self attention (group 1)")
         check(hist.dtype == torch.int32 and hist.is_contiguous() and hist.shape[0] == R, "hist must be int32 [R, T]")
     out = torch.empty((R, H * HEAD_DIM), dtype=torch.bfloat16, device=q.device) if out is None else out
+    # few items: the keys are split over workgroups (flash decoding) into this workspace
+    # (allocated per call: concurrent searches on other streams never share it; inside a
+    # captured decoder step it comes from the graph's pool)
+    nws = native().decode_attention_ws_floats(R, group, H, seq_stride, lens is not None and hist is None)
+    ws = torch.empty(nws, dtype=torch.float32, device=q.device) if nws else None
     native().decode_attention(ptr(q), row_stride(q, "q"), ptr(k), ptr(v), row_stride(k, "k"), seq_stride, group,
                               ptr(lens), ptr(step), ptr(hist), 0 if hist is None else hist.shape[1], ptr(bias_dist),
                               0 if bias_dist is None else bias_dist.shape[1], ptr(out), row_stride(out, "out"), R, H,
-                              float(scale), launch_stream(q))
+                              float(scale), launch_stream(q), ptr(ws))
     return out
 
 

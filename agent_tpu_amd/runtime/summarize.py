@@ -318,12 +318,16 @@ def _generate_body(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
     # graph cache: the source is padded to a length bucket (keys past src_lens are masked
     # in the encoder and the cross attention), the buffers of a previous search of this
     # shape are reused, and its captured step replays from the first launch
+    # (padded on every device run with the cache on, graph or not: the padded source takes
+    # other kernel paths -- split cross attention past 128 keys -- and a search's tokens
+    # must not depend on whether its step was captured)
     slot, new_slot = None, None
-    if use_graph and GRAPH_CACHE:
+    if pin and GRAPH_CACHE:
         Sb = -(-S // SRC_BUCKET) * SRC_BUCKET
         if Sb != S:
             src_ids = torch.nn.functional.pad(src_ids, (0, Sb - S), value=int(cfg.pad_id))
             S = Sb
+    if use_graph and GRAPH_CACHE:
         key = (B, S, T, nb, fused, ngram_dev, bool(gen.device_select))
         slot = slot_cache(model).acquire(key)
         if slot is not None:

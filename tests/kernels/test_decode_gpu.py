@@ -31,6 +31,45 @@ def test_decode_attention_cross(gpu, rows, group, S, H):
     assert _rel(out, ref) < 2e-2
 
 
+@pytest.mark.parametrize("lens,group,S,H,scale", [([1, 63, 64, 65, 128, 1024], 4, 1024, 12, 1.0),
+                                                   ([1000], 4, 1024, 12, 0.125), ([130, 7], 1, 130, 16, 1.0),
+                                                   ([700, 3, 640], 8, 704, 12, 1.0), ([200, 199], 3, 256, 12, 1.0)])
+def test_decode_cross_split_keys(gpu, lens, group, S, H, scale):
+    # few items: the keys are split into 64-key chunks over workgroups (flash decoding) and
+    # combined; chunks past an item's length, a 1-key item, partial last chunks, 1-8 beams
+    from agent_tpu_amd._native import native
+
+    nseq = len(lens)
+    rows = nseq * group - (1 if group > 2 else 0)  # a short last item
+    assert native().decode_attention_ws_floats(rows, group, H, S, True) > 0
+    q = _r((rows, 3 * H * 64), gpu, seed=41)[:, :H * 64]  # strided like the fused QKV output
+    kv = _r((nseq * S, 2 * H * 64), gpu, seed=42)
+    lt = torch.tensor(lens, dtype=torch.int32)
+    for bias in (None, _r((H, S), gpu, 1.0, torch.float32, seed=43)):
+        out = ops.decode_attention(q, kv[:, :H * 64], kv[:, H * 64:], H, S, group, lens=lt.to(gpu), bias_dist=bias,
+                                   scale=scale)
+        ref = _decode_attention_ref(q.cpu(), kv.cpu()[:, :H * 64], kv.cpu()[:, H * 64:], H, S, group, lt, None,
+                                    None if bias is None else bias.cpu(), scale, None)
+        assert _rel(out, ref) < 2e-2
+
+
+@pytest.mark.parametrize("rows,H,T,t", [(4, 12, 130, 70), (1, 12, 130, 0), (8, 16, 300, 299)])
+def test_decode_self_head_groups(gpu, rows, H, T, t):
+    # few rows: the per-row self-attention kernel spreads the heads over grid.y
+    d = H * 64
+    cache = _r((rows * T, 2 * d), gpu, seed=51)
+    q = _r((rows, d), gpu, seed=52)
+    g = torch.Generator().manual_seed(6)
+    hist = torch.randint(0, rows, (rows, T), generator=g, dtype=torch.int32)
+    step = torch.tensor([t], dtype=torch.int32)
+    bias = _r((H, T), gpu, 1.0, torch.float32, seed=53)
+    out = ops.decode_attention(q, cache[:, :d], cache[:, d:], H, T, 1, step=step.to(gpu), bias_dist=bias,
+                               hist=hist.to(gpu))
+    ref = _decode_attention_ref(q.cpu(), cache.cpu()[:, :d], cache.cpu()[:, d:], H, T, 1, None, step, bias.cpu(), 1.0,
+                                None, hist)
+    assert _rel(out, ref) < 2e-2
+
+
 def test_decode_self_with_bias_append_gather(gpu):
     rows, H, T = 6, 4, 20
     d = H * 64
