@@ -2167,6 +2167,155 @@ int gemm_splitk_splits(int M, int N, int K) {
   return want;
 }
 
+namespace {
+
+// ============================================================================
+// Decode GEMV (M <= 4 rows: one document x 4 beams, the reference's job shape).
+// The 64x64 "dec" kernel walks K through a chain of LDS-DMA round trips (a ~5.5 us
+// floor at 12 K-tiles) and covers N = 768 with 12 workgroups; at 4 rows the GEMM is
+// a weight stream. Here a wave owns 4 output columns and its 64 lanes split K in
+// 16-B chunks (lane l: chunks l, l+64, ...): each round issues kGemvU chunks' weight
+// and A loads at once (every load of K <= 1536 in one round), accumulates with
+// v_dot2 in fp32, and the lanes are reduced by wave sums. 4 waves = 16 columns per
+// workgroup (N = 768: 48 workgroups, 3072: 192). Epilogue as the other kernels:
+// RowRms scale, bias, GELU / ReLU, residual, bf16 store (KvScatter: K|V columns into
+// the cache row m*T + step). No split-K, no workspace.
+// ============================================================================
+constexpr int kGemvRows = 4;
+constexpr int kGemvU = 3;  // chunks per lane in flight per round
+
+template <int EPI>
+__global__ __launch_bounds__(256) void gemv_kernel(const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bt,
+                                                   int ldb, bf16* __restrict__ C, int ldc, const float* __restrict__ bias,
+                                                   const bf16* __restrict__ R, int ldr, int M, int N, int K,
+                                                   float rms_eps, KvOut kvo) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n0 = (blockIdx.x * 4 + w) * 4;  // this wave's 4 columns
+  const int nch = K / 8;
+  float acc[kGemvRows][4], ssq[kGemvRows];
+#pragma unroll
+  for (int m = 0; m < kGemvRows; ++m) {
+    ssq[m] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[m][j] = 0.f;
+  }
+  for (int base = 0; base < nch; base += 64 * kGemvU) {
+    bf16x8 wv[kGemvU][4], av[kGemvU][kGemvRows];
+#pragma unroll
+    for (int u = 0; u < kGemvU; ++u) {
+      const int c = min(base + u * 64 + lane, nch - 1);  // clamped: its products are dropped below
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wv[u][j] = *reinterpret_cast<const bf16x8*>(Bt + (size_t)(n0 + j) * ldb + c * 8);
+#pragma unroll
+      for (int m = 0; m < kGemvRows; ++m)
+        av[u][m] = *reinterpret_cast<const bf16x8*>(A + (size_t)min(m, M - 1) * lda + c * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < kGemvU; ++u) {
+      const bool ok = base + u * 64 + lane < nch;
+#pragma unroll
+      for (int m = 0; m < kGemvRows; ++m) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float d = 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            d = __builtin_amdgcn_fdot2_f32_bf16(bf16x2_t{av[u][m][2 * e], av[u][m][2 * e + 1]},
+                                                bf16x2_t{wv[u][j][2 * e], wv[u][j][2 * e + 1]}, d, false);
+          acc[m][j] += ok ? d : 0.f;
+        }
+        if constexpr (EPI & kEpiRowRms) ssq[m] += ok ? sumsq_bf16x8(av[u][m], 0.f) : 0.f;
+      }
+    }
+  }
+  // every lane gets every sum; lane (m*4 + j) finishes output (m, n0 + j)
+  float v = 0.f, rs = 0.f;
+  const int mo = lane >> 2, jo = lane & 3;
+#pragma unroll
+  for (int m = 0; m < kGemvRows; ++m) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float t = wave_sum(acc[m][j]);
+      v = (mo == m && jo == j) ? t : v;
+    }
+    if constexpr (EPI & kEpiRowRms) {
+      const float t = wave_sum(ssq[m]);
+      rs = mo == m ? t : rs;
+    }
+  }
+  if (mo >= M || lane >= 4 * kGemvRows) return;
+  const int m = mo, n = n0 + jo;
+  if constexpr (EPI & kEpiRowRms) v *= __builtin_amdgcn_rsqf(rs * (1.f / K) + rms_eps);
+  if constexpr (EPI & kEpiBias) v += bias[n];
+  if constexpr (EPI & kEpiGelu) v = gelu_fast(v);
+  if constexpr (EPI & kEpiRelu) v = fmaxf(v, 0.f);
+  if constexpr (EPI & kEpiResidual) v += bf2f(R[(size_t)m * ldr + n]);
+  const bf16 o = f2bf(v);
+  if constexpr (EPI & kEpiKvScatter) {
+    const int pos = max(*kvo.step, 0);
+    if (n < kvo.col0)
+      C[(size_t)m * ldc + n] = o;
+    else if (pos < kvo.T)  // a step past the cache (caller bug) drops the write
+      kvo.cache[((size_t)m * kvo.T + pos) * kvo.ld + (n - kvo.col0)] = o;
+  } else {
+    C[(size_t)m * ldc + n] = o;
+  }
+}
+
+constexpr int kGemvEpis = kEpiBias | kEpiGelu | kEpiRelu | kEpiResidual | kEpiRowRms | kEpiKvScatter;
+
+bool gemv_ok(const GemmArgs& g) {
+  static const bool on = [] {
+    const char* f = std::getenv("ATPU_GEMV");
+    return !(f && f[0] == '0');
+  }();
+  return on && g.M <= kGemvRows && g.N % 16 == 0 && !(g.epi & ~kGemvEpis) && gemm_force_tile(-1) == 0;
+}
+
+void launch_gemv(const GemmArgs& g, hipStream_t s) {
+  if (g.epi & kEpiKvScatter)
+    ATPU_CHECK(g.kv_cache && g.kv_step && g.kv_T > 0 && g.kv_col0 > 0 && g.kv_col0 < g.N && g.kv_ld >= g.N - g.kv_col0,
+               "gemm: KvScatter needs a cache, a device step and kv_ld >= N - kv_col0");
+  ATPU_CHECK(!(g.epi & kEpiRowRms) || g.rms_eps > 0.f, "gemm: RowRms needs rms_eps > 0");
+  const KvOut kvo{g.kv_cache, g.kv_ld, g.kv_T, g.kv_col0, g.kv_step};
+#define ATPU_GEMV_CASE(E)                                                                                       \
+  case E:                                                                                                       \
+    hipLaunchKernelGGL((gemv_kernel<E>), dim3(g.N / 16), dim3(256), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc,  \
+                       g.bias, g.R, g.ldr, g.M, g.N, g.K, g.rms_eps, kvo);                                      \
+    break;
+  switch (g.epi) {
+    ATPU_GEMV_CASE(0)
+    ATPU_GEMV_CASE(kEpiBias)
+    ATPU_GEMV_CASE(kEpiResidual)
+    ATPU_GEMV_CASE(kEpiBias | kEpiResidual)
+    ATPU_GEMV_CASE(kEpiRelu)
+    ATPU_GEMV_CASE(kEpiBias | kEpiRelu)
+    ATPU_GEMV_CASE(kEpiBias | kEpiGelu)
+    ATPU_GEMV_CASE(kEpiRowRms)
+    ATPU_GEMV_CASE(kEpiRowRms | kEpiRelu)
+    ATPU_GEMV_CASE(kEpiRowRms | kEpiKvScatter)
+    ATPU_GEMV_CASE(kEpiBias | kEpiKvScatter)
+    default:
+      throw std::invalid_argument("atpu: unsupported GEMV epilogue " + std::to_string(g.epi));
+  }
+#undef ATPU_GEMV_CASE
+  ATPU_HIP_CHECK(hipGetLastError());
+}
+
+bool gemv_has_case(int epi) {
+  switch (epi) {
+    case 0: case kEpiBias: case kEpiResidual: case kEpiBias | kEpiResidual: case kEpiRelu: case kEpiBias | kEpiRelu:
+    case kEpiBias | kEpiGelu: case kEpiRowRms: case kEpiRowRms | kEpiRelu: case kEpiRowRms | kEpiKvScatter:
+    case kEpiBias | kEpiKvScatter:
+      return true;
+    default:
+      return false;
+  }
+}
+
+}  // namespace
+
 void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
   ATPU_CHECK(g.M > 0 && g.N > 0 && g.K > 0, "gemm: empty problem");
   ATPU_CHECK(g.K % kBK == 0, "gemm: K must be a multiple of 64");
@@ -2183,6 +2332,10 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
   // times over; the 128x128 kernel (2 blocks/CU) covers small M and odd N.
   // ATPU_GEMM_TILE=128|256 forces one (benchmarks/tests).
   const int forced = gemm_force_tile(-1);
+  if (gemv_ok(g) && gemv_has_case(g.epi)) {  // <= 4 rows: weight-streaming GEMV (no split-K)
+    launch_gemv(g, stream);
+    return;
+  }
   if (g.splits > 1) {
     ATPU_CHECK(!(g.epi & (kEpiRowRms | kEpiKvScatter | kEpiRowLn | kEpiResLn | kEpiRowStats)),
                "gemm: RowRms / RowLn / ResLn / KvScatter cannot split K");

@@ -781,3 +781,60 @@ def test_decoder_graph_cache_concurrent_parts(gpu, monkeypatch):
         for r, o in zip(ref, got):
             assert r.sequences == o.sequences and r.scores == o.scores and r.steps == o.steps
     assert len(sc.slots) == 3 and sc.hits - h0 >= 3 and not any(s.busy for s in sc.slots)
+
+
+@pytest.mark.parametrize("M", [1, 3, 4])
+@pytest.mark.parametrize("N,K,epi", [(768, 768, "plain"), (768, 3072, "bias_res"), (3072, 768, "relu"),
+                                     (4096, 1024, "bias_gelu"), (2304, 768, "rms"), (3072, 768, "rms_relu"),
+                                     (1024, 1024, "res")])
+def test_gemv_few_rows(gpu, M, N, K, epi):
+    # <= 4 rows (1 document x 4 beams) run the weight-streaming GEMV; vs the fp32 reference and
+    # vs the 64x64 decode kernel (forced)
+    from agent_tpu_amd._native import native
+
+    x = _r((M, 2 * K), gpu, 1.5, seed=61)[:, :K]  # strided rows
+    w = _r((N, K), gpu, 0.05, seed=62)
+    b = _r((N,), gpu, 0.1, torch.float32, seed=63) if "bias" in epi else None
+    res = _r((M, N), gpu, 1.0, seed=64) if "res" in epi else None
+    act = "relu" if "relu" in epi else "gelu" if "gelu" in epi else None
+    eps = 1e-6 if "rms" in epi else None
+    if eps is not None:
+        gamma = 1 + _r((K,), gpu, 0.3, torch.float32, seed=65)
+        wf = ops.fold_rms_into_linear(w, gamma)
+        xf = x.cpu().float()
+        xin = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * gamma.cpu()
+    else:
+        wf, xin = w, x.cpu().float()
+    y = ops.linear(x, wf, b, act=act, residual=res, rms_eps=eps)
+    ref = xin @ w.cpu().float().t()
+    if b is not None:
+        ref = ref + b.cpu()
+    ref = torch.relu(ref) if act == "relu" else torch.nn.functional.gelu(ref) if act == "gelu" else ref
+    if res is not None:
+        ref = ref + res.cpu().float()
+    assert _rel(y, ref) < 2e-2
+    prev = native().gemm_force_tile(-1)
+    native().gemm_force_tile(64)
+    try:
+        y64 = ops.linear(x, wf, b, act=act, residual=res, rms_eps=eps)
+    finally:
+        native().gemm_force_tile(prev)
+    assert _rel(y, y64) < 1e-2
+
+
+@pytest.mark.parametrize("M,rms", [(4, True), (1, False), (3, True)])
+def test_gemv_kv_scatter(gpu, M, rms):
+    # decode QKV at <= 4 rows through the GEMV: K|V into cache row m*T + step, Q into out
+    d, T, t = 768, 9, 4
+    x = _r((M, d), gpu, 1.0, seed=71)
+    w = _r((3 * d, d), gpu, 0.05, seed=72)
+    b = None if rms else _r((3 * d,), gpu, 0.1, torch.float32, seed=73)
+    cache = torch.zeros((M * T, 2 * d), dtype=torch.bfloat16, device=gpu)
+    step = torch.tensor([t], dtype=torch.int32, device=gpu)
+    eps = 1e-6 if rms else None
+    q = ops.linear(x, w, b, rms_eps=eps, kv_cache=(cache, T, step, d))
+    full = ops.linear(x, w, b, rms_eps=eps)
+    assert torch.equal(q, full[:, :d])
+    kv = cache.view(M, T, 2 * d)
+    assert torch.equal(kv[:, t], full[:, d:])
+    assert kv[:, :t].abs().sum().item() == 0 and kv[:, t + 1:].abs().sum().item() == 0
