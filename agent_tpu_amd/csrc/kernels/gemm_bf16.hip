@@ -2184,14 +2184,19 @@ namespace {
 constexpr int kGemvRows = 4;
 constexpr int kGemvU = 3;  // chunks per lane in flight per round
 
-template <int EPI>
-__global__ __launch_bounds__(256) void gemv_kernel(const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bt,
+// BART's LayerNorm folding (RowLn / ResLn / RowStats, see LnDec): the row statistics come
+// from the <= 32 slab partials (lane = slab, wave sums); RowStats workgroups are 8 waves =
+// one 32-column slab, summed across the waves through LDS.
+template <int EPI, int NWV>
+__global__ __launch_bounds__(NWV * 64) void gemv_kernel(const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bt,
                                                    int ldb, bf16* __restrict__ C, int ldc, const float* __restrict__ bias,
                                                    const bf16* __restrict__ R, int ldr, int M, int N, int K,
-                                                   float rms_eps, KvOut kvo) {
+                                                   float rms_eps, KvOut kvo, LnDec ln) {
   typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  static_assert(!(EPI & kEpiRowStats) || NWV == 8, "RowStats: one 32-column slab per workgroup");
+  __shared__ float2 st_red[NWV][kGemvRows];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int n0 = (blockIdx.x * 4 + w) * 4;  // this wave's 4 columns
+  const int n0 = (blockIdx.x * NWV + w) * 4;  // this wave's 4 columns
   const int nch = K / 8;
   float acc[kGemvRows][4], ssq[kGemvRows];
 #pragma unroll
@@ -2244,26 +2249,71 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16* __restrict__ A, i
       rs = mo == m ? t : rs;
     }
   }
-  if (mo >= M || lane >= 4 * kGemvRows) return;
-  const int m = mo, n = n0 + jo;
-  if constexpr (EPI & kEpiRowRms) v *= __builtin_amdgcn_rsqf(rs * (1.f / K) + rms_eps);
-  if constexpr (EPI & kEpiBias) v += bias[n];
-  if constexpr (EPI & kEpiGelu) v = gelu_fast(v);
-  if constexpr (EPI & kEpiRelu) v = fmaxf(v, 0.f);
-  if constexpr (EPI & kEpiResidual) v += bf2f(R[(size_t)m * ldr + n]);
-  const bf16 o = f2bf(v);
-  if constexpr (EPI & kEpiKvScatter) {
-    const int pos = max(*kvo.step, 0);
-    if (n < kvo.col0)
+  // (rstd, rstd*mu) of A's rows (RowLn) or R's rows (ResLn) from their slab partials
+  float2 lnst = float2{1.f, 0.f};
+  if constexpr (EPI & (kEpiRowLn | kEpiResLn)) {
+    const int slots = (EPI & kEpiRowLn) ? K / 32 : N / 32;
+    const float* part = (EPI & kEpiRowLn) ? ln.in_part : ln.res_part;
+#pragma unroll
+    for (int m = 0; m < kGemvRows; ++m) {
+      const float2 pv = lane < slots ? *reinterpret_cast<const float2*>(part + 2 * ((size_t)lane * M + min(m, M - 1)))
+                                     : float2{0.f, 0.f};
+      const float S = wave_sum(pv.x), Q = wave_sum(pv.y);
+      const float inv = 1.f / (32 * slots);
+      const float mu = S * inv, var = fmaxf(Q * inv - mu * mu, 0.f);
+      const float r = __builtin_amdgcn_rsqf(var + rms_eps);
+      lnst = mo == m ? float2{r, r * mu} : lnst;
+    }
+  }
+  const bool mine = mo < M && lane < 4 * kGemvRows;
+  const int m = min(mo, M - 1), n = n0 + jo;
+  float f = 0.f;  // RowStats: the stored (bf16-rounded) value
+  if (mine) {
+    if constexpr (EPI & kEpiRowRms) v *= __builtin_amdgcn_rsqf(rs * (1.f / K) + rms_eps);
+    if constexpr (EPI & kEpiRowLn) v = fmaf(v, lnst.x, -lnst.y * ln.colsum[n]);
+    if constexpr (EPI & kEpiBias) v += bias[n];
+    if constexpr (EPI & kEpiGelu) v = gelu_fast(v);
+    if constexpr (EPI & kEpiRelu) v = fmaxf(v, 0.f);
+    if constexpr (EPI & kEpiResidual) {
+      const float r = bf2f(R[(size_t)m * ldr + n]);
+      if constexpr (EPI & kEpiResLn) v = fmaf(fmaf(r, lnst.x, -lnst.y), ln.gamma[n], v);
+      else v += r;
+    }
+    const bf16 o = f2bf(v);
+    f = bf2f(o);
+    if constexpr (EPI & kEpiKvScatter) {
+      const int pos = max(*kvo.step, 0);
+      if (n < kvo.col0)
+        C[(size_t)m * ldc + n] = o;
+      else if (pos < kvo.T)  // a step past the cache (caller bug) drops the write
+        kvo.cache[((size_t)m * kvo.T + pos) * kvo.ld + (n - kvo.col0)] = o;
+    } else {
       C[(size_t)m * ldc + n] = o;
-    else if (pos < kvo.T)  // a step past the cache (caller bug) drops the write
-      kvo.cache[((size_t)m * kvo.T + pos) * kvo.ld + (n - kvo.col0)] = o;
-  } else {
-    C[(size_t)m * ldc + n] = o;
+    }
+  }
+  if constexpr (EPI & kEpiRowStats) {
+    // this wave's 4 columns of row m (lanes m*4 .. m*4+3), then the 8 waves of the slab
+    float s1 = f, s2 = f * f;
+    s1 += __shfl_xor(s1, 1);
+    s2 += __shfl_xor(s2, 1);
+    s1 += __shfl_xor(s1, 2);
+    s2 += __shfl_xor(s2, 2);
+    if (mine && jo == 0) st_red[w][mo] = float2{s1, s2};
+    __syncthreads();
+    if (w == 0 && lane < M) {
+      float2 t = float2{0.f, 0.f};
+#pragma unroll
+      for (int x = 0; x < NWV; ++x) {
+        t.x += st_red[x][lane].x;
+        t.y += st_red[x][lane].y;
+      }
+      *reinterpret_cast<float2*>(ln.part_out + 2 * ((size_t)blockIdx.x * M + lane)) = t;
+    }
   }
 }
 
-constexpr int kGemvEpis = kEpiBias | kEpiGelu | kEpiRelu | kEpiResidual | kEpiRowRms | kEpiKvScatter;
+constexpr int kGemvEpis =
+    kEpiBias | kEpiGelu | kEpiRelu | kEpiResidual | kEpiRowRms | kEpiKvScatter | kEpiRowLn | kEpiResLn | kEpiRowStats;
 
 bool gemv_ok(const GemmArgs& g) {
   static const bool on = [] {
@@ -2277,13 +2327,20 @@ void launch_gemv(const GemmArgs& g, hipStream_t s) {
   if (g.epi & kEpiKvScatter)
     ATPU_CHECK(g.kv_cache && g.kv_step && g.kv_T > 0 && g.kv_col0 > 0 && g.kv_col0 < g.N && g.kv_ld >= g.N - g.kv_col0,
                "gemm: KvScatter needs a cache, a device step and kv_ld >= N - kv_col0");
-  ATPU_CHECK(!(g.epi & kEpiRowRms) || g.rms_eps > 0.f, "gemm: RowRms needs rms_eps > 0");
+  ATPU_CHECK(!(g.epi & (kEpiRowRms | kEpiRowLn | kEpiResLn)) || g.rms_eps > 0.f, "gemm: RowRms / RowLn / ResLn need eps > 0");
+  ATPU_CHECK(!(g.epi & kEpiRowLn) || (g.colsum && g.in_part && g.K <= 1024), "gemm: RowLn needs colsum, in_part, K <= 1024");
+  ATPU_CHECK(!(g.epi & kEpiResLn) || (g.res_part && g.gamma && g.N <= 1024 && g.N % 32 == 0),
+             "gemm: ResLn needs res_part, gamma, N <= 1024");
+  ATPU_CHECK(!(g.epi & kEpiRowStats) || (g.part_out && g.N % 32 == 0), "gemm: RowStats needs part_out and N % 32 == 0");
   const KvOut kvo{g.kv_cache, g.kv_ld, g.kv_T, g.kv_col0, g.kv_step};
+  const LnDec ln{g.colsum, g.in_part, g.res_part, g.gamma, g.part_out};
 #define ATPU_GEMV_CASE(E)                                                                                       \
-  case E:                                                                                                       \
-    hipLaunchKernelGGL((gemv_kernel<E>), dim3(g.N / 16), dim3(256), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc,  \
-                       g.bias, g.R, g.ldr, g.M, g.N, g.K, g.rms_eps, kvo);                                      \
-    break;
+  case E: {                                                                                                     \
+    constexpr int nwv = (E & kEpiRowStats) ? 8 : 4;                                                             \
+    hipLaunchKernelGGL((gemv_kernel<E, nwv>), dim3(g.N / (4 * nwv)), dim3(64 * nwv), 0, s, g.A, g.lda, g.Bt,    \
+                       g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, g.rms_eps, kvo, ln);                \
+    break;                                                                                                      \
+  }
   switch (g.epi) {
     ATPU_GEMV_CASE(0)
     ATPU_GEMV_CASE(kEpiBias)
@@ -2296,6 +2353,12 @@ void launch_gemv(const GemmArgs& g, hipStream_t s) {
     ATPU_GEMV_CASE(kEpiRowRms | kEpiRelu)
     ATPU_GEMV_CASE(kEpiRowRms | kEpiKvScatter)
     ATPU_GEMV_CASE(kEpiBias | kEpiKvScatter)
+    ATPU_GEMV_CASE(kEpiRowLn | kEpiBias)
+    ATPU_GEMV_CASE(kEpiRowLn | kEpiBias | kEpiGelu)
+    ATPU_GEMV_CASE(kEpiRowLn | kEpiBias | kEpiKvScatter)
+    ATPU_GEMV_CASE(kEpiBias | kEpiResidual | kEpiRowStats)
+    ATPU_GEMV_CASE(kEpiBias | kEpiResidual | kEpiResLn)
+    ATPU_GEMV_CASE(kEpiBias | kEpiResidual | kEpiResLn | kEpiRowStats)
     default:
       throw std::invalid_argument("atpu: unsupported GEMV epilogue " + std::to_string(g.epi));
   }
@@ -2307,7 +2370,9 @@ bool gemv_has_case(int epi) {
   switch (epi) {
     case 0: case kEpiBias: case kEpiResidual: case kEpiBias | kEpiResidual: case kEpiRelu: case kEpiBias | kEpiRelu:
     case kEpiBias | kEpiGelu: case kEpiRowRms: case kEpiRowRms | kEpiRelu: case kEpiRowRms | kEpiKvScatter:
-    case kEpiBias | kEpiKvScatter:
+    case kEpiBias | kEpiKvScatter: case kEpiRowLn | kEpiBias: case kEpiRowLn | kEpiBias | kEpiGelu:
+    case kEpiRowLn | kEpiBias | kEpiKvScatter: case kEpiBias | kEpiResidual | kEpiRowStats:
+    case kEpiBias | kEpiResidual | kEpiResLn: case kEpiBias | kEpiResidual | kEpiResLn | kEpiRowStats:
       return true;
     default:
       return false;

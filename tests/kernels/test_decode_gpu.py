@@ -531,7 +531,10 @@ def test_t5_step_rms_fold_matches_unfolded(gpu):
 @pytest.mark.parametrize("M,N,K,act,kv", [(1024, 1024, 1024, None, False), (1024, 4096, 1024, "gelu", False),
                                           (4096, 1024, 1024, None, False), (2048, 4096, 1024, "gelu", False),
                                           (1024, 3072, 1024, None, True), (4096, 3072, 1024, None, True),
-                                          (77, 192, 256, "gelu", False)])
+                                          (77, 192, 256, "gelu", False),
+                                          # <= 4 rows: the GEMV (RowStats producer, RowLn / ResLn consumers)
+                                          (4, 1024, 1024, None, False), (4, 4096, 1024, "gelu", False),
+                                          (1, 3072, 1024, None, True), (3, 1024, 1024, "gelu", False)])
 def test_gemm_row_ln_fold(gpu, M, N, K, act, kv):
     # decode LayerNorm folding (dec and 128x128 kernels): a producer GEMM writes the row
     # partials of its bf16 output (RowStats), a RowLn consumer and a ResLn consumer normalise
