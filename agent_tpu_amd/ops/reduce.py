@@ -1,7 +1,8 @@
 """Streaming count/sum/min/max in fp64 (K12) for ``risk_accumulate``.
 
 Native kernels: ``csrc/kernels/head_reduce.hip``. The multi-GPU variant (RCCL
-all-reduce of the per-rank partials) is :mod:`agent_tpu_amd.parallel.risk`.
+all-reduce of the per-rank partials) is the ``risk_accumulate`` DP task in
+:mod:`agent_tpu_amd.parallel.dp_ops` (:func:`~agent_tpu_amd.parallel.dp_ops.risk_task`).
 """
 from __future__ import annotations
 

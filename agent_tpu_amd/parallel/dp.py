@@ -101,6 +101,8 @@ def native_comm(dev: torch.device):
 
     if not (rccl.enabled() and is_dist() and dist.get_backend() == "nccl" and dev.type == "cuda"):
         return None
+    if _NATIVE is not None and not _NATIVE.healthy():
+        _NATIVE = None  # aborted by a failed wait (or an async error): rebuilt collectively below
     if _NATIVE is None:
         with watchdog.collective("rccl communicator init"):
             _NATIVE = rccl.NativeComm.from_group(dev, group=_GROUP, ranks=members())
@@ -141,6 +143,7 @@ def broadcast_pack(pack, cfg, device: torch.device, src: int = 0, builder=None):
         with watchdog.collective("weight broadcast"):
             if nc is not None:  # C1 on the native communicator (group rank of the source)
                 nc.broadcast(buf, root=members().index(src))
+                nc.wait("weight broadcast")  # complete inside the bracket: hang detection
             else:
                 dist.broadcast(buf, src=src, group=_GROUP)
         if buf is not out.buffer:
@@ -175,6 +178,7 @@ def all_gather_rows(*tensors: torch.Tensor) -> Tuple[torch.Tensor, ...]:
     with watchdog.collective("row-count gather"):
         if nc is not None:
             nc.all_gather_into(counts, cnt)
+            nc.wait("row-count gather")
         else:
             dist.all_gather_into_tensor(counts, cnt, group=_GROUP)
     counts_l: List[int] = counts.tolist()
@@ -190,6 +194,7 @@ def all_gather_rows(*tensors: torch.Tensor) -> Tuple[torch.Tensor, ...]:
         with watchdog.collective("row all-gather"):
             if nc is not None:
                 nc.all_gather_into(g, t)
+                nc.wait("row all-gather")
             else:
                 dist.all_gather_into_tensor(g, t, group=_GROUP)
         if all(c == mx for c in counts_l):

@@ -449,6 +449,7 @@ def risk_task(payload: Dict[str, Any]) -> Any:
             if nc is not None:
                 nc.all_reduce(sums, "sum")
                 nc.all_reduce(ext, "max")
+                nc.wait("risk all-reduce")
             else:
                 dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=dp.group())
                 dist.all_reduce(ext, op=dist.ReduceOp.MAX, group=dp.group())

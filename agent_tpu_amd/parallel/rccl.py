@@ -87,6 +87,36 @@ class NativeComm:
     def healthy(self) -> bool:
         return self.comm.async_error() == 0
 
+    def wait(self, stage: str = "collective", timeout: Optional[float] = None) -> None:
+        """Block until the collectives enqueued on the current stream have finished.
+
+        Native RCCL calls only ENQUEUE work, so without this the host would block later
+        (``.tolist()``, ``.cpu()``) outside the watchdog bracket, where a peer that is
+        alive but hung is never diagnosed, and this communicator has no timeout watchdog
+        of its own (ProcessGroupNCCL does). Polls the stream event and ncclCommGetAsyncError
+        with a deadline (``DP_COLLECTIVE_TIMEOUT``); on an async error or the deadline the
+        communicator is aborted (freeing the stream) and the caller gets a RuntimeError,
+        which the surrounding ``watchdog.collective`` turns into a RankLost diagnosis."""
+        import time
+
+        from . import watchdog
+
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.comm.device))
+        limit = watchdog.collective_timeout() if timeout is None else timeout
+        t_end = time.monotonic() + limit
+        pause = 20e-6
+        while not ev.query():
+            err = self.comm.async_error()
+            if err != 0:
+                self.comm.abort()
+                raise RuntimeError(f"rccl {stage}: async error {err}")
+            if time.monotonic() > t_end:
+                self.comm.abort()
+                raise RuntimeError(f"rccl {stage}: not complete after {limit:.0f} s")
+            time.sleep(pause)
+            pause = min(pause * 2, 2e-3)
+
 
 def local_comms(devices: List[int]) -> List[NativeComm]:
     """Single-process communicators over local GPUs (ncclCommInitAll):

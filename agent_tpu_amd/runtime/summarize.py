@@ -115,7 +115,13 @@ class _SlotCache:
             return False
         idle = sorted((s for s in self.slots if not s.busy), key=lambda s: s.last)
         while idle and (len(self.slots) >= self.max_slots or self.nbytes() + need > self.max_bytes):
-            self.slots.remove(idle.pop(0))
+            victim = idle.pop(0)
+            # its last replay may still run on another stream (a host-selection search can
+            # stop with a speculative step in flight): the caching allocator must not hand
+            # its buffers to a new allocation before that replay has finished
+            if victim.ev is not None:
+                victim.ev.synchronize()
+            self.slots.remove(victim)
         if len(self.slots) >= self.max_slots or self.nbytes() + need > self.max_bytes:
             return False
         sl.busy, sl.last = True, time.perf_counter()

@@ -443,9 +443,13 @@ class Agent:
         with self._inflight_lock:
             jobs, self._inflight = dict(self._inflight), {}
         err = {"type": "RankLost", "message": msg, "trace": ""}
+        # this runs on the watchdog thread while the main thread may be mid-request on
+        # self.ctl (one keep-alive http.client connection, not thread-safe): post on a
+        # connection of its own so the failures cannot interleave with that request
+        ctl = Controller(CONTROLLER_URL, HTTP_TIMEOUT_SEC)
         for job_id, (lease_id, epoch, op) in jobs.items():
             try:
-                self.ctl.result(lease_id, job_id, epoch, "failed", None, err)
+                ctl.result(lease_id, job_id, epoch, "failed", None, err)
             except Exception as exc:
                 print(f"{LOG} post result error: {exc}", flush=True)
             log_every("exec", f"{LOG} FAIL job={job_id} op={op} err={err}")

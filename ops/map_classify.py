@@ -75,29 +75,45 @@ def classify_batch(h, payloads: List[Dict[str, Any]], rank: int, ws: int) -> Opt
     from agent_tpu_amd.parallel.dp_ops import _check_errors, _err_str
 
     out: List[Any] = [None] * len(payloads)
+    # ``output`` is validated per job before any device work, on every rank (same payloads
+    # everywhere -> same outcome): a bad value fails only its own job, as in the single-job
+    # path (run() -> _output_form), never the batch it was leased with
+    for i, p in enumerate(payloads):
+        try:
+            _output_form(p)
+        except Exception as exc:
+            out[i] = ("err", exc)
     # ---- input form: rank 0 only (as the single-job path) ----
     rows = []
     if rank == 0:
         for i, p in enumerate(payloads):
-            if "input" in p:
+            if "input" in p and out[i] is None:
                 try:
                     rows.append((i,) + _input_row(h, p))
                 except Exception as exc:
                     out[i] = ("err", exc)
         if rows:
-            kmax = max(r[3] for r in rows)
-            res = h.engine.classify_ids(torch.stack([r[1] for r in rows]),
-                                        torch.tensor([r[2] for r in rows], dtype=torch.int32), kmax)
-            idx_all, sc_all = res.idx.tolist(), res.score.tolist()
-            for (i, _, _, k), ir, sr in zip(rows, idx_all, sc_all):
-                p = payloads[i]
-                out[i] = ("ok", {"op": p.get("_op", OP_NAME), "model_path": h.model_path,
-                                 "topk": _topk_list(ir[:k], sr[:k]),
-                                 "elapsed_ms": (time.time() - float(p.get("_t0", time.time()))) * 1000.0})
+            # a failure here (HIP fault, OOM on the stacked rows) fails the input jobs only:
+            # raised out of the task it would leave the workers alone in the texts
+            # section's collectives below (hang until the collective timeout)
+            try:
+                kmax = max(r[3] for r in rows)
+                res = h.engine.classify_ids(torch.stack([r[1] for r in rows]),
+                                            torch.tensor([r[2] for r in rows], dtype=torch.int32), kmax)
+                idx_all, sc_all = res.idx.tolist(), res.score.tolist()
+            except Exception as exc:
+                for r in rows:
+                    out[r[0]] = ("err", exc)
+            else:
+                for (i, _, _, k), ir, sr in zip(rows, idx_all, sc_all):
+                    p = payloads[i]
+                    out[i] = ("ok", {"op": p.get("_op", OP_NAME), "model_path": h.model_path,
+                                     "topk": _topk_list(ir[:k], sr[:k]),
+                                     "elapsed_ms": (time.time() - float(p.get("_t0", time.time()))) * 1000.0})
     # ---- texts form: every rank (same payloads everywhere -> same validation outcome) ----
     tjobs = []
     for i, p in enumerate(payloads):
-        if "input" not in p and "texts" in p:
+        if "input" not in p and "texts" in p and out[i] is None:
             try:
                 tjobs.append((i, check_texts(p), max(1, min(int(p.get("topk", 5)), h.cfg.num_labels))))
             except Exception as exc:

@@ -31,6 +31,11 @@ def _classify_jobs():
                                                        "model_path": MODEL, "topk": 3}},
         {"id": "t2", "op": "map_classify", "payload": {"texts": ["eta theta iota kappa"] * 6, "model_path": MODEL}},
         {"id": "c", "op": "map_classify", "payload": {"input": _ids(5), "model_path": MODEL, "topk": 1}},
+        # a bad ``output`` fails only its own job: texts and input forms, soft and strict
+        {"id": "bo1", "op": "map_classify", "payload": {"texts": ["x y"], "model_path": MODEL, "output": "xml"}},
+        {"id": "bo2", "op": "map_classify", "payload": {"input": _ids(3), "model_path": MODEL, "output": 7}},
+        {"id": "bo3", "op": "map_classify", "payload": {"texts": ["x"], "model_path": MODEL, "output": "xml",
+                                                        "allow_fallback": False}},
     ]
     return jobs
 
@@ -82,6 +87,13 @@ def test_classify_lease_batch_matches_single():
         for x, y in zip(rb["rows"], rs["rows"]):
             assert x["row"] == y["row"] and [t["index"] for t in x["topk"]] == [t["index"] for t in y["topk"]]
     assert len(batched["t1"]["result"]["rows"][0]["topk"]) == 3
+    for jid in ("bo1", "bo2"):
+        rb, rs = batched[jid]["result"], single[jid]["result"]
+        assert rb["fallback"] == "cpu" and rb["reason"] == rs["reason"], (rb, rs)
+        assert "payload.output must be" in rb["reason"]
+    assert batched["bo3"]["status"] == single["bo3"]["status"] == "failed"
+    assert batched["bo3"]["error"]["type"] == "ValueError"
+    assert batched["bo3"]["error"]["message"] == single["bo3"]["error"]["message"]
 
 
 def test_summarize_lease_batch_matches_single():
