@@ -15,6 +15,34 @@ import torch
 _ALIGN = 256
 
 
+def _h2d_staged(src: torch.Tensor, device: torch.device, chunk: int = 32 << 20) -> torch.Tensor:
+    """Host (pageable) -> device copy of a flat byte buffer through two pinned staging
+    buffers: the host memcpy of chunk i+1 overlaps the DMA of chunk i on a side stream.
+    A pageable ``tensor.to(device)`` is a staged copy inside the runtime at a fraction of
+    the link rate; this is the weight-upload path of every model load (C1 source, LRU miss)."""
+    n = src.numel()
+    dst = torch.empty(n, dtype=torch.uint8, device=device)
+    if n == 0:
+        return dst
+    chunk = min(chunk, n)
+    stream = torch.cuda.Stream(device)
+    pins = [torch.empty(chunk, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    done = [None, None]
+    with torch.cuda.stream(stream):
+        for i, off in enumerate(range(0, n, chunk)):
+            k = i & 1
+            m = min(chunk, n - off)
+            if done[k] is not None:
+                done[k].synchronize()  # the DMA that last read this staging buffer has finished
+            pins[k][:m].copy_(src[off:off + m])
+            dst[off:off + m].copy_(pins[k][:m], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            done[k] = ev
+    stream.synchronize()
+    return dst
+
+
 class ParamPack:
     def __init__(self, specs: Iterable[Tuple[str, Tuple[int, ...], torch.dtype]], device="cpu"):
         self.specs = list(specs)
@@ -53,7 +81,11 @@ class ParamPack:
     def to(self, device) -> "ParamPack":
         out = ParamPack.__new__(ParamPack)
         out.specs, out.layout, out.nbytes = self.specs, self.layout, self.nbytes
-        out.buffer = self.buffer.to(device)
+        device = torch.device(device)
+        if device.type == "cuda" and self.buffer.device.type == "cpu" and not self.buffer.is_pinned():
+            out.buffer = _h2d_staged(self.buffer, device)
+        else:
+            out.buffer = self.buffer.to(device)
         out._views = out._make_views()
         return out
 

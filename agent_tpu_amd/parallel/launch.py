@@ -27,6 +27,30 @@ class LaunchError(RuntimeError):
     pass
 
 
+# Environment every GPU rank process needs, whichever launcher started it.
+#
+# HSA_ENABLE_IPC_MODE_LEGACY=0: the amdgpu host driver of the MI355X pool supports only
+# dmabuf-based IPC. With the legacy IPC mode the ROCr runtime's hipIpcGetMemHandle fails
+# ("invalid argument"), and RCCL uses IPC handles to map its peer buffers between the
+# ranks' processes (intra-node P2P transport over xGMI): communicator setup then fails.
+# The variable is read when the HSA runtime initialises, i.e. at the first HIP call, so
+# each entry point applies it at import, before anything touches the GPU. setdefault: an
+# operator's explicit value wins.
+RANK_ENV_DEFAULTS = {"HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+
+
+def ensure_rank_env(env: Optional[Dict[str, str]] = None) -> Dict[str, str]:
+    """Apply :data:`RANK_ENV_DEFAULTS` to ``env`` (default: this process's environment).
+
+    Called at import by ``bench.py`` and ``app.py`` (so a rank started by an external
+    ``torch.distributed.run`` gets it exactly like one started by :func:`self_launch`)
+    and by :func:`self_launch` for the child launcher's environment."""
+    target = os.environ if env is None else env
+    for k, v in RANK_ENV_DEFAULTS.items():
+        target.setdefault(k, v)
+    return target
+
+
 def free_port() -> int:
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
@@ -90,7 +114,7 @@ def self_launch(script: str, argv: Sequence[str], nproc: int, env: Optional[Dict
     child_env = dict(os.environ)
     child_env.update(env or {})
     child_env[RESULT_ENV] = res_path
-    child_env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    ensure_rank_env(child_env)
     child_env.setdefault("OMP_NUM_THREADS", "4")
     objs: List[Dict[str, Any]] = []
     proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=None, env=child_env, text=True, bufsize=1)

@@ -49,6 +49,13 @@ except Exception:  # pragma: no cover
 
 LOG = "[agent-mi355x]"
 
+# rank-process environment (RCCL IPC mode), applied before any GPU use however the agent
+# was launched (plain, or one rank per GPU under torch.distributed.run): see
+# agent_tpu_amd.parallel.launch.RANK_ENV_DEFAULTS (a stdlib-only module)
+from agent_tpu_amd.parallel.launch import ensure_rank_env  # noqa: E402
+
+ensure_rank_env()
+
 # ------------------------------------------------------------------ config
 # identical names and defaults to the reference (app.py:21-41)
 CONTROLLER_URL = os.getenv("CONTROLLER_URL", "").rstrip("/") or "http://10.11.12.54:8080"

@@ -115,3 +115,48 @@ def test_probe_vram_sysfs(tmp_path):
         (d / "mem_info_vram_total").write_text(f"{tot}\n")
     (tmp_path / "card0-DP-1").mkdir()
     assert probe_vram(str(tmp_path)) == [(5 << 30, 288 << 30), (7 << 30, 288 << 30)]
+
+
+_ENV_PROBE = """
+import json, os, sys
+os.environ.pop("HSA_ENABLE_IPC_MODE_LEGACY", None) if os.environ.get("ATPU_PROBE_CLEAR") == "1" else None
+sys.path.insert(0, {repo!r})
+import importlib.util
+spec = importlib.util.spec_from_file_location("entry", os.path.join({repo!r}, {entry!r}))
+mod = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(mod)  # module import only: main() is not run
+from agent_tpu_amd.parallel.launch import emit_result
+rank = int(os.environ.get("RANK", "0"))
+val = os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY")
+if rank == 0:
+    emit_result({{"rank0": val}})
+print(json.dumps({{"rank": rank, "val": val}}), flush=True)
+"""
+
+
+@pytest.mark.parametrize("entry", ["bench.py", "app.py"])
+def test_rank_env_identical_under_both_launch_forms(tmp_path, entry):
+    """the rank processes see HSA_ENABLE_IPC_MODE_LEGACY=0 whether the
+    ranks come from the driver's external ``torch.distributed.run`` or from bench.py's
+    own self-launch, even when the launching environment does not carry it."""
+    from agent_tpu_amd.parallel.launch import RANK_ENV_DEFAULTS, torchrun_cmd
+
+    assert RANK_ENV_DEFAULTS == {"HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+    script = tmp_path / "probe.py"
+    script.write_text(_ENV_PROBE.format(repo=REPO, entry=entry))
+    env = {k: v for k, v in os.environ.items() if k != "HSA_ENABLE_IPC_MODE_LEGACY"}
+    env.update(OMP_NUM_THREADS="1", ATPU_PROBE_CLEAR="1", TASKS="echo")
+    # external form (as the driver runs bench.py): python -m torch.distributed.run ... script
+    r = subprocess.run(torchrun_cmd(str(script), [], 2), env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    vals = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"rank"')]
+    assert sorted(v["rank"] for v in vals) == [0, 1] and all(v["val"] == "0" for v in vals), r.stdout
+    # self-launch form: the child launcher's env gets it too (and the import sets it again)
+    rc, objs = self_launch(str(script), [], 2, env={"OMP_NUM_THREADS": "1", "ATPU_PROBE_CLEAR": "1",
+                                                    "TASKS": "echo"}, timeout=180)
+    assert rc == 0 and objs == [{"rank0": "0"}]
+    # an operator's explicit value wins (setdefault)
+    env2 = dict(env, ATPU_PROBE_CLEAR="0", HSA_ENABLE_IPC_MODE_LEGACY="1")
+    r = subprocess.run(torchrun_cmd(str(script), [], 2), env=env2, capture_output=True, text=True, timeout=180)
+    vals = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"rank"')]
+    assert r.returncode == 0 and all(v["val"] == "1" for v in vals), r.stdout + r.stderr[-1000:]
