@@ -18,6 +18,7 @@
 #include "atpu/common.h"
 #include "atpu/csv.h"
 #include "atpu/kernels.h"
+#include "atpu/risk_stream.h"
 #include "atpu/runtime.h"
 
 namespace py = pybind11;
@@ -364,6 +365,9 @@ PYBIND11_MODULE(_atpu, m) {
                              })
       .def_property_readonly("index_from_cache", &CsvTable::index_from_cache)
       .def("column_index", &CsvTable::column_index)
+      .def("parse_double", [](const CsvTable& t, size_t row, int col) { return t.parse_double(row, col); },
+           "field col of data record row as a float (extract_doubles' parse; ValueError on a bad value)")
+      .def("release_pages", &CsvTable::release_pages)
       .def("row",
            [](const CsvTable& t, size_t i) {
              std::vector<std::string> f;
@@ -396,6 +400,22 @@ PYBIND11_MODULE(_atpu, m) {
              return out;
            },
            py::arg("start"), py::arg("n"), py::arg("col"), py::arg("threads") = 8)
+      .def("extract_doubles_into",
+           [](const CsvTable& t, size_t start, size_t n, int col, py::array_t<double, py::array::c_style> out,
+              int threads) {
+             if (start > t.num_rows()) start = t.num_rows();
+             n = std::min(n, t.num_rows() - start);
+             if (static_cast<size_t>(out.size()) < n) throw std::invalid_argument("extract_doubles_into: out too small");
+             double* dst = out.mutable_data();
+             {
+               py::gil_scoped_release nogil;
+               t.extract_doubles(start, n, col, dst, threads);
+               if (n) t.release_pages(t.row_begin(start), t.row_end(start + n - 1));  // streamed: drop consumed pages
+             }
+             return n;
+           },
+           py::arg("start"), py::arg("n"), py::arg("col"), py::arg("out"), py::arg("threads") = 8,
+           "float_column into a caller-owned buffer (chunked streaming without per-chunk allocations)")
       .def("extract_column",
            [](const CsvTable& t, size_t start, size_t n, int col, size_t max_bytes, int threads) {
              if (start > t.num_rows()) start = t.num_rows();
@@ -446,6 +466,31 @@ PYBIND11_MODULE(_atpu, m) {
   m.def("rccl_group_start", &rccl_group_start);
   m.def("rccl_group_end", &rccl_group_end);
   m.def("rccl_version", &rccl_version);
+
+  py::class_<RiskStream>(m, "RiskStream")
+      .def(py::init<size_t, size_t, int>(), py::arg("slot_bytes"), py::arg("slot_rows"), py::arg("fallback_cap"))
+      .def("run",
+           [](RiskStream& r, std::shared_ptr<CsvTable> t, size_t start, size_t n, int col, uintptr_t copy_stream,
+              uintptr_t compute_stream, int threads) {
+             RiskStream::Result res;
+             {
+               py::gil_scoped_release nogil;
+               res = r.run(*t, start, n, col, S(copy_stream), S(compute_stream), threads);
+             }
+             py::dict d;
+             d["count"] = res.count;
+             d["sum"] = res.sum;
+             d["min"] = res.min;
+             d["max"] = res.max;
+             d["host_rows"] = py::array_t<int64_t>(res.host_rows.size(), res.host_rows.data());
+             d["fallback_total"] = res.fallback_total;
+             d["overflow"] = res.overflow;
+             d["chunks"] = res.chunks;
+             d["bytes"] = res.bytes;
+             return d;
+           })
+      .def_property_readonly("slot_bytes", &RiskStream::slot_bytes)
+      .def_property_readonly("slot_rows", &RiskStream::slot_rows);
 
   py::class_<HostStager>(m, "HostStager")
       .def(py::init<int, size_t, int>(), py::arg("slots"), py::arg("text_capacity"), py::arg("max_rows"))

@@ -40,6 +40,21 @@ class CsvTable {
   // std::invalid_argument naming the first bad value.
   void extract_doubles(size_t start, size_t n, int col, double* out, int threads) const;
 
+  // Field `col` of data record `row` as a double, exactly as extract_doubles parses it
+  // (same std::invalid_argument on a bad value). The streamed risk reduce's host fallback.
+  double parse_double(size_t row, int col) const;
+
+  // Raw bytes of the mapped file and the byte range of data record `row` (its start and
+  // the start of the next record, or the file end): the streamed risk reduce ships these
+  // bytes to the GPU, which parses the field itself (K13).
+  const char* data() const { return data_; }
+  uint64_t row_begin(size_t row) const { return starts_[row]; }
+  uint64_t row_end(size_t row) const { return row + 1 < starts_.size() ? starts_[row + 1] : size_; }
+  // Drop this process's mapping of the pages inside [begin, end) (page-aligned inward):
+  // a streamed pass over a large shard keeps its resident set bounded (the pages stay in
+  // the page cache; a later access faults them back in).
+  void release_pages(uint64_t begin, uint64_t end) const;
+
   // Pack field `col` of rows [start, start+n) into `out` (capacity `cap`
   // bytes) with int32 offsets[n+1]; each value truncated to `max_bytes`.
   // Work is split over `threads` host threads. Returns bytes written, or -1

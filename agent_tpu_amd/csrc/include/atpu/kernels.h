@@ -175,6 +175,16 @@ int reduce_stats_blocks(int64_t n);
 void reduce_stats_f64(const double* x, int64_t n, double* partial, int blocks, hipStream_t stream);
 void reduce_stats_f32(const float* x, int64_t n, double* partial, int blocks, hipStream_t stream);
 void reduce_stats_finalize(const double* partial, int blocks, double* out, hipStream_t stream);
+// acc[4] (+)= the reduction of a launch's block partials (first: overwrite); streamed reduces
+void reduce_stats_accumulate(const double* partial, int blocks, double* acc, bool first, hipStream_t stream);
+// K13+K12 over raw CSV records (runtime/risk_stream.cpp): record r is text[offs[r], offs[r+1]);
+// field `col` parsed on the device (exact fast path), block partials [blocks][4] like
+// reduce_stats_*; records the fast path cannot take are appended (global row row0 + r) to
+// fb_rows (first fb_cap of them; *fb_count counts all) for the host to parse.
+constexpr int kCsvMaxBlocks = 2048;
+int csv_parse_blocks(int64_t n);
+void csv_parse_reduce(const uint8_t* text, const uint32_t* offs, int n, int col, int64_t row0, double* partial,
+                      int blocks, int* fb_count, int64_t* fb_rows, int fb_cap, hipStream_t stream);
 
 }  // namespace atpu
 

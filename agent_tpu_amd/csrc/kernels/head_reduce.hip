@@ -168,6 +168,153 @@ __global__ __launch_bounds__(64) void reduce_finalize_kernel(const double* __res
   }
 }
 
+// accumulate one launch's block partials into a running device total (streamed
+// reduces: one call per chunk, in chunk order -> deterministic)
+__global__ __launch_bounds__(64) void reduce_accumulate_kernel(const double* __restrict__ partial, int blocks,
+                                                               double* __restrict__ acc, int first) {
+  double cnt = 0, sum = 0, lo = DBL_MAX, hi = -DBL_MAX;
+  for (int i = threadIdx.x; i < blocks; i += 64) {
+    cnt += partial[4 * i];
+    sum += partial[4 * i + 1];
+    lo = fmin(lo, partial[4 * i + 2]);
+    hi = fmax(hi, partial[4 * i + 3]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    cnt += __shfl_xor(cnt, o, 64);
+    sum += __shfl_xor(sum, o, 64);
+    lo = fmin(lo, __shfl_xor(lo, o, 64));
+    hi = fmax(hi, __shfl_xor(hi, o, 64));
+  }
+  if (threadIdx.x == 0) {
+    if (first) {
+      acc[0] = cnt; acc[1] = sum; acc[2] = lo; acc[3] = hi;
+    } else {
+      acc[0] += cnt; acc[1] += sum; acc[2] = fmin(acc[2], lo); acc[3] = fmax(acc[3], hi);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- K13 + K12
+// Streamed risk reduce over a raw CSV chunk (runtime/risk_stream.cpp): the host ships
+// the chunk's record bytes and per-record offsets; one thread per record finds field
+// `col` and parses it, and the values are reduced as in reduce_stats_kernel.
+
+__constant__ double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                  1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+__device__ __forceinline__ bool csv_blank(int c) { return c == ' ' || c == '\t' || c == '\v' || c == '\f'; }
+__device__ __forceinline__ bool csv_digit(int c) { return c >= '0' && c <= '9'; }
+
+// Field `col` of the record [i, e) as a double by the exact fast path (Clinger): at most 19
+// significant digits whose integer value w <= 2^53 and a decimal exponent |q| <= 22 give
+// w * 10^q (or w / 10^-q) in ONE correctly rounded IEEE operation on two exact operands,
+// i.e. the double strtod returns. Everything else (a quote before or in the field, more
+// digits, a larger exponent, inf / nan / hex, bad syntax, a missing field) returns false
+// and the host re-parses that record with strtod (CsvTable::parse_double): the same value,
+// or the same error.
+__device__ bool csv_field_number(const uint8_t* __restrict__ t, uint32_t i, uint32_t e, int col, double* out) {
+  for (int f = 0; f < col; ++f) {
+    for (;;) {
+      if (i >= e) return false;
+      const int c = t[i++];
+      if (c == ',') break;
+      if (c == '"' || c == '\n' || c == '\r') return false;
+    }
+  }
+  while (i < e && csv_blank(t[i])) ++i;
+  bool neg = false;
+  if (i < e && (t[i] == '+' || t[i] == '-')) neg = t[i++] == '-';
+  uint64_t w = 0;
+  int nd = 0, frac = 0;
+  bool any = false;
+  for (; i < e && csv_digit(t[i]); ++i) {
+    const int d = t[i] - '0';
+    any = true;
+    if (w || d) {
+      if (++nd > 19) return false;
+      w = w * 10 + d;
+    }
+  }
+  if (i < e && t[i] == '.') {
+    for (++i; i < e && csv_digit(t[i]); ++i) {
+      const int d = t[i] - '0';
+      any = true;
+      ++frac;
+      if (w || d) {
+        if (++nd > 19) return false;
+        w = w * 10 + d;
+      }
+    }
+  }
+  if (!any) return false;
+  int ex = 0;
+  if (i < e && (t[i] == 'e' || t[i] == 'E')) {
+    ++i;
+    bool eneg = false;
+    if (i < e && (t[i] == '+' || t[i] == '-')) eneg = t[i++] == '-';
+    int ed = 0;
+    for (; i < e && csv_digit(t[i]); ++i) {
+      if (++ed > 4) return false;
+      ex = ex * 10 + (t[i] - '0');
+    }
+    if (!ed) return false;
+    if (eneg) ex = -ex;
+  }
+  while (i < e && csv_blank(t[i])) ++i;
+  if (i < e && !(t[i] == ',' || t[i] == '\n' || t[i] == '\r')) return false;
+  const int q = ex - frac;
+  double v;
+  if (w == 0) {
+    v = 0.0;
+  } else if (w <= (1ull << 53) && q >= -22 && q <= 22) {
+    v = q >= 0 ? (double)w * kPow10[q] : (double)w / kPow10[-q];
+  } else {
+    return false;
+  }
+  *out = neg ? -v : v;
+  return true;
+}
+
+__global__ __launch_bounds__(kRedThreads) void csv_parse_reduce_kernel(
+    const uint8_t* __restrict__ text, const uint32_t* __restrict__ offs, int n, int col, int64_t row0,
+    double* __restrict__ partial, int* __restrict__ fb_count, int64_t* __restrict__ fb_rows, int fb_cap) {
+  __shared__ double sh[4][kRedThreads / 64];
+  RedAcc a;
+  for (int r = blockIdx.x * kRedThreads + threadIdx.x; r < n; r += gridDim.x * kRedThreads) {
+    double v;
+    if (csv_field_number(text, offs[r], offs[r + 1], col, &v)) {
+      a.add(v);
+    } else {
+      const int k = atomicAdd(fb_count, 1);  // vector atomic, returns the slot
+      if (k < fb_cap) fb_rows[k] = row0 + r;
+    }
+  }
+  double cnt = a.cnt, sum = a.sum + a.comp, lo = a.lo, hi = a.hi;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    cnt += __shfl_xor(cnt, o, 64);
+    sum += __shfl_xor(sum, o, 64);
+    lo = fmin(lo, __shfl_xor(lo, o, 64));
+    hi = fmax(hi, __shfl_xor(hi, o, 64));
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[0][w] = cnt; sh[1][w] = sum; sh[2][w] = lo; sh[3][w] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < kRedThreads / 64; ++i) {
+      sh[0][0] += sh[0][i]; sh[1][0] += sh[1][i];
+      sh[2][0] = fmin(sh[2][0], sh[2][i]); sh[3][0] = fmax(sh[3][0], sh[3][i]);
+    }
+    partial[4 * blockIdx.x + 0] = sh[0][0];
+    partial[4 * blockIdx.x + 1] = sh[1][0];
+    partial[4 * blockIdx.x + 2] = sh[2][0];
+    partial[4 * blockIdx.x + 3] = sh[3][0];
+  }
+}
+
 }  // namespace
 
 void classify_head_topk(const bf16* pooled, int ldp, const bf16* Wc, const float* bc, float* logits,
@@ -199,6 +346,25 @@ void reduce_stats_f32(const float* x, int64_t n, double* partial, int blocks, hi
 
 void reduce_stats_finalize(const double* partial, int blocks, double* out, hipStream_t stream) {
   hipLaunchKernelGGL(reduce_finalize_kernel, dim3(1), dim3(64), 0, stream, partial, blocks, out);
+  ATPU_HIP_CHECK(hipGetLastError());
+}
+
+int csv_parse_blocks(int64_t n) {
+  // ~16 records per thread, at most 2048 blocks (kCsvMaxBlocks: the partial buffers' size)
+  const int64_t want = (n + kRedThreads * 16 - 1) / (kRedThreads * 16);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(want, kCsvMaxBlocks));
+}
+
+void csv_parse_reduce(const uint8_t* text, const uint32_t* offs, int n, int col, int64_t row0, double* partial,
+                      int blocks, int* fb_count, int64_t* fb_rows, int fb_cap, hipStream_t stream) {
+  ATPU_CHECK(blocks >= 1 && blocks <= kCsvMaxBlocks && col >= 0, "csv_parse_reduce: bad launch");
+  hipLaunchKernelGGL(csv_parse_reduce_kernel, dim3(blocks), dim3(kRedThreads), 0, stream, text, offs, n, col, row0,
+                     partial, fb_count, fb_rows, fb_cap);
+  ATPU_HIP_CHECK(hipGetLastError());
+}
+
+void reduce_stats_accumulate(const double* partial, int blocks, double* acc, bool first, hipStream_t stream) {
+  hipLaunchKernelGGL(reduce_accumulate_kernel, dim3(1), dim3(64), 0, stream, partial, blocks, acc, first ? 1 : 0);
   ATPU_HIP_CHECK(hipGetLastError());
 }
 

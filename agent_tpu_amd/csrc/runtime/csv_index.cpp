@@ -292,6 +292,39 @@ int64_t CsvTable::extract_column(size_t start, size_t n, int col, uint8_t* out, 
   return static_cast<int64_t>(total);
 }
 
+namespace {
+
+// Python float() syntax minus '_' separators, surrounding whitespace ignored; false on a bad value
+bool field_to_double(const std::string& field, double* out) {
+  size_t b = 0, e = field.size();
+  while (b < e && std::isspace(static_cast<unsigned char>(field[b]))) ++b;
+  while (e > b && std::isspace(static_cast<unsigned char>(field[e - 1]))) --e;
+  const std::string v = field.substr(b, e - b);
+  char* end = nullptr;
+  const double d = v.empty() ? 0.0 : std::strtod(v.c_str(), &end);
+  if (v.empty() || end != v.c_str() + v.size()) return false;
+  *out = d;
+  return true;
+}
+
+}  // namespace
+
+double CsvTable::parse_double(size_t row, int col) const {
+  if (row >= starts_.size()) throw std::out_of_range("row out of range");
+  std::string field;
+  parse_field(starts_[row], col, field, 4096);
+  double d = 0.0;
+  if (!field_to_double(field, &d)) throw std::invalid_argument("could not convert string to float: '" + field + "'");
+  return d;
+}
+
+void CsvTable::release_pages(uint64_t begin, uint64_t end) const {
+  if (!data_ || end <= begin) return;
+  const uint64_t pg = static_cast<uint64_t>(::sysconf(_SC_PAGESIZE));
+  const uint64_t b = (begin + pg - 1) / pg * pg, e = std::min(end, size_) / pg * pg;
+  if (e > b) ::madvise(const_cast<char*>(data_) + b, e - b, MADV_DONTNEED);
+}
+
 void CsvTable::extract_doubles(size_t start, size_t n, int col, double* out, int threads) const {
   if (start > starts_.size()) start = starts_.size();
   n = std::min(n, starts_.size() - start);
@@ -302,17 +335,10 @@ void CsvTable::extract_doubles(size_t start, size_t n, int col, double* out, int
     std::string field;
     for (size_t r = lo; r < hi; ++r) {
       parse_field(starts_[r], col, field, 4096);
-      size_t b = 0, e = field.size();
-      while (b < e && std::isspace(static_cast<unsigned char>(field[b]))) ++b;
-      while (e > b && std::isspace(static_cast<unsigned char>(field[e - 1]))) --e;
-      const std::string v = field.substr(b, e - b);
-      char* end = nullptr;
-      const double d = v.empty() ? 0.0 : std::strtod(v.c_str(), &end);
-      if (v.empty() || end != v.c_str() + v.size()) {
+      if (!field_to_double(field, &out[r - start])) {
         errors[t] = "could not convert string to float: '" + field + "'";
         return;
       }
-      out[r - start] = d;
     }
   };
   if (threads == 1) {

@@ -421,6 +421,28 @@ def _local_values(payload: Dict[str, Any], rank: int, ws: int) -> Tuple[torch.Te
     return torch.from_numpy(vals[s_r:s_r + n_r].copy()), len(vals)
 
 
+def csv_stats(payload: Dict[str, Any], rank: int, ws: int, device: Optional[torch.device]):
+    """This rank's share of a CSV ``risk_accumulate``: streamed in chunks (runtime/risk.py),
+    never materialised. -> (fp64 [count, sum, min, max] on the CPU, stream info)."""
+    from ..runtime.risk import column_stats
+
+    table = _open_table(payload["source_uri"])
+    col = table.native.column_index(str(payload.get("field", "risk")))
+    if col < 0:
+        raise ValueError(f"field {payload.get('field', 'risk')!r} not in header {table.header}")
+    start = int(payload.get("start_row", 0))
+    total = max(0, min(int(payload.get("shard_size", table.num_rows)), table.num_rows - start))
+    s_r, n_r = split_range(start, total, ws, rank)
+    return column_stats(table.native, s_r, n_r, col, device)
+
+
+def risk_device() -> Optional[torch.device]:
+    """The GPU the risk reduce runs on (``RISK_DEVICE=cpu`` keeps it on the host)."""
+    if os.getenv("RISK_DEVICE", "auto").strip().lower() == "cpu" or not torch.cuda.is_available():
+        return None
+    return torch.device("cuda", torch.cuda.current_device())
+
+
 @dp_task("risk_accumulate")
 def risk_task(payload: Dict[str, Any]) -> Any:
     from ..ops.reduce import reduce_stats_tensor, stats_dict
@@ -430,12 +452,15 @@ def risk_task(payload: Dict[str, Any]) -> Any:
     err, stats = "", torch.tensor([0.0, 0.0, float("inf"), float("-inf")], dtype=torch.float64)
     try:
         maybe_inject_fault("risk")
-        x, _ = _local_values(payload, rank, ws)
-        if torch.cuda.is_available():
-            dev = torch.device("cuda", torch.cuda.current_device())
-            x = x.to(dev, non_blocking=True)
-        if x.numel():
-            stats = reduce_stats_tensor(x)
+        if "source_uri" in payload:
+            stats, _ = csv_stats(payload, rank, ws, risk_device())
+        else:
+            x, _ = _local_values(payload, rank, ws)
+            if torch.cuda.is_available():
+                dev = torch.device("cuda", torch.cuda.current_device())
+                x = x.to(dev, non_blocking=True)
+            if x.numel():
+                stats = reduce_stats_tensor(x)
     except Exception as exc:
         err = f"{type(exc).__name__}: {exc}"
     _check_errors(err)

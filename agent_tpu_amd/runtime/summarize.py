@@ -658,11 +658,25 @@ class WordMap:
 class SummarizeEngine:
     """Texts -> summaries with a device-resident T5 or BART (batched beam search)."""
 
-    def __init__(self, model, max_source_len: int = 512):
+    def __init__(self, model, max_source_len: int = 512, max_batch_docs: Optional[int] = None):
         self.model = model
         self.cfg = model.cfg
         self.device = model.device
         self.max_src = int(max_source_len)
+        # documents per device batch: what worker_sizing advertises for this model and HBM
+        # (KV cache + cross K/V + encoder activations per document); run() splits larger calls
+        self.max_batch_docs = int(max_batch_docs) if max_batch_docs else self._sized_batch_docs()
+
+    def _sized_batch_docs(self) -> int:
+        from worker_sizing import summarize_batch_docs
+
+        c = self.cfg
+        dims = (c.d_model, c.d_ff, c.enc_layers, c.dec_layers, c.vocab_size)
+        if self.device.type == "cuda":
+            total = torch.cuda.get_device_properties(self.device).total_memory
+        else:
+            total = 288 * (1 << 30)
+        return summarize_batch_docs(total, dims, self.max_src)
 
     def encode_texts(self, texts: Sequence[str], with_maps: bool = True
                      ) -> Tuple[torch.Tensor, torch.Tensor, List[Dict[int, str]]]:
@@ -740,8 +754,17 @@ class SummarizeEngine:
         One host thread runs every part's bookkeeping, so the
         split only pays once a part's GPU step outlasts the other parts' host work
         (T5-base, MI355X: 1024 docs 819 -> 845 docs/s; 256 docs as 2x128: 668 -> 654)."""
-        n = int(os.getenv("ATPU_SUMM_STREAMS", "3"))
         B = int(ids.shape[0])
+        cap = self.max_batch_docs
+        if cap and B > cap:  # HBM-sized device batches, searched one after another
+            outs = [self.run(ids[a:a + cap], lens[a:a + cap], gen) for a in range(0, B, cap)]
+            timing: Dict[str, float] = {}
+            for o in outs:
+                for k, v in o.timing_ms.items():
+                    timing[k] = timing.get(k, 0.0) + v
+            return GenResult([s for o in outs for s in o.sequences], [s for o in outs for s in o.scores],
+                             max(o.steps for o in outs), timing)
+        n = int(os.getenv("ATPU_SUMM_STREAMS", "3"))
         n = max(1, min(n, B // max(1, int(os.getenv("ATPU_SUMM_PART_MIN", "300")))))
         if n < 2 or self.device.type != "cuda" or not gen.device_select:
             return generate(self.model, ids, lens, gen)

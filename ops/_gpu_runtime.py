@@ -124,7 +124,7 @@ def _build_handle(model_path: str, device) -> GpuHandle:
 
     def post(pack):
         spec, cfg = box["spec"], box["cfg"]
-        batch = spec.batch_rows or _auto_batch_rows()
+        batch = spec.batch_rows or _auto_batch_rows(spec.preset, spec.seq_len)
         eng = ClassifyEngine(cfg, pack, device, batch_rows=batch, seq_len=spec.seq_len,
                              topk=min(cfg.num_labels, 64))
         return GpuHandle(spec, cfg, eng)
@@ -132,7 +132,9 @@ def _build_handle(model_path: str, device) -> GpuHandle:
     return load_collectively(local, collective, post)
 
 
-def _auto_batch_rows() -> int:
+def _auto_batch_rows(preset: str = "bert-base", seq_len: int = 128) -> int:
+    """The engine batch of a served model: the SAME function the worker profile advertises
+    (``worker_sizing.classify_batch_rows``, per model and sequence length)."""
     from worker_sizing import classify_batch_rows
 
     try:
@@ -141,7 +143,7 @@ def _auto_batch_rows() -> int:
         total = torch.cuda.get_device_properties(torch.cuda.current_device()).total_memory
     except Exception:
         total = 288 * 1024 ** 3
-    return min(classify_batch_rows(total), 1024)
+    return classify_batch_rows(total, preset, seq_len)
 
 
 _lock = threading.Lock()

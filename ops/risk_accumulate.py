@@ -144,18 +144,18 @@ def risk_accumulate(payload: Dict[str, Any]) -> Dict[str, Any]:
 
         return dispatch("risk_accumulate", payload)
     if "source_uri" in payload:
-        from agent_tpu_amd.ops.reduce import reduce_stats_tensor, stats_dict
-        from agent_tpu_amd.parallel.dp_ops import _local_values
+        # streamed in chunks (agent_tpu_amd/runtime/risk.py): raw record bytes -> pinned slots ->
+        # GPU parse + reduce, chunk i's copy under chunk i-1's kernels; host memory independent
+        # of shard_size
+        from agent_tpu_amd.ops.reduce import stats_dict
+        from agent_tpu_amd.parallel.dp_ops import csv_stats, risk_device
 
-        x, _ = _local_values(payload, 0, 1)
-        if _use_gpu(x.numel()):
-            import torch
-
-            x = x.to(torch.device("cuda", torch.cuda.current_device()))
-        stats = stats_dict(reduce_stats_tensor(x.contiguous()).tolist()) if x.numel() else \
-            {"count": 0, "sum": 0.0, "mean": 0.0, "min": None, "max": None}
-        if x.is_cuda:
+        dev = risk_device() if _use_gpu(GPU_MIN_VALUES) else None
+        st, info = csv_stats(payload, 0, 1, dev)
+        stats = stats_dict(st.tolist())
+        if info["device"] == "gpu":
             stats["device"] = "gpu"
+        stats["stream"] = {"chunks": info["chunks"], "bytes": info["bytes"], "host_rows": info["host_rows"]}
         stats["compute_time_ms"] = (time.time() - t0) * 1000.0
         return stats
     nat = _native()

@@ -70,11 +70,79 @@ def test_gpu_disabled_and_batch_override(kfd, monkeypatch):
 
 
 def test_batch_rows_from_small_hbm(monkeypatch):
-    monkeypatch.delenv("CLASSIFY_BATCH_ROWS", raising=False)
+    for v in ("CLASSIFY_BATCH_ROWS", "CLASSIFY_SEQ_LEN", "HBM_RESERVE_GB", "MODEL_LRU_GB", "CLASSIFY_BATCH_ROWS_CAP"):
+        monkeypatch.delenv(v, raising=False)
     assert ws.classify_batch_rows(288 * GIB) == 1024
-    small = ws.classify_batch_rows(10 * GIB)
-    assert 64 <= small < 1024
-    assert ws.classify_batch_rows(1 * GIB) == 64
+    # 12 GiB: 8 reserved, 3 for the model LRU -> 1 GiB of activations / 3.95 MB per row -> 272 -> 256
+    assert ws.classify_batch_rows(12 * GIB) == 256
+    assert ws.classify_batch_rows(10 * GIB) == 1  # nothing left after reserve + LRU: one row at a time
+
+
+def _presets():
+    from agent_tpu_amd.models import bart, bert, t5
+
+    return bert, t5, bart
+
+
+def test_sizing_tables_match_model_presets():
+    """worker_sizing stays torch-free with its own shape tables; they must match the models."""
+    bert, t5, bart = _presets()
+    for name, (H, I, L, V, P) in ws.CLASSIFY_DIMS.items():
+        c = bert.config_for(name)
+        assert (c.hidden, c.intermediate, c.layers, c.vocab_size, c.max_positions) == (H, I, L, V, P), name
+    for name, dims in ws.SUMMARIZE_DIMS.items():
+        c = (t5 if name.startswith("t5") else bart).config_for(name)
+        assert (c.d_model, c.d_ff, c.enc_layers, c.dec_layers, c.vocab_size) == dims, name
+    from agent_tpu_amd.tokenizer import DEFAULT_MAX_ROW_BYTES
+
+    assert ws.CLASSIFY_MAX_ROW_BYTES == DEFAULT_MAX_ROW_BYTES
+
+
+def test_model_aware_capacity_288gb(kfd, monkeypatch):
+    """VERDICT r3 #6: per-model numbers a 288 GB MI355X advertises, and the engines use them."""
+    for v in ("CLASSIFY_SEQ_LEN", "HBM_RESERVE_GB", "MODEL_LRU_GB", "SUMMARIZE_BATCH_DOCS", "RISK_CHUNK_ROWS",
+              "RISK_STAGING_MB", "GPU_MODEL_PATH", "CLASSIFY_MODEL", "CLASSIFY_BATCH_ROWS_CAP"):
+        monkeypatch.delenv(v, raising=False)
+    cap = ws.detect_gpu()["capacity"]
+    # per-row bytes: slots x (text staging + ids + S*2*(6H + I) activations + LN statistics)
+    assert ws.classify_row_bytes("bert-base", 128) == 3_947_536
+    assert ws.classify_row_bytes("bert-large", 128) == 5_258_256
+    assert cap["classify_batch_rows"] == {"bert-base": 1024, "bert-large": 1024}  # token target binds at 288 GB
+    assert cap["classify_seq_len"] == 128
+    # per-document bytes of a beam search at the reference's settings (src 1024, 4 beams, max 130)
+    assert ws.summarize_doc_bytes("t5-base") == 72_822_144
+    assert ws.summarize_doc_bytes("bart-large-cnn") == 97_127_232
+    assert cap["summarize_batch_docs"] == {"t5-base": 1024, "bart-large-cnn": 1024}
+    assert cap["risk_chunk_rows"] == (256 << 20) // 56  # 256 MiB of pinned staging / (2 slots x (24 + 4) B)
+    # sequence length moves the token target; HBM binds on a small device
+    monkeypatch.setenv("CLASSIFY_SEQ_LEN", "512")
+    assert ws.detect_gpu()["capacity"]["classify_batch_rows"]["bert-large"] == 256
+    assert ws.classify_batch_rows(12 * GIB, "bert-large", 128) == 192  # 1 GiB / 5.26 MB = 204 -> 192
+    assert ws.summarize_batch_docs(24 * GIB, "bart-large-cnn") == 110  # 10 GiB / 97.1 MB
+    # the served classify model's number is the top-level one
+    monkeypatch.setenv("GPU_MODEL_PATH", "bert-large?labels=4")
+    assert ws.detect_gpu()["classify_batch_rows"] == 256
+
+
+def test_engines_use_the_advertised_sizes(monkeypatch):
+    """The engine batch equals the advertised one (CPU: the runtime assumes a 288 GB device)."""
+    for v in ("CLASSIFY_BATCH_ROWS", "CLASSIFY_SEQ_LEN", "HBM_RESERVE_GB", "MODEL_LRU_GB", "SUMMARIZE_BATCH_DOCS"):
+        monkeypatch.delenv(v, raising=False)
+    from ops._gpu_runtime import _auto_batch_rows
+
+    for m, seq in (("bert-base", 128), ("bert-large", 128), ("bert-large", 512), ("bert-base", 64)):
+        assert _auto_batch_rows(m, seq) == ws.classify_batch_rows(288 * GIB, m, seq)
+    assert _auto_batch_rows("bert-base", 64) == 2048
+    import torch
+
+    from agent_tpu_amd.runtime.summarize import SummarizeEngine, build_model
+
+    model, _ = build_model("t5-tiny", device=torch.device("cpu"), seed=0, fp32=True)
+    eng = SummarizeEngine(model, 1024)
+    c = model.cfg
+    assert eng.max_batch_docs == ws.summarize_batch_docs(288 * GIB, (c.d_model, c.d_ff, c.enc_layers,
+                                                                     c.dec_layers, c.vocab_size), 1024)
+    assert SummarizeEngine(model, 64, max_batch_docs=2).max_batch_docs == 2
 
 
 def test_cpu_formulas_match_reference_probe(monkeypatch):

@@ -161,3 +161,85 @@ def test_param_pack_staged_upload(gpu):
     dev = pack.to("cuda")
     assert torch.equal(dev.buffer.cpu(), pack.buffer)
     assert all(torch.equal(dev[n].cpu(), pack[n]) for n in pack.names())
+
+
+def _risk_csv(path, vals):
+    with open(path, "w") as f:
+        f.write("id,risk,tail\n")
+        for i, v in enumerate(vals):
+            f.write(f"{i},{v},t{i % 7}\n")
+    return str(path)
+
+
+def test_risk_stream_gpu_parse_and_chunks(gpu, tmp_path, monkeypatch):
+    """K13+K12 streamed over raw CSV records (RiskStream): record-count and byte-limited
+    chunks, ragged tails; count/min/max exact and the fp64 sum to rounding against the
+    one-pass host parse of the same records."""
+    import numpy as np
+
+    from agent_tpu_amd._native import native
+    from agent_tpu_amd.runtime import risk
+
+    rng = np.random.default_rng(3)
+    vals = [f"{v:.6f}" for v in rng.uniform(-1000, 1000, 250_003)]
+    t = native().CsvTable(_risk_csv(tmp_path / "r.csv", vals))
+    col = t.column_index("risk")
+    ref_all = t.float_column(0, t.num_rows, col)
+    for rows, slot_bytes in ((1 << 20, 0), (4096, 0), (70_000, 65536 * 4)):
+        monkeypatch.setenv("RISK_SLOT_BYTES", str(slot_bytes))
+        for start, n in ((0, 250_003), (3, 123_457), (250_000, 10)):
+            st, info = risk.column_stats(t, start, n, col, gpu, rows=rows)
+            ref = ref_all[start:start + n]
+            c, s, lo, hi = st.tolist()
+            assert info["device"] == "gpu" and info["host_rows"] == 0
+            assert c == ref.size and lo == ref.min() and hi == ref.max()
+            assert abs(s - ref.sum()) <= 1e-12 * np.abs(ref).sum(), (rows, start, n, s, ref.sum())
+            if slot_bytes:
+                assert info["chunks"] >= (info["bytes"] + slot_bytes - 1) // slot_bytes
+
+
+def test_risk_stream_gpu_fallbacks_match_host(gpu, tmp_path, monkeypatch):
+    """Fields the device fast path does not take (quotes, > 19 digits, inf, exponents out of
+    range) are parsed on the host: every value equals the one-pass strtod parse, and a bad
+    value raises the same error."""
+    import numpy as np
+
+    from agent_tpu_amd._native import native
+    from agent_tpu_amd.runtime import risk
+
+    odd = ["1e5", "-2.5E-3", " 3.5 ", "+7", ".5", "5.", "-0", "0.1234567890123456789012", '"42.5"', "inf",
+           "1e400", "123456789012345678901", "9007199254740993", "1e-30", "0.000001", "00012.50"]
+    vals = [odd[i % len(odd)] if i % 3 == 0 else f"{(i % 1000) / 8:.3f}" for i in range(30_000)]
+    t = native().CsvTable(_risk_csv(tmp_path / "odd.csv", vals))
+    col = t.column_index("risk")
+    ref = t.float_column(0, t.num_rows, col)
+    st, info = risk.column_stats(t, 0, t.num_rows, col, gpu, rows=5000)
+    c, s, lo, hi = st.tolist()
+    assert info["host_rows"] > 0 and c == ref.size and lo == ref.min() and hi == ref.max()
+    assert s == ref.sum() or abs(s - ref.sum()) <= 1e-12 * np.abs(ref[np.isfinite(ref)]).sum()
+    # fast-path values themselves are strtod-exact: a column of only fast-path forms
+    exact = ["1e5", "-2.5E-3", " 3.5 ", "+7", ".5", "5.", "0.000001", "00012.50", "9007199254740992", "1e22"]
+    t2 = native().CsvTable(_risk_csv(tmp_path / "exact.csv", exact * 100))
+    st2, info2 = risk.column_stats(t2, 0, t2.num_rows, col, gpu, rows=64)
+    r2 = t2.float_column(0, t2.num_rows, col)
+    assert info2["host_rows"] == 0 and st2[2].item() == r2.min() and st2[3].item() == r2.max()
+    bad = native().CsvTable(_risk_csv(tmp_path / "bad.csv", ["1"] * 100 + ["x1"] + ["2"] * 50 + ["y"]))
+    with pytest.raises(ValueError, match="could not convert string to float: 'x1'"):
+        risk.column_stats(bad, 0, bad.num_rows, col, gpu, rows=32)
+    # more misses than the device list holds: the whole range is re-parsed on the host
+    monkeypatch.setenv("RISK_FALLBACK_CAP", "4")
+    st3, info3 = risk.column_stats(t, 0, t.num_rows, col, gpu, rows=5001)
+    assert info3["host_rows"] == t.num_rows and st3[0].item() == ref.size and st3[2].item() == ref.min()
+
+
+def test_risk_op_csv_streams_on_gpu(gpu, tmp_path, monkeypatch):
+    from ops.risk_accumulate import risk_accumulate
+
+    monkeypatch.setenv("RISK_DEVICE", "gpu")
+    monkeypatch.setenv("RISK_CHUNK_ROWS", "20000")
+    vals = [f"{(i * 7919 % 100003) / 100:.2f}" for i in range(100_000)]
+    path = _risk_csv(tmp_path / "op.csv", vals)
+    out = risk_accumulate({"source_uri": path, "field": "risk", "start_row": 1, "shard_size": 99_990})
+    ref = risk_accumulate({"values": [float(v) for v in vals[1:99_991]]})
+    assert out["device"] == "gpu" and out["stream"]["chunks"] == 5 and out["count"] == 99_990
+    assert out["min"] == ref["min"] and out["max"] == ref["max"] and abs(out["sum"] - ref["sum"]) < 1e-6

@@ -232,18 +232,133 @@ def _visible_filter(devs: List[Dict[str, Any]]) -> Optional[List[Dict[str, Any]]
     return None
 
 
-def classify_batch_rows(hbm_bytes: int) -> int:
-    """Rows per DP rank batch for BERT-base S=128 from the HBM budget."""
+# Served model shapes (kept in step with the presets in agent_tpu_amd/models/{bert,t5,bart}.py by
+# tests/contract/test_worker_sizing.py; this module stays importable without torch, like the reference's).
+#   classify: hidden, intermediate, layers, vocab, max_positions
+CLASSIFY_DIMS = {"bert-base": (768, 3072, 12, 30522, 512), "bert-large": (1024, 4096, 24, 30522, 512),
+                 "bert-tiny": (256, 1024, 2, 4096, 512)}
+#   summarize: d_model, d_ff, enc_layers, dec_layers, vocab
+SUMMARIZE_DIMS = {"t5-base": (768, 3072, 12, 12, 32128), "t5-small": (512, 2048, 6, 6, 32128),
+                  "bart-large-cnn": (1024, 4096, 12, 12, 50264), "bart-large": (1024, 4096, 12, 12, 50264),
+                  "bart-base": (768, 3072, 6, 6, 50264)}
+CLASSIFY_TOKENS_PER_BATCH = 131072  # M = rows*S where the MFMA GEMMs saturate (docs/PERF_NOTES.md, Batch size)
+CLASSIFY_MAX_ROW_BYTES = 2048       # agent_tpu_amd.tokenizer.DEFAULT_MAX_ROW_BYTES (device text staging)
+SUMMARIZE_DOCS_TARGET = 1024        # docs/PERF_NOTES.md: 1024 docs/step is the T5 / BART throughput plateau
+SUMMARIZE_SRC, SUMMARIZE_BEAMS, SUMMARIZE_MAX_LEN = 1024, 4, 130  # ref ops/map_summarize.py:49,53-59
+
+
+def _activation_budget(hbm_bytes: int) -> int:
+    """HBM one engine may spend on activations: what is left after HBM_RESERVE_GB and the
+    model LRU's share (MODEL_LRU_GB, default 25 % of the device: ops/_gpu_runtime.lru_budget_bytes)."""
+    reserve = int(env_float("HBM_RESERVE_GB", 8.0) * GIB)
+    lru_gb = env_float("MODEL_LRU_GB", 0.0)
+    lru = int(lru_gb * GIB) if lru_gb > 0 else hbm_bytes // 4
+    return max(0, hbm_bytes - reserve - lru)
+
+
+def classify_row_bytes(model: str = "bert-base", seq_len: int = 128, slots: int = 2) -> int:
+    """Device bytes one batch row costs the ClassifyEngine (agent_tpu_amd/runtime/classify.py):
+    per staging slot (``slots`` batches in flight, each with its own graph pool) the text
+    staging, ids/lengths and the encoder's activations: two hidden-state buffers, the packed
+    QKV, the attention context and the FFN intermediate (bf16), plus per-row LayerNorm
+    statistics (fp32 partials of up to 4 column tiles and the finalized pair)."""
+    H, I, _, _, _ = CLASSIFY_DIMS[model]
+    S = int(seq_len)
+    act = S * 2 * (2 * H + 3 * H + H + I) + S * 4 * (2 * 4 + 2)
+    return slots * (CLASSIFY_MAX_ROW_BYTES + 4 + S * 4 + 4 + act)
+
+
+def classify_batch_rows(hbm_bytes: int, model: str = "bert-base", seq_len: Optional[int] = None,
+                        slots: int = 2) -> int:
+    """Rows per DP-rank batch for the served classify model: the GEMM-saturating token count
+    (``CLASSIFY_TOKENS_PER_BATCH`` / S) unless the HBM activation budget is smaller.
+    ``CLASSIFY_BATCH_ROWS`` overrides; ``CLASSIFY_BATCH_ROWS_CAP`` caps."""
     explicit = env_int("CLASSIFY_BATCH_ROWS", 0)
     if explicit > 0:
         return explicit
+    if model not in CLASSIFY_DIMS:
+        model = "bert-base"
+    seq = int(seq_len) if seq_len else env_int("CLASSIFY_SEQ_LEN", 128)
+    fit = _activation_budget(hbm_bytes) // classify_row_bytes(model, seq, slots)
+    target = max(64, CLASSIFY_TOKENS_PER_BATCH // max(1, seq))
+    rows = min(fit, target, env_int("CLASSIFY_BATCH_ROWS_CAP", 1 << 30))
+    if rows >= 64:
+        rows -= rows % 64  # whole 2-row x 128-token GEMM tiles
+    return int(max(1, rows))
+
+
+def summarize_doc_bytes(model: str = "t5-base", src: int = SUMMARIZE_SRC, beams: int = SUMMARIZE_BEAMS,
+                        max_len: int = SUMMARIZE_MAX_LEN) -> int:
+    """Device bytes per document of a beam search (agent_tpu_amd/runtime/summarize.py):
+    the encoder's cross K/V for every decoder layer (one copy per document), the
+    self-attention KV cache of every beam up to ``max_len``, the encoder activations at
+    ``src`` tokens, and the per-beam decode state (hidden rows, token history, LM-head
+    partials of the fused top-k: per 128-token vocabulary tile a max, a sum and 16
+    candidates)."""
+    return summarize_doc_bytes_dims(SUMMARIZE_DIMS[model], src, beams, max_len)
+
+
+def summarize_doc_bytes_dims(dims: Tuple[int, int, int, int, int], src: int = SUMMARIZE_SRC,
+                             beams: int = SUMMARIZE_BEAMS, max_len: int = SUMMARIZE_MAX_LEN) -> int:
+    """:func:`summarize_doc_bytes` for explicit (d_model, d_ff, enc_layers, dec_layers, vocab)."""
+    d, f, _, dec, V = dims
+    cross = dec * 2 * src * d * 2
+    self_kv = beams * dec * 2 * max_len * d * 2
+    enc_act = src * 2 * (2 * d + 3 * d + d + f)
+    step = beams * (6 * d * 2 + max_len * 4 + ((V + 127) // 128) * (2 + 16 * 2) * 4)
+    return cross + self_kv + enc_act + step
+
+
+def summarize_batch_docs(hbm_bytes: int, model: Any = "t5-base", src: int = SUMMARIZE_SRC) -> int:
+    """Documents per device batch (``model``: a SUMMARIZE_DIMS name or a dims tuple): the
+    throughput plateau unless HBM is smaller. ``SUMMARIZE_BATCH_DOCS`` overrides.
+    SummarizeEngine.run splits a larger call into batches of this size."""
+    explicit = env_int("SUMMARIZE_BATCH_DOCS", 0)
+    if explicit > 0:
+        return explicit
+    dims = model if isinstance(model, tuple) else SUMMARIZE_DIMS.get(model, SUMMARIZE_DIMS["t5-base"])
+    fit = _activation_budget(hbm_bytes) // summarize_doc_bytes_dims(dims, src)
+    return int(max(1, min(fit, SUMMARIZE_DOCS_TARGET)))
+
+
+RISK_RECORD_BYTES = 24  # slot bytes per record of a streamed risk chunk (agent_tpu_amd/runtime/risk.py)
+
+
+def risk_chunk_rows(hbm_bytes: int) -> int:
+    """Records per streamed chunk of a risk_accumulate CSV shard (agent_tpu_amd/runtime/risk.py):
+    two pinned host slots and two device slots, each holding a chunk's raw record bytes
+    (``RISK_RECORD_BYTES`` per record, byte-limited chunks for longer records) and its 4-B record
+    offsets. The host staging (``RISK_STAGING_MB``, default 256 MiB for both slots) bounds it, so
+    the agent's memory does not grow with ``shard_size``; ``RISK_CHUNK_ROWS`` overrides."""
+    explicit = env_int("RISK_CHUNK_ROWS", 0)
+    if explicit > 0:
+        return explicit
+    per = 2 * (RISK_RECORD_BYTES + 4)
+    host = env_int("RISK_STAGING_MB", 256) * (1 << 20) // per
+    dev = max(1, _activation_budget(hbm_bytes) // per) if hbm_bytes else host
+    return int(max(1 << 16, min(host, dev)))
+
+
+def gpu_capacity(hbm_bytes: int) -> Dict[str, Any]:
+    """What this device can take per batch, for every servable model: advertised in the
+    lease's worker profile so a controller can size leases (ref worker_sizing.py:221-256
+    advertised only worker counts)."""
     seq = env_int("CLASSIFY_SEQ_LEN", 128)
-    reserve = int(env_float("HBM_RESERVE_GB", 8.0) * GIB)
-    weights = 512 * 1024 * 1024  # LRU headroom for one resident BERT-large (670 MB) is budgeted below
-    per_row = seq * 2 * (768 * 4 + 3 * 768 + 3072) + 2048 + 8 * seq
-    fit = max(1, (hbm_bytes - reserve - 2 * weights) // per_row)
-    # MFMA GEMMs saturate near M = rows*S ~ 128k tokens; bigger batches only add latency
-    return int(max(64, min(fit, env_int("CLASSIFY_BATCH_ROWS_CAP", 1024))))
+    return {
+        "classify_seq_len": seq,
+        "classify_batch_rows": {m: classify_batch_rows(hbm_bytes, m, seq) for m in CLASSIFY_DIMS if m != "bert-tiny"},
+        "summarize_source_tokens": SUMMARIZE_SRC,
+        "summarize_beams": SUMMARIZE_BEAMS,
+        "summarize_batch_docs": {m: summarize_batch_docs(hbm_bytes, m) for m in ("t5-base", "bart-large-cnn")},
+        "risk_chunk_rows": risk_chunk_rows(hbm_bytes),
+    }
+
+
+def _served_classify_model() -> str:
+    """Preset of the default classify model (GPU_MODEL_PATH / CLASSIFY_MODEL, ops/_gpu_runtime.py)."""
+    raw = os.getenv("GPU_MODEL_PATH") or os.getenv("CLASSIFY_MODEL") or "bert-base"
+    name = raw.split("?", 1)[0].strip()
+    return name if name in CLASSIFY_DIMS else "bert-base"
 
 
 def detect_gpu() -> Dict[str, Any]:
@@ -265,7 +380,8 @@ def detect_gpu() -> Dict[str, Any]:
         "max_gpu_workers": len(devs),  # one DP rank (process) per GPU
         "vendor": "amd",
         "hbm_gb": [round(d["total_memory_bytes"] / GIB, 2) for d in devs],
-        "classify_batch_rows": classify_batch_rows(biggest) if biggest else None,
+        "classify_batch_rows": classify_batch_rows(biggest, _served_classify_model()) if biggest else None,
+        "capacity": gpu_capacity(biggest) if biggest else None,
         "dp_world_size": env_int("DP_WORLD_SIZE", len(devs)),
     }
 
