@@ -161,27 +161,33 @@ def broadcast_task(obj: Any, src: int = 0) -> Any:
     return box[0]
 
 
-def all_gather_rows(*tensors: torch.Tensor) -> Tuple[torch.Tensor, ...]:
+def all_gather_rows(*tensors: Optional[torch.Tensor], counts: Optional[List[int]] = None
+                    ) -> Tuple[torch.Tensor, ...]:
     """C2: concatenate every rank's ``[rows_r, ...]`` tensors in rank order.
 
     Ragged shards are padded to ``max(rows_r)`` for the collective and trimmed
-    afterwards using the gathered row counts.
+    afterwards using the row counts: ``counts`` when the caller already exchanged them
+    (``dp_ops._check_errors(err, rows)`` carries them in its object exchange), else one
+    count all-gather (4 B per rank) first.
     """
     if not is_dist():
         return tensors
     _, ws = world()
     dev = tensors[0].device
     cdev = comm_device(dev)
-    cnt = torch.tensor([tensors[0].shape[0]], dtype=torch.int64, device=cdev)
-    counts = torch.empty(ws, dtype=torch.int64, device=cdev)
     nc = native_comm(cdev)
-    with watchdog.collective("row-count gather"):
-        if nc is not None:
-            nc.all_gather_into(counts, cnt)
-            nc.wait("row-count gather")
-        else:
-            dist.all_gather_into_tensor(counts, cnt, group=_GROUP)
-    counts_l: List[int] = counts.tolist()
+    if counts is None:
+        cnt = torch.tensor([tensors[0].shape[0]], dtype=torch.int64, device=cdev)
+        cts = torch.empty(ws, dtype=torch.int64, device=cdev)
+        with watchdog.collective("row-count gather"):
+            if nc is not None:
+                nc.all_gather_into(cts, cnt)
+                nc.wait("row-count gather")
+            else:
+                dist.all_gather_into_tensor(cts, cnt, group=_GROUP)
+        counts = cts.tolist()
+    counts_l: List[int] = [int(c) for c in counts]
+    assert len(counts_l) == ws and counts_l[world()[0]] == tensors[0].shape[0], (counts_l, tensors[0].shape)
     mx = max(counts_l) if counts_l else 0
     outs = []
     for t in tensors:

@@ -118,25 +118,32 @@ _ERR_TYPES = {"ValueError": ValueError, "TypeError": TypeError, "KeyError": KeyE
               "FileNotFoundError": FileNotFoundError}
 
 
-def _check_errors(err: str) -> None:
+def _check_errors(err: str, extra: Any = None) -> Optional[list]:
     """Exchange per-rank errors (``"Type: message"``) so every rank fails together.
 
     If EVERY rank failed with the same input-validation error (a bad payload is
     bad everywhere) it is re-raised with its own type and message, keeping the
     single-process op's contract; otherwise a RuntimeError names each rank.
+
+    ``extra``: a small per-rank value carried by the SAME object exchange (e.g. the
+    rank's row count for the C2 all-gather, which then needs no count collective of
+    its own); returns every rank's ``extra`` in group order (None outside a group:
+    ``[extra]``).
     """
     if not is_dist():
         if err:
             raise RuntimeError(err)
-        return
+        return [extra]
     rank, ws = world()
     errs = [None] * ws
     with watchdog.collective("error exchange"):
-        dist.all_gather_object(errs, err, group=dp.group())
+        dist.all_gather_object(errs, (err, extra), group=dp.group())
+    extras = [e[1] for e in errs]
+    errs = [e[0] for e in errs]
     glob = members()  # group index -> global rank (errors name global ranks)
     bad = [(glob[r], e) for r, e in enumerate(errs) if e]
     if not bad:
-        return
+        return extras
     if len(bad) == ws and len(set(e for _, e in bad)) == 1:
         typ, _, msg = bad[0][1].partition(": ")
         if typ in _ERR_TYPES:
@@ -330,19 +337,21 @@ def classify_csv_task(payload: Dict[str, Any]) -> Any:
         maybe_inject_fault("classify")
         with span("classify_ms", timing):
             idx, sc, st = h.engine.classify_table(table.native, s_r, n_r, col,
-                                                  stage_timing=payload.get("timing", "device") != "host")
+                                                  stage_timing=payload.get("timing", "host") == "device")
         timing.update({k: (round(v, 3) if isinstance(v, float) else v) for k, v in st.timing_ms.items()})
         meta = {"start_row": start, "end_row": start + total, "world": ws}
     except Exception as exc:
         err = f"{type(exc).__name__}: {exc}"
         if os.getenv("ATPU_DEBUG"):
             traceback.print_exc()
-    _check_errors(err)
+    # one object exchange: the errors AND every rank's row count (the C2 all-gather below
+    # needs no count collective and no host sync of its own)
+    counts = _check_errors(err, int(idx.shape[0]) if idx is not None else 0)
     dev_t = idx is not None and idx.is_cuda
     ev = DeviceStages.event if dev_t else (lambda *a: None)
     g0 = ev()
     with span("host_allgather_ms", timing):
-        idx, sc = all_gather_rows(idx, sc)
+        idx, sc = all_gather_rows(idx, sc, counts=counts)
     g1 = ev()
     if rank != 0:
         return None
@@ -382,8 +391,8 @@ def classify_rows_task(payload: Dict[str, Any]) -> Any:
         idx, sc = res.idx[:, :k].contiguous(), res.score[:, :k].contiguous()
     except Exception as exc:
         err = _err_str(exc)
-    _check_errors(err)
-    idx, sc = all_gather_rows(idx, sc)
+    counts = _check_errors(err, int(idx.shape[0]) if idx is not None else 0)
+    idx, sc = all_gather_rows(idx, sc, counts=counts)
     if rank != 0:
         return None
     return mc.texts_result(h, idx.cpu(), sc.cpu(), payload, ws)
@@ -525,9 +534,9 @@ def summarize_task(payload: Dict[str, Any]) -> Any:
         err = f"{type(exc).__name__}: {exc}"
         if os.getenv("ATPU_DEBUG"):
             traceback.print_exc()
-    _check_errors(err)
+    counts = _check_errors(err, int(seqs.shape[0]))
     with span("allgather_ms", timing):
-        (seqs,) = all_gather_rows(seqs)
+        (seqs,) = all_gather_rows(seqs, counts=counts)
     if rank != 0:
         return None
     rows = [[int(t) for t in r if t >= 0] for r in seqs.cpu().tolist()]

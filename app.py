@@ -19,7 +19,10 @@ Fixes over the reference:
 * one keep-alive HTTP connection instead of a TCP connect per request (§2.4.11);
 * failed result posts get a bounded retry on transport/5xx errors, never on
   4xx (a 409 stale epoch is final); ``job_epoch`` is passed through verbatim;
-* metrics add GPU/HBM use, completed jobs and a rolling rows/s (§5.5).
+* metrics add GPU/HBM use, completed jobs and a rolling rows/s (§5.5);
+* the next lease is taken while the current batch runs and results are posted by a
+  background thread (``LEASE_PREFETCH`` / ``RESULT_POST_ASYNC``, both on by default; 0 restores
+  the reference's serial order), so neither HTTP round trip sits between two jobs' GPU work.
 
 Data parallel: launched under ``torchrun`` (WORLD_SIZE>1), rank 0 runs this
 loop and the other ranks run :func:`agent_tpu_amd.parallel.dp_ops.worker_loop`,
@@ -73,9 +76,12 @@ RESULT_RETRIES = int(os.getenv("RESULT_RETRIES", "2"))
 # same-op jobs of one lease run as ONE device batch (map_summarize docs, map_classify rows)
 LEASE_BATCH = os.getenv("LEASE_BATCH", "1").strip().lower() not in ("0", "false", "no", "off")
 # post results from a background thread (FIFO, bounded): the next job's device work overlaps
-# the HTTP post of the previous result (and the controller's parse of it). Off = the reference's
+# the HTTP post of the previous result (and the controller's parse of it). 0 = the reference's
 # strictly serial lease -> execute -> post order.
-RESULT_POST_ASYNC = os.getenv("RESULT_POST_ASYNC", "0").strip().lower() in ("1", "true", "yes", "on")
+RESULT_POST_ASYNC = os.getenv("RESULT_POST_ASYNC", "1").strip().lower() in ("1", "true", "yes", "on")
+# lease the next task batch while the current one runs (one lease ahead, own connection): the
+# lease round trip leaves the critical path between jobs. 0 = lease only when idle (reference).
+LEASE_PREFETCH = os.getenv("LEASE_PREFETCH", "1").strip().lower() in ("1", "true", "yes", "on")
 # lease size this agent can batch well; advertised in worker_profile.limits (MAX_TASKS stays the request)
 MAX_BATCH_TASKS = int(os.getenv("MAX_BATCH_TASKS", "1024"))
 FAIL_ON_NOT_OK = os.getenv("FAIL_ON_NOT_OK", "0").strip().lower() in ("1", "true", "yes")
@@ -374,6 +380,63 @@ class Controller:
             time.sleep(min(2.0, 0.1 * 2**attempt))
 
 
+class Leaser:
+    """``LEASE_PREFETCH``: a thread that holds at most ONE lease ready for the main loop.
+
+    It leases only when nothing is queued, so the agent never holds more than the batch it
+    runs plus one; on 204 it sleeps ``IDLE_SLEEP_SEC`` and on errors ``ERROR_BACKOFF_SEC``
+    exactly like the serial loop, with its own keep-alive connection (http.client is not
+    thread-safe). ``job_epoch`` and the tasks pass through untouched. On shutdown the main
+    loop still runs a lease that was already taken (it is the agent's until its TTL)."""
+
+    def __init__(self, agent: "Agent") -> None:
+        import queue
+
+        self.agent = agent
+        self.q: "queue.Queue[Tuple[str, List[Any]]]" = queue.Queue(maxsize=1)
+        self.ctl = Controller(CONTROLLER_URL, HTTP_TIMEOUT_SEC)
+        self._stop = threading.Event()
+        self._taken = threading.Event()
+        self._taken.set()
+        self.thread = threading.Thread(target=self._loop, name="atpu-leaser", daemon=True)
+        self.thread.start()
+
+    def _loop(self) -> None:
+        while not self._stop.is_set() and _running:
+            if not self._taken.wait(0.05):
+                continue  # the previous lease is still queued
+            try:
+                leased = self.ctl.lease(self.agent.caps, self.agent.profile)
+            except Exception as exc:
+                log_every("lease", f"{LOG} lease error: {exc}")
+                self._stop.wait(ERROR_BACKOFF_SEC)
+                continue
+            if not leased:
+                self._stop.wait(IDLE_SLEEP_SEC)
+                continue
+            self._taken.clear()
+            self.q.put(leased)
+
+    def get(self, timeout: float) -> Optional[Tuple[str, List[Any]]]:
+        import queue
+
+        try:
+            leased = self.q.get(timeout=timeout)
+        except queue.Empty:
+            return None
+        self._taken.set()
+        return leased
+
+    def pending(self) -> List[Tuple[str, List[Any]]]:
+        """Leases taken from the controller but not started (rank-lost failure posts)."""
+        items = list(self.q.queue)
+        return items
+
+    def stop(self) -> None:
+        self._stop.set()
+        self.thread.join(timeout=HTTP_TIMEOUT_SEC + 5)
+
+
 def _op_span(op: str):
     """roctx range around a job under MI355X_TRACE=1 (no import cost otherwise)."""
     if os.getenv("MI355X_TRACE", "0").strip().lower() not in ("1", "true"):
@@ -421,6 +484,7 @@ class Agent:
         self._inflight: Dict[str, Tuple[str, Any, str]] = {}  # job_id -> (lease_id, epoch, op)
         self._inflight_lock = threading.Lock()
         self._poster = None
+        self._leaser: Optional[Leaser] = None
         if RESULT_POST_ASYNC:
             import queue
 
@@ -449,6 +513,14 @@ class Agent:
             pass
         with self._inflight_lock:
             jobs, self._inflight = dict(self._inflight), {}
+        if self._leaser is not None:  # leased ahead, never started: fail them too (no TTL wait)
+            for lease_id, tasks in self._leaser.pending():
+                for task in tasks:
+                    try:
+                        job_id, op, _, epoch = extract_task(task)
+                    except Exception:
+                        continue
+                    jobs.setdefault(job_id, (lease_id, epoch, op))
         err = {"type": "RankLost", "message": msg, "trace": ""}
         # this runs on the watchdog thread while the main thread may be mid-request on
         # self.ctl (one keep-alive http.client connection, not thread-safe): post on a
@@ -628,6 +700,9 @@ class Agent:
             self.profile = worker_profile(self.health, self.caps)
 
     def loop(self) -> None:
+        if LEASE_PREFETCH:
+            self._loop_prefetch()
+            return
         while _running:
             try:
                 leased = self.ctl.lease(self.caps, self.profile)
@@ -640,6 +715,22 @@ class Agent:
                 continue
             lease_id, tasks = leased
             self.run_tasks(lease_id, tasks)
+
+    def _loop_prefetch(self) -> None:
+        """The serial loop with the lease taken one batch ahead (:class:`Leaser`)."""
+        self._leaser = Leaser(self)
+        try:
+            while _running:
+                leased = self._leaser.get(timeout=0.05)
+                if leased is not None:
+                    self.run_tasks(*leased)
+        finally:
+            self._leaser.stop()
+            while True:  # a lease taken before the stop is still ours: run it
+                leased = self._leaser.get(timeout=0.0)
+                if leased is None:
+                    break
+                self.run_tasks(*leased)
 
 
 def _on_signal(signum: int, _frame: Any) -> None:

@@ -128,8 +128,8 @@ def classify_batch(h, payloads: List[Dict[str, Any]], rank: int, ws: int) -> Opt
             idx, sc = res.idx[:, :kmax].contiguous(), res.score[:, :kmax].contiguous()
         except Exception as exc:
             err = _err_str(exc)
-        _check_errors(err)
-        idx, sc = all_gather_rows(idx, sc)
+        counts = _check_errors(err, int(idx.shape[0]) if idx is not None else 0)
+        idx, sc = all_gather_rows(idx, sc, counts=counts)
         if rank == 0:
             idx, sc, pos = idx.cpu(), sc.cpu(), 0
             for i, ts, k in tjobs:

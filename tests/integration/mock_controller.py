@@ -23,6 +23,10 @@ class MockController:
         self.results: List[Dict[str, Any]] = []
         self.result_codes: Dict[str, List[int]] = {}
         self.result_attempts: Dict[str, int] = {}
+        # ("lease", lease_id or None) at each lease answer, ("result", job_id) when a result is
+        # accepted, in order; result_delay (s) holds every result answer back (a slow controller)
+        self.events: List[Tuple[str, Any]] = []
+        self.result_delay = 0.0
         self._lock = threading.Lock()
         self._cv = threading.Condition(self._lock)
         ctl = self
@@ -50,16 +54,23 @@ class MockController:
                     with ctl._cv:
                         ctl.lease_requests.append(body)
                         item = ctl.leases.popleft() if ctl.leases else (204, None)
+                        lid = item[1].get("lease_id") if isinstance(item[1], dict) else None
+                        ctl.events.append(("lease", lid))
                         ctl._cv.notify_all()
                     self._send(*item)
                 elif self.path == "/v1/results":
                     jid = body.get("job_id")
+                    if ctl.result_delay:
+                        import time
+
+                        time.sleep(ctl.result_delay)
                     with ctl._cv:
                         ctl.result_attempts[jid] = ctl.result_attempts.get(jid, 0) + 1
                         codes = ctl.result_codes.get(jid)
                         code = codes.pop(0) if codes else 200
                         if code < 400:
                             ctl.results.append(body)
+                            ctl.events.append(("result", jid))
                         ctl._cv.notify_all()
                     self._send(code, {"ok": code < 400})
                 else:

@@ -172,3 +172,55 @@ def test_async_result_poster_keeps_every_result(ctl):
     assert code == 0, out
     got = [(r["job_id"], r["job_epoch"], r["result"]["echo"]["i"]) for r in ctl.results]
     assert got == [(f"a{i}", i, i) for i in range(12)]
+
+
+def _order(ctl):
+    return [e for e in ctl.events if e != ("lease", None)]
+
+
+def test_lease_prefetch_and_async_post_overlap_jobs(ctl):
+    """with the defaults the next lease is taken while the current job's
+    result is still being posted (a slow controller: 0.3 s per result answer), results stay
+    in FIFO order with their epochs; LEASE_PREFETCH=0 RESULT_POST_ASYNC=0 is the reference's
+    strict lease -> execute -> post order."""
+    ctl.result_delay = 0.3
+    for i in range(3):
+        ctl.lease({"id": f"p{i}", "op": "echo", "payload": {"i": i}, "job_epoch": 10 + i}, lease_id=f"P{i}")
+    p = start_agent(ctl, tasks="echo")
+    try:
+        assert ctl.wait(lambda c: len(c.results) >= 3, 60), ctl.results
+    finally:
+        code, out = stop_agent(p)
+    assert code == 0, out
+    ev = _order(ctl)
+    assert ev.index(("lease", "P1")) < ev.index(("result", "p0")), ev  # leased ahead, posted behind
+    assert [(r["job_id"], r["job_epoch"], r["lease_id"]) for r in ctl.results] == \
+        [(f"p{i}", 10 + i, f"P{i}") for i in range(3)]
+
+
+def test_serial_order_when_disabled(ctl):
+    ctl.result_delay = 0.1
+    for i in range(3):
+        ctl.lease({"id": f"s{i}", "op": "echo", "payload": {}}, lease_id=f"S{i}")
+    p = start_agent(ctl, tasks="echo", LEASE_PREFETCH="0", RESULT_POST_ASYNC="0")
+    try:
+        assert ctl.wait(lambda c: len(c.results) >= 3, 60), ctl.results
+    finally:
+        code, out = stop_agent(p)
+    assert code == 0, out
+    assert _order(ctl)[:6] == [("lease", "S0"), ("result", "s0"), ("lease", "S1"), ("result", "s1"),
+                               ("lease", "S2"), ("result", "s2")]
+
+
+def test_sigterm_runs_the_prefetched_lease(ctl):
+    """A lease taken ahead belongs to the agent: SIGTERM still runs and results it."""
+    ctl.result_delay = 0.5
+    ctl.lease({"id": "t0", "op": "echo", "payload": {}}, lease_id="T0")
+    ctl.lease({"id": "t1", "op": "echo", "payload": {}}, lease_id="T1")
+    p = start_agent(ctl, tasks="echo")
+    try:
+        assert ctl.wait(lambda c: ("lease", "T1") in c.events, 60)
+    finally:
+        code, out = stop_agent(p)
+    assert code == 0, out
+    assert {r["job_id"] for r in ctl.results} == {"t0", "t1"}

@@ -36,7 +36,7 @@ def test_map_classify_op_forms(gpu, tmp_path, monkeypatch):
     assert texts["ok"] and texts["row_count"] == 3 and len(texts["rows"][2]["topk"]) == 2
     path = str(tmp_path / "rows.csv")
     write_csv(path, 300, 40)
-    csv = mc.map_classify({"source_uri": path, "start_row": 10, "shard_size": 150, "topk": 2})
+    csv = mc.map_classify({"source_uri": path, "start_row": 10, "shard_size": 150, "topk": 2, "timing": "device"})
     assert csv["ok"] and csv["row_count"] == 150 and csv["start_row"] == 10 and csv["end_row"] == 160
     assert csv["rows"][0]["row"] == 10 and csv["dp_world_size"] == 1
     # CSV path == texts path on the same rows (same tokenizer, same weights)
