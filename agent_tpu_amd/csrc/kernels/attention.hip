@@ -698,16 +698,22 @@ void attention_fwd_strided(const bf16* q, int ldq, const bf16* k, int ldk, const
     const int nb = 2 * num_cus();  // two workgroups per CU (80 KiB LDS each)
 
     const int items = B * H;
-    if (attention_persist_mode(-1) == 2) {
-      hipLaunchKernelGGL((attention_packed_persist_kernel<2, false, true>), dim3(std::min(items, nb)), dim3(kThreads),
-                         0, stream, q, ldq, out, ldo, lens, Sq, H, items, scale);
-      ATPU_HIP_CHECK(hipGetLastError());
-      return;
-    }
+    // ATPU_ATTN_NT=0: Q/K/V loads with the default cache policy (kept in L2 / the Infinity
+    // Cache) instead of streaming nt loads: for batches whose QKV fits the 256 MiB MALL
     static const bool nt = [] {
       const char* f = std::getenv("ATPU_ATTN_NT");
       return !(f && f[0] == '0');
     }();
+    if (attention_persist_mode(-1) == 2) {
+      if (nt)
+        hipLaunchKernelGGL((attention_packed_persist_kernel<2, false, true>), dim3(std::min(items, nb)),
+                           dim3(kThreads), 0, stream, q, ldq, out, ldo, lens, Sq, H, items, scale);
+      else
+        hipLaunchKernelGGL((attention_packed_persist_kernel<0, false, true>), dim3(std::min(items, nb)),
+                           dim3(kThreads), 0, stream, q, ldq, out, ldo, lens, Sq, H, items, scale);
+      ATPU_HIP_CHECK(hipGetLastError());
+      return;
+    }
     static const bool hot = [] {
       const char* f = std::getenv("ATPU_ATTN_HOT");
       return f && f[0] == '1';
