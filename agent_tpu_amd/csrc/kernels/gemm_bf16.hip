@@ -36,6 +36,9 @@
 #ifndef ATPU_GEMM_SYNC_EPI
 #define ATPU_GEMM_SYNC_EPI 1
 #endif
+#ifndef ATPU_GEMM_EARLY_KT1
+#define ATPU_GEMM_EARLY_KT1 0
+#endif
 
 namespace atpu {
 namespace {
@@ -902,11 +905,19 @@ struct LnLds {
 // IN_ACC (InNorm): the caller started the accumulators at -mu*colsum (else the
 // epilogue applies -rstd*mu*colsum itself, from LDS colsum)
 // NOST (timing-only ablation, results WRONG): the output values are computed but not stored
-template <int EPI, bool NT, bool IN_ACC = true, int GM = 0, bool NOST = false>
+// EARLY: VMEM ops `early()` issues (the persistent kernel's next-tile K-tile-1 staging), called
+// after the residual loads are issued and BEFORE any store, so they are older than every
+// store; the counted residual waits see EARLY more younger ops
+struct NoEarly {
+  __device__ __forceinline__ void operator()() const {}
+};
+template <int EPI, bool NT, bool IN_ACC = true, int GM = 0, bool NOST = false, int EARLY = 0, typename F = NoEarly>
 __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int m0, int n0, int wm, int wn, int lane,
                                                   bf16* __restrict__ C, int ldc, const bf16* __restrict__ R, int ldr,
                                                   const float* lds_bias, char* scratch,
-                                                  const u32x4 (&pre)[2][2], LnLds ln = {}) {
+                                                  const u32x4 (&pre)[2][2], LnLds ln = {}, F early = F{}) {
+  constexpr int kResWait = kLineResWait + EARLY;
+  static_assert(kResWait < 64, "vmcnt field is 6 bits on gfx950");
   constexpr bool kIn = EPI & kEpiInNorm, kRes = EPI & kEpiResNorm, kSt = EPI & kEpiStatsOut;
   const int fr = lane & 15, fc = lane >> 4;
   // per-column LDS vectors (bias, colsum, gamma) at this lane's 4 columns of fragment j
@@ -953,6 +964,11 @@ __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int 
       res[i][0] = load16_untracked(rp);
       res[i][1] = load16_untracked(rp + 8 * (size_t)ldr);
     }
+  }
+  if constexpr (EARLY > 0) {
+    __builtin_amdgcn_sched_barrier(0);
+    early();  // after every load of the tail, before its first store (EARLY ops)
+    __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -1001,7 +1017,7 @@ __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int 
       // pending: blocks 0-1 (issued in the last MMA phase) are followed by the
       // other pre load pair and 12 loads; block i >= 2 by 2 (7 - i) loads; and
       // every earlier block added its 2 stores -> 14 for every i
-      asm volatile("s_waitcnt vmcnt(%2)" : "+v"(res[i][0]), "+v"(res[i][1]) : "n"(kLineResWait) : "memory");
+      asm volatile("s_waitcnt vmcnt(%2)" : "+v"(res[i][0]), "+v"(res[i][1]) : "n"(kResWait) : "memory");
       __builtin_amdgcn_sched_barrier(0);
       *reinterpret_cast<u32x4*>(scratch + line_off0) = res[i][0];
       *reinterpret_cast<u32x4*>(scratch + line_off1) = res[i][1];
@@ -1174,6 +1190,21 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
   // LDS, where the previous tile's last K-tile staged it) instead of adding it in the
   // epilogue: 16 fewer VGPRs and one op fewer per value pair on the epilogue chain
   constexpr bool kBiasAcc = (kRes || kSt) && (EPI & kEpiBias);
+  // Early K-tile-1 staging (ATPU_GEMM_EARLY_KT1, LN-folding variants; docs/PERF_NOTES.md round 4):
+  // vmcnt retires VMEM ops in issue order, so the wait that covers the next tile's K-tile-1
+  // quarters (staged during its K-tile 0) also waited for every epilogue store issued
+  // before them: the stores of a tile were exposed at K-tile 0 phase 2 of the next. Here
+  // the epilogue stages K-tile 1 of the next tile (into the buffer the last K-tile just
+  // freed) BEFORE its stores, K-tile 0 stages nothing, and its waits leave the stores in
+  // flight (they are the youngest ops); they are first retired at K-tile 1 phase 1,
+  // one and a half K-tiles after their issue. The last tile stages a dummy K-tile 1 of
+  // itself (same op counts), drained before the kernel exits.
+  constexpr bool kEarly = ATPU_GEMM_EARLY_KT1 && LINE && kPeel && DBG == 0 && !kInAcc;
+  constexpr int kEarlyOps = kEarly ? 8 : 0;  // 4 quarters x 2 DMA per wave
+  // VMEM ops issued at K-tile 0 phase 0 before its wait (this tile's bias -> LDS)
+  constexpr int kB0 = ((EPI & kEpiBias) && !kBiasAcc) ? 1 : 0;
+  // VMEM ops issued at K-tile 1 phase 0 before the staging: LN data staging (2), StatsOut flush (1)
+  constexpr int kLn1 = ((kRes || (kIn && !kInAcc)) ? 2 : 0) + (kSt ? 1 : 0);
   const bf16* src[4][2];
   uint32_t soff[4][2];
   auto set_src = [&](int tm0, int tn0) {
@@ -1358,6 +1389,8 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
         kn = 0;
       }
       const bool relax = is_t0 && !first;  // epilogue stores of the previous tile may be in flight
+      // kEarly: K-tile 1 was staged by the previous tile's epilogue (not for the first tile)
+      const bool pre_staged = kEarly && !first && (P == 0 || P == 1);
       // p0
       read_a(buf, 0);
       read_b(bl, buf, 0);
@@ -1383,19 +1416,44 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
           if (!first) ln_flush(pm0, pn0);
         }
       }
-      if (more) {
+      // kEarly, K-tile 0: outstanding (oldest first) Q2, Q3 of K-tile 0, the 8 K-tile-1 DMAs,
+      // the 16 stores, the bias DMA (kB0). Each wait retires the quarter read one phase
+      // later and leaves every younger op (stores included) in flight:
+      //   p0 -> Q2(0): 2 + 8 + 16 + kB0   p1 -> Q3(0): 8 + 16 + kB0
+      //   p2 -> Q0, Q1(1): 4 + 16 + kB0    p3 -> Q2(1): 2 + 16 + kB0
+      // K-tile 1, p0 -> Q3(1): 16 + kB0 + kLn1 + 2 (its own staging of K-tile 2)
+      if constexpr (kEarly && P == 0) {
+        if (pre_staged) {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + 8 + kEpiOps + kB0) : "memory");
+        } else {
+          stage(0, kn, buf ^ 1);
+          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // first tile: no stores in flight
+        }
+      } else if (more) {
         stage(0, kn, buf ^ 1);
-        if (relax) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + kEpiOps) : "memory");
-        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        if constexpr (kEarly && P == 1) {
+          if (pre_staged) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kEpiOps + kB0 + kLn1 + 2) : "memory");
+          else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+          if (relax) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + kEpiOps) : "memory");
+          else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        }
       } else {
         asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
       }
       ATPU_PS_SYNC_MMA(bl, 0, 0);
       // p1
       read_b(br, buf, 1);
-      if (more) {
+      if constexpr (kEarly && P == 0) {
+        if (pre_staged) {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + kEpiOps + kB0) : "memory");
+        } else {
+          stage(1, kn, buf ^ 1);
+          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        }
+      } else if (more) {
         stage(1, kn, buf ^ 1);
-        if (relax) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + kEpiOps) : "memory");
+        if (relax && !kEarly) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + kEpiOps) : "memory");
         else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1403,13 +1461,27 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
       ATPU_PS_SYNC_MMA(br, 0, 1);
       // p2
       read_a(buf, 1);
-      if (more) {
+      if constexpr (kEarly && P == 0) {
+        if (pre_staged) {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + kEpiOps + kB0) : "memory");
+        } else {
+          stage(2, kn, buf ^ 1);
+          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        }
+      } else if (more) {
         stage(2, kn, buf ^ 1);
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       }
       ATPU_PS_SYNC_MMA(br, 1, 1);
       // p3
-      if (more) {
+      if constexpr (kEarly && P == 0) {
+        if (pre_staged) {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + kEpiOps + kB0) : "memory");
+        } else {
+          stage(3, kn, buf ^ 1);
+          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        }
+      } else if (more) {
         stage(3, kn, buf ^ 1);
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       }
@@ -1469,13 +1541,20 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
       // tile-loop structure, the plain epilogue (no LN math, no statistics)
       constexpr int kEpiRun0 = kBiasAcc ? (EPI & ~kEpiBias) : EPI;
       constexpr int kEpiRun = (DBG & 8) ? (kEpiRun0 & ~(kEpiInNorm | kEpiResNorm | kEpiStatsOut)) : kEpiRun0;
+      // kEarly: the next tile's K-tile 1 into the buffer the last K-tile freed (buf ^ 1 after the
+      // flip; a dummy K-tile 1 of this tile when there is no next one: same op count)
+      const int ebuf = buf ^ 1;
+      auto early = [&] {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) stage(q, 1, ebuf);
+      };
       if constexpr (LINE)
-        epilogue_256_line<kEpiRun, NT, kInAcc, ((DBG >> 5) & 3), bool(DBG & 256)>(acc, cm0, cn0, wm, wn, (kIn || kRes || kSt) ? opaque_lane() : lane, C, ldc, R, ldr,
-                                   reinterpret_cast<const float*>(lds + kBiasOff) + tile_par * 256,
-                                   lds + kEpiOff + wave * 2048, pre,
-                                   LnLds{reinterpret_cast<const float*>(lds + kFinOff + (kInAcc ? tile_par * 2048 : 0)),
-                                         reinterpret_cast<const float*>(lds + kColOff),
-                                         reinterpret_cast<float*>(lds + kStOff)});
+        epilogue_256_line<kEpiRun, NT, kInAcc, ((DBG >> 5) & 3), bool(DBG & 256), kEarlyOps>(
+            acc, cm0, cn0, wm, wn, (kIn || kRes || kSt) ? opaque_lane() : lane, C, ldc, R, ldr,
+            reinterpret_cast<const float*>(lds + kBiasOff) + tile_par * 256, lds + kEpiOff + wave * 2048, pre,
+            LnLds{reinterpret_cast<const float*>(lds + kFinOff + (kInAcc ? tile_par * 2048 : 0)),
+                  reinterpret_cast<const float*>(lds + kColOff), reinterpret_cast<float*>(lds + kStOff)},
+            early);
       else
         epilogue_256<EPI, true, (DBG >> 1), NT>(acc, cm0, cn0, wm, wn, lane, C, ldc, bias, R, ldr, M,
                                             reinterpret_cast<const float*>(lds + kBiasOff) + tile_par * 256);
@@ -1493,6 +1572,8 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
   }
 #undef ATPU_PS_SYNC_MMA
   if (wm == 0) __builtin_amdgcn_s_barrier();  // close the stagger (equal barrier counts)
+  // kEarly: the last tile's dummy K-tile-1 DMAs land in LDS before the workgroup exits
+  if constexpr (kEarly) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr (kSt) {
     // the last tile's row partials: every wave's epilogue LDS writes done, then flushed
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
