@@ -1421,7 +1421,8 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
       // later and leaves every younger op (stores included) in flight:
       //   p0 -> Q2(0): 2 + 8 + 16 + kB0   p1 -> Q3(0): 8 + 16 + kB0
       //   p2 -> Q0, Q1(1): 4 + 16 + kB0    p3 -> Q2(1): 2 + 16 + kB0
-      // K-tile 1, p0 -> Q3(1): 16 + kB0 + kLn1 + 2 (its own staging of K-tile 2)
+      // K-tile 1, p0 -> Q3(1): 16 + kB0 + kLn1 + 2 (its own staging of K-tile 2); p1 -> nothing
+      // new (4 + 16 + kB0 + kLn1); the stores are retired at K-tile 1 p2 (vmcnt(4))
       if constexpr (kEarly && P == 0) {
         if (pre_staged) {
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + 8 + kEpiOps + kB0) : "memory");
@@ -1453,8 +1454,15 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
         }
       } else if (more) {
         stage(1, kn, buf ^ 1);
-        if (relax && !kEarly) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + kEpiOps) : "memory");
-        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        if constexpr (kEarly && P == 1) {
+          // nothing older than the stores is still needed (Q3(1) retired at p0): the stores are
+          // first retired at p2, whose wait covers K-tile 2's Q0 (issued after them)
+          if (pre_staged) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + kEpiOps + kB0 + kLn1) : "memory");
+          else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+          if (relax && !kEarly) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + kEpiOps) : "memory");
+          else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        }
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
