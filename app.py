@@ -381,59 +381,113 @@ class Controller:
 
 
 class Leaser:
-    """``LEASE_PREFETCH``: a thread that holds at most ONE lease ready for the main loop.
+    """``LEASE_PREFETCH``: lease the next task batch while the current one runs.
 
-    It leases only when nothing is queued, so the agent never holds more than the batch it
-    runs plus one; on 204 it sleeps ``IDLE_SLEEP_SEC`` and on errors ``ERROR_BACKOFF_SEC``
-    exactly like the serial loop, with its own keep-alive connection (http.client is not
-    thread-safe). ``job_epoch`` and the tasks pass through untouched. On shutdown the main
-    loop still runs a lease that was already taken (it is the agent's until its TTL)."""
+    The main loop leases for itself whenever nothing is ready (the reference's serial
+    order, no thread hand-off for sub-millisecond jobs). A helper thread takes ONE lease
+    ahead, on its own keep-alive connection (http.client is not thread-safe), only once
+    the running batch has been busy for ``LEASE_PREFETCH_AFTER_MS`` (default 2 ms): GPU
+    jobs then find their next lease waiting, while CPU-trivial jobs (echo) never pay for
+    a second thread contending for the GIL. At most one lease is held ahead and at most
+    one lease request is in flight; ``job_epoch`` and the tasks pass through untouched.
+    A lease taken ahead is still executed on shutdown (it is the agent's until its TTL)
+    and is failed with the rest on a lost DP rank."""
 
     def __init__(self, agent: "Agent") -> None:
-        import queue
-
         self.agent = agent
-        self.q: "queue.Queue[Tuple[str, List[Any]]]" = queue.Queue(maxsize=1)
         self.ctl = Controller(CONTROLLER_URL, HTTP_TIMEOUT_SEC)
-        self._stop = threading.Event()
-        self._taken = threading.Event()
-        self._taken.set()
+        self.after = max(0.0, float(os.getenv("LEASE_PREFETCH_AFTER_MS", "2"))) / 1000.0
+        self._cv = threading.Condition()
+        self._ahead: Optional[Tuple[str, List[Any]]] = None
+        self._inflight = False  # a lease request (either thread) is on the wire
+        self._running = False   # the main loop is executing a batch
+        self._epoch = 0         # batches started; one prefetch attempt per batch
+        self._tried = -1
+        self._stop = False
         self.thread = threading.Thread(target=self._loop, name="atpu-leaser", daemon=True)
         self.thread.start()
 
+    # ------------------------------------------------------------- helper thread
     def _loop(self) -> None:
-        while not self._stop.is_set() and _running:
-            if not self._taken.wait(0.05):
-                continue  # the previous lease is still queued
-            try:
-                leased = self.ctl.lease(self.agent.caps, self.agent.profile)
-            except Exception as exc:
-                log_every("lease", f"{LOG} lease error: {exc}")
-                self._stop.wait(ERROR_BACKOFF_SEC)
-                continue
-            if not leased:
-                self._stop.wait(IDLE_SLEEP_SEC)
-                continue
-            self._taken.clear()
-            self.q.put(leased)
+        with self._cv:
+            while True:
+                while not self._stop and not (self._running and self._ahead is None and not self._inflight
+                                              and self._tried != self._epoch):
+                    self._cv.wait()
+                if self._stop:
+                    return
+                epoch = self._epoch
+                # only long-running batches get a lease ahead
+                self._cv.wait_for(lambda: self._stop or not self._running or self._epoch != epoch, self.after)
+                if self._stop:
+                    return
+                if not self._running or self._epoch != epoch or self._ahead is not None or self._inflight:
+                    continue
+                self._tried, self._inflight = epoch, True
+            # lease outside the lock: the main thread keeps running its batch
+                self._cv.release()
+                try:
+                    leased = self.ctl.lease(self.agent.caps, self.agent.profile)
+                except Exception as exc:
+                    log_every("lease", f"{LOG} lease error: {exc}")
+                    leased = None
+                finally:
+                    self._cv.acquire()
+                self._inflight = False
+                if leased:
+                    self._ahead = leased
+                self._cv.notify_all()
 
-    def get(self, timeout: float) -> Optional[Tuple[str, List[Any]]]:
-        import queue
-
+    # --------------------------------------------------------------- main thread
+    def next(self) -> Optional[Tuple[str, List[Any]]]:
+        """The lease taken ahead if any, else one leased now (None on 204 / error, after
+        the serial loop's IDLE_SLEEP_SEC / ERROR_BACKOFF_SEC)."""
+        with self._cv:
+            self._cv.wait_for(lambda: not self._inflight)
+            if self._ahead is not None:
+                leased, self._ahead = self._ahead, None
+                return leased
+            self._inflight = True
         try:
-            leased = self.q.get(timeout=timeout)
-        except queue.Empty:
-            return None
-        self._taken.set()
+            leased = self.agent.ctl.lease(self.agent.caps, self.agent.profile)
+        except Exception as exc:
+            log_every("lease", f"{LOG} lease error: {exc}")
+            time.sleep(ERROR_BACKOFF_SEC)
+            leased = None
+        else:
+            if not leased:
+                time.sleep(IDLE_SLEEP_SEC)
+        finally:
+            with self._cv:
+                self._inflight = False
+                self._cv.notify_all()
         return leased
+
+    def started(self) -> None:
+        with self._cv:
+            self._running, self._epoch = True, self._epoch + 1
+            self._cv.notify_all()
+
+    def finished(self) -> None:
+        with self._cv:
+            self._running = False
+            self._cv.notify_all()
+
+    def take_ahead(self) -> Optional[Tuple[str, List[Any]]]:
+        with self._cv:
+            self._cv.wait_for(lambda: not self._inflight)
+            leased, self._ahead = self._ahead, None
+            return leased
 
     def pending(self) -> List[Tuple[str, List[Any]]]:
         """Leases taken from the controller but not started (rank-lost failure posts)."""
-        items = list(self.q.queue)
-        return items
+        with self._cv:
+            return [self._ahead] if self._ahead is not None else []
 
     def stop(self) -> None:
-        self._stop.set()
+        with self._cv:
+            self._stop = True
+            self._cv.notify_all()
         self.thread.join(timeout=HTTP_TIMEOUT_SEC + 5)
 
 
@@ -717,19 +771,22 @@ class Agent:
             self.run_tasks(lease_id, tasks)
 
     def _loop_prefetch(self) -> None:
-        """The serial loop with the lease taken one batch ahead (:class:`Leaser`)."""
-        self._leaser = Leaser(self)
+        """The serial loop with the next lease taken while a batch runs (:class:`Leaser`)."""
+        self._leaser = lz = Leaser(self)
         try:
             while _running:
-                leased = self._leaser.get(timeout=0.05)
-                if leased is not None:
-                    self.run_tasks(*leased)
-        finally:
-            self._leaser.stop()
-            while True:  # a lease taken before the stop is still ours: run it
-                leased = self._leaser.get(timeout=0.0)
+                leased = lz.next()
                 if leased is None:
-                    break
+                    continue
+                lz.started()
+                try:
+                    self.run_tasks(*leased)
+                finally:
+                    lz.finished()
+        finally:
+            lz.stop()
+            leased = lz.take_ahead()  # a lease taken before the stop is still ours: run it
+            if leased is not None:
                 self.run_tasks(*leased)
 
 

@@ -1,0 +1,72 @@
+"""app.Leaser (LEASE_PREFETCH): the next lease is taken by a helper thread only while a
+batch has been running for LEASE_PREFETCH_AFTER_MS; short batches keep the serial order."""
+import threading
+import time
+
+import pytest
+
+
+class FakeCtl:
+    log = []
+    queue = []
+    lock = threading.Lock()
+
+    def __init__(self, *a, **k):
+        pass
+
+    def lease(self, caps, profile):
+        with FakeCtl.lock:
+            FakeCtl.log.append((threading.current_thread().name, time.monotonic()))
+            return FakeCtl.queue.pop(0) if FakeCtl.queue else None
+
+
+class FakeAgent:
+    caps = ["echo"]
+    profile = {}
+    ctl = FakeCtl()
+
+
+@pytest.fixture
+def leaser(monkeypatch):
+    import app
+
+    monkeypatch.setattr(app, "Controller", FakeCtl)
+    monkeypatch.setattr(app, "IDLE_SLEEP_SEC", 0.0)
+    monkeypatch.setenv("LEASE_PREFETCH_AFTER_MS", "5")
+    FakeCtl.log, FakeCtl.queue = [], [("L%d" % i, [{"id": str(i)}]) for i in range(4)]
+    lz = app.Leaser(FakeAgent())
+    yield lz
+    lz.stop()
+
+
+def test_long_batch_gets_its_next_lease_ahead(leaser):
+    first = leaser.next()
+    assert first[0] == "L0" and FakeCtl.log[-1][0] == "MainThread"
+    leaser.started()
+    time.sleep(0.1)  # a long batch: the helper leases L1 after 5 ms
+    assert leaser.pending() == [("L1", [{"id": "1"}])]
+    assert [n for n, _ in FakeCtl.log] == ["MainThread", "atpu-leaser"]
+    leaser.finished()
+    assert leaser.next()[0] == "L1" and len(FakeCtl.log) == 2  # no new request
+    leaser.started()
+    time.sleep(0.1)
+    leaser.finished()
+    assert leaser.pending() == [("L2", [{"id": "2"}])]  # one ahead per batch, never more
+
+
+def test_short_batches_stay_serial(leaser):
+    for i in range(3):
+        assert leaser.next()[0] == f"L{i}"
+        leaser.started()
+        leaser.finished()  # sub-millisecond batch: the helper never fires
+    time.sleep(0.05)
+    assert [n for n, _ in FakeCtl.log] == ["MainThread"] * 3 and leaser.pending() == []
+
+
+def test_stop_hands_back_the_lease_taken_ahead(leaser):
+    leaser.next()
+    leaser.started()
+    time.sleep(0.1)
+    leaser.finished()
+    leaser.stop()
+    assert leaser.take_ahead()[0] == "L1" and leaser.take_ahead() is None
