@@ -46,8 +46,10 @@ def test_headline_engine_vs_serial_eager_every_row(headline):
     from agent_tpu_amd.runtime.classify import ClassifyEngine
 
     h = headline
+    # two staging slots (the stager's pipeline needs them) but ONE compute stream, eager
     ref = ClassifyEngine(h["cfg"], h["pack"], h["dev"], batch_rows=B, seq_len=S, topk=2, use_graph=False,
-                         slots=1, concurrent=False)
+                         slots=2, concurrent=False)
+    assert not ref.concurrent and not ref.use_graph
     ref.model.ln_fold = False
     ref.model.cls_only_last = False
     ri, rs, _ = ref.classify_table(h["table"], 0, h["n"], h["col"])
