@@ -15,34 +15,6 @@ import torch
 _ALIGN = 256
 
 
-def _h2d_staged(src: torch.Tensor, device: torch.device, chunk: int = 32 << 20) -> torch.Tensor:
-    """Host (pageable) -> device copy of a flat byte buffer through two pinned staging
-    buffers: the host memcpy of chunk i+1 overlaps the DMA of chunk i on a side stream.
-    A pageable ``tensor.to(device)`` is a staged copy inside the runtime at a fraction of
-    the link rate; this is the weight-upload path of every model load (C1 source, LRU miss)."""
-    n = src.numel()
-    dst = torch.empty(n, dtype=torch.uint8, device=device)
-    if n == 0:
-        return dst
-    chunk = min(chunk, n)
-    stream = torch.cuda.Stream(device)
-    pins = [torch.empty(chunk, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
-    done = [None, None]
-    with torch.cuda.stream(stream):
-        for i, off in enumerate(range(0, n, chunk)):
-            k = i & 1
-            m = min(chunk, n - off)
-            if done[k] is not None:
-                done[k].synchronize()  # the DMA that last read this staging buffer has finished
-            pins[k][:m].copy_(src[off:off + m])
-            dst[off:off + m].copy_(pins[k][:m], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(stream)
-            done[k] = ev
-    stream.synchronize()
-    return dst
-
-
 class ParamPack:
     def __init__(self, specs: Iterable[Tuple[str, Tuple[int, ...], torch.dtype]], device="cpu"):
         self.specs = list(specs)
@@ -78,14 +50,21 @@ class ParamPack:
     def names(self):
         return list(self.layout)
 
+    def adopt(self, buffer: torch.Tensor) -> "ParamPack":
+        """A pack with this layout over ``buffer`` (a copy of this pack's bytes, e.g. on a GPU)."""
+        assert buffer.numel() == self.nbytes and buffer.dtype == torch.uint8
+        out = ParamPack.__new__(ParamPack)
+        out.specs, out.layout, out.nbytes = self.specs, self.layout, self.nbytes
+        out.buffer = buffer
+        out._views = out._make_views()
+        return out
+
     def to(self, device) -> "ParamPack":
         out = ParamPack.__new__(ParamPack)
         out.specs, out.layout, out.nbytes = self.specs, self.layout, self.nbytes
-        device = torch.device(device)
-        if device.type == "cuda" and self.buffer.device.type == "cpu" and not self.buffer.is_pinned():
-            out.buffer = _h2d_staged(self.buffer, device)
-        else:
-            out.buffer = self.buffer.to(device)
+        # a pageable host -> HBM copy runs at ~56 GB/s on MI355X (tools/probe_h2d.py: as fast as
+        # from pinned memory; two-slot pinned staging measured 40 GB/s), so no staging here
+        out.buffer = self.buffer.to(device)
         out._views = out._make_views()
         return out
 

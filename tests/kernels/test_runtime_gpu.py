@@ -147,19 +147,13 @@ def test_small_job_bucket_graphs_match_eager(gpu, n):
     assert torch.equal(a.idx, ri.cpu())
 
 
-def test_param_pack_staged_upload(gpu):
-    """ParamPack.to(cuda) from pageable host memory goes through the pinned two-buffer
-    staging (several chunks, ragged tail): bit-identical to the host buffer."""
-    from agent_tpu_amd.models import params
-
-    src = torch.randint(0, 256, ((70 << 20) + 12345,), dtype=torch.uint8)
-    dst = params._h2d_staged(src, torch.device("cuda", 0), chunk=16 << 20)
-    assert dst.is_cuda and torch.equal(dst.cpu(), src)
+def test_param_pack_upload(gpu):
+    """ParamPack.to(cuda): bit-identical buffer and views (the weight upload of every model load)."""
     from agent_tpu_amd.models.bert import config_for, init_random
 
     pack = init_random(config_for("bert-tiny", num_labels=3), seed=1)
     dev = pack.to("cuda")
-    assert torch.equal(dev.buffer.cpu(), pack.buffer)
+    assert dev.buffer.is_cuda and torch.equal(dev.buffer.cpu(), pack.buffer)
     assert all(torch.equal(dev[n].cpu(), pack[n]) for n in pack.names())
 
 

@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
 """Host -> HBM upload of a model-sized byte buffer, by method (weights upload, C1 source).
 
-Prints ms and GB/s per method for a 219 MB (BERT-base bf16) pageable buffer: plain
-pageable .to(), the two-slot pinned staging of ParamPack.to (several chunk sizes),
-pin_memory() + async copy, and a copy from an already pinned buffer (the DMA floor)."""
+Prints ms and GB/s (best of 3) for a 219 MB (BERT-base bf16) pageable buffer: plain
+pageable .to(), pin_memory() + async copy, and a copy from an already pinned buffer (the
+DMA floor). Round 4 measured pageable 56 GB/s = pinned 57.5 (and a two-slot pinned
+staging in 32 MiB chunks 40 GB/s, since removed): ParamPack.to stays a plain copy
+(profiles/h2d_upload_r04.json)."""
 import json
 import os
 import sys
@@ -12,7 +14,6 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from agent_tpu_amd.models import params  # noqa: E402
 
 
 def timed(fn, reps=3):
@@ -34,8 +35,6 @@ def main():
     pinned = src.pin_memory()
     res = {"bytes": n, "torch_threads": torch.get_num_threads()}
     res["pageable_to"] = timed(lambda: src.to(dev))
-    for ch in (8, 32, 64):
-        res[f"staged_{ch}MiB"] = timed(lambda: params._h2d_staged(src, dev, chunk=ch << 20))
     res["pin_then_copy"] = timed(lambda: src.pin_memory().to(dev, non_blocking=True))
     res["from_pinned"] = timed(lambda: pinned.to(dev, non_blocking=True))
     out = {k: (round(v, 2) if isinstance(v, float) else v) for k, v in res.items()}
