@@ -34,6 +34,10 @@ def main() -> int:
                     help="csv: CSV-shard jobs; input: the reference job shape, one pre-tokenized row per job")
     ap.add_argument("--max-tasks", type=int, default=1, help="MAX_TASKS (input form: jobs per lease, batched)")
     ap.add_argument("--batch", default="1", help="LEASE_BATCH")
+    ap.add_argument("--dp", type=int, default=1,
+                    help="agent ranks (torch.distributed.run, one process per GPU; rank 0 leases)")
+    ap.add_argument("--dp-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse N ranks on fewer GPUs (ranks share a card)")
     a = ap.parse_args()
     if a.form == "input":
         return input_form(a)
@@ -52,9 +56,13 @@ def main() -> int:
 
     ctl.lease(job(0), lease_id="Lwarm")  # model load + graph capture
     env = dict(os.environ, CONTROLLER_URL=ctl.url, TASKS="map_classify", IDLE_SLEEP_SEC="0.01", MAX_TASKS="1",
-               GPU_MODEL_PATH=a.model, PYTHONUNBUFFERED="1")
-    p = subprocess.Popen([sys.executable, "app.py"], cwd=REPO, env=env, stdout=subprocess.DEVNULL,
-                         stderr=subprocess.DEVNULL)
+               GPU_MODEL_PATH=a.model, PYTHONUNBUFFERED="1", ATPU_DP_BACKEND=a.dp_backend)
+    cmd = [sys.executable, "app.py"]
+    if a.dp > 1:
+        from agent_tpu_amd.parallel.launch import torchrun_cmd
+
+        cmd = torchrun_cmd("app.py", [], a.dp)
+    p = subprocess.Popen(cmd, cwd=REPO, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
     try:
         ok = ctl.wait(lambda c: len(c.results) >= 1, 600)
         for i in range(1, a.jobs + 1):
@@ -81,6 +89,7 @@ def main() -> int:
     print(json.dumps({"metric": f"classified rows/sec end to end through the agent ({a.model}, 1 GPU)",
                       "value": round(n / el, 1), "unit": "rows/s", "higher_is_better": True,
                       "config": {"jobs": a.jobs, "rows_per_job": a.shard, "output": a.output,
+                                 "dp_ranks": a.dp, "dp_backend": a.dp_backend if a.dp > 1 else None,
                                  "median_op_rows_per_sec": round(engine_rps, 1),
                                  "median_op_elapsed_ms": op_ms, "median_op_timing_ms": timing,
                                  "transport": "HTTP/1.1 keep-alive, loopback mock controller",
