@@ -101,6 +101,34 @@ PYBIND11_MODULE(_atpu, m) {
       py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("in_fin"), py::arg("colsum"),
       py::arg("res_fin"), py::arg("gamma"), py::arg("part_out"), py::arg("stream"));
   m.def(
+      "gemm256h",
+      [](uintptr_t A, int lda, uintptr_t Bt, int ldb, uintptr_t C, int ldc, uintptr_t bias, int M, int N, int K,
+         int epi, uintptr_t in_fin, uintptr_t colsum, int mode, uintptr_t stream) {
+        GemmArgs g;
+        g.A = P<const bf16>(A); g.lda = lda; g.Bt = P<const bf16>(Bt); g.ldb = ldb; g.C = P<bf16>(C); g.ldc = ldc;
+        g.bias = P<const float>(bias); g.M = M; g.N = N; g.K = K; g.epi = epi;
+        g.in_fin = P<const float>(in_fin); g.colsum = P<const float>(colsum);
+        gemm256h(g, mode, S(stream));
+      },
+      "persistent 256x192 bf16 GEMM (one head's Q|K|V per tile); mode 1 = timing only", py::arg("A"),
+      py::arg("lda"), py::arg("Bt"), py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("bias"), py::arg("M"),
+      py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("in_fin"), py::arg("colsum"), py::arg("mode"),
+      py::arg("stream"));
+  m.def(
+      "qkv_attention",
+      [](uintptr_t A, int lda, uintptr_t Bt, int ldb, uintptr_t ctx, int ldo, uintptr_t bias, int M, int N, int K,
+         int epi, uintptr_t in_fin, uintptr_t colsum, uintptr_t lens, float scale, uintptr_t stream) {
+        GemmArgs g;
+        g.A = P<const bf16>(A); g.lda = lda; g.Bt = P<const bf16>(Bt); g.ldb = ldb; g.C = P<bf16>(ctx); g.ldc = ldo;
+        g.bias = P<const float>(bias); g.M = M; g.N = N; g.K = K; g.epi = epi;
+        g.in_fin = P<const float>(in_fin); g.colsum = P<const float>(colsum);
+        qkv_attention(g, P<const int32_t>(lens), scale, S(stream));
+      },
+      "BERT QKV projection + self-attention (S = 128) in one persistent kernel; Bt rows per head [Q|K|V]",
+      py::arg("A"), py::arg("lda"), py::arg("Bt"), py::arg("ldb"), py::arg("ctx"), py::arg("ldo"), py::arg("bias"),
+      py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("in_fin"), py::arg("colsum"),
+      py::arg("lens"), py::arg("scale"), py::arg("stream"));
+  m.def(
       "ln_stats_finalize",
       [](uintptr_t part, int slots, int M, int K, float eps, uintptr_t fin, uintptr_t stream) {
         ln_stats_finalize(P<const float>(part), slots, M, K, eps, P<float>(fin), S(stream));

@@ -81,6 +81,13 @@ int gemm_force_tile(int set);
 // 256x256 schedule selector (benchmarks): set >= 0 switches; returns the current
 int gemm_256_variant(int set);
 int gemm_ablate(int set);  // timing-only ablations of the persistent 256x256 kernel (results wrong); -1 reads
+// persistent 256 x 192 GEMM (qkv_attn.hip; one BERT head's Q|K|V per tile): epi = Bias or
+// Bias|InNorm; mode 0 stores C, 1 = timing only (no epilogue, C untouched)
+void gemm256h(const GemmArgs& g, int mode, hipStream_t stream);
+// BERT QKV projection + self-attention in one persistent kernel (S = 128, head dim 64):
+// Bt = the QKV weight with rows in [head][Q 64 | K 64 | V 64] order (bias / colsum likewise),
+// g.C = the context [M, N / 3] (row stride g.ldc), lens[M / 128] the sequence lengths
+void qkv_attention(const GemmArgs& g, const int32_t* lens, float scale, hipStream_t stream);
 int attention_persist_mode(int set);  // packed BERT attention: 1 persistent (default), 0 per-item
 int num_cus();                        // CUs a persistent grid is sized for (device count, or the budget below)
 int cu_budget(int set);               // >0: size persistent grids for this many CUs (CU-masked streams)

@@ -1,0 +1,529 @@
+// BERT encoder QKV projection on 256 x 192 tiles: one tile = the Q | K | V columns of ONE
+// head (192 = 3 x 64) for 256 rows = two 128-token sequences, so a tile holds everything
+// the head's attention needs for both sequences.
+//
+// Persistent ping-pong schedule of the 256 x 256 "256s" kernel (gemm_bf16.hip), adapted to a
+// 192-column B tile: wave (wm, wn) owns rows wm*128..+128 (sequence wm of the tile) and
+// columns wn*48..+48 (3 MFMA column fragments). Per 64-deep K-tile, four phases:
+//   p0: read A-top (4 frags) + B frags 0-1 -> MFMA (top, 0-1)    16 MFMA   stage Q0, Q1 (4 DMA)
+//   p1: read B frag 2                     -> MFMA (top, 2)       8 MFMA   stage Q2 (1 DMA)
+//   p2: read A-bottom                     -> MFMA (bottom, 2)    8 MFMA   stage Q3 (2 DMA)
+//   p3: (registers only)                  -> MFMA (bottom, 0-1) 16 MFMA
+// Quarters = row sets of the 128-B-row images of the NEXT K-tile, by the phase that first
+// reads them: Q0 = A rows {0-63, 128-191}, Q1 = B rows wn*48 + {0..31} (both read at p0),
+// Q2 = B rows wn*48 + {32..47} (p1), Q3 = A rows {64-127, 192-255} (p2). A quarter is staged
+// the phase its buffer half was read one K-tile earlier, and retired by the wait of the phase
+// before its first read (a wait before phase p's barrier covers reads in phase p+1, for both
+// staggered wave groups): Q0/Q1 at p3 (vmcnt 3), Q2 at p0 (6), Q3 at p1 (5) - 32, 32 and 40
+// MFMAs of the wave after their issue, at least the 256s kernel's 32.
+//
+// MODE 0 stores Q|K|V (bf16) like the general GEMM; MODE 1 is a timing-only build with no
+// epilogue (accumulators kept live). EPI: bias, optionally InNorm (the QKV of BERT layers
+// >= 1 consumes LN2 of the previous layer folded into the weights, as gemm256s).
+#include "atpu/common.h"
+#include "atpu/kernels.h"
+
+#include <algorithm>
+
+namespace atpu {
+namespace {
+
+constexpr int kHImgA = 256 * 128;             // A image: 256 rows x 128 B
+constexpr int kHImgB = 192 * 128;             // B image: 192 rows x 128 B
+constexpr int kHBuf = kHImgA + kHImgB;        // one K-tile
+constexpr int kHStores = 24;                  // MODE 0 epilogue stores per wave (8 row x 3 col fragments)
+
+__device__ __forceinline__ int hsw(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+// image row of staging round i (of the quarter) for the wave's 8-row group g8 = (i*8 + wave)*8
+__device__ __forceinline__ int hq_row(int q, int ql) {
+  switch (q) {
+    case 0: return (ql & 63) + (ql >> 6) * 128;
+    case 3: return (ql & 63) + (ql >> 6) * 128 + 64;
+    case 1: return (ql >> 5) * 48 + (ql & 31);
+    default: return (ql >> 4) * 48 + 32 + (ql & 15);
+  }
+}
+constexpr int hq_rounds(int q) { return q == 2 ? 1 : 2; }
+
+// attention images (MODE 2): per sequence s of the tile, Q, K, V of the head as [128][128 B]
+// bf16 images, Q and K chunk-swizzled like the operand images (conflict-free fragment
+// reads), V with the swizzle of the transposed reads (attention.hip vswz)
+constexpr int kAImg = 128 * 128;
+__device__ __forceinline__ int vsw(int r, int c) { return c ^ (((r >> 1) & 3) << 1); }
+
+typedef short hv4s __attribute__((vector_size(8)));
+// ds_read_b64_tr_b16 (per 16-lane group: lane 4q+p addresses row q, elements 4p..4p+3 of a
+// 4 x 16 block; lane i receives column i of the 4 rows). Inline asm: the builtin makes the
+// waitcnt pass drain the LDS-DMA stream in flight to the other operand buffer.
+__device__ __forceinline__ bf16x4 tr16(const char* p) {
+  hv4s r;
+  const unsigned a = (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return __builtin_bit_cast(bf16x4, r);
+}
+
+template <int EPI, int MODE>
+__global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict__ A, int lda,
+                                                          const bf16* __restrict__ Bt, int ldb,
+                                                          bf16* __restrict__ C, int ldc,
+                                                          const float* __restrict__ bias,
+                                                          const float* __restrict__ in_fin,
+                                                          const float* __restrict__ colsum, int M, int N, int K,
+                                                          const int32_t* __restrict__ lens, float scale) {
+  constexpr bool kIn = EPI & kEpiInNorm;
+  // MODE 2: the 6 attention images (96 KiB) start at operand buffer 1, which holds the last
+  // K-tile of every tile (host: K / 64 even), and run 40 KiB past it
+  constexpr int kImgOff = kHBuf;
+  constexpr int kBiasOff = MODE == 2 ? kImgOff + 6 * kAImg : 2 * kHBuf;  // [2 tiles][4 x 64] fp32 (wn-padded)
+  constexpr int kFinOff = kBiasOff + 2 * 1024;  // [256][2] (rstd, rstd*mu) of the tile's rows
+  constexpr int kColOff = kFinOff + 2048;       // [4 x 64] colsum (wn-padded)
+  constexpr int kLds = kColOff + 1024;
+  // VMEM ops a tile's epilogue leaves in flight: C stores (MODE 0) or context stores (MODE 2)
+  constexpr int kEpiOps = MODE == 0 ? kHStores : MODE == 2 ? 4 : 0;
+  constexpr int kLn1 = kIn ? 2 : 0;
+  static_assert(kLds <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char lds[kLds];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int ntn = N / 192, ntiles = (M / 256) * ntn;
+  const int G = gridDim.x;
+  int v = blockIdx.x;
+  if (v >= ntiles) return;
+
+  auto opaque_lane = [] {
+    int l = __lane_id();
+    asm volatile("" : "+v"(l));
+    return l;
+  };
+  // per (quarter, round): wave-uniform LDS destination and 32-bit byte offset of the lane's source
+  int dst[4][2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      dst[q][i] = (q == 0 || q == 3 ? 0 : kHImgA) + hq_row(q, (i * 8 + wave) * 8) * 128;
+  uint32_t soff[4][2];
+  auto set_src = [&](int tm0, int tn0) {
+    const int ln = opaque_lane();
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < hq_rounds(q); ++i) {
+        const int r = hq_row(q, (i * 8 + wave) * 8 + (ln >> 3));
+        const size_t e = (q == 0 || q == 3) ? (size_t)(tm0 + r) * lda + hsw(r, ln & 7) * 8
+                                            : (size_t)(tn0 + r) * ldb + hsw(r, ln & 7) * 8;
+        soff[q][i] = (uint32_t)(e * 2);
+      }
+  };
+  auto stage = [&](int q, int kt, int buf) {
+    char* base = lds + buf * kHBuf;
+    const char* g = reinterpret_cast<const char*>((q == 0 || q == 3) ? A : Bt) + kt * 128;
+#pragma unroll
+    for (int i = 0; i < hq_rounds(q); ++i) glds16(g + soff[q][i], base + dst[q][i]);
+  };
+  // 4-byte LDS-DMA of 64 floats per wave: wn-padded [4][64] rows, lanes past 48 clamped
+  // (their copies land in the padding)
+  auto glds4 = [&](const float* ubase, int nvalid, char* ldst) {
+    const int l = opaque_lane();
+    __builtin_amdgcn_global_load_lds((const ATPU_GLOBAL_AS void*)(ubase + min(l, nvalid - 1)),
+                                     (ATPU_LDS_AS void*)ldst, 4, 0, 0);
+  };
+
+  const int fr = lane & 15, fc = lane >> 4;
+  f32x4 acc[8][3];
+  bf16x8 af[2][4], b01[2][2], b2[2];
+  auto read_a = [&](int buf, int qm) {
+    const char* img = lds + buf * kHBuf;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wm * 128 + qm * 64 + i * 16 + fr;
+        af[ks][i] = *reinterpret_cast<const bf16x8*>(img + r * 128 + hsw(r, ks * 4 + fc) * 16);
+      }
+  };
+  auto read_b01 = [&](int buf) {
+    const char* img = lds + buf * kHBuf + kHImgA;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wn * 48 + j * 16 + fr;
+        b01[ks][j] = *reinterpret_cast<const bf16x8*>(img + r * 128 + hsw(r, ks * 4 + fc) * 16);
+      }
+  };
+  auto read_b2 = [&](int buf) {
+    const char* img = lds + buf * kHBuf + kHImgA;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int r = wn * 48 + 32 + fr;
+      b2[ks] = *reinterpret_cast<const bf16x8*>(img + r * 128 + hsw(r, ks * 4 + fc) * 16);
+    }
+  };
+  auto mma01 = [&](int qm) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[qm * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b01[ks][j], af[ks][i], acc[qm * 4 + i][j], 0, 0, 0);
+  };
+  auto mma2 = [&](int qm) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        acc[qm * 4 + i][2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2[ks], af[ks][i], acc[qm * 4 + i][2], 0, 0, 0);
+  };
+
+  // ---- MODE 2: attention of sequence wm of the tile, head h, query rows wn*32..+32 ----
+  // Two 16-query blocks share every K / V fragment read. Scores, softmax and P.V as the
+  // packed attention kernel (attention.hip): S = K.Q^T per 16 x 16 block (lane: query fr,
+  // keys 4fc..+4), row max / sum over the 4 lanes of a query in registers, exp2 with the
+  // scale folded, P as the A operand of P.V in the key order of its two score blocks, V
+  // through transposed reads. The context goes out through the wave's own Q rows (free
+  // once read) as whole 128-B rows: 4 stores per wave.
+  auto attend = [&](int tm0, int h) {
+    const char* qi = lds + kImgOff + wm * 3 * kAImg;
+    const char* ki = qi + kAImg;
+    const char* vi = qi + 2 * kAImg;
+    bf16x8 qf[2][2];
+#pragma unroll
+    for (int qp = 0; qp < 2; ++qp)
+#pragma unroll
+      for (int ds = 0; ds < 2; ++ds) {
+        const int r = wn * 32 + qp * 16 + fr;
+        qf[qp][ds] = *reinterpret_cast<const bf16x8*>(qi + r * 128 + hsw(r, ds * 4 + fc) * 16);
+      }
+    f32x4 s[2][8];
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      s[0][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      s[1][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ds = 0; ds < 2; ++ds) {
+        const int r = kt * 16 + fr;
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ki + r * 128 + hsw(r, ds * 4 + fc) * 16);
+        s[0][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][ds], s[0][kt], 0, 0, 0);
+        s[1][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][ds], s[1][kt], 0, 0, 0);
+      }
+    }
+    const int len = min(lens[(tm0 >> 7) + wm], 128);  // wave-uniform (scalar load)
+    const float cl = scale * 1.4426950408889634f;
+    float inv[2];
+#pragma unroll
+    for (int qp = 0; qp < 2; ++qp) {
+      float mx = -1e30f, psum = 0.f;
+      if (len >= 128) {
+#pragma unroll
+        for (int kt = 0; kt < 8; ++kt)
+          mx = fmaxf(mx, fmaxf(fmaxf(s[qp][kt][0], s[qp][kt][1]), fmaxf(s[qp][kt][2], s[qp][kt][3])));
+        const float moff = lane_rows_max(mx) * cl;
+#pragma unroll
+        for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float p = __builtin_amdgcn_exp2f(fmaf(s[qp][kt][e], cl, -moff));
+            s[qp][kt][e] = p;
+            psum += p;
+          }
+      } else {
+#pragma unroll
+        for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x = kt * 16 + fc * 4 + e < len ? s[qp][kt][e] : -1e30f;
+            s[qp][kt][e] = x;
+            mx = fmaxf(mx, x);
+          }
+        const float moff = lane_rows_max(mx) * cl;
+#pragma unroll
+        for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x = s[qp][kt][e];
+            const float p = x <= -1e29f ? 0.f : __builtin_amdgcn_exp2f(fmaf(x, cl, -moff));
+            s[qp][kt][e] = p;
+            psum += p;
+          }
+      }
+      psum = lane_rows_sum(psum);
+      inv[qp] = psum > 0.f ? 1.f / psum : 0.f;
+    }
+    f32x4 o[2][4];
+#pragma unroll
+    for (int qp = 0; qp < 2; ++qp)
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[qp][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int tq = fr >> 2, tp = fr & 3;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      bf16x8 pf[2];
+#pragma unroll
+      for (int qp = 0; qp < 2; ++qp)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          pf[qp][e] = f2bf(s[qp][2 * ks][e]);
+          pf[qp][4 + e] = f2bf(s[qp][2 * ks + 1][e]);
+        }
+      const int klo = ks * 32 + fc * 4 + tq, khi = klo + 16;
+#pragma unroll
+      for (int dh = 0; dh < 4; dh += 2) {
+        bf16x4 lo[2], hi[2];
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const int c = (dh + d) * 2 + (tp >> 1);
+          lo[d] = tr16(vi + klo * 128 + vsw(klo, c) * 16 + (tp & 1) * 8);
+          hi[d] = tr16(vi + khi * 128 + vsw(khi, c) * 16 + (tp & 1) * 8);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          bf16x8 vf;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            vf[e] = lo[d][e];
+            vf[4 + e] = hi[d][e];
+          }
+          o[0][dh + d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[0], o[0][dh + d], 0, 0, 0);
+          o[1][dh + d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[1], o[1][dh + d], 0, 0, 0);
+        }
+      }
+    }
+    // context rows -> this wave's 32 Q rows (row-chunk swizzle ch ^ (row & 7)), then whole lines out
+    char* ost = const_cast<char*>(qi) + wn * 32 * 128;
+#pragma unroll
+    for (int qp = 0; qp < 2; ++qp)
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        bf16x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = f2bf(o[qp][dt][e] * inv[qp]);
+        const int ro = qp * 16 + fr, ch = dt * 2 + (fc >> 1);
+        *reinterpret_cast<bf16x4*>(ost + ro * 128 + ((ch ^ (ro & 7)) << 4) + (fc & 1) * 8) = w;
+      }
+    const int l2 = opaque_lane();
+    const int lr = l2 >> 3, lc8 = l2 & 7;
+    bf16* obase = C + (size_t)(tm0 + wm * 128 + wn * 32) * ldc + h * 64 + lc8 * 8;
+#pragma unroll
+    for (int hh = 0; hh < 4; ++hh) {
+      const int ro = hh * 8 + lr;
+      const u32x4 val = *reinterpret_cast<const u32x4*>(ost + ro * 128 + ((lc8 ^ (ro & 7)) << 4));
+      *reinterpret_cast<u32x4*>(obase + (size_t)ro * ldc) = val;
+    }
+  };
+
+  const int nk = K / 64;
+  int tile = xcd_remap(v, ntiles);
+  int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 192;
+  set_src(m0, n0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) stage(q, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger: group 1 runs one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+#define ATPU_H_SYNC_MMA(MMA)                                \
+  __builtin_amdgcn_sched_barrier(0);                        \
+  __builtin_amdgcn_s_barrier();                             \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        \
+  __builtin_amdgcn_sched_barrier(0);                        \
+  __builtin_amdgcn_s_setprio(1);                            \
+  MMA;                                                      \
+  __builtin_amdgcn_s_setprio(0);                            \
+  __builtin_amdgcn_sched_barrier(0);                        \
+  __builtin_amdgcn_s_barrier();                             \
+  __builtin_amdgcn_sched_barrier(0)
+
+  int buf = 0, tile_par = 0;
+  bool first = true;
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int vn = v + G;
+    const bool has_next = vn < ntiles;
+    const int cm0 = m0, cn0 = n0;
+    // P: K-tile 0 / 1 (compile time: bias / LN staging) or -1
+    auto kstep = [&](int t, auto last_c, auto peel_c) {
+      constexpr bool last = decltype(last_c)::value;
+      constexpr int P = decltype(peel_c)::value;
+      const bool more = !last || has_next;
+      int kn = t + 1;
+      if (last && has_next) {  // the stream runs on into K-tile 0 of the next tile
+        tile = xcd_remap(vn, ntiles);
+        m0 = (tile / ntn) * 256;
+        n0 = (tile % ntn) * 192;
+        set_src(m0, n0);
+        kn = 0;
+      }
+      // VMEM ops (oldest first) a wait may leave in flight. K-tile 0 of a tile after the
+      // first: the previous tile's epilogue stores (kEpiOps) sit between the last quarters
+      // of this K-tile and the next K-tile's; they are retired with Q0/Q1 at p3. Extra ops
+      // are issued after the phase-0 staging: this tile's bias at K-tile 0 (1) and the LN
+      // data at K-tile 1 (kLn1, 2 with InNorm); the counts below include them (kX) and they
+      // retire at the next K-tile's p0, long before the epilogue reads them.
+      const bool relax = P == 0 && !first;
+      constexpr int kX = P == 0 ? 1 : (P == 1 ? kLn1 : 0);
+      // p0
+      read_a(buf, 0);
+      read_b01(buf);
+      if (more) {
+        stage(0, kn, buf ^ 1);
+        stage(1, kn, buf ^ 1);
+        if constexpr (P == 0) {
+          // this tile's bias -> LDS (every wave issues one op; waves w and w+4 write the same bytes)
+          glds4(bias + cn0 + wn * 48, 48, lds + kBiasOff + tile_par * 1024 + wn * 256);
+        }
+        if constexpr (P == 1 && kIn) {
+          glds4(in_fin + (size_t)cm0 * 2 + wave * 64, 64, lds + kFinOff + wave * 256);
+          glds4(colsum + cn0 + wn * 48, 48, lds + kColOff + wn * 256);
+        }
+        // retires Q2 (read at p1); Q3 (2) + epilogue stores + Q0/Q1 (4) + extras may fly
+        if (relax) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 + kEpiOps + kX) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 + kX) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // Q2 landed, Q3 (2) may fly
+      }
+      ATPU_H_SYNC_MMA(mma01(0));
+      // p1
+      read_b2(buf);
+      if (more) {
+        stage(2, kn, buf ^ 1);
+        // retires Q3 (read at p2)
+        if (relax) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 + kEpiOps + kX) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 + kX) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      ATPU_H_SYNC_MMA(mma2(0));
+      // p2
+      read_a(buf, 1);
+      if (more) stage(3, kn, buf ^ 1);
+      ATPU_H_SYNC_MMA(mma2(1));
+      // p3: retires Q0/Q1 of the next K-tile (read at its p0) and everything older
+      if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 + kX) : "memory");
+      ATPU_H_SYNC_MMA(mma01(1));
+      buf ^= 1;
+    };
+    kstep(0, std::false_type{}, std::integral_constant<int, 0>{});
+    kstep(1, std::false_type{}, std::integral_constant<int, 1>{});
+    for (int t = 2; t + 1 < nk; ++t) kstep(t, std::false_type{}, std::integral_constant<int, -1>{});
+    kstep(nk - 1, std::true_type{}, std::integral_constant<int, -1>{});
+    // both wave groups run the epilogue side by side (as gemm256s)
+    __builtin_amdgcn_sched_barrier(0);
+    if (wm == 0) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (MODE == 1) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) asm volatile("" ::"v"(acc[i][j]));
+    } else {
+      const int ol = kIn ? opaque_lane() : lane;
+      const int ofr = ol & 15, ofc = ol >> 4;
+      const float* lb = reinterpret_cast<const float*>(lds + kBiasOff + tile_par * 1024 + wn * 256);
+      const float* lc = reinterpret_cast<const float*>(lds + kColOff + wn * 256);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int lrow = wm * 128 + i * 16 + ofr;
+        f32x2 rsm = f32x2{1.f, 0.f};
+        if constexpr (kIn) rsm = *reinterpret_cast<const f32x2*>(lds + kFinOff + lrow * 8);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const int c = j * 16 + ofc * 4;
+          const f32x4 b4 = *reinterpret_cast<const f32x4*>(lb + c);
+          f32x4 t;
+          if constexpr (kIn) {
+            const f32x4 c4 = *reinterpret_cast<const f32x4*>(lc + c);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) t[e] = fmaf(acc[i][j][e], rsm[0], fmaf(-rsm[1], c4[e], b4[e]));
+          } else {
+            t = acc[i][j] + b4;
+          }
+          typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+          const u32x2 o = u32x2{pack_bf16x2(t[0], t[1]), pack_bf16x2(t[2], t[3])};
+          if constexpr (MODE == 0) {
+            *reinterpret_cast<u32x2*>(C + (size_t)(cm0 + lrow) * ldc + cn0 + wn * 48 + c) = o;
+          } else {
+            // 16-column fragments never straddle Q | K | V (48 = 3 x 16): the image is wave-uniform
+            const int cb = wn * 48 + j * 16, typ = cb >> 6;
+            const int d0 = (cb & 63) + ofc * 4, r = i * 16 + ofr, ch = d0 >> 3;
+            const int sc = typ == 2 ? vsw(r, ch) : hsw(r, ch);
+            *reinterpret_cast<u32x2*>(lds + kImgOff + (wm * 3 + typ) * kAImg + r * 128 + sc * 16 + ((d0 >> 2) & 1) * 8) = o;
+          }
+        }
+      }
+      if constexpr (MODE == 2) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // the images of both sequences are complete
+        __builtin_amdgcn_sched_barrier(0);
+        attend(cm0, cn0 / 192);
+        // every wave's image reads are done before group 0 runs ahead into the next tile,
+        // whose K-tile 1 is staged into operand buffer 1 (= part of the images)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (wm == 1) __builtin_amdgcn_s_barrier();
+    if (!has_next) break;
+    v = vn;
+    first = false;
+    tile_par ^= 1;
+  }
+#undef ATPU_H_SYNC_MMA
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // close the stagger (equal barrier counts)
+}
+
+}  // namespace
+
+static void launch_256h(const GemmArgs& g, int mode, const int32_t* lens, float scale, hipStream_t s) {
+  ATPU_CHECK(g.N % 192 == 0 && g.M % 256 == 0 && g.K % 64 == 0 && g.K >= 256,
+             "gemm256h: N % 192, M % 256 == 0, K % 64 == 0 and K >= 256");
+  ATPU_CHECK(g.epi == kEpiBias || g.epi == (kEpiBias | kEpiInNorm), "gemm256h: epilogue bias or bias|InNorm");
+  ATPU_CHECK(!(g.epi & kEpiInNorm) || (g.in_fin && g.colsum), "gemm256h: InNorm needs in_fin and colsum");
+  ATPU_CHECK(g.bias && g.ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(g.C) & 7) == 0, "gemm256h: bias, 8-B rows");
+  ATPU_CHECK((size_t)g.M * g.lda * 2 < (1ull << 32) && (size_t)g.N * g.ldb * 2 < (1ull << 32),
+             "gemm256h: A and Bt under 4 GiB (32-bit staging offsets)");
+  ATPU_CHECK(mode >= 0 && mode <= 2, "gemm256h: mode 0 (store), 1 (timing only) or 2 (attention)");
+  if (mode == 2) {
+    // the images live in operand buffer 1: the last K-tile of every tile must be staged there
+    ATPU_CHECK((g.K / 64) % 2 == 0, "qkv_attention: K / 64 must be even");
+    ATPU_CHECK(lens && g.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(g.C) & 15) == 0,
+               "qkv_attention: lens and 16-B aligned context rows");
+  }
+  const int tiles = (g.M / 256) * (g.N / 192);
+  int nb = std::min(tiles, num_cus());
+  if (nb >= 8) nb &= ~7;
+#define ATPU_GH(E, MD)                                                                                          \
+  hipLaunchKernelGGL((gemm256h_kernel<E, MD>), dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, \
+                     g.bias, g.in_fin, g.colsum, g.M, g.N, g.K, lens, scale)
+  if (g.epi & kEpiInNorm) {
+    if (mode == 0) ATPU_GH(kEpiBias | kEpiInNorm, 0);
+    else if (mode == 1) ATPU_GH(kEpiBias | kEpiInNorm, 1);
+    else ATPU_GH(kEpiBias | kEpiInNorm, 2);
+  } else {
+    if (mode == 0) ATPU_GH(kEpiBias, 0);
+    else if (mode == 1) ATPU_GH(kEpiBias, 1);
+    else ATPU_GH(kEpiBias, 2);
+  }
+#undef ATPU_GH
+  ATPU_HIP_CHECK(hipGetLastError());
+}
+
+void gemm256h(const GemmArgs& g, int mode, hipStream_t s) {
+  ATPU_CHECK(mode == 0 || mode == 1, "gemm256h: mode 0 (store) or 1 (timing only, no epilogue)");
+  launch_256h(g, mode, nullptr, 0.f, s);
+}
+
+void qkv_attention(const GemmArgs& g, const int32_t* lens, float scale, hipStream_t s) {
+  launch_256h(g, 2, lens, scale, s);
+}
+
+}  // namespace atpu

@@ -192,6 +192,9 @@ class BertClassifier:
         self.ln_fold = (self.device.type == "cuda" and not fp32
                         and os.getenv("ATPU_LN_FOLD", "1") not in ("0", "false", "no"))
         self._folded: Optional[Dict[str, torch.Tensor]] = None
+        # QKV projection + attention fused into one kernel (S = 128, LN-folded encoder):
+        # ATPU_QKV_ATTN=0 runs the QKV GEMM and the packed attention kernel separately
+        self.fused_qkv_attention = os.getenv("ATPU_QKV_ATTN", "1") not in ("0", "false", "no")
 
     # ------------------------------------------------------------ LN folding
     def folded(self) -> Dict[str, torch.Tensor]:
@@ -214,6 +217,13 @@ class BertClassifier:
                 f[q + "f1_w"], f[q + "f1_c"], f[q + "f1_b"] = ops.fold_ln_into_linear(
                     p[q + "f1_w"], p[q + "f1_b"], p[q + "ln1_g"], p[q + "ln1_b"])
                 f[q + "f2_b"] = (p[q + "f2_b"] + p[q + "ln1_b"]).contiguous()
+                # head-ordered copies for the fused QKV + attention kernel ([h][Q|K|V] rows)
+                perm = ops.qkv_head_order(self.cfg.heads, self.device)
+                src = f if i > 0 else p
+                f[q + "qkv_wh"] = src[q + "qkv_w"][perm].contiguous()
+                f[q + "qkv_bh"] = src[q + "qkv_b"][perm].float().contiguous()
+                if i > 0:
+                    f[q + "qkv_ch"] = f[q + "qkv_c"][perm].contiguous()
             self._folded = f
         return self._folded
 
@@ -241,14 +251,20 @@ class BertClassifier:
         part = torch.empty((H // 256, M, 2), dtype=torch.float32, device=dev)  # raw rows' partials
         fin = torch.empty((M, 2), dtype=torch.float32, device=dev)             # (rstd, rstd*mu)
         last_full = cfg.layers - 1 if cls_only_last else cfg.layers
+        fused = self.fused_qkv_attention and ops.qkv_attention_ok(M, 3 * H, H, S) and cfg.head_dim == 64
         g = h0
         for i in range(last_full):
             q = f"l{i}."
-            if i == 0:
-                qkv = ops.linear(h0, p[q + "qkv_w"], p[q + "qkv_b"])
-            else:  # consumes LN2_{i-1}(g); fin = its statistics (also the out-proj residual's)
-                qkv = ops.linear_ln(g, f[q + "qkv_w"], f[q + "qkv_b"], in_fin=fin, colsum=f[q + "qkv_c"])
-            ctx = ops.attention_packed(qkv, lens, B, S, cfg.heads)
+            if fused:
+                # QKV projection + attention in one kernel: the [M, 3H] QKV tensor never exists
+                ctx = ops.qkv_attention(g, f[q + "qkv_wh"], f[q + "qkv_bh"], lens, cfg.heads,
+                                        in_fin=fin if i > 0 else None, colsum_h=f.get(q + "qkv_ch") if i > 0 else None)
+            else:
+                if i == 0:
+                    qkv = ops.linear(h0, p[q + "qkv_w"], p[q + "qkv_b"])
+                else:  # consumes LN2_{i-1}(g); fin = its statistics (also the out-proj residual's)
+                    qkv = ops.linear_ln(g, f[q + "qkv_w"], f[q + "qkv_b"], in_fin=fin, colsum=f[q + "qkv_c"])
+                ctx = ops.attention_packed(qkv, lens, B, S, cfg.heads)
             if i == 0:
                 a = ops.linear_ln(ctx, p[q + "o_w"], p[q + "o_b"], residual=h0, part_out=part)
             else:

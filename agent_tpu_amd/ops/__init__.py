@@ -10,6 +10,7 @@ from .linear import linear_ln, fold_ln_into_linear, fold_ok, ln_partials_ref, ln
 from .decode import decode_attention, kv_append, gather_rows, beam_topk_rows, beam_reorder_hist, MAX_BANS  # noqa: F401
 from .decode import beam_select, beam_select_ref, ngram_bans, lm_head_topk, lm_head, LmHead, LM_HEAD_MAX_K  # noqa: F401
 from .attention import attention_packed, attention  # noqa: F401
+from .qkv_attention import qkv_attention, qkv_attention_ok, qkv_head_order  # noqa: F401
 from .norm import layernorm, rmsnorm, embed_layernorm, embed_gather  # noqa: F401
 from .tokenize import tokenize  # noqa: F401
 from .head import classify_head_topk  # noqa: F401
