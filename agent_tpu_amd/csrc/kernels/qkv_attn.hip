@@ -25,6 +25,12 @@
 
 #include <algorithm>
 
+// timing-only ablations (A/B builds, results WRONG): 1 = no attention (images + barriers),
+// 2 = no softmax (P = raw scores)
+#ifndef ATPU_QA_ABL
+#define ATPU_QA_ABL 0
+#endif
+
 namespace atpu {
 namespace {
 
@@ -47,10 +53,23 @@ __device__ __forceinline__ int hq_row(int q, int ql) {
 constexpr int hq_rounds(int q) { return q == 2 ? 1 : 2; }
 
 // attention images (MODE 2): per sequence s of the tile, Q, K, V of the head as [128][128 B]
-// bf16 images, Q and K chunk-swizzled like the operand images (conflict-free fragment
-// reads), V with the swizzle of the transposed reads (attention.hip vswz)
+// bf16 images, 16-B chunk c of row r at slot c ^ (r & 7). One swizzle is bank-conflict-free
+// for all three access patterns (checked by simulation, tools/lds_banks_qkv_attn.py): the
+// 16-B image writes (8-lane groups = 8 consecutive rows of one chunk, mod 32 banks), the
+// ds_read_b128 fragment reads of Q and K, and the transposed ds_read_b64_tr_b16 reads of V
+// (32-lane groups = 8 rows x 2 chunks, mod 64 banks). The operand-image swizzle c ^ ((r>>1)&7)
+// was 2-way on the writes and, for V, 2-way on the transposed reads.
 constexpr int kAImg = 128 * 128;
-__device__ __forceinline__ int vsw(int r, int c) { return c ^ (((r >> 1) & 3) << 1); }
+__device__ __forceinline__ int asw(int r, int c) { return c ^ (r & 7); }
+
+// v_permlane16_swap: lane rows (16-lane groups) 1 and 3 of x trade places with rows 0 and 2
+// of y. On the two packed halves of MFMA fragments of row blocks i (x) and i+1 (y) it leaves
+// lane row G holding 8 consecutive columns (G >> 1: which 8 of the 16) of block i + (G & 1):
+// one 16-B LDS write per lane instead of two 8-B writes. The s_nop covers the VALU-write ->
+// permlane-read hazard.
+__device__ __forceinline__ void swap16(unsigned& x, unsigned& y) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
 
 typedef short hv4s __attribute__((vector_size(8)));
 // ds_read_b64_tr_b16 (per 16-lane group: lane 4q+p addresses row q, elements 4p..4p+3 of a
@@ -180,12 +199,14 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
   };
 
   // ---- MODE 2: attention of sequence wm of the tile, head h, query rows wn*32..+32 ----
-  // Two 16-query blocks share every K / V fragment read. Scores, softmax and P.V as the
-  // packed attention kernel (attention.hip): S = K.Q^T per 16 x 16 block (lane: query fr,
-  // keys 4fc..+4), row max / sum over the 4 lanes of a query in registers, exp2 with the
+  // Two 16-query blocks share every K / V fragment read. S = K.Q^T per 16 x 16 block (lane:
+  // query fr, keys 4fc..+4), row max over the 4 lanes of a query in registers, exp2 with the
   // scale folded, P as the A operand of P.V in the key order of its two score blocks, V
-  // through transposed reads. The context goes out through the wave's own Q rows (free
-  // once read) as whole 128-B rows: 4 stores per wave.
+  // through transposed reads (each key step's 8 reads issued one step ahead: the first
+  // step's under the softmax). The row sums come from the MFMA too: P times a ones tile
+  // (one extra 16-column output block), so every lane holds its query's sum of the same
+  // bf16-rounded P the context is made of, with no VALU adds or cross-lane reduction. The
+  // context goes out through the wave's own Q rows (free once read) as whole 128-B rows.
   auto attend = [&](int tm0, int h) {
     const char* qi = lds + kImgOff + wm * 3 * kAImg;
     const char* ki = qi + kAImg;
@@ -196,7 +217,7 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
 #pragma unroll
       for (int ds = 0; ds < 2; ++ds) {
         const int r = wn * 32 + qp * 16 + fr;
-        qf[qp][ds] = *reinterpret_cast<const bf16x8*>(qi + r * 128 + hsw(r, ds * 4 + fc) * 16);
+        qf[qp][ds] = *reinterpret_cast<const bf16x8*>(qi + r * 128 + asw(r, ds * 4 + fc) * 16);
       }
     f32x4 s[2][8];
 #pragma unroll
@@ -206,18 +227,37 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
 #pragma unroll
       for (int ds = 0; ds < 2; ++ds) {
         const int r = kt * 16 + fr;
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ki + r * 128 + hsw(r, ds * 4 + fc) * 16);
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ki + r * 128 + asw(r, ds * 4 + fc) * 16);
         s[0][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][ds], s[0][kt], 0, 0, 0);
         s[1][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][ds], s[1][kt], 0, 0, 0);
       }
     }
+    // V fragments of key step ks: lane (tq, tp) of each 16-lane row addresses key row
+    // ks*32 + fc*4 + tq (+16), columns 4tp.. of d-tile dt
+    // (addresses from an opaque lane id per step: hoisted, the 32 per-step addresses spilled)
+    bf16x4 vlo[2][4], vhi[2][4];
+    auto read_v = [&](int ks, bf16x4 (&lo)[4], bf16x4 (&hi)[4]) {
+      const int l = opaque_lane();
+      const int tq = (l >> 2) & 3, tp = l & 3;
+      const int klo = ks * 32 + (l >> 4) * 4 + tq;  // khi = klo + 16: same (row & 7), +2 KiB
+      const char* row = vi + klo * 128 + (tp & 1) * 8;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int c = asw(klo, dt * 2 + (tp >> 1));
+        lo[dt] = tr16(row + c * 16);
+        hi[dt] = tr16(row + 16 * 128 + c * 16);
+      }
+    };
+    __builtin_amdgcn_sched_barrier(0);
+    read_v(0, vlo[0], vhi[0]);
+    __builtin_amdgcn_sched_barrier(0);
     const int len = min(lens[(tm0 >> 7) + wm], 128);  // wave-uniform (scalar load)
     const float cl = scale * 1.4426950408889634f;
-    float inv[2];
 #pragma unroll
     for (int qp = 0; qp < 2; ++qp) {
-      float mx = -1e30f, psum = 0.f;
-      if (len >= 128) {
+      float mx = -1e30f;
+      if (ATPU_QA_ABL == 2) {
+      } else if (len >= 128) {
 #pragma unroll
         for (int kt = 0; kt < 8; ++kt)
           mx = fmaxf(mx, fmaxf(fmaxf(s[qp][kt][0], s[qp][kt][1]), fmaxf(s[qp][kt][2], s[qp][kt][3])));
@@ -225,17 +265,14 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
 #pragma unroll
         for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float p = __builtin_amdgcn_exp2f(fmaf(s[qp][kt][e], cl, -moff));
-            s[qp][kt][e] = p;
-            psum += p;
-          }
+          for (int e = 0; e < 4; ++e) s[qp][kt][e] = __builtin_amdgcn_exp2f(fmaf(s[qp][kt][e], cl, -moff));
       } else {
 #pragma unroll
         for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const float x = kt * 16 + fc * 4 + e < len ? s[qp][kt][e] : -1e30f;
+            // key index from an opaque lane id: computed here, not hoisted above the branch
+            const float x = kt * 16 + (opaque_lane() >> 4) * 4 + e < len ? s[qp][kt][e] : -1e30f;
             s[qp][kt][e] = x;
             mx = fmaxf(mx, x);
           }
@@ -245,22 +282,21 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const float x = s[qp][kt][e];
-            const float p = x <= -1e29f ? 0.f : __builtin_amdgcn_exp2f(fmaf(x, cl, -moff));
-            s[qp][kt][e] = p;
-            psum += p;
+            s[qp][kt][e] = x <= -1e29f ? 0.f : __builtin_amdgcn_exp2f(fmaf(x, cl, -moff));
           }
       }
-      psum = lane_rows_sum(psum);
-      inv[qp] = psum > 0.f ? 1.f / psum : 0.f;
     }
-    f32x4 o[2][4];
+    f32x4 o[2][5];  // [4] = row sums (P times ones)
 #pragma unroll
     for (int qp = 0; qp < 2; ++qp)
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[qp][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int tq = fr >> 2, tp = fr & 3;
+      for (int dt = 0; dt < 5; ++dt) o[qp][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 ones;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.0f;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
+      const int cur = ks & 1;
       bf16x8 pf[2];
 #pragma unroll
       for (int qp = 0; qp < 2; ++qp)
@@ -269,50 +305,47 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
           pf[qp][e] = f2bf(s[qp][2 * ks][e]);
           pf[qp][4 + e] = f2bf(s[qp][2 * ks + 1][e]);
         }
-      const int klo = ks * 32 + fc * 4 + tq, khi = klo + 16;
-#pragma unroll
-      for (int dh = 0; dh < 4; dh += 2) {
-        bf16x4 lo[2], hi[2];
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          const int c = (dh + d) * 2 + (tp >> 1);
-          lo[d] = tr16(vi + klo * 128 + vsw(klo, c) * 16 + (tp & 1) * 8);
-          hi[d] = tr16(vi + khi * 128 + vsw(khi, c) * 16 + (tp & 1) * 8);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          bf16x8 vf;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            vf[e] = lo[d][e];
-            vf[4 + e] = hi[d][e];
-          }
-          o[0][dh + d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[0], o[0][dh + d], 0, 0, 0);
-          o[1][dh + d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[1], o[1][dh + d], 0, 0, 0);
-        }
-      }
-    }
-    // context rows -> this wave's 32 Q rows (row-chunk swizzle ch ^ (row & 7)), then whole lines out
-    char* ost = const_cast<char*>(qi) + wn * 32 * 128;
-#pragma unroll
-    for (int qp = 0; qp < 2; ++qp)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this step's V fragments
+      __builtin_amdgcn_sched_barrier(0);
+      if (ks + 1 < 4) read_v(ks + 1, vlo[cur ^ 1], vhi[cur ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        bf16x4 w;
+        bf16x8 vf;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) w[e] = f2bf(o[qp][dt][e] * inv[qp]);
-        const int ro = qp * 16 + fr, ch = dt * 2 + (fc >> 1);
-        *reinterpret_cast<bf16x4*>(ost + ro * 128 + ((ch ^ (ro & 7)) << 4) + (fc & 1) * 8) = w;
+        for (int e = 0; e < 4; ++e) {
+          vf[e] = vlo[cur][dt][e];
+          vf[4 + e] = vhi[cur][dt][e];
+        }
+        o[0][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[0], o[0][dt], 0, 0, 0);
+        o[1][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[1], o[1][dt], 0, 0, 0);
       }
+      o[0][4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[0], o[0][4], 0, 0, 0);
+      o[1][4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[1], o[1][4], 0, 0, 0);
+    }
+    // context -> this wave's 32 Q rows (asw image layout), one 16-B write per lane per d-tile
+    // (qp 0 / 1 fragments paired by swap16), then whole 128-B lines out
+    char* ost = const_cast<char*>(qi) + wn * 32 * 128;
+    const float inv0 = o[0][4][0] > 0.f ? 1.f / o[0][4][0] : 0.f;
+    const float inv1 = o[1][4][0] > 0.f ? 1.f / o[1][4][0] : 0.f;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      unsigned x0 = pack_bf16x2(o[0][dt][0] * inv0, o[0][dt][1] * inv0);
+      unsigned x1 = pack_bf16x2(o[0][dt][2] * inv0, o[0][dt][3] * inv0);
+      unsigned y0 = pack_bf16x2(o[1][dt][0] * inv1, o[1][dt][1] * inv1);
+      unsigned y1 = pack_bf16x2(o[1][dt][2] * inv1, o[1][dt][3] * inv1);
+      swap16(x0, y0);
+      swap16(x1, y1);
+      const int ro = (fc & 1) * 16 + fr, ch = dt * 2 + (fc >> 1);
+      *reinterpret_cast<u32x4*>(ost + ro * 128 + asw(ro, ch) * 16) = u32x4{x0, x1, y0, y1};
+    }
     const int l2 = opaque_lane();
     const int lr = l2 >> 3, lc8 = l2 & 7;
     bf16* obase = C + (size_t)(tm0 + wm * 128 + wn * 32) * ldc + h * 64 + lc8 * 8;
 #pragma unroll
     for (int hh = 0; hh < 4; ++hh) {
       const int ro = hh * 8 + lr;
-      const u32x4 val = *reinterpret_cast<const u32x4*>(ost + ro * 128 + ((lc8 ^ (ro & 7)) << 4));
+      const u32x4 val = *reinterpret_cast<const u32x4*>(ost + ro * 128 + asw(ro, lc8) * 16);
       *reinterpret_cast<u32x4*>(obase + (size_t)ro * ldc) = val;
     }
   };
@@ -429,33 +462,63 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
       const int ofr = ol & 15, ofc = ol >> 4;
       const float* lb = reinterpret_cast<const float*>(lds + kBiasOff + tile_par * 1024 + wn * 256);
       const float* lc = reinterpret_cast<const float*>(lds + kColOff + wn * 256);
+      auto row_fin = [&](int i) {
+        return kIn ? *reinterpret_cast<const f32x2*>(lds + kFinOff + (wm * 128 + i * 16 + ofr) * 8) : f32x2{1.f, 0.f};
+      };
+      // value pairs of fragment (i, j) as packed bf16: (acc*rstd - rstd*mu*colsum + bias), the LN
+      // math on pairs (v_pk_fma_f32, row scalars broadcast)
+      auto frag = [&](int i, int j, f32x2 rsm, unsigned& p0, unsigned& p1) {
+        const int c = j * 16 + ofc * 4;
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(lb + c);
+        f32x4 t;
+        if constexpr (kIn) {
+          const f32x4 c4 = *reinterpret_cast<const f32x4*>(lc + c);
+          const f32x2 rs2 = f32x2{rsm[0], rsm[0]}, nrm2 = f32x2{-rsm[1], -rsm[1]};
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int lrow = wm * 128 + i * 16 + ofr;
-        f32x2 rsm = f32x2{1.f, 0.f};
-        if constexpr (kIn) rsm = *reinterpret_cast<const f32x2*>(lds + kFinOff + lrow * 8);
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const int c = j * 16 + ofc * 4;
-          const f32x4 b4 = *reinterpret_cast<const f32x4*>(lb + c);
-          f32x4 t;
-          if constexpr (kIn) {
-            const f32x4 c4 = *reinterpret_cast<const f32x4*>(lc + c);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) t[e] = fmaf(acc[i][j][e], rsm[0], fmaf(-rsm[1], c4[e], b4[e]));
-          } else {
-            t = acc[i][j] + b4;
+          for (int hh = 0; hh < 2; ++hh) {
+            const f32x2 c2 = __builtin_elementwise_fma(nrm2, f32x2{c4[2 * hh], c4[2 * hh + 1]},
+                                                       f32x2{b4[2 * hh], b4[2 * hh + 1]});
+            const f32x2 o = __builtin_elementwise_fma(f32x2{acc[i][j][2 * hh], acc[i][j][2 * hh + 1]}, rs2, c2);
+            t[2 * hh] = o[0];
+            t[2 * hh + 1] = o[1];
           }
-          typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-          const u32x2 o = u32x2{pack_bf16x2(t[0], t[1]), pack_bf16x2(t[2], t[3])};
-          if constexpr (MODE == 0) {
-            *reinterpret_cast<u32x2*>(C + (size_t)(cm0 + lrow) * ldc + cn0 + wn * 48 + c) = o;
-          } else {
-            // 16-column fragments never straddle Q | K | V (48 = 3 x 16): the image is wave-uniform
+        } else {
+          t = acc[i][j] + b4;
+        }
+        p0 = pack_bf16x2(t[0], t[1]);
+        p1 = pack_bf16x2(t[2], t[3]);
+      };
+      if constexpr (MODE == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const f32x2 rsm = row_fin(i);
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            unsigned p0, p1;
+            frag(i, j, rsm, p0, p1);
+            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+            *reinterpret_cast<u32x2*>(C + (size_t)(cm0 + wm * 128 + i * 16 + ofr) * ldc + cn0 + wn * 48 + j * 16 +
+                                      ofc * 4) = u32x2{p0, p1};
+          }
+        }
+      } else {
+        // Q / K / V images of sequence wm: fragments of row blocks i, i+1 paired by swap16, one
+        // 16-B write per lane (lane row G: block i + (G & 1), 8 columns (G >> 1)). 16-column
+        // fragments never straddle Q | K | V (48 = 3 x 16): the image is wave-uniform.
+#pragma unroll
+        for (int i = 0; i < 8; i += 2) {
+          const f32x2 rs0 = row_fin(i), rs1 = row_fin(i + 1);
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            unsigned x0, x1, y0, y1;
+            frag(i, j, rs0, x0, x1);
+            frag(i + 1, j, rs1, y0, y1);
+            swap16(x0, y0);
+            swap16(x1, y1);
             const int cb = wn * 48 + j * 16, typ = cb >> 6;
-            const int d0 = (cb & 63) + ofc * 4, r = i * 16 + ofr, ch = d0 >> 3;
-            const int sc = typ == 2 ? vsw(r, ch) : hsw(r, ch);
-            *reinterpret_cast<u32x2*>(lds + kImgOff + (wm * 3 + typ) * kAImg + r * 128 + sc * 16 + ((d0 >> 2) & 1) * 8) = o;
+            const int r = (i + (ofc & 1)) * 16 + ofr, ch = ((cb & 63) >> 3) + (ofc >> 1);
+            *reinterpret_cast<u32x4*>(lds + kImgOff + (wm * 3 + typ) * kAImg + r * 128 + asw(r, ch) * 16) =
+                u32x4{x0, x1, y0, y1};
           }
         }
       }
@@ -463,7 +526,9 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // the images of both sequences are complete
         __builtin_amdgcn_sched_barrier(0);
+#if ATPU_QA_ABL != 1
         attend(cm0, cn0 / 192);
+#endif
         // every wave's image reads are done before group 0 runs ahead into the next tile,
         // whose K-tile 1 is staged into operand buffer 1 (= part of the images)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

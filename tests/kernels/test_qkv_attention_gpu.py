@@ -77,9 +77,11 @@ def test_fused_matches_unfused_kernels(innorm):
                             in_fin=fin.to(dev) if innorm else None,
                             colsum_h=col.to(dev)[p].contiguous() if innorm else None)
     torch.cuda.synchronize()
-    # same bf16 QKV rounding on both sides up to accumulation order: near-identical contexts
+    # same bf16 QKV rounding on both sides up to accumulation order; the fused kernel normalises
+    # by the sum of the bf16-rounded P (an MFMA row sum), the unfused one by the fp32 sum: the
+    # contexts differ by at most ~2 bf16 ulps of the largest magnitude
     err = (got.float() - ref.float()).abs().max().item()
-    assert err < 1.5e-2, err
+    assert err <= 2.0 ** -7 * ref.float().abs().max().item(), err
     assert (got.float() - ref.float()).abs().mean().item() < 1e-3
 
 
