@@ -26,9 +26,14 @@
 #include <algorithm>
 
 // timing-only ablations (A/B builds, results WRONG): 1 = no attention (images + barriers),
-// 2 = no softmax (P = raw scores)
+// 2 = no softmax (P = raw scores), 4 = no context stores, 5 = no P.V (no V reads), 6 = no QK^T
+// (no K reads)
 #ifndef ATPU_QA_ABL
 #define ATPU_QA_ABL 0
+#endif
+// context stores non-temporal (A/B)
+#ifndef ATPU_QA_NT
+#define ATPU_QA_NT 0
 #endif
 
 namespace atpu {
@@ -69,6 +74,22 @@ __device__ __forceinline__ int asw(int r, int c) { return c ^ (r & 7); }
 // permlane-read hazard.
 __device__ __forceinline__ void swap16(unsigned& x, unsigned& y) {
   asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+
+// ds_read_b128 by inline asm, waited for by lgkm_wait below: for the compiler-visible form the
+// waitcnt pass put one lgkmcnt(0) after all 20 Q/K reads of the attention instead of counted
+// waits, so the first QK^T MFMA waited for the last K fragment
+__device__ __forceinline__ bf16x8 ds_read128(const char* p) {
+  bf16x8 r;
+  const unsigned a = (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+// s_waitcnt lgkmcnt(N) that the two registers it retires pass through (so their consumers
+// cannot be scheduled above it)
+template <int N>
+__device__ __forceinline__ void lgkm_wait(bf16x8& a, bf16x8& b) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
 }
 
 typedef short hv4s __attribute__((vector_size(8)));
@@ -202,62 +223,78 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
   // Two 16-query blocks share every K / V fragment read. S = K.Q^T per 16 x 16 block (lane:
   // query fr, keys 4fc..+4), row max over the 4 lanes of a query in registers, exp2 with the
   // scale folded, P as the A operand of P.V in the key order of its two score blocks, V
-  // through transposed reads (each key step's 8 reads issued one step ahead: the first
-  // step's under the softmax). The row sums come from the MFMA too: P times a ones tile
-  // (one extra 16-column output block), so every lane holds its query's sum of the same
-  // bf16-rounded P the context is made of, with no VALU adds or cross-lane reduction. The
-  // context goes out through the wave's own Q rows (free once read) as whole 128-B rows.
-  auto attend = [&](int tm0, int h) {
+  // through transposed reads. Loads are issued in batches far ahead of their use (the
+  // accumulator registers are free by now): Q and all of K before the first QK^T MFMA
+  // (counted waits from the compiler), all of V right after QK^T so it lands under the
+  // softmax. The row sums come from the MFMA too: P times a ones tile (one extra 16-column
+  // output block), so every lane holds its query's sum of the same bf16-rounded P the context
+  // is made of, with no VALU adds or cross-lane reduction. The context goes out through the
+  // wave's own Q rows (free once read) as whole 128-B rows.
+  auto attend = [&](int tm0, int h, int len) {
     const char* qi = lds + kImgOff + wm * 3 * kAImg;
     const char* ki = qi + kAImg;
     const char* vi = qi + 2 * kAImg;
-    bf16x8 qf[2][2];
+    bf16x8 qf[2][2], kf[8][2];
 #pragma unroll
     for (int qp = 0; qp < 2; ++qp)
 #pragma unroll
       for (int ds = 0; ds < 2; ++ds) {
         const int r = wn * 32 + qp * 16 + fr;
-        qf[qp][ds] = *reinterpret_cast<const bf16x8*>(qi + r * 128 + asw(r, ds * 4 + fc) * 16);
+        qf[qp][ds] = ds_read128(qi + r * 128 + asw(r, ds * 4 + fc) * 16);
       }
-    f32x4 s[2][8];
 #pragma unroll
-    for (int kt = 0; kt < 8; ++kt) {
-      s[0][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      s[1][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
       for (int ds = 0; ds < 2; ++ds) {
         const int r = kt * 16 + fr;
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ki + r * 128 + asw(r, ds * 4 + fc) * 16);
-        s[0][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][ds], s[0][kt], 0, 0, 0);
-        s[1][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][ds], s[1][kt], 0, 0, 0);
+        if constexpr (ATPU_QA_ABL == 6) kf[kt][ds] = qf[ds][ds];
+        else kf[kt][ds] = ds_read128(ki + r * 128 + asw(r, ds * 4 + fc) * 16);
       }
-    }
-    // V fragments of key step ks: lane (tq, tp) of each 16-lane row addresses key row
-    // ks*32 + fc*4 + tq (+16), columns 4tp.. of d-tile dt
-    // (addresses from an opaque lane id per step: hoisted, the 32 per-step addresses spilled)
-    bf16x4 vlo[2][4], vhi[2][4];
-    auto read_v = [&](int ks, bf16x4 (&lo)[4], bf16x4 (&hi)[4]) {
-      const int l = opaque_lane();
-      const int tq = (l >> 2) & 3, tp = l & 3;
-      const int klo = ks * 32 + (l >> 4) * 4 + tq;  // khi = klo + 16: same (row & 7), +2 KiB
-      const char* row = vi + klo * 128 + (tp & 1) * 8;
+    // 20 reads in flight, retired in issue order: K-tile kt's MFMAs wait for lgkmcnt(14 - 2 kt).
+    // Phase A: S(qp 0) = K.Q0^T, counted waits.
+    f32x4 s[2][8];
+    auto qk0 = [&](auto kt_c) {
+      constexpr int kt = decltype(kt_c)::value;
+      if constexpr (kt == 0) {
+        lgkm_wait<14>(qf[0][0], qf[0][1]);
+        asm volatile("" : "+v"(qf[1][0]), "+v"(qf[1][1]), "+v"(kf[0][0]), "+v"(kf[0][1]));
+      } else {
+        lgkm_wait<14 - 2 * kt>(kf[kt][0], kf[kt][1]);
+      }
+      if constexpr (ATPU_QA_ABL == 6) {
+        s[0][kt] = f32x4{(float)kf[kt][0][kt], (float)kf[kt][1][kt], 0.f, 1.f};
+      } else {
+        s[0][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][0], qf[0][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        s[0][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][1], qf[0][1], s[0][kt], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // K-tile kt's MFMAs before the next wait
+    };
+    qk0(std::integral_constant<int, 0>{});
+    qk0(std::integral_constant<int, 1>{});
+    qk0(std::integral_constant<int, 2>{});
+    qk0(std::integral_constant<int, 3>{});
+    qk0(std::integral_constant<int, 4>{});
+    qk0(std::integral_constant<int, 5>{});
+    qk0(std::integral_constant<int, 6>{});
+    qk0(std::integral_constant<int, 7>{});
+    const float cl = scale * 1.4426950408889634f;
+    bf16x8 pf[2][4];  // P in bf16, A operand of key step ks
+    // softmax of query block qp -> pf[qp] (VALU; interleaved below with the other block's MFMAs)
+    // Keys >= len: scores set to -1e30 by a small separate block (mask(qp)), so the softmax
+    // itself is branch-free, one basic block the scheduler can interleave with MFMAs (exp2 of
+    // the masked scores underflows to 0; len == 0 is caught at the normalisation).
+    auto mask = [&](int qp) {
+      if (len < 128) {
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int c = asw(klo, dt * 2 + (tp >> 1));
-        lo[dt] = tr16(row + c * 16);
-        hi[dt] = tr16(row + 16 * 128 + c * 16);
+        for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (kt * 16 + (opaque_lane() >> 4) * 4 + e >= len) s[qp][kt][e] = -1e30f;
       }
     };
-    __builtin_amdgcn_sched_barrier(0);
-    read_v(0, vlo[0], vhi[0]);
-    __builtin_amdgcn_sched_barrier(0);
-    const int len = min(lens[(tm0 >> 7) + wm], 128);  // wave-uniform (scalar load)
-    const float cl = scale * 1.4426950408889634f;
-#pragma unroll
-    for (int qp = 0; qp < 2; ++qp) {
-      float mx = -1e30f;
-      if (ATPU_QA_ABL == 2) {
-      } else if (len >= 128) {
+    auto softmax = [&](int qp) {
+      if constexpr (ATPU_QA_ABL != 2) {
+        float mx = -1e30f;
 #pragma unroll
         for (int kt = 0; kt < 8; ++kt)
           mx = fmaxf(mx, fmaxf(fmaxf(s[qp][kt][0], s[qp][kt][1]), fmaxf(s[qp][kt][2], s[qp][kt][3])));
@@ -266,72 +303,128 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
         for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
           for (int e = 0; e < 4; ++e) s[qp][kt][e] = __builtin_amdgcn_exp2f(fmaf(s[qp][kt][e], cl, -moff));
+      }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          pf[qp][ks][e] = f2bf(s[qp][2 * ks][e]);
+          pf[qp][ks][4 + e] = f2bf(s[qp][2 * ks + 1][e]);
+        }
+    };
+    f32x4 o[2][5];  // [4] = row sums (P times ones)
+    unsigned xw[4][2];
+    bf16x4 vlo[4][4], vhi[4][4];
+    mask(0);
+    // Phase B: S(qp 1) MFMAs beside softmax(qp 0) VALU (one wave's MFMA leaves the SIMD's
+    // vector issue free for half its cycles)
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      if constexpr (ATPU_QA_ABL == 6) {
+        s[1][kt] = f32x4{(float)qf[1][0][kt], (float)qf[1][1][kt], 0.f, 1.f};
       } else {
-#pragma unroll
-        for (int kt = 0; kt < 8; ++kt)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            // key index from an opaque lane id: computed here, not hoisted above the branch
-            const float x = kt * 16 + (opaque_lane() >> 4) * 4 + e < len ? s[qp][kt][e] : -1e30f;
-            s[qp][kt][e] = x;
-            mx = fmaxf(mx, x);
-          }
-        const float moff = lane_rows_max(mx) * cl;
-#pragma unroll
-        for (int kt = 0; kt < 8; ++kt)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float x = s[qp][kt][e];
-            s[qp][kt][e] = x <= -1e29f ? 0.f : __builtin_amdgcn_exp2f(fmaf(x, cl, -moff));
-          }
+        s[1][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][0], qf[1][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        s[1][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][1], qf[1][1], s[1][kt], 0, 0, 0);
       }
     }
-    f32x4 o[2][5];  // [4] = row sums (P times ones)
+    softmax(0);
 #pragma unroll
-    for (int qp = 0; qp < 2; ++qp)
+    for (int g = 0; g < 16; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // V fragments of key step ks (lane (tq, tp) of each 16-lane row addresses key row
+    // ks*32 + fc*4 + tq (+16), columns 4tp.. of d-tile dt), all 32 reads issued now (K is
+    // dead); addresses from an opaque lane id (hoisted, the per-step addresses spilled)
+    {
+      const int l = opaque_lane();
+      const int tq = (l >> 2) & 3, tp = l & 3;
+      const int k0 = (l >> 4) * 4 + tq;  // (k0 + ks*32 (+16)) & 7 == k0 & 7
+      const char* row = vi + k0 * 128 + (tp & 1) * 8;
 #pragma unroll
-      for (int dt = 0; dt < 5; ++dt) o[qp][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const int c = asw(k0, dt * 2 + (tp >> 1)) * 16;
+          if constexpr (ATPU_QA_ABL == 5) {
+            vlo[ks][dt] = bf16x4{(bf16)(float)c, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+            vhi[ks][dt] = vlo[ks][dt];
+          } else {
+            vlo[ks][dt] = tr16(row + ks * 32 * 128 + c);
+            vhi[ks][dt] = tr16(row + (ks * 32 + 16) * 128 + c);
+          }
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
     bf16x8 ones;
 #pragma unroll
     for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.0f;
+    auto vfrag = [&](int ks, int dt) {
+      bf16x8 vf;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        vf[e] = vlo[ks][dt][e];
+        vf[4 + e] = vhi[ks][dt][e];
+      }
+      return vf;
+    };
+    mask(1);
+    __builtin_amdgcn_sched_barrier(0);
+    // Phase C: P0.V MFMAs beside softmax(qp 1); key step ks waits for its 8 V reads (the
+    // lgkmcnt field holds at most 15: steps 0-1 wait for 17 of the 32 reads)
+    softmax(1);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      const int cur = ks & 1;
-      bf16x8 pf[2];
+      if (ks == 0) asm volatile("s_waitcnt lgkmcnt(15)" : "+v"(vlo[0][0]), "+v"(vlo[0][1]), "+v"(vlo[0][2]), "+v"(vlo[0][3]),
+                                "+v"(vhi[0][0]), "+v"(vhi[0][1]), "+v"(vhi[0][2]), "+v"(vhi[0][3])::"memory");
+      if (ks == 1) asm volatile("s_waitcnt lgkmcnt(15)" : "+v"(vlo[1][0]), "+v"(vlo[1][1]), "+v"(vlo[1][2]), "+v"(vlo[1][3]),
+                                "+v"(vhi[1][0]), "+v"(vhi[1][1]), "+v"(vhi[1][2]), "+v"(vhi[1][3])::"memory");
+      if (ks == 2) asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(vlo[2][0]), "+v"(vlo[2][1]), "+v"(vlo[2][2]), "+v"(vlo[2][3]),
+                                "+v"(vhi[2][0]), "+v"(vhi[2][1]), "+v"(vhi[2][2]), "+v"(vhi[2][3])::"memory");
+      if (ks == 3) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vlo[3][0]), "+v"(vlo[3][1]), "+v"(vlo[3][2]), "+v"(vlo[3][3]),
+                                "+v"(vhi[3][0]), "+v"(vhi[3][1]), "+v"(vhi[3][2]), "+v"(vhi[3][3])::"memory");
 #pragma unroll
-      for (int qp = 0; qp < 2; ++qp)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          pf[qp][e] = f2bf(s[qp][2 * ks][e]);
-          pf[qp][4 + e] = f2bf(s[qp][2 * ks + 1][e]);
-        }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this step's V fragments
-      __builtin_amdgcn_sched_barrier(0);
-      if (ks + 1 < 4) read_v(ks + 1, vlo[cur ^ 1], vhi[cur ^ 1]);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        bf16x8 vf;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          vf[e] = vlo[cur][dt][e];
-          vf[4 + e] = vhi[cur][dt][e];
-        }
-        o[0][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[0], o[0][dt], 0, 0, 0);
-        o[1][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[1], o[1][dt], 0, 0, 0);
-      }
-      o[0][4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[0], o[0][4], 0, 0, 0);
-      o[1][4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[1], o[1][4], 0, 0, 0);
+      for (int dt = 0; dt < 4; ++dt)
+        if constexpr (ATPU_QA_ABL == 5)
+          o[0][dt] = f32x4{(float)pf[0][ks][dt], (float)vfrag(ks, dt)[0], 0.f, ks ? o[0][dt][3] : 1.f};
+        else
+          o[0][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vfrag(ks, dt), pf[0][ks],
+                                                             ks ? o[0][dt] : f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      o[0][4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[0][ks], ks ? o[0][4] : f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     }
+#pragma unroll
+    for (int g = 0; g < 20; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+      __builtin_amdgcn_sched_group_barrier(0x002, 5, 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // Phase D: P1.V MFMAs beside the scaling / packing of the qp 0 context
+    const float inv0 = len > 0 && o[0][4][0] > 0.f ? 1.f / o[0][4][0] : 0.f;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      xw[dt][0] = pack_bf16x2(o[0][dt][0] * inv0, o[0][dt][1] * inv0);
+      xw[dt][1] = pack_bf16x2(o[0][dt][2] * inv0, o[0][dt][3] * inv0);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        if constexpr (ATPU_QA_ABL == 5)
+          o[1][dt] = f32x4{(float)pf[1][ks][dt], (float)vfrag(ks, dt)[0], 0.f, ks ? o[1][dt][3] : 1.f};
+        else
+          o[1][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vfrag(ks, dt), pf[1][ks],
+                                                             ks ? o[1][dt] : f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      o[1][4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[1][ks], ks ? o[1][4] : f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
     // context -> this wave's 32 Q rows (asw image layout), one 16-B write per lane per d-tile
     // (qp 0 / 1 fragments paired by swap16), then whole 128-B lines out
     char* ost = const_cast<char*>(qi) + wn * 32 * 128;
-    const float inv0 = o[0][4][0] > 0.f ? 1.f / o[0][4][0] : 0.f;
-    const float inv1 = o[1][4][0] > 0.f ? 1.f / o[1][4][0] : 0.f;
+    const float inv1 = len > 0 && o[1][4][0] > 0.f ? 1.f / o[1][4][0] : 0.f;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-      unsigned x0 = pack_bf16x2(o[0][dt][0] * inv0, o[0][dt][1] * inv0);
-      unsigned x1 = pack_bf16x2(o[0][dt][2] * inv0, o[0][dt][3] * inv0);
+      unsigned x0 = xw[dt][0], x1 = xw[dt][1];
       unsigned y0 = pack_bf16x2(o[1][dt][0] * inv1, o[1][dt][1] * inv1);
       unsigned y1 = pack_bf16x2(o[1][dt][2] * inv1, o[1][dt][3] * inv1);
       swap16(x0, y0);
@@ -341,12 +434,15 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
     }
     const int l2 = opaque_lane();
     const int lr = l2 >> 3, lc8 = l2 & 7;
-    bf16* obase = C + (size_t)(tm0 + wm * 128 + wn * 32) * ldc + h * 64 + lc8 * 8;
+    bf16* obase = C + (size_t)(tm0 + wm * 128 + wn * 32 + lr) * ldc + h * 64 + lc8 * 8;
 #pragma unroll
     for (int hh = 0; hh < 4; ++hh) {
       const int ro = hh * 8 + lr;
       const u32x4 val = *reinterpret_cast<const u32x4*>(ost + ro * 128 + asw(ro, lc8) * 16);
-      *reinterpret_cast<u32x4*>(obase + (size_t)ro * ldc) = val;
+      u32x4* dst = reinterpret_cast<u32x4*>(obase + (size_t)(hh * 8) * ldc);
+      if constexpr (ATPU_QA_ABL == 4) asm volatile("" ::"v"(val), "v"(dst));
+      else if constexpr (ATPU_QA_NT) __builtin_nontemporal_store(val, dst);
+      else *dst = val;
     }
   };
 
@@ -462,18 +558,33 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
       const int ofr = ol & 15, ofc = ol >> 4;
       const float* lb = reinterpret_cast<const float*>(lds + kBiasOff + tile_par * 1024 + wn * 256);
       const float* lc = reinterpret_cast<const float*>(lds + kColOff + wn * 256);
-      auto row_fin = [&](int i) {
-        return kIn ? *reinterpret_cast<const f32x2*>(lds + kFinOff + (wm * 128 + i * 16 + ofr) * 8) : f32x2{1.f, 0.f};
-      };
+      // MODE 2: the sequence length (scalar load), consumed here: an SMEM load still in flight
+      // at the attention would turn every counted LDS wait there into lgkmcnt(0)
+      int len = 0;
+      if constexpr (MODE == 2) {
+        len = min(lens[(cm0 >> 7) + wm], 128);
+        asm volatile("" : "+s"(len));
+      }
+      // the tile's per-column (bias, colsum) and per-row (rstd, rstd*mu) vectors, read from LDS
+      // in one batch (read per fragment, each read's latency was exposed on its own)
+      f32x4 bv[3], cv[3];
+      f32x2 rf[8];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        bv[j] = *reinterpret_cast<const f32x4*>(lb + j * 16 + ofc * 4);
+        if constexpr (kIn) cv[j] = *reinterpret_cast<const f32x4*>(lc + j * 16 + ofc * 4);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        rf[i] = kIn ? *reinterpret_cast<const f32x2*>(lds + kFinOff + (wm * 128 + i * 16 + ofr) * 8) : f32x2{1.f, 0.f};
       // value pairs of fragment (i, j) as packed bf16: (acc*rstd - rstd*mu*colsum + bias), the LN
       // math on pairs (v_pk_fma_f32, row scalars broadcast)
-      auto frag = [&](int i, int j, f32x2 rsm, unsigned& p0, unsigned& p1) {
-        const int c = j * 16 + ofc * 4;
-        const f32x4 b4 = *reinterpret_cast<const f32x4*>(lb + c);
+      auto frag = [&](int i, int j, unsigned& p0, unsigned& p1) {
+        const f32x4 b4 = bv[j];
         f32x4 t;
         if constexpr (kIn) {
-          const f32x4 c4 = *reinterpret_cast<const f32x4*>(lc + c);
-          const f32x2 rs2 = f32x2{rsm[0], rsm[0]}, nrm2 = f32x2{-rsm[1], -rsm[1]};
+          const f32x4 c4 = cv[j];
+          const f32x2 rs2 = f32x2{rf[i][0], rf[i][0]}, nrm2 = f32x2{-rf[i][1], -rf[i][1]};
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) {
             const f32x2 c2 = __builtin_elementwise_fma(nrm2, f32x2{c4[2 * hh], c4[2 * hh + 1]},
@@ -491,11 +602,10 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
       if constexpr (MODE == 0) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const f32x2 rsm = row_fin(i);
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
             unsigned p0, p1;
-            frag(i, j, rsm, p0, p1);
+            frag(i, j, p0, p1);
             typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
             *reinterpret_cast<u32x2*>(C + (size_t)(cm0 + wm * 128 + i * 16 + ofr) * ldc + cn0 + wn * 48 + j * 16 +
                                       ofc * 4) = u32x2{p0, p1};
@@ -507,12 +617,11 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
         // fragments never straddle Q | K | V (48 = 3 x 16): the image is wave-uniform.
 #pragma unroll
         for (int i = 0; i < 8; i += 2) {
-          const f32x2 rs0 = row_fin(i), rs1 = row_fin(i + 1);
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
             unsigned x0, x1, y0, y1;
-            frag(i, j, rs0, x0, x1);
-            frag(i + 1, j, rs1, y0, y1);
+            frag(i, j, x0, x1);
+            frag(i + 1, j, y0, y1);
             swap16(x0, y0);
             swap16(x1, y1);
             const int cb = wn * 48 + j * 16, typ = cb >> 6;
@@ -527,7 +636,7 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
         __builtin_amdgcn_s_barrier();  // the images of both sequences are complete
         __builtin_amdgcn_sched_barrier(0);
 #if ATPU_QA_ABL != 1
-        attend(cm0, cn0 / 192);
+        attend(cm0, cn0 / 192, len);
 #endif
         // every wave's image reads are done before group 0 runs ahead into the next tile,
         // whose K-tile 1 is staged into operand buffer 1 (= part of the images)
