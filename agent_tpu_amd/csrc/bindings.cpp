@@ -67,7 +67,8 @@ PYBIND11_MODULE(_atpu, m) {
       [](uintptr_t A, int lda, uintptr_t Bt, int ldb, uintptr_t C, int ldc, uintptr_t bias, uintptr_t R, int ldr, int M,
          int N, int K, int epi, uintptr_t stream, int splits, uintptr_t ws, float rms_eps, uintptr_t kv_cache,
          int kv_ld, int kv_T, int kv_col0, uintptr_t kv_step, uintptr_t colsum, uintptr_t in_part,
-         uintptr_t res_part, uintptr_t gamma, uintptr_t part_out) {
+         uintptr_t res_part, uintptr_t gamma, uintptr_t part_out, uintptr_t pf_w, int pf_ld, int pf_k, int pf_n,
+         int pf_rpb) {
         GemmArgs g;
         g.A = P<const bf16>(A); g.lda = lda; g.Bt = P<const bf16>(Bt); g.ldb = ldb; g.C = P<bf16>(C); g.ldc = ldc;
         g.bias = P<const float>(bias); g.R = P<const bf16>(R); g.ldr = ldr; g.M = M; g.N = N; g.K = K; g.epi = epi;
@@ -76,6 +77,7 @@ PYBIND11_MODULE(_atpu, m) {
         g.kv_step = P<const int32_t>(kv_step);
         g.colsum = P<const float>(colsum); g.in_part = P<const float>(in_part);
         g.res_part = P<const float>(res_part); g.gamma = P<const float>(gamma); g.part_out = P<float>(part_out);
+        g.pf_w = P<const bf16>(pf_w); g.pf_ld = pf_ld; g.pf_k = pf_k; g.pf_n = pf_n; g.pf_rpb = pf_rpb;
         gemm_bf16(g, S(stream));
       },
       "bf16 MFMA GEMM C = epi(A @ Bt^T)", py::arg("A"), py::arg("lda"), py::arg("Bt"), py::arg("ldb"), py::arg("C"),
@@ -83,7 +85,8 @@ PYBIND11_MODULE(_atpu, m) {
       py::arg("epi"), py::arg("stream"), py::arg("splits") = 1, py::arg("ws") = 0, py::arg("rms_eps") = 0.f,
       py::arg("kv_cache") = 0, py::arg("kv_ld") = 0, py::arg("kv_T") = 0, py::arg("kv_col0") = 0,
       py::arg("kv_step") = 0, py::arg("colsum") = 0, py::arg("in_part") = 0, py::arg("res_part") = 0,
-      py::arg("gamma") = 0, py::arg("part_out") = 0);
+      py::arg("gamma") = 0, py::arg("part_out") = 0, py::arg("pf_w") = 0, py::arg("pf_ld") = 0, py::arg("pf_k") = 0,
+      py::arg("pf_n") = 0, py::arg("pf_rpb") = 16);
   m.def(
       "gemm_ln",
       [](uintptr_t A, int lda, uintptr_t Bt, int ldb, uintptr_t C, int ldc, uintptr_t bias, uintptr_t R, int ldr, int M,

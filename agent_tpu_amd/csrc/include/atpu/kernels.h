@@ -70,6 +70,11 @@ struct GemmArgs {
   bf16* kv_cache = nullptr;        // KvScatter: cache [rows * kv_T, kv_ld]
   int kv_ld = 0, kv_T = 0, kv_col0 = 0;
   const int32_t* kv_step = nullptr;  // device scalar: the position being written
+  // GEMV (<= 4 rows) only: the weight [pf_n, pf_k] (row stride pf_ld) of the NEXT GEMV of a
+  // decode chain, pulled into the L2 of the XCD that will read it (ATPU_GEMV_PREFETCH)
+  const bf16* pf_w = nullptr;
+  int pf_ld = 0, pf_k = 0, pf_n = 0;
+  int pf_rpb = 16;  // weight rows per workgroup of that next GEMV (32 when it writes RowStats)
 };
 void gemm_bf16(const GemmArgs& g, hipStream_t stream);
 // split count the library picks for an [M,N,K] problem (1 = no split-K)

@@ -2271,20 +2271,61 @@ namespace {
 // the cache row m*T + step). No split-K, no workspace.
 // ============================================================================
 constexpr int kGemvRows = 4;
-constexpr int kGemvU = 3;  // chunks per lane in flight per round
+// chunks per lane in flight per round (template U): 3 up to K = 1536, 6 up to K = 3072, so
+// every K of the T5 / BART decoders but BART's fc2 (4096: two rounds) issues all of its loads
+// in ONE round (two rounds serialised two memory latencies: 7.5 vs 4.5 us at K = 3072 cold,
+// tools/probe_gemv_l2.py)
+constexpr int gemv_u(int K) { return K <= 64 * 8 * 3 ? 3 : 6; }
+
+// Prefetch of the next GEMV's weight (PF): one extra wave per workgroup issues a dword load per
+// 128-B line of the rows the NEXT kernel's workgroups b' = blockIdx.x + k * gridDim.x will read
+// (16 rows each), waits for them and exits; the compute waves never wait for it. Workgroups are
+// dealt to the XCDs round robin, so with gridDim.x % 8 == 0 the lines land in the L2 of the XCD
+// whose workgroup reads them next (a speed-only assumption: a different placement only loses
+// the L2 hit). A 4-row GEMV on L2-resident weights ran 3.6-4.5 us against 4.9-7.5 us from HBM.
+struct GemvPf {
+  const bf16* w;
+  int ld, k, n, rpb;  // rpb: weight rows per workgroup of the next kernel (16, or 32 for RowStats)
+};
+// The loads are 4-byte LDS-DMAs into a 256-B scratch nobody reads: a VGPR-destination load
+// issued from inline asm would let the compiler reuse its register before the data returns.
+__device__ __forceinline__ void gemv_prefetch(const GemvPf& pf, int lane, char* scratch) {
+  const int lpr = (pf.k * 2 + 127) / 128;  // 128-B lines per row
+  const int blocks = (pf.n + pf.rpb - 1) / pf.rpb;
+  for (int bb = blockIdx.x; bb < blocks; bb += gridDim.x) {
+    const int r0 = bb * pf.rpb, nl = min(pf.rpb, pf.n - r0) * lpr;
+    for (int i0 = 0; i0 < nl; i0 += 64) {  // wave-uniform trip count: every lane issues the DMA
+      const int i = min(i0 + lane, nl - 1);
+      const int r = r0 + i / lpr, l = i - (i / lpr) * lpr;
+      const char* p = reinterpret_cast<const char*>(pf.w + (size_t)r * pf.ld) + l * 128;
+      __builtin_amdgcn_global_load_lds((const ATPU_GLOBAL_AS void*)p, (ATPU_LDS_AS void*)scratch, 4, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 
 // BART's LayerNorm folding (RowLn / ResLn / RowStats, see LnDec): the row statistics come
 // from the <= 32 slab partials (lane = slab, wave sums); RowStats workgroups are 8 waves =
 // one 32-column slab, summed across the waves through LDS.
-template <int EPI, int NWV>
-__global__ __launch_bounds__(NWV * 64) void gemv_kernel(const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bt,
-                                                   int ldb, bf16* __restrict__ C, int ldc, const float* __restrict__ bias,
-                                                   const bf16* __restrict__ R, int ldr, int M, int N, int K,
-                                                   float rms_eps, KvOut kvo, LnDec ln) {
+template <int EPI, int NWV, int U, bool PF>
+__global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __restrict__ A, int lda,
+                                                              const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C,
+                                                              int ldc, const float* __restrict__ bias,
+                                                              const bf16* __restrict__ R, int ldr, int M, int N, int K,
+                                                              float rms_eps, KvOut kvo, LnDec ln, GemvPf pf) {
   typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
   static_assert(!(EPI & kEpiRowStats) || NWV == 8, "RowStats: one 32-column slab per workgroup");
+  constexpr int kGemvU = U;
   __shared__ float2 st_red[NWV][kGemvRows];
+  __shared__ __attribute__((aligned(16))) char pf_scratch[PF ? 256 : 4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if constexpr (PF) {
+    if (w == NWV) {
+      gemv_prefetch(pf, lane, pf_scratch);
+      if constexpr (EPI & kEpiRowStats) __syncthreads();  // RowStats' one workgroup barrier (unused: host)
+      return;
+    }
+  }
   const int n0 = (blockIdx.x * NWV + w) * 4;  // this wave's 4 columns
   const int nch = K / 8;
   float acc[kGemvRows][4], ssq[kGemvRows];
@@ -2305,6 +2346,9 @@ __global__ __launch_bounds__(NWV * 64) void gemv_kernel(const bf16* __restrict__
       for (int m = 0; m < kGemvRows; ++m)
         av[u][m] = *reinterpret_cast<const bf16x8*>(A + (size_t)min(m, M - 1) * lda + c * 8);
     }
+    // every load of the round is issued before the first use: left alone, the scheduler issued
+    // them in groups of 8 with a full wait in between (U serialised memory latencies)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < kGemvU; ++u) {
       const bool ok = base + u * 64 + lane < nch;
@@ -2423,11 +2467,33 @@ void launch_gemv(const GemmArgs& g, hipStream_t s) {
   ATPU_CHECK(!(g.epi & kEpiRowStats) || (g.part_out && g.N % 32 == 0), "gemm: RowStats needs part_out and N % 32 == 0");
   const KvOut kvo{g.kv_cache, g.kv_ld, g.kv_T, g.kv_col0, g.kv_step};
   const LnDec ln{g.colsum, g.in_part, g.res_part, g.gamma, g.part_out};
+  static const bool pf_on = [] {
+    const char* f = std::getenv("ATPU_GEMV_PREFETCH");
+    return !(f && f[0] == '0');
+  }();
+  // not from RowStats GEMVs: their prefetch wave joins the slab barrier, which then waited for
+  // its loads (BART 1-doc A/B: 8.20 -> 7.98 docs/s with it)
+  const bool pf = pf_on && g.pf_w && g.pf_n > 0 && g.pf_k > 0 && !(g.epi & kEpiRowStats);
+  const GemvPf pfa{g.pf_w, g.pf_ld, g.pf_k, g.pf_n, g.pf_rpb > 0 ? g.pf_rpb : 16};
+  const bool u6 = gemv_u(g.K) == 6;
+#define ATPU_GEMV_GO(E, UU, P)                                                                                   \
+  hipLaunchKernelGGL((gemv_kernel<E, nwv, UU, P>), dim3(g.N / (4 * nwv)), dim3(64 * (nwv + P)), 0, s, g.A, g.lda, \
+                     g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, g.rms_eps, kvo, ln, pfa)
+// (E) parenthesised: for E = kEpiBias | kEpiResidual, `E & kEpiRowStats` parsed as
+// kEpiBias | (kEpiResidual & kEpiRowStats) and gave 8-wave workgroups to every multi-flag
+// epilogue (round 3). The 8-wave RowStats kernels keep 3 chunks per lane in flight: with the
+// prefetch wave (9 waves, <= 168 VGPRs) 6 spilled.
 #define ATPU_GEMV_CASE(E)                                                                                       \
   case E: {                                                                                                     \
-    constexpr int nwv = (E & kEpiRowStats) ? 8 : 4;                                                             \
-    hipLaunchKernelGGL((gemv_kernel<E, nwv>), dim3(g.N / (4 * nwv)), dim3(64 * nwv), 0, s, g.A, g.lda, g.Bt,    \
-                       g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, g.rms_eps, kvo, ln);                \
+    constexpr int nwv = ((E) & kEpiRowStats) ? 8 : 4;                                                           \
+    constexpr int kU6 = nwv == 4 ? 6 : 3;                                                                       \
+    if (pf) {                                                                                                   \
+      if (u6) ATPU_GEMV_GO(E, kU6, true);                                                                       \
+      else ATPU_GEMV_GO(E, 3, true);                                                                            \
+    } else {                                                                                                    \
+      if (u6) ATPU_GEMV_GO(E, kU6, false);                                                                      \
+      else ATPU_GEMV_GO(E, 3, false);                                                                           \
+    }                                                                                                           \
     break;                                                                                                      \
   }
   switch (g.epi) {
@@ -2452,6 +2518,7 @@ void launch_gemv(const GemmArgs& g, hipStream_t s) {
       throw std::invalid_argument("atpu: unsupported GEMV epilogue " + std::to_string(g.epi));
   }
 #undef ATPU_GEMV_CASE
+#undef ATPU_GEMV_GO
   ATPU_HIP_CHECK(hipGetLastError());
 }
 

@@ -305,25 +305,30 @@ class BartModel:
             # layer 0: x = the embedding LayerNorm's output; later: raw pre-LN rows of the last FFN
             w, b, rl = ((p[q + "qkv_w"], p[q + "qkv_b"], None) if i == 0 else
                         (f[q + "qkv_w"], f[q + "qkv_b"], (eps, f[q + "qkv_c"], px)))
+            # each <= 4-row GEMV pulls the next one's weight into L2 (ops.linear prefetch; the
+            # stats_out GEMVs have 32 weight rows per workgroup)
+            nxt = f[f"dec.l{i + 1}.qkv_w"] if i + 1 < L else None
             if self.kv_scatter:
-                qh = ops.linear(x, w, b, kv_cache=(c, T, step, d), row_ln=rl)
+                qh = ops.linear(x, w, b, kv_cache=(c, T, step, d), row_ln=rl, prefetch=(p[q + "o_w"], 32))
             else:
-                qkv = ops.linear(x, w, b, row_ln=rl)
+                qkv = ops.linear(x, w, b, row_ln=rl, prefetch=(p[q + "o_w"], 32))
                 ops.kv_append(qkv, d, 2 * d, c, T, step)
                 qh = qkv[:, :d]
             ctx = ops.decode_attention(qh, c[:, :d], c[:, d:], H, T, 1, step=step, scale=scale, hist=hist)
             if i == 0:
-                x1 = ops.linear(ctx, p[q + "o_w"], p[q + "o_b"], residual=x, stats_out=p1)
+                x1 = ops.linear(ctx, p[q + "o_w"], p[q + "o_b"], residual=x, stats_out=p1, prefetch=f[q + "cq_w"])
             else:
                 x1 = ops.linear(ctx, p[q + "o_w"], f[q + "o_b"], residual=x, res_ln=(eps, px, p[prev + "ln2_g"]),
-                                stats_out=p1)
-            cq = ops.linear(x1, f[q + "cq_w"], f[q + "cq_b"], row_ln=(eps, f[q + "cq_c"], p1))
+                                stats_out=p1, prefetch=f[q + "cq_w"])
+            cq = ops.linear(x1, f[q + "cq_w"], f[q + "cq_b"], row_ln=(eps, f[q + "cq_c"], p1),
+                            prefetch=(p[q + "co_w"], 32))
             kv = ckv[:, i * 2 * d:(i + 1) * 2 * d]
             ctx = ops.decode_attention(cq, kv[:, :d], kv[:, d:], H, S, group, lens=src_lens, scale=scale)
             x2 = ops.linear(ctx, p[q + "co_w"], f[q + "co_b"], residual=x1, res_ln=(eps, p1, p[q + "ln1_g"]),
-                            stats_out=p2)
-            h = ops.linear(x2, f[q + "f1_w"], f[q + "f1_b"], act="gelu", row_ln=(eps, f[q + "f1_c"], p2))
+                            stats_out=p2, prefetch=f[q + "f1_w"])
+            h = ops.linear(x2, f[q + "f1_w"], f[q + "f1_b"], act="gelu", row_ln=(eps, f[q + "f1_c"], p2),
+                           prefetch=(p[q + "f2_w"], 32))
             x = ops.linear(h, p[q + "f2_w"], f[q + "f2_b"], residual=x2, res_ln=(eps, p2, p[q + "lnc_g"]),
-                           stats_out=px)
+                           stats_out=px, prefetch=nxt)
         x = ops.layernorm(x, p[f"dec.l{L - 1}.ln2_g"], p[f"dec.l{L - 1}.ln2_b"], eps)
         return ops.lm_head(x, p["shared"], p["final_logits_bias"], 0.0, logits)

@@ -323,21 +323,24 @@ class T5Model:
         per step, no normalised copy of x); logits equal the unfolded step to bf16 rounding."""
         cfg, p, f = self.cfg, self.p, self.rms_folded()
         d, H, eps = cfg.d_model, cfg.heads, cfg.eps
-        for i in range(cfg.dec_layers):
+        # each <= 4-row GEMV pulls the next one's weight into L2 (ops.linear prefetch)
+        L = cfg.dec_layers
+        nxt_qkv = [f[f"dec.l{i + 1}.qkv"] if i + 1 < L else None for i in range(L)]
+        for i in range(L):
             q = f"dec.l{i}."
             c = cache[i]
             if self.kv_scatter:  # K|V written straight into the cache by the GEMM (no kv_append)
-                qh = ops.linear(x, f[q + "qkv"], rms_eps=eps, kv_cache=(c, T, step, d))
+                qh = ops.linear(x, f[q + "qkv"], rms_eps=eps, kv_cache=(c, T, step, d), prefetch=p[q + "o"])
             else:
-                qkv = ops.linear(x, f[q + "qkv"], rms_eps=eps)
+                qkv = ops.linear(x, f[q + "qkv"], rms_eps=eps, prefetch=p[q + "o"])
                 ops.kv_append(qkv, d, 2 * d, c, T, step)
                 qh = qkv[:, :d]
             ctx = ops.decode_attention(qh, c[:, :d], c[:, d:], H, T, 1, step=step, bias_dist=dbias, hist=hist)
-            x = ops.linear(ctx, p[q + "o"], residual=x)
-            cq = ops.linear(x, f[q + "cq"], rms_eps=eps)
+            x = ops.linear(ctx, p[q + "o"], residual=x, prefetch=f[q + "cq"])
+            cq = ops.linear(x, f[q + "cq"], rms_eps=eps, prefetch=p[q + "co"])
             kv = ckv[:, i * 2 * d:(i + 1) * 2 * d]
             ctx = ops.decode_attention(cq, kv[:, :d], kv[:, d:], H, S, group, lens=src_lens)
-            x = ops.linear(ctx, p[q + "co"], residual=x)
-            h = ops.linear(x, f[q + "wi"], act="relu", rms_eps=eps)
-            x = ops.linear(h, p[q + "wo"], residual=x)
+            x = ops.linear(ctx, p[q + "co"], residual=x, prefetch=f[q + "wi"])
+            h = ops.linear(x, f[q + "wi"], act="relu", rms_eps=eps, prefetch=p[q + "wo"])
+            x = ops.linear(h, p[q + "wo"], residual=x, prefetch=nxt_qkv[i])
         return ops.lm_head(x, f["lm"], None, eps, logits)

@@ -80,7 +80,8 @@ def _splits(M: int, N: int, K: int) -> int:
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: Optional[str] = None,
            residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
            out_f32: bool = False, rms_eps: Optional[float] = None, kv_cache=None, row_ln=None,
-           res_ln=None, stats_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+           res_ln=None, stats_out: Optional[torch.Tensor] = None,
+           prefetch: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``act(x @ w.T + bias) + residual``; ``out_f32`` returns fp32 (LM-head logits).
 
     ``rms_eps``: ``x`` rows are raw RMSNorm inputs and ``w`` carries the norm's gamma
@@ -97,7 +98,11 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     ``row_ln = (eps, colsum, in_part)``: ``x`` rows are raw LN inputs with partials ``in_part``,
     ``w``/``bias`` folded: ``y = rstd*(x @ w.T) - rstd*mu*colsum + bias``;
     ``res_ln = (eps, res_part, gamma)``: ``residual`` rows are raw LN inputs with partials
-    ``res_part``, added as ``(r - mu)*rstd*gamma`` (beta folded into ``bias``)."""
+    ``res_part``, added as ``(r - mu)*rstd*gamma`` (beta folded into ``bias``).
+
+    ``prefetch``: the weight of the NEXT linear of a decode chain (or ``(weight, 32)`` when that
+    linear writes ``stats_out``: 32 weight rows per workgroup). A <= 4-row GEMV pulls it into the
+    L2 of the XCDs that will read it while it runs (a hint; ignored elsewhere and on CPU)."""
     check(act in _ACTS, f"unknown activation {act!r}")
     M0, N0 = x.shape[0], w.shape[0]
 
@@ -209,8 +214,13 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     ws = torch.empty(splits * M * N, dtype=torch.float32, device=x.device) if splits > 1 else None
     if not kv_args:
         kv_args = (0, 0, 0, 0, 0)
+    pf_args = (0, 0, 0, 0, 16)
+    if prefetch is not None and M <= 4:
+        pw, rpb = prefetch if isinstance(prefetch, tuple) else (prefetch, 16)
+        if pw.is_cuda and pw.dim() == 2 and pw.stride(1) == 1:
+            pf_args = (ptr(pw), pw.stride(0), pw.shape[1], pw.shape[0], int(rpb))
     native().gemm(ptr(x), lda, ptr(w), ldb, ptr(out), ldc, ptr(bias), ptr(residual), ldr, M, N, K, epi,
-                  launch_stream(x), splits, ptr(ws), eps_arg, *kv_args, *ln_args)
+                  launch_stream(x), splits, ptr(ws), eps_arg, *kv_args, *ln_args, *pf_args)
     return out
 
 
