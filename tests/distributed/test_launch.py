@@ -2,6 +2,7 @@
 self-launch N distinct-device ranks, and no kernel may launch on another GPU's stream."""
 import json
 import os
+import re
 import subprocess
 import sys
 import textwrap
@@ -149,7 +150,9 @@ def test_rank_env_identical_under_both_launch_forms(tmp_path, entry):
     # external form (as the driver runs bench.py): python -m torch.distributed.run ... script
     r = subprocess.run(torchrun_cmd(str(script), [], 2), env=env, capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stderr[-2000:]
-    vals = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"rank"')]
+    # the ranks share one stdout pipe: lines of the two processes can interleave, so the
+    # records are matched anywhere in the text, not per line
+    vals = [json.loads(x) for x in re.findall(r'\{"rank": \d+, "val": [^}]*\}', r.stdout)]
     assert sorted(v["rank"] for v in vals) == [0, 1] and all(v["val"] == "0" for v in vals), r.stdout
     # self-launch form: the child launcher's env gets it too (and the import sets it again)
     rc, objs = self_launch(str(script), [], 2, env={"OMP_NUM_THREADS": "1", "ATPU_PROBE_CLEAR": "1",
@@ -158,5 +161,5 @@ def test_rank_env_identical_under_both_launch_forms(tmp_path, entry):
     # an operator's explicit value wins (setdefault)
     env2 = dict(env, ATPU_PROBE_CLEAR="0", HSA_ENABLE_IPC_MODE_LEGACY="1")
     r = subprocess.run(torchrun_cmd(str(script), [], 2), env=env2, capture_output=True, text=True, timeout=180)
-    vals = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"rank"')]
-    assert r.returncode == 0 and all(v["val"] == "1" for v in vals), r.stdout + r.stderr[-1000:]
+    vals = [json.loads(x) for x in re.findall(r'\{"rank": \d+, "val": [^}]*\}', r.stdout)]
+    assert r.returncode == 0 and len(vals) == 2 and all(v["val"] == "1" for v in vals), r.stdout + r.stderr[-1000:]
