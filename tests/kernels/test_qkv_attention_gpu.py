@@ -96,6 +96,34 @@ def test_cpu_reference_path_matches_unfused():
 
 
 @pytest.mark.gpu
+def test_fused_bert_large_shape():
+    """16 heads, hidden 1024 (K / 64 = 16): the bert-large encoder runs the fused kernel too."""
+    Hl, Kl, B = 16, 1024, 34
+    g = torch.Generator().manual_seed(21)
+    dev = torch.device("cuda", 0)
+    M = B * 128
+    x = (torch.randn(M, Kl, generator=g) * 1.2).to(torch.bfloat16)
+    w = (torch.randn(3 * Hl * D, Kl, generator=g) * 0.03).to(torch.bfloat16)
+    b = torch.randn(3 * Hl * D, generator=g) * 0.1
+    lens = torch.randint(1, 129, (B,), generator=g, dtype=torch.int32)
+    xf = x.float()
+    rstd = torch.rsqrt(xf.var(1, unbiased=False) + 1e-12)
+    fin = torch.stack([rstd, rstd * xf.mean(1)], 1).contiguous()
+    col = w.float().sum(1).contiguous()
+    assert ops.qkv_attention_ok(M, 3 * Hl * D, Kl, 128)
+    p = ops.qkv_head_order(Hl)
+    got = ops.qkv_attention(x.to(dev), w[p].contiguous().to(dev), b[p].contiguous().to(dev), lens.to(dev), Hl,
+                            in_fin=fin.to(dev), colsum_h=col[p].contiguous().to(dev))
+    torch.cuda.synchronize()
+    y = (xf @ w.float().t()) * fin[:, :1] - fin[:, 1:] * col.unsqueeze(0) + b
+    qkv = y.to(torch.bfloat16)
+    hd = Hl * D
+    ref = attention_ref(qkv[:, :hd], qkv[:, hd:2 * hd], qkv[:, 2 * hd:], lens, B, 128, 128, Hl, 1.0 / math.sqrt(D)).float()
+    err = (got.float().cpu() - ref).abs().max().item()
+    assert err < 2e-2 * max(ref.abs().max().item(), 1.0), err
+
+
+@pytest.mark.gpu
 def test_gemm256h_store_mode_exact():
     """Mode 0 of the 256 x 192 persistent GEMM: C = A.Bt^T + bias against fp32."""
     from agent_tpu_amd._native import native
