@@ -39,6 +39,9 @@
 #ifndef ATPU_GEMM_EARLY_KT1
 #define ATPU_GEMM_EARLY_KT1 0
 #endif
+#ifndef ATPU_GEMM_DESYNC
+#define ATPU_GEMM_DESYNC 0
+#endif
 
 namespace atpu {
 namespace {
@@ -1147,6 +1150,12 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
   const int wm = wave >> 2, wn = wave & 3;
   int v = blockIdx.x;
   if (v >= ntiles) return;
+#if ATPU_GEMM_DESYNC
+  // A/B experiment: every other CU of each XCD starts ATPU_GEMM_DESYNC x s_sleep(127) (~4 us
+  // each) late, so the CUs' tile epilogues (store bursts) stop coinciding
+  if ((blockIdx.x >> 3) & 1)
+    for (int i = 0; i < ATPU_GEMM_DESYNC; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
 
   // staging rows of quarter q / instruction i (same map as 256p); the lane's
   // row is recomputed per tile (registers are the budget here), the LDS
