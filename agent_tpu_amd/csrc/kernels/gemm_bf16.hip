@@ -42,6 +42,10 @@
 #ifndef ATPU_GEMM_DESYNC
 #define ATPU_GEMM_DESYNC 0
 #endif
+// persistent 256x256 kernel tile order: groups of this many tile rows (0 = row-major, N fastest)
+#ifndef ATPU_GEMM_GROUP
+#define ATPU_GEMM_GROUP 0
+#endif
 
 namespace atpu {
 namespace {
@@ -1316,7 +1320,7 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
   };
   int pm0 = 0, pn0 = 0;  // StatsOut: the tile whose row partials sit in LDS
 
-  int tile = xcd_remap(v, ntiles);
+  int tile = group_tiles(xcd_remap(v, ntiles), ntm, ntn, ATPU_GEMM_GROUP);
   int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 256;
   set_src(m0, n0);
   if constexpr (kBiasAcc) glds4(bias + n0 + (wave & 3) * 64, lds + kBiasOff + (wave & 3) * 256);
@@ -1391,7 +1395,7 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
       int kn = t + 1;  // K-tile staged during this one
       if (last && has_next) {
         // the stream runs on into K-tile 0 of the next tile
-        tile = xcd_remap(vn, ntiles);
+        tile = group_tiles(xcd_remap(vn, ntiles), ntm, ntn, ATPU_GEMM_GROUP);
         m0 = (tile / ntn) * 256;
         n0 = (tile % ntn) * 256;
         set_src(m0, n0);

@@ -32,6 +32,10 @@
 #define ATPU_QA_ABL 0
 #endif
 // context stores non-temporal (A/B)
+// tile order: groups of this many 256-row blocks (0 = row-major, heads fastest)
+#ifndef ATPU_QA_GROUP
+#define ATPU_QA_GROUP 0
+#endif
 #ifndef ATPU_QA_NT
 #define ATPU_QA_NT 0
 #endif
@@ -447,7 +451,7 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
   };
 
   const int nk = K / 64;
-  int tile = xcd_remap(v, ntiles);
+  int tile = group_tiles(xcd_remap(v, ntiles), M / 256, ntn, ATPU_QA_GROUP);
   int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 192;
   set_src(m0, n0);
 #pragma unroll
@@ -485,7 +489,7 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
       const bool more = !last || has_next;
       int kn = t + 1;
       if (last && has_next) {  // the stream runs on into K-tile 0 of the next tile
-        tile = xcd_remap(vn, ntiles);
+        tile = group_tiles(xcd_remap(vn, ntiles), M / 256, ntn, ATPU_QA_GROUP);
         m0 = (tile / ntn) * 256;
         n0 = (tile % ntn) * 192;
         set_src(m0, n0);
