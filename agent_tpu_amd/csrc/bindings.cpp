@@ -191,6 +191,17 @@ PYBIND11_MODULE(_atpu, m) {
                 P<int32_t>(rec), S(stream));
   });
   m.def(
+      "decode_advance",
+      [](uintptr_t hist, uintptr_t seq, int rows, int stride, uintptr_t par, uintptr_t tok, uintptr_t tokens,
+         uintptr_t step_dev, uintptr_t stream) {
+        decode_advance(P<int32_t>(hist), P<int32_t>(seq), rows, stride, P<const int32_t>(par), P<const int32_t>(tok),
+                       P<int32_t>(tokens), P<int32_t>(step_dev), S(stream));
+      },
+      "one-workgroup beam state advance: hist/seq reordered in place, tokens = tok, step += 1", py::arg("hist"),
+      py::arg("seq"), py::arg("rows"), py::arg("stride"), py::arg("par"), py::arg("tok"), py::arg("tokens"),
+      py::arg("step"), py::arg("stream"));
+  m.def("decode_advance_lds", &decode_advance_lds, py::arg("rows"), py::arg("stride"), py::arg("seq"));
+  m.def(
       "beam_reorder_hist",
       [](uintptr_t src, uintptr_t dst, uintptr_t parent, int rows, int stride, uintptr_t step_dev, uintptr_t stream,
          uintptr_t last, int off) {

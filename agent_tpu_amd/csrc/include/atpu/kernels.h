@@ -114,6 +114,12 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
 // (flash decoding) when given a workspace of this many floats (0: no split for the shape).
 int decode_attention_splits(int rows, int group, int H, int seq_stride, bool cross);
 size_t decode_attention_ws_floats(int rows, int group, int H, int seq_stride, bool cross);
+// one-workgroup state advance of a small beam search (rows x stride x 4 B x (seq ? 2 : 1) <= 64 KiB):
+// hist / seq reordered in place by par (as beam_reorder_hist, seq with last = tok, off 1),
+// tokens = tok, *step_dev += 1
+size_t decode_advance_lds(int rows, int stride, bool seq);
+void decode_advance(int32_t* hist, int32_t* seq, int rows, int stride, const int32_t* par, const int32_t* tok,
+                    int32_t* tokens, int32_t* step_dev, hipStream_t stream);
 // dst[r][j] = src[parent[r]][j] (j < t), dst[r][t] = last ? last[r] : parent[r]; t = *step_dev + off
 // device beam selection (runtime/summarize.py): item top-K2 over its beams' candidates, hits,
 // next running beams -> stage [parents | tokens | score bits] and a host record per item

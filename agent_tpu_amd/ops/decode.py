@@ -119,6 +119,37 @@ def beam_reorder_hist(src: torch.Tensor, dst: torch.Tensor, parent: torch.Tensor
                                ptr(last) if last is not None else 0, int(off))
 
 
+def decode_advance_ok(rows: int, T: int, seq: bool) -> bool:
+    """The one-workgroup :func:`decode_advance` takes this beam batch (<= 64 KiB of LDS)."""
+    return rows * T * 4 * (2 if seq else 1) <= 64 * 1024
+
+
+def decode_advance(hist: torch.Tensor, seq: Optional[torch.Tensor], parent: torch.Tensor, tok: torch.Tensor,
+                   tokens: torch.Tensor, step: torch.Tensor) -> None:
+    """A small beam search's per-step state advance in ONE launch, in place: ``hist`` reordered
+    by ``parent`` (:func:`beam_reorder_hist`, t = step), ``seq`` likewise with the new tokens
+    (off 1), ``tokens = tok``, ``step += 1`` (replaces 2 reorders, 3 copies and an add)."""
+    R, T = hist.shape
+    if not hist.is_cuda:
+        alt = torch.empty_like(hist)
+        beam_reorder_hist(hist, alt, parent, step)
+        hist.copy_(alt)
+        if seq is not None:
+            alt = torch.empty_like(seq)
+            beam_reorder_hist(seq, alt, parent, step, last=tok, off=1)
+            seq.copy_(alt)
+        tokens.copy_(tok)
+        step.add_(1)
+        return
+    for t, n in ((hist, "hist"), (parent, "parent"), (tok, "tok"), (tokens, "tokens"), (step, "step")):
+        check(t.dtype == torch.int32 and t.is_cuda and t.is_contiguous(), f"decode_advance: {n} must be int32 on device")
+    check(seq is None or (seq.dtype == torch.int32 and tuple(seq.shape) == (R, T) and seq.is_contiguous()),
+          "decode_advance: seq must be int32 [R, T]")
+    check(decode_advance_ok(R, T, seq is not None), "decode_advance: batch too large for one workgroup")
+    native().decode_advance(ptr(hist), ptr(seq), R, T, ptr(parent), ptr(tok), ptr(tokens), ptr(step),
+                            launch_stream(hist))
+
+
 def gather_rows(src: torch.Tensor, dst: torch.Tensor, parent: torch.Tensor, nrows: int, seq_stride: int,
                 step: torch.Tensor, slabs: int = 1) -> None:
     """dst[slab, r, :t+1] = src[slab, parent[r], :t+1]; tensors [slabs, nrows*seq_stride, C]."""

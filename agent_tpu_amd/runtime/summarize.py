@@ -410,16 +410,21 @@ def _generate_body(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
     lp = float(gen.length_penalty)
     graph, g_logits = (slot.graph, slot.out) if slot is not None else (None, None)
 
+    small = dev.type == "cuda" and ops.decode_advance_ok(rows, T, seq_dev is not None)
+
     def advance() -> torch.Tensor:
         """Histories follow their parent beams (backpointers, no KV copy), new tokens in,
         position + 1, decoder step -> logits. Static buffers only (graph-capturable)."""
-        ops.beam_reorder_hist(hist, hist_alt, par_dev, step_dev)
-        hist.copy_(hist_alt)  # keep the captured buffer address
-        if seq_dev is not None:  # token history for the in-kernel n-gram bans
-            ops.beam_reorder_hist(seq_dev, seq_alt, par_dev, step_dev, last=tok_dev, off=1)
-            seq_dev.copy_(seq_alt)
-        tokens.copy_(tok_dev)
-        step_dev.add_(1)
+        if small:  # one launch for the whole state advance (1-document searches)
+            ops.decode_advance(hist, seq_dev, par_dev, tok_dev, tokens, step_dev)
+        else:
+            ops.beam_reorder_hist(hist, hist_alt, par_dev, step_dev)
+            hist.copy_(hist_alt)  # keep the captured buffer address
+            if seq_dev is not None:  # token history for the in-kernel n-gram bans
+                ops.beam_reorder_hist(seq_dev, seq_alt, par_dev, step_dev, last=tok_dev, off=1)
+                seq_dev.copy_(seq_alt)
+            tokens.copy_(tok_dev)
+            step_dev.add_(1)
         return model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist, logits=not fused)
 
     def launch_next() -> torch.Tensor:

@@ -841,3 +841,36 @@ def test_gemv_kv_scatter(gpu, M, rms):
     kv = cache.view(M, T, 2 * d)
     assert torch.equal(kv[:, t], full[:, d:])
     assert kv[:, :t].abs().sum().item() == 0 and kv[:, t + 1:].abs().sum().item() == 0
+
+
+@pytest.mark.parametrize("rows,T,with_seq", [(4, 130, True), (4, 130, False), (8, 200, True), (1, 7, True)])
+def test_decode_advance_matches_reorder_path(gpu, rows, T, with_seq):
+    """The one-workgroup state advance == beam_reorder_hist + copies + add, at several steps
+    (including the clamped last position)."""
+    g = torch.Generator().manual_seed(rows * 1000 + T)
+    for step in (0, 1, T // 2, T - 2, T - 1):
+        hist = torch.randint(0, rows, (rows, T), generator=g, dtype=torch.int32)
+        seq = torch.randint(0, 50000, (rows, T), generator=g, dtype=torch.int32) if with_seq else None
+        par = torch.randint(0, rows, (rows,), generator=g, dtype=torch.int32)
+        tok = torch.randint(0, 50000, (rows,), generator=g, dtype=torch.int32)
+        st = torch.tensor([step], dtype=torch.int32)
+        # reference: the multi-launch path on the CPU twin
+        h_ref, s_ref = hist.clone(), (seq.clone() if with_seq else None)
+        alt = torch.empty_like(h_ref)
+        ops.beam_reorder_hist(h_ref, alt, par, st)
+        h_ref = alt
+        if with_seq:
+            alt2 = torch.empty_like(s_ref)
+            ops.beam_reorder_hist(s_ref, alt2, par, st, last=tok, off=1)
+            s_ref = alt2
+        hd, sd = hist.to(gpu), (seq.to(gpu) if with_seq else None)
+        tokens = torch.zeros(rows, dtype=torch.int32, device=gpu)
+        std = st.to(gpu)
+        ops.decode_advance(hd, sd, par.to(gpu), tok.to(gpu), tokens, std)
+        torch.cuda.synchronize()
+        t = min(step, T - 1)
+        assert torch.equal(hd.cpu()[:, :t + 1], h_ref[:, :t + 1]), step
+        if with_seq:
+            t2 = min(step + 1, T - 1)
+            assert torch.equal(sd.cpu()[:, :t2 + 1], s_ref[:, :t2 + 1]), step
+        assert torch.equal(tokens.cpu(), tok) and int(std.item()) == step + 1
