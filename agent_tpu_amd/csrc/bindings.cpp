@@ -234,6 +234,8 @@ PYBIND11_MODULE(_atpu, m) {
       py::arg("nbmax") = 0, py::arg("seq") = 0, py::arg("seq_stride") = 0, py::arg("cur") = 0, py::arg("ngram") = 0);
   m.def("lm_head_ws_bytes", &lm_head_ws_bytes);
   m.def("lm_head_stages", &lm_head_stages, py::arg("set") = -1);
+  m.def("lm_head_wide", &lm_head_wide, py::arg("set") = -1);
+  m.def("decode_cross_wg", &decode_cross_wg, py::arg("set") = -1);
   m.def(
       "lm_head_topk",
       [](uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t bias, float rms_eps, int M, int V, int K, int topk,

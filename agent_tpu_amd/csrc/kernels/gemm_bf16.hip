@@ -2341,6 +2341,31 @@ __global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __res
   }
   const int n0 = (blockIdx.x * NWV + w) * 4;  // this wave's 4 columns
   const int nch = K / 8;
+  // lane (mo*4 + jo) finishes output (mo, n0 + jo). Its epilogue operands (bias, residual,
+  // LN column sums / gamma, row-statistics partials, the cache step) do not depend on the
+  // dot products: loaded first, they arrive under the main loop instead of as a dependent
+  // round trip after the reductions
+  const int mo = lane >> 2, jo = lane & 3;
+  const bool mine = mo < M && lane < 4 * kGemvRows;
+  const int om = min(mo, M - 1), n = n0 + jo;  // (clamped) output row
+  float e_bias = 0.f, e_res = 0.f, e_col = 0.f, e_gam = 0.f;
+  int e_step = 0;
+  if (mine) {
+    if constexpr (EPI & kEpiBias) e_bias = bias[n];
+    if constexpr (EPI & kEpiResidual) e_res = bf2f(R[(size_t)om * ldr + n]);
+    if constexpr (EPI & kEpiRowLn) e_col = ln.colsum[n];
+    if constexpr (EPI & kEpiResLn) e_gam = ln.gamma[n];
+    if constexpr (EPI & kEpiKvScatter) e_step = *kvo.step;
+  }
+  float2 e_part[kGemvRows];
+  if constexpr (EPI & (kEpiRowLn | kEpiResLn)) {
+    const int slots = (EPI & kEpiRowLn) ? K / 32 : N / 32;
+    const float* part = (EPI & kEpiRowLn) ? ln.in_part : ln.res_part;
+#pragma unroll
+    for (int r = 0; r < kGemvRows; ++r)
+      e_part[r] = lane < slots ? *reinterpret_cast<const float2*>(part + 2 * ((size_t)lane * M + min(r, M - 1)))
+                               : float2{0.f, 0.f};
+  }
   float acc[kGemvRows][4], ssq[kGemvRows];
 #pragma unroll
   for (int m = 0; m < kGemvRows; ++m) {
@@ -2382,7 +2407,6 @@ __global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __res
   }
   // every lane gets every sum; lane (m*4 + j) finishes output (m, n0 + j)
   float v = 0.f, rs = 0.f;
-  const int mo = lane >> 2, jo = lane & 3;
 #pragma unroll
   for (int m = 0; m < kGemvRows; ++m) {
 #pragma unroll
@@ -2399,42 +2423,36 @@ __global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __res
   float2 lnst = float2{1.f, 0.f};
   if constexpr (EPI & (kEpiRowLn | kEpiResLn)) {
     const int slots = (EPI & kEpiRowLn) ? K / 32 : N / 32;
-    const float* part = (EPI & kEpiRowLn) ? ln.in_part : ln.res_part;
 #pragma unroll
-    for (int m = 0; m < kGemvRows; ++m) {
-      const float2 pv = lane < slots ? *reinterpret_cast<const float2*>(part + 2 * ((size_t)lane * M + min(m, M - 1)))
-                                     : float2{0.f, 0.f};
-      const float S = wave_sum(pv.x), Q = wave_sum(pv.y);
+    for (int r = 0; r < kGemvRows; ++r) {
+      const float S = wave_sum(e_part[r].x), Q = wave_sum(e_part[r].y);
       const float inv = 1.f / (32 * slots);
       const float mu = S * inv, var = fmaxf(Q * inv - mu * mu, 0.f);
-      const float r = __builtin_amdgcn_rsqf(var + rms_eps);
-      lnst = mo == m ? float2{r, r * mu} : lnst;
+      const float rr = __builtin_amdgcn_rsqf(var + rms_eps);
+      lnst = mo == r ? float2{rr, rr * mu} : lnst;
     }
   }
-  const bool mine = mo < M && lane < 4 * kGemvRows;
-  const int m = min(mo, M - 1), n = n0 + jo;
   float f = 0.f;  // RowStats: the stored (bf16-rounded) value
   if (mine) {
     if constexpr (EPI & kEpiRowRms) v *= __builtin_amdgcn_rsqf(rs * (1.f / K) + rms_eps);
-    if constexpr (EPI & kEpiRowLn) v = fmaf(v, lnst.x, -lnst.y * ln.colsum[n]);
-    if constexpr (EPI & kEpiBias) v += bias[n];
+    if constexpr (EPI & kEpiRowLn) v = fmaf(v, lnst.x, -lnst.y * e_col);
+    if constexpr (EPI & kEpiBias) v += e_bias;
     if constexpr (EPI & kEpiGelu) v = gelu_fast(v);
     if constexpr (EPI & kEpiRelu) v = fmaxf(v, 0.f);
     if constexpr (EPI & kEpiResidual) {
-      const float r = bf2f(R[(size_t)m * ldr + n]);
-      if constexpr (EPI & kEpiResLn) v = fmaf(fmaf(r, lnst.x, -lnst.y), ln.gamma[n], v);
-      else v += r;
+      if constexpr (EPI & kEpiResLn) v = fmaf(fmaf(e_res, lnst.x, -lnst.y), e_gam, v);
+      else v += e_res;
     }
     const bf16 o = f2bf(v);
     f = bf2f(o);
     if constexpr (EPI & kEpiKvScatter) {
-      const int pos = max(*kvo.step, 0);
+      const int pos = max(e_step, 0);
       if (n < kvo.col0)
-        C[(size_t)m * ldc + n] = o;
+        C[(size_t)om * ldc + n] = o;
       else if (pos < kvo.T)  // a step past the cache (caller bug) drops the write
-        kvo.cache[((size_t)m * kvo.T + pos) * kvo.ld + (n - kvo.col0)] = o;
+        kvo.cache[((size_t)om * kvo.T + pos) * kvo.ld + (n - kvo.col0)] = o;
     } else {
-      C[(size_t)m * ldc + n] = o;
+      C[(size_t)om * ldc + n] = o;
     }
   }
   if constexpr (EPI & kEpiRowStats) {
