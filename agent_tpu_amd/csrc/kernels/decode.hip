@@ -461,6 +461,124 @@ __global__ __launch_bounds__(64) void decode_attn_combine_kernel(const float* __
 }
 
 // ----------------------------------------------------------------------------
+// Self attention of few rows (the 1-document job: 4 beam rows) with a short cache
+// (T <= 64 KC keys): ONE wave per (row, head), 48 waves over 48 CUs, two memory round
+// trips in all. Round 1: the step, the row's backpointers (every key the cache can hold,
+// masked by the length later) and the head's query; round 2: the K row of every key
+// (lane = key, KC chunks) and the V slabs of every key (lane = (key sub, 8 dims)), all
+// issued before the first use. decode_self_attention_kernel walks the same keys in up to
+// 3 + 5 dependent load rounds per head (6.3 us per call at 4 rows x 12 heads).
+// ----------------------------------------------------------------------------
+template <int KC>
+__global__ __launch_bounds__(64) void decode_self_few_kernel(const bf16* __restrict__ q, int ldq,
+                                                             const bf16* __restrict__ k, const bf16* __restrict__ v,
+                                                             int ldkv, int seq_stride,
+                                                             const int32_t* __restrict__ step_dev,
+                                                             const int32_t* __restrict__ hist, int hist_stride,
+                                                             const float* __restrict__ bias_dist, int bias_stride,
+                                                             bf16* __restrict__ out, int ldo, float scale) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  constexpr int NK = KC * 64, NV = NK / 8;
+  __shared__ int prow[NK];
+  __shared__ float pw[NK];
+  const int seq = xcd_remap(blockIdx.x, gridDim.x), h = blockIdx.y, lane = threadIdx.x;
+  const int ksub = lane >> 3, dc = (lane & 7) * 8;
+  // round 1
+  const int stp = *step_dev;
+  int hv[KC];
+#pragma unroll
+  for (int c = 0; c < KC; ++c) {
+    const int j = c * 64 + lane;
+    hv[c] = (hist && j < hist_stride) ? hist[(size_t)seq * hist_stride + j] : seq;
+  }
+  bf16x8 qq[8];
+  const bf16* qr = q + (size_t)seq * ldq + h * kD;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) qq[e] = *reinterpret_cast<const bf16x8*>(qr + e * 8);
+  const int len = min(stp + 1, seq_stride);
+  auto at = [&](int r, int j) -> size_t { return ((size_t)r * seq_stride + j) * ldkv + h * kD; };
+#pragma unroll
+  for (int c = 0; c < KC; ++c) {
+    const int j = c * 64 + lane;
+    hv[c] = (hist && j < len - 1) ? hv[c] : seq;
+    prow[j] = hv[c];
+  }
+  __syncthreads();  // one wave: orders the prow writes before the V address reads
+  // round 2: every K row and V slab of the cache's first len keys
+  bf16x8 kk[KC][8], vv[NV];
+#pragma unroll
+  for (int c = 0; c < KC; ++c) {
+    if (c * 64 < len) {  // wave-uniform
+      const int j = min(c * 64 + lane, len - 1);
+      const bf16* kr = k + at(j == c * 64 + lane ? hv[c] : prow[j], j);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) kk[c][e] = *reinterpret_cast<const bf16x8*>(kr + e * 8);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    if (u * 8 < len) {
+      const int j = min(u * 8 + ksub, len - 1);
+      vv[u] = *reinterpret_cast<const bf16x8*>(v + at(prow[j], j) + dc);
+    }
+  }
+  float mx = -FLT_MAX;
+#pragma unroll
+  for (int c = 0; c < KC; ++c) {
+    const int j = c * 64 + lane;
+    if (c * 64 < len) {
+      float d[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          d[t] = __builtin_amdgcn_fdot2_f32_bf16(bf16x2_t{kk[c][e][2 * t], kk[c][e][2 * t + 1]},
+                                                 bf16x2_t{qq[e][2 * t], qq[e][2 * t + 1]}, d[t], false);
+      const float sj = j < len ? ((d[0] + d[1]) + (d[2] + d[3])) * scale +
+                                     (bias_dist ? bias_dist[h * bias_stride + (len - 1 - j)] : 0.f)
+                               : -FLT_MAX;
+      pw[j] = sj;
+      mx = fmaxf(mx, sj);
+    }
+  }
+  mx = wave_max(mx);
+  float sum = 0.f;
+#pragma unroll
+  for (int c = 0; c < KC; ++c) {
+    const int j = c * 64 + lane;
+    if (c * 64 < len) {
+      const float e = j < len ? __expf(pw[j] - mx) : 0.f;
+      pw[j] = e;
+      sum += e;
+    }
+  }
+  sum = wave_sum(sum);
+  float o[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = 0.f;
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    if (u * 8 < len) {
+      const int j = u * 8 + ksub;
+      const float pj = j < len ? pw[j] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] += pj * bf2f(vv[u][e]);
+    }
+  }
+  const float inv = sum > 0.f ? 1.f / sum : 0.f;
+  bf16x8 ov;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float x = o[e];
+    x += __shfl_xor(x, 8);
+    x += __shfl_xor(x, 16);
+    x += __shfl_xor(x, 32);
+    ov[e] = f2bf(x * inv);
+  }
+  if (ksub == 0) *reinterpret_cast<bf16x8*>(out + (size_t)seq * ldo + h * kD + dc) = ov;
+}
+
+// ----------------------------------------------------------------------------
 // Cross attention of few items, split and combined in ONE workgroup per (item, head):
 // its 16 waves take one 64-key chunk each (the split kernel's per-chunk math: every K
 // and V load of the wave issued before the first use), the chunks' {max, sum, o[64]}
@@ -1007,12 +1125,25 @@ __global__ __launch_bounds__(kSelMax) void beam_select_kernel(const float* __res
 
 }  // namespace
 
+int decode_self_few(int set) {
+  // few-row self attention: one wave per (row, head), all loads in two rounds
+  // (decode_self_few_kernel); ATPU_DEC_SELF_FEW=0 or decode_self_few(0) turns it off
+  static int v = [] {
+    const char* f = std::getenv("ATPU_DEC_SELF_FEW");
+    return (f && f[0] == '0') ? 0 : 1;
+  }();
+  if (set == 0 || set == 1) v = set;
+  return v;
+}
+
 int decode_cross_wg(int set) {
   // few-item cross attention in one workgroup per (item, head) (decode_cross_wg_kernel)
-  // instead of the split + combine pair; ATPU_DEC_XWG=0 or decode_cross_wg(0) turns it off
+  // instead of the split + combine pair: measured SLOWER (1-doc T5 9.7 vs 11.4 docs/s, BART
+  // 7.6 vs 8.7: one CU's address/L1 pipeline issues the 1024 scattered 128-B K rows of a
+  // head ~16x slower than the split grid spread over 192 CUs), so off unless ATPU_DEC_XWG=1
   static int v = [] {
     const char* f = std::getenv("ATPU_DEC_XWG");
-    return (f && f[0] == '0') ? 0 : 1;
+    return (f && f[0] == '1') ? 1 : 0;
   }();
   if (set == 0 || set == 1) v = set;
   return v;
@@ -1057,6 +1188,20 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
     ATPU_CHECK(!hist || hist_stride >= seq_stride, "decode_attention: hist rows shorter than the cache");
     ATPU_CHECK(ldo % 8 == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 && (reinterpret_cast<uintptr_t>(q) & 15) == 0,
                "decode_attention: q / out need 16-B rows");
+    if (rows * H <= num_cus() && seq_stride <= 192 && decode_self_few(-1)) {
+#define ATPU_SF(KC)                                                                                              \
+  hipLaunchKernelGGL((decode_self_few_kernel<KC>), dim3(rows, H), dim3(64), 0, stream, q, ldq, k, v, ldkv, seq_stride, \
+                     step_dev, hist, hist_stride, bias_dist, bias_stride, out, ldo, scale)
+      if (seq_stride <= 64)
+        ATPU_SF(1);
+      else if (seq_stride <= 128)
+        ATPU_SF(2);
+      else
+        ATPU_SF(3);
+#undef ATPU_SF
+      ATPU_HIP_CHECK(hipGetLastError());
+      return;
+    }
     constexpr int NW = 4;
     const size_t smem = (size_t)((seq_stride + 3) & ~3) * 4 * (1 + NW);
     // few rows: head groups over grid.y (one head per wave) so the launch covers more CUs

@@ -262,6 +262,22 @@ template <int OFF0, int STEP, int N, int... I>
 __device__ __forceinline__ void lds_read_frags(bf16x8 (&f)[N], unsigned a, std::integer_sequence<int, I...>) {
   ((f[I] = lds_read128_off<OFF0 + I * STEP>(a)), ...);
 }
+// fragment F of a K-tile half: F < 4 the A rows, else vocabulary fragment F - 4
+template <int F>
+__device__ __forceinline__ void read_frag(unsigned xba, unsigned xbb, bf16x8 (&xa)[4], bf16x8 (&xb)[kWTN]) {
+  if constexpr (F < 4)
+    xa[F] = lds_read128_off<F * 16 * kRowB>(xba);
+  else
+    xb[F - 4] = lds_read128_off<(kWM + (F - 4) * 16) * kRowB>(xbb);
+}
+template <class Fn, int... I>
+__device__ __forceinline__ void static_for_impl(Fn&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class Fn>
+__device__ __forceinline__ void static_for(Fn&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 // s_waitcnt lgkmcnt(N) that a fragment set passes through (its consumers cannot move above it)
 template <int N>
 __device__ __forceinline__ void lds_wait14(bf16x8 (&a)[4], bf16x8 (&b)[kWTN]) {
@@ -291,19 +307,43 @@ __global__ __launch_bounds__(256, 1) void lm_head_wide_kernel(
   const int srow = lane >> 3;
   const int sw = ((lane & 7) ^ (((srow >> 1) + 4 * (wave & 1)) & 7)) * 8;
   auto tile_of = [&](int t) { return xcd_remap(b + t * G, ntiles); };
-  auto stage = [&](int s) {  // wave-uniform s
-    if (s >= nstage) return;
+  // a K-tile's 13 LDS-DMAs, issued one at a time between MFMAs: lane row b0 + 32 i of the
+  // tile (clamped to the last row / vocabulary entry: branch-free tails), scalar tile / K bases
+  const int b0 = wave * 8 + srow;
+  struct StageP {
+    const char *a, *w;
+    char* l;
+    int lima, limw;
+    bool live;
+  };
+  auto plan = [&](int s) {  // wave-uniform s
+    StageP p{};
+    p.live = s < nstage;
+    if (!p.live) return p;
     const int t = s / nk, kt = s - t * nk;
     const int tile = tile_of(t);
     const int m0 = (tile % ntm) * kWM, n0 = (tile / ntm) * kWN;
-    char* base = lds + (s % kWNst) * kWStage + wave * 8 * kRowB;
-#pragma unroll
-    for (int i = 0; i < kWLps; ++i) {
-      const int r = i * 32 + wave * 8 + srow;
-      const bf16* src = i < kWLpsA ? A + (size_t)min(m0 + r, M - 1) * lda
-                                   : W + (size_t)min(n0 + r - kWM, V - 1) * ldw;
-      glds16(src + kt * kBK + sw, base + i * 32 * kRowB);
+    p.lima = M - 1 - m0;
+    p.limw = V - 1 - n0;
+    p.a = reinterpret_cast<const char*>(A + (size_t)m0 * lda + kt * kBK);
+    p.w = reinterpret_cast<const char*>(W + (size_t)n0 * ldw + kt * kBK);
+    p.l = lds + (s % kWNst) * kWStage + wave * 8 * kRowB;
+    return p;
+  };
+  auto dma = [&](const StageP& p, auto ic) {
+    constexpr int i = decltype(ic)::value;
+    if (!p.live) return;
+    if constexpr (i < kWLpsA) {
+      const unsigned r = min(b0 + 32 * i, p.lima);
+      glds16(p.a + (r * (unsigned)lda + sw) * 2u, p.l + i * 32 * kRowB);
+    } else {
+      const unsigned r = min(b0 + 32 * (i - kWLpsA), p.limw);
+      glds16(p.w + (r * (unsigned)ldw + sw) * 2u, p.l + i * 32 * kRowB);
     }
+  };
+  auto stage = [&](int s) {
+    const StageP p = plan(s);
+    static_for<kWLps>([&](auto ic) { dma(p, ic); });
   };
 
   // fragment reads: A rows wave*64 + i*16 + fr, vocabulary rows 256 + j*16 + fr; swizzle fr >> 1
@@ -312,9 +352,12 @@ __global__ __launch_bounds__(256, 1) void lm_head_wide_kernel(
   const int sx = fr >> 1;
   // by inline asm with counted waits (lds_wait14): for compiler-visible reads the waitcnt pass
   // put an lgkmcnt(0) in front of the first MFMA, i.e. waited for the other half's 14 reads too
+  auto rd_base = [&](int s, int ks) {
+    return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)lds + (s % kWNst) * kWStage + rdo +
+           (((ks * 4 + fc) ^ sx) * 16);
+  };
   auto rd = [&](int s, int ks, bf16x8 (&af)[4], bf16x8 (&bw)[kWTN]) {
-    const unsigned base = (unsigned)(size_t)(const __attribute__((address_space(3))) char*)lds +
-                          (s % kWNst) * kWStage + rdo + (((ks * 4 + fc) ^ sx) * 16);
+    const unsigned base = rd_base(s, ks);
     const unsigned ba = base + wave * 64 * kRowB;
     lds_read_frags<0, 16 * kRowB>(af, ba, std::make_integer_sequence<int, 4>{});
     lds_read_frags<kWM * kRowB, 16 * kRowB>(bw, base, std::make_integer_sequence<int, kWTN>{});
@@ -372,10 +415,37 @@ __global__ __launch_bounds__(256, 1) void lm_head_wide_kernel(
         wait_vm<0>();
       asm volatile("s_barrier" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      stage(g + 3);
-      if (g + 1 < nstage) rd(g + 1, 0, xa, xb);
+      // the second half's 40 MFMAs in 10 vocabulary-fragment groups; ahead of each group one
+      // or two of K-tile g+3's DMAs and of K-tile g+1's first-half reads, so the issue slots
+      // of the 13 DMAs (and their address math) and 14 reads hide under MFMAs
+      const StageP sp = plan(g + 3);
+      const bool more = g + 1 < nstage;
+      const unsigned xbb = more ? rd_base(g + 1, 0) : 0u, xba = xbb + wave * 64 * kRowB;
       lds_wait14<14>(ya, yb);  // retired by the lgkmcnt(0) above; ties the registers
-      mma(ya, yb);
+      static_for<kWTN>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if constexpr (j < 3) {
+          dma(sp, std::integral_constant<int, 2 * j>{});
+          dma(sp, std::integral_constant<int, 2 * j + 1>{});
+        } else {
+          dma(sp, std::integral_constant<int, j + 3>{});
+        }
+        if (more) {
+          if constexpr (j < 4) {
+            read_frag<2 * j>(xba, xbb, xa, xb);
+            read_frag<2 * j + 1>(xba, xbb, xa, xb);
+          } else {
+            read_frag<j + 4>(xba, xbb, xa, xb);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if constexpr (RMS && j == 0) ssq[i] = sumsq_chunk(ya[i], ssq[i]);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(yb[j], ya[i], acc[i][j], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
     }
 
     // ---------------------------------------------------------------- epilogue
@@ -609,14 +679,14 @@ int lm_head_stages(int set) {
 #endif
 }
 
-// 256 x 160 persistent kernel for step batches of >= kWideMinRows rows (ATPU_LM_WIDE=0 or
-// lm_head_wide(0) keeps every batch on the 128 x 128 kernel)
+// 256 x 160 persistent kernel for step batches of >= kWideMinRows rows: ATPU_LM_WIDE=1 or
+// lm_head_wide(1) (default off until it beats the 128 x 128 kernel: docs/PERF_NOTES.md)
 constexpr int kWideMinRows = 512;
 
 int lm_head_wide(int set) {
   static int v = [] {
     const char* f = std::getenv("ATPU_LM_WIDE");
-    return (f && f[0] == '0') ? 0 : 1;
+    return (f && f[0] == '1') ? 1 : 0;
   }();
   if (set == 0 || set == 1) v = set;
   return v;

@@ -86,6 +86,34 @@ def test_decode_self_head_groups(gpu, rows, H, T, t):
     assert _rel(out, ref) < 2e-2
 
 
+@pytest.mark.parametrize("rows,H,T,t,hist_on", [(4, 12, 130, 70, True), (4, 12, 130, 129, True), (1, 12, 130, 0, True),
+                                                (4, 12, 64, 63, False), (3, 16, 100, 64, True), (4, 12, 192, 150, True)])
+def test_decode_self_few_matches_row_kernel(gpu, rows, H, T, t, hist_on):
+    # few rows, T <= 192: one wave per (row, head) with every load in two rounds
+    # (decode_self_few_kernel) against the per-row kernel: same key / dimension order of
+    # every sum, so bit-identical; KC = 1-3 key chunks, a step at the cache end, no hist
+    nat = __import__("agent_tpu_amd._native", fromlist=["native"]).native()
+    d = H * 64
+    cache = _r((rows * T, 2 * d), gpu, seed=61)
+    q = _r((rows, 3 * d), gpu, seed=62)[:, :d]
+    g = torch.Generator().manual_seed(7)
+    hist = torch.randint(0, rows, (rows, T), generator=g, dtype=torch.int32).to(gpu) if hist_on else None
+    step = torch.tensor([t], dtype=torch.int32, device=gpu)
+    bias = _r((H, T), gpu, 1.0, torch.float32, seed=63)
+    prev = nat.decode_self_few(-1)
+    try:
+        outs = []
+        for few in (1, 0):
+            nat.decode_self_few(few)
+            outs.append(ops.decode_attention(q, cache[:, :d], cache[:, d:], H, T, 1, step=step, bias_dist=bias, hist=hist))
+    finally:
+        nat.decode_self_few(prev)
+    assert torch.equal(outs[0], outs[1])
+    ref = _decode_attention_ref(q.cpu(), cache.cpu()[:, :d], cache.cpu()[:, d:], H, T, 1, None, step.cpu(), bias.cpu(),
+                                1.0, None, None if hist is None else hist.cpu())
+    assert _rel(outs[0], ref) < 2e-2
+
+
 def test_decode_self_with_bias_append_gather(gpu):
     rows, H, T = 6, 4, 20
     d = H * 64
