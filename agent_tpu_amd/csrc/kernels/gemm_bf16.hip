@@ -2302,6 +2302,36 @@ struct GemvPf {
 };
 // The loads are 4-byte LDS-DMAs into a 256-B scratch nobody reads: a VGPR-destination load
 // issued from inline asm would let the compiler reuse its register before the data returns.
+// A/B build switches (python -m agent_tpu_amd.csrc.build -D NAME=V --out ...)
+#ifndef ATPU_GEMV_BFLY
+#define ATPU_GEMV_BFLY 1  // butterfly reduction of the GEMV partials (0: 16 wave sums)
+#endif
+#ifndef ATPU_GEMV_EARLY
+#define ATPU_GEMV_EARLY 1  // epilogue operands loaded before the main loop: 0 never, 1 LN-folded, 2 all
+#endif
+#ifndef ATPU_GEMV_PF_RS
+#define ATPU_GEMV_PF_RS 0  // L2 prefetch from RowStats GEMVs too
+#endif
+
+// v_permlane32_swap / v_permlane16_swap of two values (x's upper 32 lanes <-> y's lower 32;
+// x's odd 16-lane rows <-> y's even rows), laundered into early-clobber outputs as in
+// lane_rows_sum (common.h)
+__device__ __forceinline__ float2 pl32_swap(float x, float y) {
+  float a, b;
+  asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %3\n\ts_nop 1\n\tv_permlane32_swap_b32 %0, %1"
+               : "=&v"(a), "=&v"(b)
+               : "v"(x), "v"(y));
+  return float2{a, b};
+}
+__device__ __forceinline__ float2 pl16_swap(float x, float y) {
+  float a, b;
+  asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %3\n\ts_nop 1\n\tv_permlane16_swap_b32 %0, %1"
+               : "=&v"(a), "=&v"(b)
+               : "v"(x), "v"(y));
+  return float2{a, b};
+}
+
+template <bool BARRIER>
 __device__ __forceinline__ void gemv_prefetch(const GemvPf& pf, int lane, char* scratch) {
   const int lpr = (pf.k * 2 + 127) / 128;  // 128-B lines per row
   const int blocks = (pf.n + pf.rpb - 1) / pf.rpb;
@@ -2314,6 +2344,10 @@ __device__ __forceinline__ void gemv_prefetch(const GemvPf& pf, int lane, char* 
       __builtin_amdgcn_global_load_lds((const ATPU_GLOBAL_AS void*)p, (ATPU_LDS_AS void*)scratch, 4, 0, 0);
     }
   }
+  // RowStats workgroups: the wave's share of the slab barrier, taken with its loads still in
+  // flight (a raw s_barrier; __syncthreads would drain them first and hold the compute waves,
+  // which measured slower than no prefetch), then the drain before the wave ends
+  if constexpr (BARRIER) asm volatile("s_barrier" ::: "memory");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -2334,29 +2368,33 @@ __global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __res
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if constexpr (PF) {
     if (w == NWV) {
-      gemv_prefetch(pf, lane, pf_scratch);
-      if constexpr (EPI & kEpiRowStats) __syncthreads();  // RowStats' one workgroup barrier (unused: host)
+      gemv_prefetch<(EPI & kEpiRowStats) != 0>(pf, lane, pf_scratch);
       return;
     }
   }
   const int n0 = (blockIdx.x * NWV + w) * 4;  // this wave's 4 columns
   const int nch = K / 8;
-  // lane (mo*4 + jo) finishes output (mo, n0 + jo). Its epilogue operands (bias, residual,
-  // LN column sums / gamma, row-statistics partials, the cache step) do not depend on the
-  // dot products: loaded first, they arrive under the main loop instead of as a dependent
-  // round trip after the reductions
-  const int mo = lane >> 2, jo = lane & 3;
-  const bool mine = mo < M && lane < 4 * kGemvRows;
+  // lanes 16 mo + 4 jo finish output (mo, n0 + jo). With LayerNorm folding (BART) its
+  // epilogue operands (bias, residual, LN column sums / gamma, the row-statistics partials)
+  // are loaded before the main loop and arrive under it instead of as a dependent round trip
+  // after the reductions: BART 1-doc 8.5 -> 8.8 docs/s; for the T5 epilogues (RowRms, ReLU,
+  // residual, KV scatter) the same early loads measured slower (12.3 -> 11.7), so those load
+  // in the epilogue (profiles/summarize_1doc_gemv_early_loads_r04.txt)
+  constexpr bool kEarly = ATPU_GEMV_EARLY == 2 || (ATPU_GEMV_EARLY == 1 && (EPI & (kEpiRowLn | kEpiResLn)) != 0);
+  const int mo = lane >> 4, jo = (lane >> 2) & 3;  // the reduction's output lanes (below)
+  const bool mine = mo < M && (lane & 3) == 0;
   const int om = min(mo, M - 1), n = n0 + jo;  // (clamped) output row
   float e_bias = 0.f, e_res = 0.f, e_col = 0.f, e_gam = 0.f;
   int e_step = 0;
-  if (mine) {
+  auto epi_loads = [&] {
+    if (!mine) return;
     if constexpr (EPI & kEpiBias) e_bias = bias[n];
     if constexpr (EPI & kEpiResidual) e_res = bf2f(R[(size_t)om * ldr + n]);
     if constexpr (EPI & kEpiRowLn) e_col = ln.colsum[n];
     if constexpr (EPI & kEpiResLn) e_gam = ln.gamma[n];
     if constexpr (EPI & kEpiKvScatter) e_step = *kvo.step;
-  }
+  };
+  if constexpr (kEarly) epi_loads();
   float2 e_part[kGemvRows];
   if constexpr (EPI & (kEpiRowLn | kEpiResLn)) {
     const int slots = (EPI & kEpiRowLn) ? K / 32 : N / 32;
@@ -2405,18 +2443,55 @@ __global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __res
       }
     }
   }
-  // every lane gets every sum; lane (m*4 + j) finishes output (m, n0 + j)
-  float v = 0.f, rs = 0.f;
+  // the 16 partials (m, j) summed over the wave by a butterfly that halves the values each
+  // step (two permlane swaps, then xor shuffles): 17 cross-lane ops instead of 16 x 6, and
+  // lanes 4i..4i+3 end with output i = m*4 + j (RowRms: lanes 16m.. with row m's sum of squares)
+  float v, rs = 0.f;
+  if constexpr (!ATPU_GEMV_BFLY) {  // A/B build: 16 (+4) independent wave sums
+    v = 0.f;
 #pragma unroll
-  for (int m = 0; m < kGemvRows; ++m) {
+    for (int m = 0; m < kGemvRows; ++m) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float t = wave_sum(acc[m][j]);
-      v = (mo == m && jo == j) ? t : v;
+      for (int j = 0; j < 4; ++j) {
+        const float t = wave_sum(acc[m][j]);
+        v = (mo == m && jo == j) ? t : v;
+      }
+      if constexpr (EPI & kEpiRowRms) {
+        const float t = wave_sum(ssq[m]);
+        rs = mo == m ? t : rs;
+      }
     }
+  } else {
+    float h8[8], h4[4], h2[2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float2 p = pl32_swap(acc[i >> 2][i & 3], acc[(i + 8) >> 2][(i + 8) & 3]);
+      h8[i] = p.x + p.y;  // lanes < 32: output i, lanes >= 32: output i + 8
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float2 p = pl16_swap(h8[i], h8[i + 4]);
+      h4[i] = p.x + p.y;  // + 4 on odd 16-lane rows
+    }
+    const bool b3 = lane & 8, b2 = lane & 4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) h2[i] = (b3 ? h4[i + 2] : h4[i]) + __shfl_xor(b3 ? h4[i] : h4[i + 2], 8);
+    v = (b2 ? h2[1] : h2[0]) + __shfl_xor(b2 ? h2[0] : h2[1], 4);
+    v += __shfl_xor(v, 2);
+    v += __shfl_xor(v, 1);
     if constexpr (EPI & kEpiRowRms) {
-      const float t = wave_sum(ssq[m]);
-      rs = mo == m ? t : rs;
+      float s2[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float2 p = pl32_swap(ssq[i], ssq[i + 2]);
+        s2[i] = p.x + p.y;
+      }
+      const float2 p = pl16_swap(s2[0], s2[1]);
+      rs = p.x + p.y;  // row (lane >> 4), summed over lanes l, l^16, l^32, l^48
+      rs += __shfl_xor(rs, 8);
+      rs += __shfl_xor(rs, 4);
+      rs += __shfl_xor(rs, 2);
+      rs += __shfl_xor(rs, 1);
     }
   }
   // (rstd, rstd*mu) of A's rows (RowLn) or R's rows (ResLn) from their slab partials
@@ -2432,6 +2507,7 @@ __global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __res
       lnst = mo == r ? float2{rr, rr * mu} : lnst;
     }
   }
+  if constexpr (!kEarly) epi_loads();
   float f = 0.f;  // RowStats: the stored (bf16-rounded) value
   if (mine) {
     if constexpr (EPI & kEpiRowRms) v *= __builtin_amdgcn_rsqf(rs * (1.f / K) + rms_eps);
@@ -2456,12 +2532,12 @@ __global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __res
     }
   }
   if constexpr (EPI & kEpiRowStats) {
-    // this wave's 4 columns of row m (lanes m*4 .. m*4+3), then the 8 waves of the slab
+    // this wave's 4 columns of row m (lanes 16m + 4j), then the 8 waves of the slab
     float s1 = f, s2 = f * f;
-    s1 += __shfl_xor(s1, 1);
-    s2 += __shfl_xor(s2, 1);
-    s1 += __shfl_xor(s1, 2);
-    s2 += __shfl_xor(s2, 2);
+    s1 += __shfl_xor(s1, 4);
+    s2 += __shfl_xor(s2, 4);
+    s1 += __shfl_xor(s1, 8);
+    s2 += __shfl_xor(s2, 8);
     if (mine && jo == 0) st_red[w][mo] = float2{s1, s2};
     __syncthreads();
     if (w == 0 && lane < M) {
@@ -2502,9 +2578,11 @@ void launch_gemv(const GemmArgs& g, hipStream_t s) {
     const char* f = std::getenv("ATPU_GEMV_PREFETCH");
     return !(f && f[0] == '0');
   }();
-  // not from RowStats GEMVs: their prefetch wave joins the slab barrier, which then waited for
-  // its loads (BART 1-doc A/B: 8.20 -> 7.98 docs/s with it)
-  const bool pf = pf_on && g.pf_w && g.pf_n > 0 && g.pf_k > 0 && !(g.epi & kEpiRowStats);
+  // not from RowStats GEMVs (A/B build ATPU_GEMV_PF_RS=1: their prefetch wave takes the slab
+  // barrier before draining its loads; with __syncthreads it drained them first, BART 1-doc
+  // 8.20 -> 7.98 docs/s): their 32 workgroups would stream the next weight alone, and the
+  // kernel ends only when the prefetch waves do
+  const bool pf = pf_on && g.pf_w && g.pf_n > 0 && g.pf_k > 0 && (ATPU_GEMV_PF_RS || !(g.epi & kEpiRowStats));
   const GemvPf pfa{g.pf_w, g.pf_ld, g.pf_k, g.pf_n, g.pf_rpb > 0 ? g.pf_rpb : 16};
   const bool u6 = gemv_u(g.K) == 6;
 #define ATPU_GEMV_GO(E, UU, P)                                                                                   \

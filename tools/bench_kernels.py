@@ -113,8 +113,8 @@ def main():
                 finally:
                     nat.lm_head_wide(prev)
 
-            extra[name] = {"gemm_only": lambda h=head: h.logits(), "lm128": lambda: with_wide(0),
-                           "lm_wide": lambda: with_wide(1)}
+            extra[name] = {"gemm_only": lambda h=head: h.logits(), "lm128": lambda f=with_wide: f(0),
+                           "lm_wide": lambda f=with_wide: f(1)}
     gam, bet = r(H, dtype=torch.float32), r(H, dtype=torch.float32)
     cases["layernorm"] = (lambda: ops.layernorm(x768, gam, bet, 1e-12),
                           lambda: torch.nn.functional.layer_norm(x768, (H,), gam.bfloat16(), bet.bfloat16(), 1e-12),
