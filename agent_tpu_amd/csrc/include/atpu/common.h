@@ -65,6 +65,73 @@ __device__ __forceinline__ float lane_rows_max(float x) {
   return fmaxf(c, d);
 }
 
+// v_permlane32_swap / v_permlane16_swap of two values (x's upper 32 lanes <-> y's lower 32;
+// x's odd 16-lane rows <-> y's even rows), laundered into early-clobber outputs as above
+__device__ __forceinline__ float2 pl32_swap(float x, float y) {
+  float a, b;
+  asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %3\n\ts_nop 1\n\tv_permlane32_swap_b32 %0, %1"
+               : "=&v"(a), "=&v"(b)
+               : "v"(x), "v"(y));
+  return float2{a, b};
+}
+__device__ __forceinline__ float2 pl16_swap(float x, float y) {
+  float a, b;
+  asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %3\n\ts_nop 1\n\tv_permlane16_swap_b32 %0, %1"
+               : "=&v"(a), "=&v"(b)
+               : "v"(x), "v"(y));
+  return float2{a, b};
+}
+
+// Butterfly all-reduce of N (1..16, a power of two) per-lane values over the wave: every step
+// halves the values (a permlane32 swap pairs i / i + N/2 across the lane halves, a permlane16
+// swap the 16-lane rows, then xor shuffles), the lane bits left over are reduced as a plain
+// xor tree. Lane l ends with the reduction of value l >> (6 - log2 N) (N + 5 - log2 N
+// cross-lane ops instead of 6 N independent wave reductions).
+template <int N, class Op>
+__device__ __forceinline__ float wave_bfly(const float (&v)[N], Op op) {
+  static_assert(N == 1 || N == 2 || N == 4 || N == 8 || N == 16, "wave_bfly: N in 1..16, power of two");
+  const int lane = threadIdx.x & 63;
+  float a[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) a[i] = v[i];
+  if constexpr (N >= 2) {
+#pragma unroll
+    for (int i = 0; i < N / 2; ++i) {
+      const float2 p = pl32_swap(a[i], a[i + N / 2]);
+      a[i] = op(p.x, p.y);
+    }
+  }
+  if constexpr (N >= 4) {
+#pragma unroll
+    for (int i = 0; i < N / 4; ++i) {
+      const float2 p = pl16_swap(a[i], a[i + N / 4]);
+      a[i] = op(p.x, p.y);
+    }
+  }
+  if constexpr (N >= 8) {
+    const bool b = lane & 8;
+#pragma unroll
+    for (int i = 0; i < N / 8; ++i) a[i] = op(b ? a[i + N / 8] : a[i], __shfl_xor(b ? a[i] : a[i + N / 8], 8));
+  }
+  if constexpr (N >= 16) {
+    const bool b = lane & 4;
+    a[0] = op(b ? a[1] : a[0], __shfl_xor(b ? a[0] : a[1], 4));
+  }
+  float x = a[0];
+  if constexpr (N < 2) x = op(x, __shfl_xor(x, 32));
+  if constexpr (N < 4) x = op(x, __shfl_xor(x, 16));
+  if constexpr (N < 8) x = op(x, __shfl_xor(x, 8));
+  if constexpr (N < 16) x = op(x, __shfl_xor(x, 4));
+  x = op(x, __shfl_xor(x, 2));
+  return op(x, __shfl_xor(x, 1));
+}
+struct OpAdd {
+  __device__ float operator()(float a, float b) const { return a + b; }
+};
+struct OpMax {
+  __device__ float operator()(float a, float b) const { return fmaxf(a, b); }
+};
+
 __device__ __forceinline__ double wave_sum_f64(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

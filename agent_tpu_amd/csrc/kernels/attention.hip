@@ -151,8 +151,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(HAS_BI
           cmax = fmaxf(cmax, x);
         }
       }
-      cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
-      cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+      cmax = lane_rows_max(cmax);  // l, l^16, l^32, l^48 by permlane swaps
       const float m_new = fmaxf(m_run, cmax);
       const float alpha = __expf(m_run - m_new);
       float psum = 0.f;
@@ -165,8 +164,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(HAS_BI
           s[kt][r] = p;
           psum += p;
         }
-      psum += __shfl_xor(psum, 16, 64);
-      psum += __shfl_xor(psum, 32, 64);
+      psum = lane_rows_sum(psum);
       l_run = l_run * alpha + psum;
       m_run = m_new;
 #pragma unroll
@@ -341,8 +339,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         cmax = fmaxf(cmax, x);
       }
     }
-    cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
-    cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+    cmax = lane_rows_max(cmax);  // l, l^16, l^32, l^48 by permlane swaps
     const float m_new = fmaxf(m_run, cmax);
     const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
     float psum = 0.f;
@@ -356,8 +353,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         s[kt][r] = p;
         psum += p;
       }
-    psum += __shfl_xor(psum, 16, 64);
-    psum += __shfl_xor(psum, 32, 64);
+    psum = lane_rows_sum(psum);
     l_run = l_run * alpha + psum;
     m_run = m_new;
 #pragma unroll

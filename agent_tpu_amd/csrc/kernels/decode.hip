@@ -44,6 +44,26 @@ constexpr int kMaxKeys = 2048;
 constexpr int kUnrollS = 4;  // 16-key score tiles in flight per wave
 constexpr int kUnrollV = 4;  // 8-key V slabs in flight per wave
 
+// o[8] summed over the 8 key subs (lane bits 3-5) by butterfly: two permlane swaps and one
+// xor-8 shuffle (7 cross-lane ops instead of 24); lane l ends with element l >> 3 of its sum
+__device__ __forceinline__ float wave_bfly_rows8(const float (&o)[8]) {
+  const int lane = threadIdx.x & 63;
+  float a[4], b2[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float2 p = pl32_swap(o[i], o[i + 4]);
+    a[i] = p.x + p.y;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float2 p = pl16_swap(a[i], a[i + 2]);
+    b2[i] = p.x + p.y;
+  }
+  const bool b3 = lane & 8;
+  return (b3 ? b2[1] : b2[0]) + __shfl_xor(b3 ? b2[0] : b2[1], 8);
+}
+
+
 template <int GM, int NW>
 __global__ __launch_bounds__(NW * 64) void decode_attention_kernel(
     const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k, const bf16* __restrict__ v, int ldkv,
@@ -305,16 +325,8 @@ __global__ __launch_bounds__(NW * 64) void decode_self_attention_kernel(
       }
     }
     const float inv = sum > 0.f ? 1.f / sum : 0.f;
-    bf16x8 ov;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float x = o[e];
-      x += __shfl_xor(x, 8);
-      x += __shfl_xor(x, 16);
-      x += __shfl_xor(x, 32);
-      ov[e] = f2bf(x * inv);
-    }
-    if (ksub == 0) *reinterpret_cast<bf16x8*>(out + (size_t)seq * ldo + h * kD + dc) = ov;
+    // key subs reduced by butterfly: lane l holds dim dc + ksub (one 2-B store per lane)
+    out[(size_t)seq * ldo + h * kD + dc + ksub] = f2bf(wave_bfly_rows8(o) * inv);
   }
 }
 
@@ -374,9 +386,13 @@ __global__ __launch_bounds__(64) void decode_cross_split_kernel(
     vv[u] = *reinterpret_cast<const bf16x8*>(v + at(jb + min(u * 8 + ksub, n - 1)) + dc);
   if (qg < G) qsh[qg][qe] = qv;
   __syncthreads();
-  float mxg[GM], smg[GM];
+  // every beam's score first, then ONE butterfly max and ONE butterfly sum over the beams
+  // (wave_bfly: lane l ends with beam l >> kSh) instead of a wave max and sum per beam
+  constexpr int kSh = GM == 1 ? 6 : GM == 4 ? 4 : 3;
+  float sjv[GM];
 #pragma unroll
   for (int g = 0; g < GM; ++g) {
+    sjv[g] = -FLT_MAX;
     if (g < G) {  // G is uniform: no divergence
       float d[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -387,14 +403,18 @@ __global__ __launch_bounds__(64) void decode_cross_split_kernel(
           d[t] = __builtin_amdgcn_fdot2_f32_bf16(bf16x2_t{kk[e][2 * t], kk[e][2 * t + 1]},
                                                  bf16x2_t{qq[2 * t], qq[2 * t + 1]}, d[t], false);
       }
-      const float sj = lane < n ? ((d[0] + d[1]) + (d[2] + d[3])) * scale + bj : -FLT_MAX;
-      const float m = wave_max(sj);
-      const float p = lane < n ? __expf(sj - m) : 0.f;
-      pl[g][lane] = p;
-      mxg[g] = m;
-      smg[g] = wave_sum(p);
+      sjv[g] = lane < n ? ((d[0] + d[1]) + (d[2] + d[3])) * scale + bj : -FLT_MAX;
     }
   }
+  const float mxl = wave_bfly<GM>(sjv, OpMax{});
+  float pv[GM], mxg[GM];
+#pragma unroll
+  for (int g = 0; g < GM; ++g) {
+    mxg[g] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mxl), g << kSh));
+    pv[g] = (g < G && lane < n) ? __expf(sjv[g] - mxg[g]) : 0.f;
+    if (g < G) pl[g][lane] = pv[g];
+  }
+  const float sml = wave_bfly<GM>(pv, OpAdd{});  // beam lane >> kSh
   __syncthreads();
   float o[GM][8];
 #pragma unroll
@@ -417,21 +437,11 @@ __global__ __launch_bounds__(64) void decode_cross_split_kernel(
   for (int g = 0; g < GM; ++g) {
     if (g < G) {
       float* r = rec(g);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float x = o[g][e];
-        x += __shfl_xor(x, 8);
-        x += __shfl_xor(x, 16);
-        x += __shfl_xor(x, 32);
-        o[g][e] = x;
-      }
-      if (ksub == 0) {
-        *reinterpret_cast<float4*>(r + 2 + dc) = make_float4(o[g][0], o[g][1], o[g][2], o[g][3]);
-        *reinterpret_cast<float4*>(r + 2 + dc + 4) = make_float4(o[g][4], o[g][5], o[g][6], o[g][7]);
-      }
-      if (lane == 0) {
+      // the 8 dims over the key subs (lane bits 3-5) by butterfly: lane l ends with dim dc + ksub
+      r[2 + dc + ksub] = wave_bfly_rows8(o[g]);
+      if (lane == (g << kSh)) {
         r[0] = mxg[g];
-        r[1] = smg[g];
+        r[1] = sml;
       }
     }
   }
@@ -456,7 +466,8 @@ __global__ __launch_bounds__(64) void decode_attn_combine_kernel(const float* __
   const float L = wave_sum(w * l);
   float o = 0.f;
 #pragma unroll
-  for (int c = 0; c < kMaxSplits; ++c) o += (c < NS ? __shfl(w, c) : 0.f) * ov[c];
+  for (int c = 0; c < kMaxSplits; ++c)
+    o += (c < NS ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), c)) : 0.f) * ov[c];
   out[(size_t)row * ldo + h * kD + lane] = f2bf(L > 0.f ? o / L : 0.f);
 }
 
@@ -566,16 +577,8 @@ __global__ __launch_bounds__(64) void decode_self_few_kernel(const bf16* __restr
     }
   }
   const float inv = sum > 0.f ? 1.f / sum : 0.f;
-  bf16x8 ov;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    float x = o[e];
-    x += __shfl_xor(x, 8);
-    x += __shfl_xor(x, 16);
-    x += __shfl_xor(x, 32);
-    ov[e] = f2bf(x * inv);
-  }
-  if (ksub == 0) *reinterpret_cast<bf16x8*>(out + (size_t)seq * ldo + h * kD + dc) = ov;
+  // key subs reduced by the row kernel's butterfly (bit-identical to it)
+  out[(size_t)seq * ldo + h * kD + dc + ksub] = f2bf(wave_bfly_rows8(o) * inv);
 }
 
 // ----------------------------------------------------------------------------

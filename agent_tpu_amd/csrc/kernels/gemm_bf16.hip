@@ -2313,24 +2313,6 @@ struct GemvPf {
 #define ATPU_GEMV_PF_RS 0  // L2 prefetch from RowStats GEMVs too
 #endif
 
-// v_permlane32_swap / v_permlane16_swap of two values (x's upper 32 lanes <-> y's lower 32;
-// x's odd 16-lane rows <-> y's even rows), laundered into early-clobber outputs as in
-// lane_rows_sum (common.h)
-__device__ __forceinline__ float2 pl32_swap(float x, float y) {
-  float a, b;
-  asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %3\n\ts_nop 1\n\tv_permlane32_swap_b32 %0, %1"
-               : "=&v"(a), "=&v"(b)
-               : "v"(x), "v"(y));
-  return float2{a, b};
-}
-__device__ __forceinline__ float2 pl16_swap(float x, float y) {
-  float a, b;
-  asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %3\n\ts_nop 1\n\tv_permlane16_swap_b32 %0, %1"
-               : "=&v"(a), "=&v"(b)
-               : "v"(x), "v"(y));
-  return float2{a, b};
-}
-
 template <bool BARRIER>
 __device__ __forceinline__ void gemv_prefetch(const GemvPf& pf, int lane, char* scratch) {
   const int lpr = (pf.k * 2 + 127) / 128;  // 128-B lines per row
@@ -2462,50 +2444,40 @@ __global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __res
       }
     }
   } else {
-    float h8[8], h4[4], h2[2];
+    float a16[16];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float2 p = pl32_swap(acc[i >> 2][i & 3], acc[(i + 8) >> 2][(i + 8) & 3]);
-      h8[i] = p.x + p.y;  // lanes < 32: output i, lanes >= 32: output i + 8
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float2 p = pl16_swap(h8[i], h8[i + 4]);
-      h4[i] = p.x + p.y;  // + 4 on odd 16-lane rows
-    }
-    const bool b3 = lane & 8, b2 = lane & 4;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) h2[i] = (b3 ? h4[i + 2] : h4[i]) + __shfl_xor(b3 ? h4[i] : h4[i + 2], 8);
-    v = (b2 ? h2[1] : h2[0]) + __shfl_xor(b2 ? h2[0] : h2[1], 4);
-    v += __shfl_xor(v, 2);
-    v += __shfl_xor(v, 1);
-    if constexpr (EPI & kEpiRowRms) {
-      float s2[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const float2 p = pl32_swap(ssq[i], ssq[i + 2]);
-        s2[i] = p.x + p.y;
-      }
-      const float2 p = pl16_swap(s2[0], s2[1]);
-      rs = p.x + p.y;  // row (lane >> 4), summed over lanes l, l^16, l^32, l^48
-      rs += __shfl_xor(rs, 8);
-      rs += __shfl_xor(rs, 4);
-      rs += __shfl_xor(rs, 2);
-      rs += __shfl_xor(rs, 1);
-    }
+    for (int i = 0; i < 16; ++i) a16[i] = acc[i >> 2][i & 3];
+    v = wave_bfly<16>(a16, OpAdd{});
+    if constexpr (EPI & kEpiRowRms) rs = wave_bfly<kGemvRows>(ssq, OpAdd{});  // row lane >> 4
   }
   // (rstd, rstd*mu) of A's rows (RowLn) or R's rows (ResLn) from their slab partials
   float2 lnst = float2{1.f, 0.f};
   if constexpr (EPI & (kEpiRowLn | kEpiResLn)) {
     const int slots = (EPI & kEpiRowLn) ? K / 32 : N / 32;
+    const float inv = 1.f / (32 * slots);
+    float S = 0.f, Q = 0.f;
+    if constexpr (!ATPU_GEMV_BFLY) {
 #pragma unroll
-    for (int r = 0; r < kGemvRows; ++r) {
-      const float S = wave_sum(e_part[r].x), Q = wave_sum(e_part[r].y);
-      const float inv = 1.f / (32 * slots);
-      const float mu = S * inv, var = fmaxf(Q * inv - mu * mu, 0.f);
-      const float rr = __builtin_amdgcn_rsqf(var + rms_eps);
-      lnst = mo == r ? float2{rr, rr * mu} : lnst;
+      for (int r = 0; r < kGemvRows; ++r) {
+        const float s0 = wave_sum(e_part[r].x), q0 = wave_sum(e_part[r].y);
+        S = mo == r ? s0 : S;
+        Q = mo == r ? q0 : Q;
+      }
+    } else {
+      // the 8 sums (row r: S = 2r, Q = 2r + 1) by the same butterfly as the outputs: lane l
+      // ends with sum l >> 3, i.e. row l >> 4 (= mo), its partner lane l ^ 8 the other one
+      float a8[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a8[i] = i & 1 ? e_part[i >> 1].y : e_part[i >> 1].x;
+      const float h = wave_bfly<8>(a8, OpAdd{});
+      const float o = __shfl_xor(h, 8);
+      const bool b3 = lane & 8;
+      S = b3 ? o : h;
+      Q = b3 ? h : o;
     }
+    const float mu = S * inv, var = fmaxf(Q * inv - mu * mu, 0.f);
+    const float rr = __builtin_amdgcn_rsqf(var + rms_eps);
+    lnst = float2{rr, rr * mu};
   }
   if constexpr (!kEarly) epi_loads();
   float f = 0.f;  // RowStats: the stored (bf16-rounded) value
