@@ -28,16 +28,35 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds) {
 
 __device__ __forceinline__ void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// DPP lane permutations inside a 16-lane row, VALU only (no ds_bpermute round trip through
+// the LDS crossbar, which is what __shfl_xor compiles to): row_mirror pairs lane l with
+// l ^ 15, row_half_mirror with l ^ 7, the quad perms with l ^ 2 and l ^ 1. The masks
+// 15, 7, 2, 1 span the 4 row bits, so a butterfly over them reduces all 16 lanes.
+template <int CTRL>
+__device__ __forceinline__ float dppf(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+constexpr int kDppMirror = 0x140, kDppHalfMirror = 0x141, kDppXor2 = 0x4E, kDppXor1 = 0xB1;
+
+__device__ __forceinline__ float lane_rows_sum(float x);
+__device__ __forceinline__ float lane_rows_max(float x);
+
+// whole-wave reductions: the 4 lane rows by permlane swaps (lane_rows_*), then the 16 lanes
+// of a row by DPP; every lane gets the result
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v = lane_rows_sum(v);
+  v += dppf<kDppMirror>(v);
+  v += dppf<kDppHalfMirror>(v);
+  v += dppf<kDppXor2>(v);
+  return v + dppf<kDppXor1>(v);
 }
 
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = lane_rows_max(v);
+  v = fmaxf(v, dppf<kDppMirror>(v));
+  v = fmaxf(v, dppf<kDppHalfMirror>(v));
+  v = fmaxf(v, dppf<kDppXor2>(v));
+  return fmaxf(v, dppf<kDppXor1>(v));
 }
 
 // Reductions over the 4 lanes l, l^16, l^32, l^48 (the 4 lane rows holding one
@@ -82,6 +101,22 @@ __device__ __forceinline__ float2 pl16_swap(float x, float y) {
   return float2{a, b};
 }
 
+// the value of lane l ^ 16 / l ^ 32 (exact partner, by one permlane swap and a select)
+__device__ __forceinline__ float xor16f(float x) {
+  const float2 p = pl16_swap(x, x);
+  return (threadIdx.x & 16) ? p.x : p.y;
+}
+__device__ __forceinline__ float xor32f(float x) {
+  const float2 p = pl32_swap(x, x);
+  return (threadIdx.x & 32) ? p.x : p.y;
+}
+__device__ __forceinline__ int xor16i(int x) { return __float_as_int(xor16f(__int_as_float(x))); }
+__device__ __forceinline__ int xor32i(int x) { return __float_as_int(xor32f(__int_as_float(x))); }
+template <int CTRL>
+__device__ __forceinline__ int dppi(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false);
+}
+
 // Butterfly all-reduce of N (1..16, a power of two) per-lane values over the wave: every step
 // halves the values (a permlane32 swap pairs i / i + N/2 across the lane halves, a permlane16
 // swap the 16-lane rows, then xor shuffles), the lane bits left over are reduced as a plain
@@ -108,22 +143,30 @@ __device__ __forceinline__ float wave_bfly(const float (&v)[N], Op op) {
       a[i] = op(p.x, p.y);
     }
   }
+  // inside the 16-lane rows by DPP: partners l ^ 15 (splitting on bit 3), l ^ 7 (bit 2), then
+  // l ^ 2, l ^ 1; each splitting partner has the other value of the bit, and the rest share it
   if constexpr (N >= 8) {
     const bool b = lane & 8;
 #pragma unroll
-    for (int i = 0; i < N / 8; ++i) a[i] = op(b ? a[i + N / 8] : a[i], __shfl_xor(b ? a[i] : a[i + N / 8], 8));
+    for (int i = 0; i < N / 8; ++i) a[i] = op(b ? a[i + N / 8] : a[i], dppf<kDppMirror>(b ? a[i] : a[i + N / 8]));
   }
   if constexpr (N >= 16) {
     const bool b = lane & 4;
-    a[0] = op(b ? a[1] : a[0], __shfl_xor(b ? a[0] : a[1], 4));
+    a[0] = op(b ? a[1] : a[0], dppf<kDppHalfMirror>(b ? a[0] : a[1]));
   }
   float x = a[0];
-  if constexpr (N < 2) x = op(x, __shfl_xor(x, 32));
-  if constexpr (N < 4) x = op(x, __shfl_xor(x, 16));
-  if constexpr (N < 8) x = op(x, __shfl_xor(x, 8));
-  if constexpr (N < 16) x = op(x, __shfl_xor(x, 4));
-  x = op(x, __shfl_xor(x, 2));
-  return op(x, __shfl_xor(x, 1));
+  if constexpr (N < 2) {
+    const float2 p = pl32_swap(x, x);
+    x = op(p.x, p.y);
+  }
+  if constexpr (N < 4) {
+    const float2 p = pl16_swap(x, x);
+    x = op(p.x, p.y);
+  }
+  if constexpr (N < 8) x = op(x, dppf<kDppMirror>(x));
+  if constexpr (N < 16) x = op(x, dppf<kDppHalfMirror>(x));
+  x = op(x, dppf<kDppXor2>(x));
+  return op(x, dppf<kDppXor1>(x));
 }
 struct OpAdd {
   __device__ float operator()(float a, float b) const { return a + b; }

@@ -38,12 +38,20 @@ __device__ __forceinline__ void wave_topk(float (&tv)[KM], int (&ti)[KM], float&
   for (int r = 0; r < KM; ++r) {
     float bv = tv[0];
     int bi = ti[0];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const float ov = __shfl_xor(bv, off);
-      const int oi = __shfl_xor(bi, off);
-      if (better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
-    }
+    // partners l ^ 32, l ^ 16 by permlane swaps, then the 16-lane row by DPP (l ^ 15, l ^ 7,
+    // l ^ 2, l ^ 1): register and VALU only, no ds_bpermute round trips
+    auto step = [&](float ov, int oi) {
+      if (better(ov, oi, bv, bi)) {
+        bv = ov;
+        bi = oi;
+      }
+    };
+    step(xor32f(bv), xor32i(bi));
+    step(xor16f(bv), xor16i(bi));
+    step(dppf<kDppMirror>(bv), dppi<kDppMirror>(bi));
+    step(dppf<kDppHalfMirror>(bv), dppi<kDppHalfMirror>(bi));
+    step(dppf<kDppXor2>(bv), dppi<kDppXor2>(bi));
+    step(dppf<kDppXor1>(bv), dppi<kDppXor1>(bi));
     if (lane == r) { res_v = bv; res_i = bi; }
     if (ti[0] == bi && tv[0] == bv && bi != 0x7fffffff) {  // owner pops its head
 #pragma unroll
@@ -88,7 +96,7 @@ __device__ __forceinline__ float row_kth8(const float (&t)[4]) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     u[k] = t[k];
-    u[7 - k] = __shfl_xor(t[k], 16);  // partner's list reversed: u is bitonic
+    u[7 - k] = xor16f(t[k]);  // partner's list reversed: u is bitonic
   }
 #pragma unroll
   for (int st = 4; st > 0; st >>= 1)
@@ -97,7 +105,7 @@ __device__ __forceinline__ float row_kth8(const float (&t)[4]) {
       if ((i & st) == 0) ce_desc(u[i], u[i + st]);
   float q[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) q[k] = __shfl_xor(u[k], 32);
+  for (int k = 0; k < 8; ++k) q[k] = xor32f(u[k]);
   // 8th largest of two sorted 8-lists: max_i min(u_i, q_{8-i}), u_0 = q_0 = +inf
   float L = fmaxf(u[7], q[7]);
 #pragma unroll
@@ -124,7 +132,7 @@ __device__ __forceinline__ void tile_row_emit(const float (&sel)[J][4], int c0, 
   for (int j = 0; j < J; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) cnt += (sel[j][e] >= L && sel[j][e] > -FLT_MAX) ? 1 : 0;
-  const int x1 = __shfl_xor(cnt, 16), x2 = __shfl_xor(cnt, 32), x3 = __shfl_xor(cnt, 48);
+  const int x1 = xor16i(cnt), x2 = xor32i(cnt), x3 = xor32i(x1);  // lanes l ^ 16, l ^ 32, l ^ 48
   int total = cnt + x1 + x2 + x3;
   const int pre = ((fc & 1) ? x1 : 0) + ((fc & 2) ? x2 + x3 : 0);  // lanes of lower fc first
   if (__ballot(live && total > kTileCand) == 0) {
@@ -156,10 +164,17 @@ __device__ __forceinline__ void tile_row_emit(const float (&sel)[J][4], int c0, 
             bi = id;
           }
         }
-#pragma unroll
-      for (int off = 16; off <= 32; off <<= 1) {
-        const float ov = __shfl_xor(bv, off);
-        const int oi = __shfl_xor(bi, off);
+      {
+        const float ov = xor16f(bv);
+        const int oi = xor16i(bi);
+        if (better(ov, oi, bv, bi)) {
+          bv = ov;
+          bi = oi;
+        }
+      }
+      {
+        const float ov = xor32f(bv);
+        const int oi = xor32i(bi);
         if (better(ov, oi, bv, bi)) {
           bv = ov;
           bi = oi;

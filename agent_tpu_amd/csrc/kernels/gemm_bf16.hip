@@ -2470,7 +2470,7 @@ __global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __res
 #pragma unroll
       for (int i = 0; i < 8; ++i) a8[i] = i & 1 ? e_part[i >> 1].y : e_part[i >> 1].x;
       const float h = wave_bfly<8>(a8, OpAdd{});
-      const float o = __shfl_xor(h, 8);
+      const float o = dppf<kDppMirror>(h);  // a lane of the other bit-3 half of the row
       const bool b3 = lane & 8;
       S = b3 ? o : h;
       Q = b3 ? h : o;
