@@ -142,8 +142,7 @@ __global__ __launch_bounds__(NW * 64) void decode_attention_kernel(
       }
     }
   }
-  mxl = fmaxf(mxl, __shfl_xor(mxl, 16));
-  mxl = fmaxf(mxl, __shfl_xor(mxl, 32));
+  mxl = lane_rows_max(mxl);  // lanes l, l^16, l^32, l^48 by permlane swaps
   if (lane < 16) red[w][lane] = mxl;
   __syncthreads();
   // ---- P·V operands: lane = (key sub 0..7, dims (lane&7)*8 .. +8) ----
@@ -209,23 +208,10 @@ __global__ __launch_bounds__(NW * 64) void decode_attention_kernel(
       }
     }
   }
-  // reduce the 8 key-subgroups of the wave (lanes with equal lane&7)
+  // reduce the 8 key-subgroups of the wave (lanes with equal lane&7) by butterfly: lane l
+  // keeps dimension dc + ksub of each beam
 #pragma unroll
-  for (int g = 0; g < GM; ++g)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float x = o[g][e];
-      x += __shfl_xor(x, 8);
-      x += __shfl_xor(x, 16);
-      x += __shfl_xor(x, 32);
-      o[g][e] = x;
-    }
-  if (ksub == 0) {
-#pragma unroll
-    for (int g = 0; g < GM; ++g)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) po[w][g][dc + e] = o[g][e];
-  }
+  for (int g = 0; g < GM; ++g) po[w][g][dc + ksub] = wave_bfly_rows8(o[g]);
   __syncthreads();
   for (int i = tid; i < G * kD; i += NW * 64) {
     const int g = i / kD, d = i % kD;
@@ -889,7 +875,7 @@ __global__ __launch_bounds__(kTopkThreads) void beam_topk_kernel(const float* __
     wave_topk<KM>(tv, ti, rv, ri);
     __builtin_amdgcn_wave_barrier();
     if (lane < K) { bv[lane] = rv; bi[lane] = ri; }
-    thr = fmaxf(thr, __shfl(rv, K - 1, 64));
+    thr = fmaxf(thr, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rv), K - 1)));
     cnt = K;
     __builtin_amdgcn_wave_barrier();
   };
