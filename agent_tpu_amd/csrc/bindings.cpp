@@ -18,6 +18,7 @@
 #include "atpu/common.h"
 #include "atpu/csv.h"
 #include "atpu/kernels.h"
+#include "atpu/l2_prefetch.h"
 #include "atpu/risk_stream.h"
 #include "atpu/runtime.h"
 
@@ -175,13 +176,16 @@ PYBIND11_MODULE(_atpu, m) {
   m.def("decode_attention", [](uintptr_t q, int ldq, uintptr_t k, uintptr_t v, int ldkv, int seq_stride, int group,
                                uintptr_t lens, uintptr_t step_dev, uintptr_t hist, int hist_stride, uintptr_t bias,
                                int bias_stride, uintptr_t out, int ldo, int rows, int H, float scale, uintptr_t stream,
-                               uintptr_t ws) {
+                               uintptr_t ws, uintptr_t pf_w, int pf_ld, int pf_k, int pf_n, int pf_rpb) {
+    const L2Pf pf{P<const bf16>(pf_w), pf_ld, pf_k, pf_n, pf_rpb > 0 ? pf_rpb : 16};
     decode_attention(P<const bf16>(q), ldq, P<const bf16>(k), P<const bf16>(v), ldkv, seq_stride, group,
                      P<const int32_t>(lens), P<const int32_t>(step_dev), P<const int32_t>(hist), hist_stride,
-                     P<const float>(bias), bias_stride, P<bf16>(out), ldo, rows, H, scale, S(stream), P<float>(ws));
+                     P<const float>(bias), bias_stride, P<bf16>(out), ldo, rows, H, scale, S(stream), P<float>(ws),
+                     pf_w ? &pf : nullptr);
   }, py::arg("q"), py::arg("ldq"), py::arg("k"), py::arg("v"), py::arg("ldkv"), py::arg("seq_stride"), py::arg("group"),
      py::arg("lens"), py::arg("step_dev"), py::arg("hist"), py::arg("hist_stride"), py::arg("bias"), py::arg("bias_stride"),
-     py::arg("out"), py::arg("ldo"), py::arg("rows"), py::arg("H"), py::arg("scale"), py::arg("stream"), py::arg("ws") = 0);
+     py::arg("out"), py::arg("ldo"), py::arg("rows"), py::arg("H"), py::arg("scale"), py::arg("stream"), py::arg("ws") = 0,
+     py::arg("pf_w") = 0, py::arg("pf_ld") = 0, py::arg("pf_k") = 0, py::arg("pf_n") = 0, py::arg("pf_rpb") = 16);
   m.def("decode_attention_ws_floats", [](int rows, int group, int H, int seq_stride, bool cross) {
     return decode_attention_ws_floats(rows, group, H, seq_stride, cross);
   });

@@ -106,10 +106,11 @@ int64_t make_cu_mask_stream(int first_bit, int nbits);  // hipStream_t over CU-m
 // of row r lives in physical row hist[r * hist_stride + j] when hist is given
 // (beam backpointers), else in row r. bias_dist (fp32 [H, bias_stride]) adds
 // bias_dist[h][len-1-j] (T5 decoder relative position bias).
+struct L2Pf;  // l2_prefetch.h: a later kernel's weight rows to pull into L2 (split cross attention only)
 void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int ldkv, int seq_stride, int group,
                       const int32_t* lens, const int32_t* step_dev, const int32_t* hist, int hist_stride,
                       const float* bias_dist, int bias_stride, bf16* out, int ldo, int rows, int H, float scale,
-                      hipStream_t stream, float* ws = nullptr);
+                      hipStream_t stream, float* ws = nullptr, const L2Pf* pf = nullptr);
 // Cross attention (lens) over a grid of few items splits the keys into 64-key chunks
 // (flash decoding) when given a workspace of this many floats (0: no split for the shape).
 int decode_attention_splits(int rows, int group, int H, int seq_stride, bool cross);

@@ -25,6 +25,7 @@
 //    blocks that share an A panel run on one XCD and hit its L2.
 #include "atpu/common.h"
 #include "atpu/kernels.h"
+#include "atpu/l2_prefetch.h"
 
 #include <hip/hip_ext.h>
 
@@ -2290,18 +2291,9 @@ constexpr int kGemvRows = 4;
 // tools/probe_gemv_l2.py)
 constexpr int gemv_u(int K) { return K <= 64 * 8 * 3 ? 3 : 6; }
 
-// Prefetch of the next GEMV's weight (PF): one extra wave per workgroup issues a dword load per
-// 128-B line of the rows the NEXT kernel's workgroups b' = blockIdx.x + k * gridDim.x will read
-// (16 rows each), waits for them and exits; the compute waves never wait for it. Workgroups are
-// dealt to the XCDs round robin, so with gridDim.x % 8 == 0 the lines land in the L2 of the XCD
-// whose workgroup reads them next (a speed-only assumption: a different placement only loses
-// the L2 hit). A 4-row GEMV on L2-resident weights ran 3.6-4.5 us against 4.9-7.5 us from HBM.
-struct GemvPf {
-  const bf16* w;
-  int ld, k, n, rpb;  // rpb: weight rows per workgroup of the next kernel (16, or 32 for RowStats)
-};
-// The loads are 4-byte LDS-DMAs into a 256-B scratch nobody reads: a VGPR-destination load
-// issued from inline asm would let the compiler reuse its register before the data returns.
+// Prefetch of the next GEMV's weight (PF): one extra wave per workgroup (l2_prefetch.h). A 4-row
+// GEMV on L2-resident weights ran 3.6-4.5 us against 4.9-7.5 us from HBM.
+using GemvPf = L2Pf;
 // A/B build switches (python -m agent_tpu_amd.csrc.build -D NAME=V --out ...)
 #ifndef ATPU_GEMV_BFLY
 #define ATPU_GEMV_BFLY 1  // butterfly reduction of the GEMV partials (0: 16 wave sums)
@@ -2312,26 +2304,6 @@ struct GemvPf {
 #ifndef ATPU_GEMV_PF_RS
 #define ATPU_GEMV_PF_RS 0  // L2 prefetch from RowStats GEMVs too
 #endif
-
-template <bool BARRIER>
-__device__ __forceinline__ void gemv_prefetch(const GemvPf& pf, int lane, char* scratch) {
-  const int lpr = (pf.k * 2 + 127) / 128;  // 128-B lines per row
-  const int blocks = (pf.n + pf.rpb - 1) / pf.rpb;
-  for (int bb = blockIdx.x; bb < blocks; bb += gridDim.x) {
-    const int r0 = bb * pf.rpb, nl = min(pf.rpb, pf.n - r0) * lpr;
-    for (int i0 = 0; i0 < nl; i0 += 64) {  // wave-uniform trip count: every lane issues the DMA
-      const int i = min(i0 + lane, nl - 1);
-      const int r = r0 + i / lpr, l = i - (i / lpr) * lpr;
-      const char* p = reinterpret_cast<const char*>(pf.w + (size_t)r * pf.ld) + l * 128;
-      __builtin_amdgcn_global_load_lds((const ATPU_GLOBAL_AS void*)p, (ATPU_LDS_AS void*)scratch, 4, 0, 0);
-    }
-  }
-  // RowStats workgroups: the wave's share of the slab barrier, taken with its loads still in
-  // flight (a raw s_barrier; __syncthreads would drain them first and hold the compute waves,
-  // which measured slower than no prefetch), then the drain before the wave ends
-  if constexpr (BARRIER) asm volatile("s_barrier" ::: "memory");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
 
 // BART's LayerNorm folding (RowLn / ResLn / RowStats, see LnDec): the row statistics come
 // from the <= 32 slab partials (lane = slab, wave sums); RowStats workgroups are 8 waves =
@@ -2350,7 +2322,8 @@ __global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __res
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if constexpr (PF) {
     if (w == NWV) {
-      gemv_prefetch<(EPI & kEpiRowStats) != 0>(pf, lane, pf_scratch);
+      // RowStats workgroups have one barrier (the slab sum), taken with the loads in flight
+      l2_prefetch_rows<(EPI & kEpiRowStats) != 0 ? 1 : 0>(pf, lane, pf_scratch, blockIdx.x, gridDim.x);
       return;
     }
   }

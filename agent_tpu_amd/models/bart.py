@@ -314,7 +314,10 @@ class BartModel:
                 qkv = ops.linear(x, w, b, row_ln=rl, prefetch=(p[q + "o_w"], 32))
                 ops.kv_append(qkv, d, 2 * d, c, T, step)
                 qh = qkv[:, :d]
-            ctx = ops.decode_attention(qh, c[:, :d], c[:, d:], H, T, 1, step=step, scale=scale, hist=hist)
+            # the cross query projection's weight: its predecessor (the RowStats o GEMV) does not
+            # prefetch, the self attention before it does
+            ctx = ops.decode_attention(qh, c[:, :d], c[:, d:], H, T, 1, step=step, scale=scale, hist=hist,
+                                       prefetch=f[q + "cq_w"])
             if i == 0:
                 x1 = ops.linear(ctx, p[q + "o_w"], p[q + "o_b"], residual=x, stats_out=p1, prefetch=f[q + "cq_w"])
             else:
@@ -323,7 +326,10 @@ class BartModel:
             cq = ops.linear(x1, f[q + "cq_w"], f[q + "cq_b"], row_ln=(eps, f[q + "cq_c"], p1),
                             prefetch=(p[q + "co_w"], 32))
             kv = ckv[:, i * 2 * d:(i + 1) * 2 * d]
-            ctx = ops.decode_attention(cq, kv[:, :d], kv[:, d:], H, S, group, lens=src_lens, scale=scale)
+            # fc1's weight: its predecessor (the RowStats co GEMV) does not prefetch, the split
+            # cross attention two kernels earlier does
+            ctx = ops.decode_attention(cq, kv[:, :d], kv[:, d:], H, S, group, lens=src_lens, scale=scale,
+                                       prefetch=f[q + "f1_w"])
             x2 = ops.linear(ctx, p[q + "co_w"], f[q + "co_b"], residual=x1, res_ln=(eps, p1, p[q + "ln1_g"]),
                             stats_out=p2, prefetch=f[q + "f1_w"])
             h = ops.linear(x2, f[q + "f1_w"], f[q + "f1_b"], act="gelu", row_ln=(eps, f[q + "f1_c"], p2),

@@ -30,11 +30,15 @@ HEAD_DIM = 64
 def decode_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, H: int, seq_stride: int, group: int = 1,
                      lens: Optional[torch.Tensor] = None, step: Optional[torch.Tensor] = None,
                      bias_dist: Optional[torch.Tensor] = None, scale: float = 1.0,
-                     out: Optional[torch.Tensor] = None, hist: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     out: Optional[torch.Tensor] = None, hist: Optional[torch.Tensor] = None,
+                     prefetch: Optional[torch.Tensor] = None) -> torch.Tensor:
     """q [R, >=H*64]; k/v 2-D row views with ``seq_stride`` rows per sequence.
 
     ``hist`` (int32 [R, T], self attention only): key j < t of row r lives in
     the cache of row ``hist[r, j]``.
+    ``prefetch``: the weight of a later <= 4-row decode GEMV (16 rows per workgroup); the few-item
+    split cross attention and few-row self attention pull it into L2 with a second wave per
+    workgroup (a hint only; the other kernels ignore it).
     """
     R = q.shape[0]
     if not q.is_cuda:
@@ -54,10 +58,13 @@ def decode_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, H: int, 
     # captured decoder step it comes from the graph's pool)
     nws = native().decode_attention_ws_floats(R, group, H, seq_stride, lens is not None and hist is None)
     ws = torch.empty(nws, dtype=torch.float32, device=q.device) if nws else None
+    pf_args = (0, 0, 0, 0, 16)
+    if prefetch is not None and prefetch.is_cuda and prefetch.dim() == 2 and prefetch.stride(1) == 1:
+        pf_args = (ptr(prefetch), prefetch.stride(0), prefetch.shape[1], prefetch.shape[0], 16)
     native().decode_attention(ptr(q), row_stride(q, "q"), ptr(k), ptr(v), row_stride(k, "k"), seq_stride, group,
                               ptr(lens), ptr(step), ptr(hist), 0 if hist is None else hist.shape[1], ptr(bias_dist),
                               0 if bias_dist is None else bias_dist.shape[1], ptr(out), row_stride(out, "out"), R, H,
-                              float(scale), launch_stream(q), ptr(ws))
+                              float(scale), launch_stream(q), ptr(ws), *pf_args)
     return out
 
 
