@@ -241,6 +241,7 @@ PYBIND11_MODULE(_atpu, m) {
   m.def("lm_head_wide", &lm_head_wide, py::arg("set") = -1);
   m.def("decode_cross_wg", &decode_cross_wg, py::arg("set") = -1);
   m.def("decode_self_few", &decode_self_few, py::arg("set") = -1);
+  m.def("decode_xattn_prefetch", &decode_xattn_prefetch, py::arg("set") = -1);
   m.def(
       "lm_head_topk",
       [](uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t bias, float rms_eps, int M, int V, int K, int topk,

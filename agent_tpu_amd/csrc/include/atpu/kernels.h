@@ -116,6 +116,7 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
 int decode_attention_splits(int rows, int group, int H, int seq_stride, bool cross);
 size_t decode_attention_ws_floats(int rows, int group, int H, int seq_stride, bool cross);
 int decode_self_few(int set);  // 1: few-row self attention one wave per (row, head), T <= 192 (default); -1 reads
+int decode_xattn_prefetch(int set);  // 1: few-item attention kernels prefetch a later GEMV weight (default 0); -1 reads
 int decode_cross_wg(int set);  // 1: few-item cross attention in one workgroup per (item, head) (default 0: slower); -1 reads
 // one-workgroup state advance of a small beam search (rows x stride x 4 B x (seq ? 2 : 1) <= 64 KiB):
 // hist / seq reordered in place by par (as beam_reorder_hist, seq with last = tok, off 1),

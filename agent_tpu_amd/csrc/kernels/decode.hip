@@ -1139,13 +1139,15 @@ __global__ __launch_bounds__(kSelMax) void beam_select_kernel(const float* __res
 // L2 prefetch of a later GEMV's weight from the few-item attention kernels (BART's fc1 and cross
 // query weights, whose predecessors are RowStats GEMVs). Measured within noise (1-doc BART
 // 10.49 vs 10.47 docs/s, profiles/xattn_prefetch_ab_r04.txt): off unless ATPU_XATTN_PREFETCH=1
-static bool xattn_prefetch() {
-  static const bool on = [] {
+int decode_xattn_prefetch(int set) {
+  static int on = [] {
     const char* f = std::getenv("ATPU_XATTN_PREFETCH");
-    return f && f[0] == '1';
+    return (f && f[0] == '1') ? 1 : 0;
   }();
+  if (set == 0 || set == 1) on = set;
   return on;
 }
+static bool xattn_prefetch() { return decode_xattn_prefetch(-1) != 0; }
 
 int decode_self_few(int set) {
   // few-row self attention: one wave per (row, head), all loads in two rounds
