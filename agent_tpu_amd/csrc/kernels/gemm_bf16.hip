@@ -2299,7 +2299,8 @@ using GemvPf = L2Pf;
 #define ATPU_GEMV_BFLY 1  // butterfly reduction of the GEMV partials (0: 16 wave sums)
 #endif
 #ifndef ATPU_GEMV_EARLY
-#define ATPU_GEMV_EARLY 1  // epilogue operands loaded before the main loop: 0 never, 1 LN-folded, 2 all
+#define ATPU_GEMV_EARLY 1  // epilogue operands loaded before the main loop: 0 never, 1 LN-folded, 2 all,
+                           // 3 LN-folded before, the rest right after the first round's loads
 #endif
 #ifndef ATPU_GEMV_PF_RS
 #define ATPU_GEMV_PF_RS 0  // L2 prefetch from RowStats GEMVs too
@@ -2335,7 +2336,11 @@ __global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __res
   // after the reductions: BART 1-doc 8.5 -> 8.8 docs/s; for the T5 epilogues (RowRms, ReLU,
   // residual, KV scatter) the same early loads measured slower (12.3 -> 11.7), so those load
   // in the epilogue (profiles/summarize_1doc_gemv_early_loads_r04.txt)
-  constexpr bool kEarly = ATPU_GEMV_EARLY == 2 || (ATPU_GEMV_EARLY == 1 && (EPI & (kEpiRowLn | kEpiResLn)) != 0);
+  constexpr bool kLn = (EPI & (kEpiRowLn | kEpiResLn)) != 0;
+  constexpr bool kEarly = ATPU_GEMV_EARLY == 2 || ((ATPU_GEMV_EARLY == 1 || ATPU_GEMV_EARLY == 3) && kLn);
+  // ATPU_GEMV_EARLY == 3: the other epilogues load theirs right after the first round's weight
+  // and A loads (younger than them, so the main loop's counted waits do not wait for them)
+  constexpr bool kMid = ATPU_GEMV_EARLY == 3 && !kLn;
   const int mo = lane >> 4, jo = (lane >> 2) & 3;  // the reduction's output lanes (below)
   const bool mine = mo < M && (lane & 3) == 0;
   const int om = min(mo, M - 1), n = n0 + jo;  // (clamped) output row
@@ -2376,6 +2381,9 @@ __global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __res
 #pragma unroll
       for (int m = 0; m < kGemvRows; ++m)
         av[u][m] = *reinterpret_cast<const bf16x8*>(A + (size_t)min(m, M - 1) * lda + c * 8);
+    }
+    if constexpr (kMid) {
+      if (base == 0) epi_loads();
     }
     // every load of the round is issued before the first use: left alone, the scheduler issued
     // them in groups of 8 with a full wait in between (U serialised memory latencies)
@@ -2452,7 +2460,7 @@ __global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __res
     const float rr = __builtin_amdgcn_rsqf(var + rms_eps);
     lnst = float2{rr, rr * mu};
   }
-  if constexpr (!kEarly) epi_loads();
+  if constexpr (!kEarly && !kMid) epi_loads();
   float f = 0.f;  // RowStats: the stored (bf16-rounded) value
   if (mine) {
     if constexpr (EPI & kEpiRowRms) v *= __builtin_amdgcn_rsqf(rs * (1.f / K) + rms_eps);
