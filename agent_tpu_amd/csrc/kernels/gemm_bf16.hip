@@ -82,6 +82,15 @@ __device__ __forceinline__ float sumsq_bf16x8(bf16x8 a, float acc) {
   }
   return acc;
 }
+// sum of the 8 values of a 16-B chunk (fdot2 against ones), fp32
+__device__ __forceinline__ float sum_bf16x8(bf16x8 a, float acc) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  const bf16x2_t one = bf16x2_t{(__bf16)1.0f, (__bf16)1.0f};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_fdot2_f32_bf16(bf16x2_t{a[2 * e], a[2 * e + 1]}, one, acc, false);
+  return acc;
+}
+
 
 // Decode LayerNorm folding (kEpiRowLn / kEpiResLn / kEpiRowStats; GemmArgs fields of the
 // same names). A row's statistics travel as partial (sum, sumsq) per 32-column slab, written
@@ -2355,13 +2364,17 @@ __global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __res
     if constexpr (EPI & kEpiKvScatter) e_step = *kvo.step;
   };
   if constexpr (kEarly) epi_loads();
+  // (sum, sum of squares) per row, lane-partial: RowLn takes its A rows' statistics from the A
+  // chunks it loads anyway (the whole row: K is the LN width), so it needs no producer partials;
+  // ResLn reads the slab partials of its residual rows
   float2 e_part[kGemvRows];
-  if constexpr (EPI & (kEpiRowLn | kEpiResLn)) {
-    const int slots = (EPI & kEpiRowLn) ? K / 32 : N / 32;
-    const float* part = (EPI & kEpiRowLn) ? ln.in_part : ln.res_part;
+#pragma unroll
+  for (int r = 0; r < kGemvRows; ++r) e_part[r] = float2{0.f, 0.f};
+  if constexpr ((EPI & kEpiResLn) && !(EPI & kEpiRowLn)) {
+    const int slots = N / 32;
 #pragma unroll
     for (int r = 0; r < kGemvRows; ++r)
-      e_part[r] = lane < slots ? *reinterpret_cast<const float2*>(part + 2 * ((size_t)lane * M + min(r, M - 1)))
+      e_part[r] = lane < slots ? *reinterpret_cast<const float2*>(ln.res_part + 2 * ((size_t)lane * M + min(r, M - 1)))
                                : float2{0.f, 0.f};
   }
   float acc[kGemvRows][4], ssq[kGemvRows];
@@ -2403,6 +2416,10 @@ __global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __res
           acc[m][j] += ok ? d : 0.f;
         }
         if constexpr (EPI & kEpiRowRms) ssq[m] += ok ? sumsq_bf16x8(av[u][m], 0.f) : 0.f;
+        if constexpr (EPI & kEpiRowLn) {
+          e_part[m].x += ok ? sum_bf16x8(av[u][m], 0.f) : 0.f;
+          e_part[m].y += ok ? sumsq_bf16x8(av[u][m], 0.f) : 0.f;
+        }
       }
     }
   }
@@ -2434,8 +2451,7 @@ __global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __res
   // (rstd, rstd*mu) of A's rows (RowLn) or R's rows (ResLn) from their slab partials
   float2 lnst = float2{1.f, 0.f};
   if constexpr (EPI & (kEpiRowLn | kEpiResLn)) {
-    const int slots = (EPI & kEpiRowLn) ? K / 32 : N / 32;
-    const float inv = 1.f / (32 * slots);
+    const float inv = 1.f / ((EPI & kEpiRowLn) ? K : N);
     float S = 0.f, Q = 0.f;
     if constexpr (!ATPU_GEMV_BFLY) {
 #pragma unroll
@@ -2459,6 +2475,26 @@ __global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __res
     const float mu = S * inv, var = fmaxf(Q * inv - mu * mu, 0.f);
     const float rr = __builtin_amdgcn_rsqf(var + rms_eps);
     lnst = float2{rr, rr * mu};
+    if constexpr (EPI & kEpiRowLn) {
+      // part_out (optional): A's rows in the [K/32][M][2] partial format of a RowStats producer,
+      // the row totals in slot 0 and zeros elsewhere, for the ResLn GEMV that adds LN(A) as its
+      // residual (workgroup 0, wave 0; lanes 16 r hold row r)
+      if (ln.part_out && blockIdx.x == 0 && w == 0) {
+        const int slots = K / 32;
+        float2 tot[kGemvRows];
+#pragma unroll
+        for (int r = 0; r < kGemvRows; ++r)
+          tot[r] = float2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(S), 16 * r)),
+                          __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Q), 16 * r))};
+        for (int i = lane; i < slots * M; i += 64) {
+          const int sl = i / M, r = i - sl * M;
+          float2 val = float2{0.f, 0.f};
+#pragma unroll
+          for (int rr2 = 0; rr2 < kGemvRows; ++rr2) val = (sl == 0 && r == rr2) ? tot[rr2] : val;
+          *reinterpret_cast<float2*>(ln.part_out + 2 * (size_t)i) = val;
+        }
+      }
+    }
   }
   if constexpr (!kEarly && !kMid) epi_loads();
   float f = 0.f;  // RowStats: the stored (bf16-rounded) value
@@ -2521,7 +2557,8 @@ void launch_gemv(const GemmArgs& g, hipStream_t s) {
     ATPU_CHECK(g.kv_cache && g.kv_step && g.kv_T > 0 && g.kv_col0 > 0 && g.kv_col0 < g.N && g.kv_ld >= g.N - g.kv_col0,
                "gemm: KvScatter needs a cache, a device step and kv_ld >= N - kv_col0");
   ATPU_CHECK(!(g.epi & (kEpiRowRms | kEpiRowLn | kEpiResLn)) || g.rms_eps > 0.f, "gemm: RowRms / RowLn / ResLn need eps > 0");
-  ATPU_CHECK(!(g.epi & kEpiRowLn) || (g.colsum && g.in_part && g.K <= 1024), "gemm: RowLn needs colsum, in_part, K <= 1024");
+  // RowLn: the statistics come from A itself (in_part unused); part_out, if given, receives them
+  ATPU_CHECK(!(g.epi & kEpiRowLn) || (g.colsum && g.K <= 1024 && g.K % 32 == 0), "gemm: RowLn needs colsum, K <= 1024");
   ATPU_CHECK(!(g.epi & kEpiResLn) || (g.res_part && g.gamma && g.N <= 1024 && g.N % 32 == 0),
              "gemm: ResLn needs res_part, gamma, N <= 1024");
   ATPU_CHECK(!(g.epi & kEpiRowStats) || (g.part_out && g.N % 32 == 0), "gemm: RowStats needs part_out and N % 32 == 0");
@@ -2619,6 +2656,9 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
     launch_gemv(g, stream);
     return;
   }
+  // the A-row statistics output of a RowLn GEMV (ops.linear row_ln_out) exists on the GEMV only
+  ATPU_CHECK(!((g.epi & kEpiRowLn) && !(g.epi & kEpiRowStats) && g.part_out),
+             "gemm: RowLn with an A-statistics output runs on the <= 4-row GEMV only");
   if (g.splits > 1) {
     ATPU_CHECK(!(g.epi & (kEpiRowRms | kEpiKvScatter | kEpiRowLn | kEpiResLn | kEpiRowStats)),
                "gemm: RowRms / RowLn / ResLn / KvScatter cannot split K");

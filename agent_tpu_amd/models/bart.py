@@ -292,49 +292,56 @@ class BartModel:
         """:meth:`step` with the decoder LayerNorms folded into the GEMMs (only the last one
         runs as a pass). The GEMM producing a pre-LN row writes its partial (sum, sumsq) per
         32-column slab; the GEMM reading LN(x) as input and the one adding LN(x) as its
-        residual both normalise from those partials. Logits equal the unfolded step to bf16
-        rounding (tests/kernels/test_decode_gpu.py)."""
+        residual both normalise from those partials. On <= 4 rows (the decode GEMV) the GEMV
+        reading LN(x) as input takes x's statistics from the rows it loads and hands them on
+        to the residual consumer (``row_ln_out``), so the producers need no partials. Logits
+        equal the unfolded step to bf16 rounding (tests/kernels/test_decode_gpu.py)."""
         cfg, p, f = self.cfg, self.p, self.ln_folded()
         d, H, eps, L = cfg.d_model, cfg.heads, cfg.eps, cfg.dec_layers
         scale = (d // H) ** -0.5
         # partials of: the layer input (last FFN2 out), the self-attention block out, the cross block out
         px, p1, p2 = torch.empty((3, d // 32, x.shape[0], 2), dtype=torch.float32, device=x.device).unbind(0)
+        gemv = (x.is_cuda and x.shape[0] <= 4 and os.environ.get("ATPU_GEMV", "1") != "0"
+                and os.environ.get("ATPU_BART_SELF_STATS", "1") != "0")
+        so = (lambda t: None) if gemv else (lambda t: t)  # producer partials: not on the GEMV path
+        ro = (lambda t: t) if gemv else (lambda t: None)  # row_ln consumer hands x's statistics on
+        inp = (lambda t: None) if gemv else (lambda t: t)  # the GEMV row_ln reads none
         for i in range(L):
             q, prev = f"dec.l{i}.", f"dec.l{i - 1}."
             c = cache[i]
             # layer 0: x = the embedding LayerNorm's output; later: raw pre-LN rows of the last FFN
-            w, b, rl = ((p[q + "qkv_w"], p[q + "qkv_b"], None) if i == 0 else
-                        (f[q + "qkv_w"], f[q + "qkv_b"], (eps, f[q + "qkv_c"], px)))
+            w, b, rl, rlo = ((p[q + "qkv_w"], p[q + "qkv_b"], None, None) if i == 0 else
+                             (f[q + "qkv_w"], f[q + "qkv_b"], (eps, f[q + "qkv_c"], inp(px)), ro(px)))
             # each <= 4-row GEMV pulls the next one's weight into L2 (ops.linear prefetch; the
             # stats_out GEMVs have 32 weight rows per workgroup)
+            rpb = 16 if gemv else 32
             nxt = f[f"dec.l{i + 1}.qkv_w"] if i + 1 < L else None
             if self.kv_scatter:
-                qh = ops.linear(x, w, b, kv_cache=(c, T, step, d), row_ln=rl, prefetch=(p[q + "o_w"], 32))
+                qh = ops.linear(x, w, b, kv_cache=(c, T, step, d), row_ln=rl, row_ln_out=rlo,
+                                prefetch=(p[q + "o_w"], rpb))
             else:
-                qkv = ops.linear(x, w, b, row_ln=rl, prefetch=(p[q + "o_w"], 32))
+                qkv = ops.linear(x, w, b, row_ln=rl, row_ln_out=rlo, prefetch=(p[q + "o_w"], rpb))
                 ops.kv_append(qkv, d, 2 * d, c, T, step)
                 qh = qkv[:, :d]
-            # the cross query projection's weight: its predecessor (the RowStats o GEMV) does not
-            # prefetch, the self attention before it does
+            # the cross query projection's weight: prefetched by the o GEMV on the GEMV path, by
+            # the self attention (ATPU_XATTN_PREFETCH) when o is a RowStats producer
             ctx = ops.decode_attention(qh, c[:, :d], c[:, d:], H, T, 1, step=step, scale=scale, hist=hist,
                                        prefetch=f[q + "cq_w"])
             if i == 0:
-                x1 = ops.linear(ctx, p[q + "o_w"], p[q + "o_b"], residual=x, stats_out=p1, prefetch=f[q + "cq_w"])
+                x1 = ops.linear(ctx, p[q + "o_w"], p[q + "o_b"], residual=x, stats_out=so(p1), prefetch=f[q + "cq_w"])
             else:
                 x1 = ops.linear(ctx, p[q + "o_w"], f[q + "o_b"], residual=x, res_ln=(eps, px, p[prev + "ln2_g"]),
-                                stats_out=p1, prefetch=f[q + "cq_w"])
-            cq = ops.linear(x1, f[q + "cq_w"], f[q + "cq_b"], row_ln=(eps, f[q + "cq_c"], p1),
-                            prefetch=(p[q + "co_w"], 32))
+                                stats_out=so(p1), prefetch=f[q + "cq_w"])
+            cq = ops.linear(x1, f[q + "cq_w"], f[q + "cq_b"], row_ln=(eps, f[q + "cq_c"], inp(p1)), row_ln_out=ro(p1),
+                            prefetch=(p[q + "co_w"], rpb))
             kv = ckv[:, i * 2 * d:(i + 1) * 2 * d]
-            # fc1's weight: its predecessor (the RowStats co GEMV) does not prefetch, the split
-            # cross attention two kernels earlier does
             ctx = ops.decode_attention(cq, kv[:, :d], kv[:, d:], H, S, group, lens=src_lens, scale=scale,
                                        prefetch=f[q + "f1_w"])
             x2 = ops.linear(ctx, p[q + "co_w"], f[q + "co_b"], residual=x1, res_ln=(eps, p1, p[q + "ln1_g"]),
-                            stats_out=p2, prefetch=f[q + "f1_w"])
-            h = ops.linear(x2, f[q + "f1_w"], f[q + "f1_b"], act="gelu", row_ln=(eps, f[q + "f1_c"], p2),
-                           prefetch=(p[q + "f2_w"], 32))
+                            stats_out=so(p2), prefetch=f[q + "f1_w"])
+            h = ops.linear(x2, f[q + "f1_w"], f[q + "f1_b"], act="gelu", row_ln=(eps, f[q + "f1_c"], inp(p2)),
+                           row_ln_out=ro(p2), prefetch=(p[q + "f2_w"], rpb))
             x = ops.linear(h, p[q + "f2_w"], f[q + "f2_b"], residual=x2, res_ln=(eps, p2, p[q + "lnc_g"]),
-                           stats_out=px, prefetch=nxt)
+                           stats_out=so(px), prefetch=nxt)
         x = ops.layernorm(x, p[f"dec.l{L - 1}.ln2_g"], p[f"dec.l{L - 1}.ln2_b"], eps)
         return ops.lm_head(x, p["shared"], p["final_logits_bias"], 0.0, logits)

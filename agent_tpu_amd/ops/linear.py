@@ -42,15 +42,28 @@ def row_ln_from_parts_ref(part: torch.Tensor, eps: float) -> torch.Tensor:
     return torch.stack([rs, rs * mu], -1)
 
 
+def row_totals_parts_ref(x: torch.Tensor) -> torch.Tensor:
+    """The ``row_ln_out`` format: ``[K/32, M, 2]`` with each row's (sum, sum of squares) in slot 0
+    and zeros elsewhere (summing the slots gives the row totals, as partials do)."""
+    M, K = x.shape
+    xf = x.float()
+    out = torch.zeros((K // 32, M, 2), dtype=torch.float32, device=x.device)
+    out[0, :, 0] = xf.sum(-1)
+    out[0, :, 1] = (xf * xf).sum(-1)
+    return out
+
+
 def linear_ref(x, w, bias=None, act=None, residual=None, out_f32=False, rms_eps=None, row_ln=None, res_ln=None,
-               stats_out=None):
+               stats_out=None, row_ln_out=None):
     y = x.float() @ w.float().t()
     if rms_eps is not None:
         y = y * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + rms_eps)
     if row_ln is not None:
         eps, colsum, in_part = row_ln
-        st = row_ln_from_parts_ref(in_part, eps)
+        st = row_ln_from_parts_ref(in_part if in_part is not None else row_totals_parts_ref(x), eps)
         y = y * st[:, :1] - st[:, 1:] * colsum.float().unsqueeze(0)
+        if row_ln_out is not None:
+            row_ln_out.copy_(row_totals_parts_ref(x))
     if bias is not None:
         y = y + bias.float()
     if act == "gelu":
@@ -81,7 +94,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
            residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
            out_f32: bool = False, rms_eps: Optional[float] = None, kv_cache=None, row_ln=None,
            res_ln=None, stats_out: Optional[torch.Tensor] = None,
-           prefetch: Optional[torch.Tensor] = None) -> torch.Tensor:
+           prefetch: Optional[torch.Tensor] = None, row_ln_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``act(x @ w.T + bias) + residual``; ``out_f32`` returns fp32 (LM-head logits).
 
     ``rms_eps``: ``x`` rows are raw RMSNorm inputs and ``w`` carries the norm's gamma
@@ -99,6 +112,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     ``w``/``bias`` folded: ``y = rstd*(x @ w.T) - rstd*mu*colsum + bias``;
     ``res_ln = (eps, res_part, gamma)``: ``residual`` rows are raw LN inputs with partials
     ``res_part``, added as ``(r - mu)*rstd*gamma`` (beta folded into ``bias``).
+    On <= 4 rows (the decode GEMV) a ``row_ln`` GEMV takes the statistics of ``x`` from the
+    rows it reads anyway (``in_part`` may be None) and ``row_ln_out`` receives them in the
+    partial format (totals in slot 0) for a later ``res_ln`` GEMV on the same rows, so no
+    producer needs ``stats_out`` (its 8-wave, 32-column-slab workgroups).
 
     ``prefetch``: the weight of the NEXT linear of a decode chain (or ``(weight, 32)`` when that
     linear writes ``stats_out``: 32 weight rows per workgroup). A <= 4-row GEMV pulls it into the
@@ -117,8 +134,14 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         check(eps > 0, "linear: row_ln eps must be > 0")
         check(colsum.dtype == torch.float32 and colsum.is_contiguous() and colsum.numel() == N0,
               "linear: row_ln colsum must be contiguous fp32 [N]")
-        parts(in_part, x.shape[1], "row_ln in_part")
+        if in_part is not None:
+            parts(in_part, x.shape[1], "row_ln in_part")
+        else:
+            check(M0 <= 4 or not x.is_cuda, "linear: row_ln without in_part runs on <= 4 rows (the GEMV) only")
         check(x.shape[1] <= 1024, "linear: row_ln rows must be <= 1024 wide")
+    if row_ln_out is not None:
+        check(row_ln is not None and (M0 <= 4 or not x.is_cuda), "linear: row_ln_out needs row_ln on <= 4 rows")
+        parts(row_ln_out, x.shape[1], "row_ln_out")
     if res_ln is not None:
         eps, res_part, gamma = res_ln
         check(residual is not None and bias is not None and act in (None, "none") and kv_cache is None
@@ -140,7 +163,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         check(cache.dim() == 2 and cache.shape[1] >= N0 - col0 and cache.shape[0] == x.shape[0] * T
               and cache.dtype == torch.bfloat16, "linear: cache must be bf16 [M*T, >= N-col0]")
         if not x.is_cuda:
-            y = linear_ref(x, w, bias, act, None, False, rms_eps, row_ln)
+            y = linear_ref(x, w, bias, act, None, False, rms_eps, row_ln, row_ln_out=row_ln_out)
             rows = torch.arange(x.shape[0]) * T + int(step.reshape(-1)[0])
             cache[rows, :N0 - col0] = y[:, col0:]
             q = y[:, :col0]
@@ -150,7 +173,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
               "linear: rms_eps takes no bias / residual and only a ReLU")
         check(rms_eps > 0, "linear: rms_eps must be > 0")
     if not x.is_cuda:
-        y = linear_ref(x, w, bias, act, residual, out_f32, rms_eps, row_ln, res_ln, stats_out)
+        y = linear_ref(x, w, bias, act, residual, out_f32, rms_eps, row_ln, res_ln, stats_out, row_ln_out)
         if out is not None:
             out.copy_(y)
             return out
@@ -191,10 +214,13 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     eps_arg = float(rms_eps or 0.0)
     if row_ln is not None:
         eps, colsum, in_part = row_ln
-        same_device(x, colsum, in_part)
+        same_device(x, colsum)
         epi |= EPI_ROW_LN
         eps_arg = float(eps)
         ln_args[0], ln_args[1] = ptr(colsum), ptr(in_part)
+        if row_ln_out is not None:
+            same_device(x, row_ln_out)
+            ln_args[4] = ptr(row_ln_out)
     if res_ln is not None:
         eps, res_part, gamma = res_ln
         same_device(x, res_part, gamma)

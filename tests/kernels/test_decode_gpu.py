@@ -688,6 +688,48 @@ def test_gemm_row_ln_fold(gpu, M, N, K, act, kv):
     assert _rel(z, zref) < 2e-2
 
 
+@pytest.mark.parametrize("M,K,N,act,kv", [(4, 1024, 1024, None, False), (1, 1024, 4096, "gelu", False),
+                                          (3, 1024, 3072, None, True), (2, 768, 768, None, False)])
+def test_gemv_row_ln_self_stats(gpu, M, K, N, act, kv):
+    # <= 4 rows: the RowLn GEMV takes x's LayerNorm statistics from the rows it loads (no
+    # producer partials) and hands them on (row_ln_out: totals in slot 0) to the ResLn GEMV
+    # that adds LN(x) as its residual; against the fp32 LayerNorm references
+    import torch.nn.functional as F
+
+    x = _r((M, K), gpu, 2.0, seed=90) + 0.3
+    w = _r((N, K), gpu, 0.05, seed=91)
+    b = _r((N,), gpu, 0.1, torch.float32, seed=92)
+    gam = 1 + _r((K,), gpu, 0.3, torch.float32, seed=93)
+    bet = _r((K,), gpu, 0.2, torch.float32, seed=94)
+    eps = 1e-5
+    wf, cs, bf = ops.fold_ln_into_linear(w, b, gam, bet)
+    out_parts = torch.full((K // 32, M, 2), float("nan"), dtype=torch.float32, device=gpu)
+    xf = x.cpu().float()
+    xn = F.layer_norm(xf, (K,), gam.cpu(), bet.cpu(), eps)
+    ref = xn @ w.cpu().float().t() + b.cpu()
+    if act == "gelu":
+        ref = F.gelu(ref)
+    if kv:
+        d = N // 3
+        T, t = 5, 2
+        cache = torch.zeros((M * T, 2 * d), dtype=torch.bfloat16, device=gpu)
+        step = torch.tensor([t], dtype=torch.int32, device=gpu)
+        q = ops.linear(x, wf, bf, kv_cache=(cache, T, step, d), row_ln=(eps, cs, None), row_ln_out=out_parts)
+        assert _rel(q, ref[:, :d]) < 2e-2
+        assert _rel(cache.view(M, T, 2 * d)[:, t], ref[:, d:]) < 2e-2
+    else:
+        y = ops.linear(x, wf, bf, act=act, row_ln=(eps, cs, None), row_ln_out=out_parts)
+        assert _rel(y, ref) < 2e-2
+    torch.testing.assert_close(out_parts.cpu(), ops.row_totals_parts_ref(x.cpu()), rtol=1e-4, atol=1e-2)
+    # the residual consumer reads the handed-on statistics
+    ctx = _r((M, 256), gpu, 1.0, seed=95)
+    wo = _r((K, 256), gpu, 0.05, seed=96)
+    bo = _r((K,), gpu, 0.1, torch.float32, seed=97)
+    z = ops.linear(ctx, wo, (bo + bet).contiguous(), residual=x, res_ln=(eps, out_parts, gam))
+    zref = ctx.cpu().float() @ wo.cpu().float().t() + bo.cpu() + xn
+    assert _rel(z, zref) < 2e-2
+
+
 def test_bart_step_ln_fold_matches_unfolded(gpu):
     # non-trivial LayerNorm gammas / betas: the folded BART decoder step vs the layernorm +
     # linear step (GPU) and the fp32 oracle
