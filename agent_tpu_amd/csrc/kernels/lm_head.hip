@@ -758,7 +758,20 @@ void lm_head_topk(const bf16* A, int lda, const bf16* W, int ldw, const float* b
       ATPU_LM(R, B, X, 128, 2, 1);    \
   }
 #else
-#define ATPU_LM_CFG(R, B, X) ATPU_LM(R, B, X, 128, 2, 1);
+  // one row tile (<= 128 rows: the 1-document step) with ATPU_LM_SMALL_RING=4: a 4-slot ring (one
+  // workgroup per CU, three K-tiles in flight). Measured (profiles/lm_head_small_ring_ab_r04.txt):
+  // T5 1-doc 14.52 -> 14.57 docs/s (noise), BART 11.07 -> 10.90 (its 393 vocabulary tiles take two
+  // rounds at one workgroup per CU): 2 slots stay the default
+  static const int small_ring = [] {
+    const char* f = std::getenv("ATPU_LM_SMALL_RING");
+    return (f && f[0] == '4') ? 4 : 2;
+  }();
+#define ATPU_LM_CFG(R, B, X)            \
+  if (M <= 128 && small_ring == 4) {    \
+    ATPU_LM(R, B, X, 128, 4, 1);        \
+  } else {                              \
+    ATPU_LM(R, B, X, 128, 2, 1);        \
+  }
 #endif
 #define ATPU_LM_WIDE(R, B, X)                                                                                    \
   hipLaunchKernelGGL((lm_head_wide_kernel<R, B, X>), dim3(std::min(ntiles_w, num_cus())), dim3(256), 0, stream, A,    \
