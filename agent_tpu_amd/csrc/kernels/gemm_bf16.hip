@@ -2311,6 +2311,21 @@ using GemvPf = L2Pf;
 #define ATPU_GEMV_EARLY 1  // epilogue operands loaded before the main loop: 0 never, 1 LN-folded, 2 all,
                            // 3 LN-folded before, the rest right after the first round's loads
 #endif
+#ifndef ATPU_GEMV_NWV
+#define ATPU_GEMV_NWV 4  // waves (4-column groups) per workgroup of the unsplit GEMVs but RowStats
+#endif
+constexpr int kGemvNwv = ATPU_GEMV_NWV;
+#ifndef ATPU_GEMV_KS_NWV
+#define ATPU_GEMV_KS_NWV 1  // column groups per K-split workgroup (x KS slices + the prefetch wave)
+#endif
+#ifndef ATPU_GEMV_KS
+#define ATPU_GEMV_KS 2  // K slices of the split GEMV
+#endif
+#ifndef ATPU_GEMV_KS_MINK
+#define ATPU_GEMV_KS_MINK 512  // split K above this
+#endif
+constexpr int kGemvKs = ATPU_GEMV_KS, kGemvKsU = 4096 / (512 * ATPU_GEMV_KS);  // K = 4096: one round
+constexpr int kKsNwv = ATPU_GEMV_KS_NWV;
 #ifndef ATPU_GEMV_PF_RS
 #define ATPU_GEMV_PF_RS 0  // L2 prefetch from RowStats GEMVs too
 #endif
@@ -2318,27 +2333,37 @@ using GemvPf = L2Pf;
 // BART's LayerNorm folding (RowLn / ResLn / RowStats, see LnDec): the row statistics come
 // from the <= 32 slab partials (lane = slab, wave sums); RowStats workgroups are 8 waves =
 // one 32-column slab, summed across the waves through LDS.
-template <int EPI, int NWV, int U, bool PF>
-__global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __restrict__ A, int lda,
+// KS > 1 (epilogues without row statistics taken from A, K > 512: the attention-out and FF-out
+// GEMVs): KS waves per column group, each over 1/KS of K, their partials summed through LDS.
+// One column group per workgroup (N/4 workgroups + the prefetch wave): 1-doc BART 11.1 -> 12.2,
+// T5 14.6 -> 15.4 docs/s against the unsplit 4-wave workgroups (and K = 4096 no longer takes two
+// serialised load rounds); profiles/gemv_ksplit_ab_r04.txt.
+template <int EPI, int NWV, int U, bool PF, int KS = 1>
+__global__ __launch_bounds__((NWV * KS + PF) * 64) void gemv_kernel(const bf16* __restrict__ A, int lda,
                                                               const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C,
                                                               int ldc, const float* __restrict__ bias,
                                                               const bf16* __restrict__ R, int ldr, int M, int N, int K,
                                                               float rms_eps, KvOut kvo, LnDec ln, GemvPf pf) {
   typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
   static_assert(!(EPI & kEpiRowStats) || NWV == 8, "RowStats: one 32-column slab per workgroup");
+  static_assert(KS == 1 || !(EPI & (kEpiRowStats | kEpiRowRms | kEpiRowLn)),
+                "K split: no statistics over A's rows, one barrier");
   constexpr int kGemvU = U;
   __shared__ float2 st_red[NWV][kGemvRows];
+  __shared__ float ks_red[KS > 1 ? KS - 1 : 1][NWV][16];
   __shared__ __attribute__((aligned(16))) char pf_scratch[PF ? 256 : 4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if constexpr (PF) {
-    if (w == NWV) {
-      // RowStats workgroups have one barrier (the slab sum), taken with the loads in flight
-      l2_prefetch_rows<(EPI & kEpiRowStats) != 0 ? 1 : 0>(pf, lane, pf_scratch, blockIdx.x, gridDim.x);
+    if (w == NWV * KS) {
+      // RowStats workgroups have one barrier (the slab sum), K-split ones one (the half sum),
+      // taken with the loads in flight
+      l2_prefetch_rows<((EPI & kEpiRowStats) != 0 || KS > 1) ? 1 : 0>(pf, lane, pf_scratch, blockIdx.x, gridDim.x);
       return;
     }
   }
-  const int n0 = (blockIdx.x * NWV + w) * 4;  // this wave's 4 columns
-  const int nch = K / 8;
+  const int cg = KS > 1 ? w % NWV : w, ks = KS > 1 ? w / NWV : 0;  // column group, K slice
+  const int n0 = (blockIdx.x * NWV + cg) * 4;                      // this wave's 4 columns
+  const int nch = K / (8 * KS), c0 = ks * nch;                     // its 16-B chunks of K
   // lanes 16 mo + 4 jo finish output (mo, n0 + jo). With LayerNorm folding (BART) its
   // epilogue operands (bias, residual, LN column sums / gamma, the row-statistics partials)
   // are loaded before the main loop and arrive under it instead of as a dependent round trip
@@ -2388,7 +2413,7 @@ __global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __res
     bf16x8 wv[kGemvU][4], av[kGemvU][kGemvRows];
 #pragma unroll
     for (int u = 0; u < kGemvU; ++u) {
-      const int c = min(base + u * 64 + lane, nch - 1);  // clamped: its products are dropped below
+      const int c = c0 + min(base + u * 64 + lane, nch - 1);  // clamped: its products are dropped below
 #pragma unroll
       for (int j = 0; j < 4; ++j) wv[u][j] = *reinterpret_cast<const bf16x8*>(Bt + (size_t)(n0 + j) * ldb + c * 8);
 #pragma unroll
@@ -2447,6 +2472,13 @@ __global__ __launch_bounds__((NWV + PF) * 64) void gemv_kernel(const bf16* __res
     for (int i = 0; i < 16; ++i) a16[i] = acc[i >> 2][i & 3];
     v = wave_bfly<16>(a16, OpAdd{});
     if constexpr (EPI & kEpiRowRms) rs = wave_bfly<kGemvRows>(ssq, OpAdd{});  // row lane >> 4
+  }
+  if constexpr (KS > 1) {  // the upper K slices hand their 16 sums to slice 0's wave
+    if (ks > 0 && (lane & 3) == 0) ks_red[ks - 1][cg][lane >> 2] = v;
+    __syncthreads();
+    if (ks > 0) return;
+#pragma unroll
+    for (int i = 0; i < KS - 1; ++i) v += ks_red[i][cg][lane >> 2];
   }
   // (rstd, rstd*mu) of A's rows (RowLn) or R's rows (ResLn) from their slab partials
   float2 lnst = float2{1.f, 0.f};
@@ -2575,18 +2607,41 @@ void launch_gemv(const GemmArgs& g, hipStream_t s) {
   const bool pf = pf_on && g.pf_w && g.pf_n > 0 && g.pf_k > 0 && (ATPU_GEMV_PF_RS || !(g.epi & kEpiRowStats));
   const GemvPf pfa{g.pf_w, g.pf_ld, g.pf_k, g.pf_n, g.pf_rpb > 0 ? g.pf_rpb : 16};
   const bool u6 = gemv_u(g.K) == 6;
+  static const bool ks_on = [] {
+    const char* f = std::getenv("ATPU_GEMV_KSPLIT");
+    return !(f && f[0] == '0');
+  }();
+  // K split (KS slices, up to 4096 / (512 KS) chunks per lane and slice in one round)
+  const bool ks2 = ks_on && g.K > ATPU_GEMV_KS_MINK && g.K % (8 * kGemvKs) == 0;
+  const bool ks_u1 = g.K <= 512 * kGemvKs;  // one chunk per lane and slice
 #define ATPU_GEMV_GO(E, UU, P)                                                                                   \
   hipLaunchKernelGGL((gemv_kernel<E, nwv, UU, P>), dim3(g.N / (4 * nwv)), dim3(64 * (nwv + P)), 0, s, g.A, g.lda, \
                      g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, g.rms_eps, kvo, ln, pfa)
+// K-split epilogues (no A-row statistics) launch <E, nwv, 4, P, 2>; for the others the same
+// expression names their existing <E, nwv, 3, P, 1> instantiation (never launched with ks2)
+#define ATPU_GEMV_GO_KS(E, UU, P)                                                                                \
+  hipLaunchKernelGGL((gemv_kernel<E, kKs ? kKsNwv : nwv, kKs ? UU : 3, P, kKs ? kGemvKs : 1>),                  \
+                     dim3(g.N / (4 * (kKs ? kKsNwv : nwv))), dim3(64 * (kKs ? kGemvKs * kKsNwv : nwv) + 64 * P), 0, s, \
+                     g.A,                                                                                        \
+                     g.lda, g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, g.rms_eps, kvo, ln, pfa)
 // (E) parenthesised: for E = kEpiBias | kEpiResidual, `E & kEpiRowStats` parsed as
 // kEpiBias | (kEpiResidual & kEpiRowStats) and gave 8-wave workgroups to every multi-flag
 // epilogue (round 3). The 8-wave RowStats kernels keep 3 chunks per lane in flight: with the
 // prefetch wave (9 waves, <= 168 VGPRs) 6 spilled.
 #define ATPU_GEMV_CASE(E)                                                                                       \
   case E: {                                                                                                     \
-    constexpr int nwv = ((E) & kEpiRowStats) ? 8 : 4;                                                           \
-    constexpr int kU6 = nwv == 4 ? 6 : 3;                                                                       \
-    if (pf) {                                                                                                   \
+    constexpr int nwv = ((E) & kEpiRowStats) ? 8 : kGemvNwv;                                                    \
+    constexpr int kU6 = nwv < 8 ? 6 : 3;                                                                        \
+    constexpr bool kKs = !((E) & (kEpiRowStats | kEpiRowRms | kEpiRowLn));                                      \
+    if (kKs && ks2) {                                                                                           \
+      if (pf) {                                                                                                 \
+        if (ks_u1) ATPU_GEMV_GO_KS(E, 1, true);                                                                 \
+        else ATPU_GEMV_GO_KS(E, kGemvKsU, true);                                                                \
+      } else {                                                                                                  \
+        if (ks_u1) ATPU_GEMV_GO_KS(E, 1, false);                                                                \
+        else ATPU_GEMV_GO_KS(E, kGemvKsU, false);                                                               \
+      }                                                                                                         \
+    } else if (pf) {                                                                                            \
       if (u6) ATPU_GEMV_GO(E, kU6, true);                                                                       \
       else ATPU_GEMV_GO(E, 3, true);                                                                            \
     } else {                                                                                                    \
@@ -2617,6 +2672,7 @@ void launch_gemv(const GemmArgs& g, hipStream_t s) {
       throw std::invalid_argument("atpu: unsupported GEMV epilogue " + std::to_string(g.epi));
   }
 #undef ATPU_GEMV_CASE
+#undef ATPU_GEMV_GO_KS
 #undef ATPU_GEMV_GO
   ATPU_HIP_CHECK(hipGetLastError());
 }

@@ -721,9 +721,11 @@ def test_gemv_row_ln_self_stats(gpu, M, K, N, act, kv):
         y = ops.linear(x, wf, bf, act=act, row_ln=(eps, cs, None), row_ln_out=out_parts)
         assert _rel(y, ref) < 2e-2
     torch.testing.assert_close(out_parts.cpu(), ops.row_totals_parts_ref(x.cpu()), rtol=1e-4, atol=1e-2)
-    # the residual consumer reads the handed-on statistics
-    ctx = _r((M, 256), gpu, 1.0, seed=95)
-    wo = _r((K, 256), gpu, 0.05, seed=96)
+    # the residual consumer reads the handed-on statistics (the fc1 -> fc2 shape: K = 4096 runs
+    # the K-split GEMV)
+    kc = N if act == "gelu" else 256
+    ctx = _r((M, kc), gpu, 1.0, seed=95)
+    wo = _r((K, kc), gpu, 0.05, seed=96)
     bo = _r((K,), gpu, 0.1, torch.float32, seed=97)
     z = ops.linear(ctx, wo, (bo + bet).contiguous(), residual=x, res_ln=(eps, out_parts, gam))
     zref = ctx.cpu().float() @ wo.cpu().float().t() + bo.cpu() + xn
@@ -940,7 +942,7 @@ def test_decoder_graph_cache_concurrent_parts(gpu, monkeypatch):
 @pytest.mark.parametrize("M", [1, 3, 4])
 @pytest.mark.parametrize("N,K,epi", [(768, 768, "plain"), (768, 3072, "bias_res"), (3072, 768, "relu"),
                                      (4096, 1024, "bias_gelu"), (2304, 768, "rms"), (3072, 768, "rms_relu"),
-                                     (1024, 1024, "res")])
+                                     (1024, 1024, "res"), (1024, 4096, "bias_res"), (512, 6144, "plain")])
 def test_gemv_few_rows(gpu, M, N, K, epi):
     # <= 4 rows (1 document x 4 beams) run the weight-streaming GEMV; vs the fp32 reference and
     # vs the 64x64 decode kernel (forced)
