@@ -2321,6 +2321,10 @@ constexpr int kGemvNwv = ATPU_GEMV_NWV;
 #ifndef ATPU_GEMV_KS
 #define ATPU_GEMV_KS 2  // K slices of the split GEMV
 #endif
+#ifndef ATPU_GEMV_KS_STATS
+#define ATPU_GEMV_KS_STATS 0  // split the RowRms / RowLn GEMVs too (row statistics summed with the
+                              // partials): 1-doc BART / T5 within noise (profiles/gemv_ksplit_ab_r04.txt)
+#endif
 #ifndef ATPU_GEMV_KS_MINK
 #define ATPU_GEMV_KS_MINK 512  // split K above this
 #endif
@@ -2346,11 +2350,11 @@ __global__ __launch_bounds__((NWV * KS + PF) * 64) void gemv_kernel(const bf16* 
                                                               float rms_eps, KvOut kvo, LnDec ln, GemvPf pf) {
   typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
   static_assert(!(EPI & kEpiRowStats) || NWV == 8, "RowStats: one 32-column slab per workgroup");
-  static_assert(KS == 1 || !(EPI & (kEpiRowStats | kEpiRowRms | kEpiRowLn)),
-                "K split: no statistics over A's rows, one barrier");
+  static_assert(KS == 1 || !(EPI & kEpiRowStats), "K split: one barrier, not with the slab sum");
   constexpr int kGemvU = U;
   __shared__ float2 st_red[NWV][kGemvRows];
   __shared__ float ks_red[KS > 1 ? KS - 1 : 1][NWV][16];
+  __shared__ float2 ks_row[KS > 1 ? KS - 1 : 1][NWV][kGemvRows];
   __shared__ __attribute__((aligned(16))) char pf_scratch[PF ? 256 : 4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if constexpr (PF) {
@@ -2473,18 +2477,9 @@ __global__ __launch_bounds__((NWV * KS + PF) * 64) void gemv_kernel(const bf16* 
     v = wave_bfly<16>(a16, OpAdd{});
     if constexpr (EPI & kEpiRowRms) rs = wave_bfly<kGemvRows>(ssq, OpAdd{});  // row lane >> 4
   }
-  if constexpr (KS > 1) {  // the upper K slices hand their 16 sums to slice 0's wave
-    if (ks > 0 && (lane & 3) == 0) ks_red[ks - 1][cg][lane >> 2] = v;
-    __syncthreads();
-    if (ks > 0) return;
-#pragma unroll
-    for (int i = 0; i < KS - 1; ++i) v += ks_red[i][cg][lane >> 2];
-  }
-  // (rstd, rstd*mu) of A's rows (RowLn) or R's rows (ResLn) from their slab partials
-  float2 lnst = float2{1.f, 0.f};
+  // (sum, sum of squares) of A's rows (RowLn) or R's rows (ResLn), row mo
+  float S = 0.f, Q = 0.f;
   if constexpr (EPI & (kEpiRowLn | kEpiResLn)) {
-    const float inv = 1.f / ((EPI & kEpiRowLn) ? K : N);
-    float S = 0.f, Q = 0.f;
     if constexpr (!ATPU_GEMV_BFLY) {
 #pragma unroll
       for (int r = 0; r < kGemvRows; ++r) {
@@ -2504,6 +2499,30 @@ __global__ __launch_bounds__((NWV * KS + PF) * 64) void gemv_kernel(const bf16* 
       S = b3 ? o : h;
       Q = b3 ? h : o;
     }
+  }
+  if constexpr (KS > 1) {
+    // the upper K slices hand their 16 sums (and A-row statistics) to slice 0's wave: one barrier
+    if (ks > 0) {
+      if ((lane & 3) == 0) ks_red[ks - 1][cg][lane >> 2] = v;
+      if ((lane & 15) == 0) ks_row[ks - 1][cg][mo] = float2{(EPI & kEpiRowRms) ? rs : S, Q};
+    }
+    __syncthreads();
+    if (ks > 0) return;
+#pragma unroll
+    for (int i = 0; i < KS - 1; ++i) {
+      v += ks_red[i][cg][lane >> 2];
+      const float2 t = ks_row[i][cg][mo];
+      if constexpr (EPI & kEpiRowRms) rs += t.x;
+      if constexpr (EPI & kEpiRowLn) {
+        S += t.x;
+        Q += t.y;
+      }
+    }
+  }
+  // (rstd, rstd*mu) of A's rows (RowLn) or R's rows (ResLn)
+  float2 lnst = float2{1.f, 0.f};
+  if constexpr (EPI & (kEpiRowLn | kEpiResLn)) {
+    const float inv = 1.f / ((EPI & kEpiRowLn) ? K : N);
     const float mu = S * inv, var = fmaxf(Q * inv - mu * mu, 0.f);
     const float rr = __builtin_amdgcn_rsqf(var + rms_eps);
     lnst = float2{rr, rr * mu};
@@ -2632,7 +2651,7 @@ void launch_gemv(const GemmArgs& g, hipStream_t s) {
   case E: {                                                                                                     \
     constexpr int nwv = ((E) & kEpiRowStats) ? 8 : kGemvNwv;                                                    \
     constexpr int kU6 = nwv < 8 ? 6 : 3;                                                                        \
-    constexpr bool kKs = !((E) & (kEpiRowStats | kEpiRowRms | kEpiRowLn));                                      \
+    constexpr bool kKs = !((E) & kEpiRowStats) && (ATPU_GEMV_KS_STATS || !((E) & (kEpiRowRms | kEpiRowLn)));    \
     if (kKs && ks2) {                                                                                           \
       if (pf) {                                                                                                 \
         if (ks_u1) ATPU_GEMV_GO_KS(E, 1, true);                                                                 \
