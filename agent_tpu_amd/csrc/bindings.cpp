@@ -144,6 +144,8 @@ PYBIND11_MODULE(_atpu, m) {
   m.def("trace_pop", &trace_pop);
   m.def("trace_mark", [](const std::string& n) { trace_mark(n.c_str()); });
   m.def("gemm_splitk_splits", &gemm_splitk_splits, "split-K factor chosen for an [M,N,K] GEMM");
+  m.def("gemv_selected", &gemv_selected, py::arg("M"), py::arg("N"), py::arg("epi"),
+        "true when gemm_bf16 runs this [M, N] problem / epilogue on the <= 4-row GEMV");
   m.def("gemm_force_tile", &gemm_force_tile, py::arg("set") = -1, "GEMM kernel family override: 0 auto, 64, 128, 256");
   m.def("gemm_dec_mode", &gemm_dec_mode, py::arg("set") = -1,
         "skinny-M GEMM path: 1 = 64x64 multi-stage dec kernel, 0 = 128x128 split-K; returns the current");
@@ -238,8 +240,6 @@ PYBIND11_MODULE(_atpu, m) {
       py::arg("nbmax") = 0, py::arg("seq") = 0, py::arg("seq_stride") = 0, py::arg("cur") = 0, py::arg("ngram") = 0);
   m.def("lm_head_ws_bytes", &lm_head_ws_bytes);
   m.def("lm_head_stages", &lm_head_stages, py::arg("set") = -1);
-  m.def("lm_head_wide", &lm_head_wide, py::arg("set") = -1);
-  m.def("decode_cross_wg", &decode_cross_wg, py::arg("set") = -1);
   m.def("decode_self_few", &decode_self_few, py::arg("set") = -1);
   m.def("decode_xattn_prefetch", &decode_xattn_prefetch, py::arg("set") = -1);
   m.def(

@@ -343,17 +343,6 @@ __device__ __forceinline__ int xcd_remap(int b, int nblocks) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-// Tile t of a row-major [ntm x ntn] tile grid re-ordered in groups of R tile rows walked
-// column by column (R = 0: unchanged). Consecutive indices then cover R row blocks x (n / R)
-// column tiles instead of n / ntn row blocks x ntn columns: the operand working set of the
-// tiles an XCD runs at once (A rows + B columns) shrinks when ntn is large. A bijection.
-__device__ __forceinline__ int group_tiles(int t, int ntm, int ntn, int R) {
-  if (R <= 0) return t;
-  const int per = R * ntn, g = t / per, r = t - g * per;
-  const int rows = min(R, ntm - g * R);
-  return (g * R + r % rows) * ntn + r / rows;
-}
-
 }  // namespace atpu
 
 #define ATPU_HIP_CHECK(expr)                                                              \

@@ -77,6 +77,9 @@ struct GemmArgs {
   int pf_rpb = 16;  // weight rows per workgroup of that next GEMV (32 when it writes RowStats)
 };
 void gemm_bf16(const GemmArgs& g, hipStream_t stream);
+// true when gemm_bf16 runs an [M, N] problem with epilogue `epi` on the <= 4-row GEMV (the
+// same test it applies: ATPU_GEMV, ATPU_GEMM_TILE, N % 16, an instantiated epilogue)
+bool gemv_selected(int M, int N, int epi);
 // split count the library picks for an [M,N,K] problem (1 = no split-K)
 int gemm_splitk_splits(int M, int N, int K);
 // skinny-M selector (benchmarks): 1 = 64x64 multi-stage dec kernel, 0 = 128x128 split-K
@@ -117,7 +120,6 @@ int decode_attention_splits(int rows, int group, int H, int seq_stride, bool cro
 size_t decode_attention_ws_floats(int rows, int group, int H, int seq_stride, bool cross);
 int decode_self_few(int set);  // 1: few-row self attention one wave per (row, head), T <= 192 (default); -1 reads
 int decode_xattn_prefetch(int set);  // 1: few-item attention kernels prefetch a later GEMV weight (default 0); -1 reads
-int decode_cross_wg(int set);  // 1: few-item cross attention in one workgroup per (item, head) (default 0: slower); -1 reads
 // one-workgroup state advance of a small beam search (rows x stride x 4 B x (seq ? 2 : 1) <= 64 KiB):
 // hist / seq reordered in place by par (as beam_reorder_hist, seq with last = tok, off 1),
 // tokens = tok, *step_dev += 1
@@ -144,7 +146,6 @@ void beam_topk_rows(const float* logits, int rows, int V, const float* beam_scor
 // fp32 logits. topk <= 8. ws: lm_head_ws_bytes(M, V) bytes, 16-B aligned (per-tile partials
 // and the per-row ban bitmap).
 size_t lm_head_ws_bytes(int M, int V);
-int lm_head_wide(int set);    // 1: 256x160 persistent kernel for >= 512 rows (env ATPU_LM_WIDE=1; default off); -1 reads
 int lm_head_stages(int set);  // tile / ring / wave-grid config 0-5 (dev builds; release: 0); -1 reads
 void lm_head_topk(const bf16* A, int lda, const bf16* W, int ldw, const float* bias, float rms_eps, int M, int V,
                   int K, int topk, const float* beam_scores, int eos, int mask_eos, const int32_t* bans, int nbmax,

@@ -589,132 +589,6 @@ __global__ __launch_bounds__(64 * (1 + PF)) void decode_self_few_kernel(
   out[(size_t)seq * ldo + h * kD + dc + ksub] = f2bf(wave_bfly_rows8(o) * inv);
 }
 
-// ----------------------------------------------------------------------------
-// Cross attention of few items, split and combined in ONE workgroup per (item, head):
-// its 16 waves take one 64-key chunk each (the split kernel's per-chunk math: every K
-// and V load of the wave issued before the first use), the chunks' {max, sum, o[64]}
-// go through LDS, and waves 0..G-1 combine them for their beam row exactly as
-// decode_attn_combine_kernel does (same chunk order). The whole source (<= 1024 keys,
-// 256 KiB of K/V per head) is in flight at once from one CU, and the split kernel's
-// second launch and its global round trip of partials are gone.
-// ----------------------------------------------------------------------------
-constexpr int kWgWaves = 16;
-constexpr int kWgMaxKeys = kWgWaves * kSplitKeys;
-
-template <int GM>
-__global__ __launch_bounds__(kWgWaves * 64) void decode_cross_wg_kernel(
-    const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k, const bf16* __restrict__ v, int ldkv,
-    int seq_stride, int group, int nrows, const int32_t* __restrict__ lens, const float* __restrict__ bias_dist,
-    int bias_stride, bf16* __restrict__ out, int ldo, float scale) {
-  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-  __shared__ bf16x8 qsh[GM][8];
-  __shared__ float pl[kWgWaves][GM][kSplitKeys];
-  __shared__ float rm[kWgWaves][GM], rl[kWgWaves][GM];
-  __shared__ float ro[kWgWaves][GM][kD];
-  const int seq = blockIdx.x, h = blockIdx.y;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int G = min(group, nrows - seq * group);
-  const int len = min(lens[seq], seq_stride);
-  const int jb = wave * kSplitKeys, n = max(0, min(kSplitKeys, len - jb));
-  auto at = [&](int j) -> size_t { return ((size_t)seq * seq_stride + j) * ldkv + h * kD; };
-  const int qg = lane >> 3, qe = lane & 7;
-  const int ksub = lane >> 3, dc = (lane & 7) * 8;
-  bf16x8 qv, kk[8], vv[kSplitKeys / 8];
-  float bj = 0.f;
-  if (wave == 0 && qg < G) qv = *reinterpret_cast<const bf16x8*>(q + (size_t)(seq * group + qg) * ldq + h * kD + qe * 8);
-  if (n > 0) {  // wave-uniform
-    const int jk = jb + min(lane, n - 1);
-    if (bias_dist) bj = bias_dist[h * bias_stride + (len - 1 - jk)];
-    const bf16* kr = k + at(jk);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) kk[e] = *reinterpret_cast<const bf16x8*>(kr + e * 8);
-#pragma unroll
-    for (int u = 0; u < kSplitKeys / 8; ++u)
-      vv[u] = *reinterpret_cast<const bf16x8*>(v + at(jb + min(u * 8 + ksub, n - 1)) + dc);
-  }
-  if (wave == 0 && qg < G) qsh[qg][qe] = qv;
-  __syncthreads();
-  float o[GM][8];
-#pragma unroll
-  for (int g = 0; g < GM; ++g)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[g][e] = 0.f;
-  if (n > 0) {
-#pragma unroll
-    for (int g = 0; g < GM; ++g) {
-      if (g < G) {
-        float d[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const bf16x8 qq = qsh[g][e];
-#pragma unroll
-          for (int t = 0; t < 4; ++t)
-            d[t] = __builtin_amdgcn_fdot2_f32_bf16(bf16x2_t{kk[e][2 * t], kk[e][2 * t + 1]},
-                                                   bf16x2_t{qq[2 * t], qq[2 * t + 1]}, d[t], false);
-        }
-        const float sj = lane < n ? ((d[0] + d[1]) + (d[2] + d[3])) * scale + bj : -FLT_MAX;
-        const float m = wave_max(sj);
-        const float p = lane < n ? __expf(sj - m) : 0.f;
-        pl[wave][g][lane] = p;
-        const float sm = wave_sum(p);
-        if (lane == 0) {
-          rm[wave][g] = m;
-          rl[wave][g] = sm;
-        }
-      }
-    }
-    // pl of this wave is written and read by this wave only (wave-synchronous LDS)
-#pragma unroll
-    for (int u = 0; u < kSplitKeys / 8; ++u) {
-      const int jl = u * 8 + ksub;
-#pragma unroll
-      for (int g = 0; g < GM; ++g) {
-        if (g < G) {
-          const float pj = jl < n ? pl[wave][g][jl] : 0.f;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[g][e] += pj * bf2f(vv[u][e]);
-        }
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < GM; ++g) {
-      if (g < G) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float x = o[g][e];
-          x += __shfl_xor(x, 8);
-          x += __shfl_xor(x, 16);
-          x += __shfl_xor(x, 32);
-          o[g][e] = x;
-        }
-        if (ksub == 0) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) ro[wave][g][dc + e] = o[g][e];
-        }
-      }
-    }
-  } else if (lane < GM) {  // a chunk past the source length contributes nothing
-    rm[wave][lane] = -FLT_MAX;
-    rl[wave][lane] = 0.f;
-  }
-  __syncthreads();
-  if (wave < G) {  // combine, one wave per beam row: lane = dimension
-    const int g = wave;
-    float M = -FLT_MAX;
-#pragma unroll
-    for (int c = 0; c < kWgWaves; ++c) M = fmaxf(M, rm[c][g]);
-    float L = 0.f, acc = 0.f;
-#pragma unroll
-    for (int c = 0; c < kWgWaves; ++c) {
-      const float m = rm[c][g];
-      const float w = m == -FLT_MAX ? 0.f : __expf(m - M);
-      L += w * rl[c][g];
-      acc += w == 0.f ? 0.f : w * ro[c][g][lane];
-    }
-    out[(size_t)(seq * group + g) * ldo + h * kD + lane] = f2bf(L > 0.f ? acc / L : 0.f);
-  }
-}
-
 // hist'[r][j] = hist[parent[r]][j] for j < t; hist'[r][t] = last ? last[r] : parent[r],
 // t = *step_dev + off (token histories: last = the new tokens, off = 1)
 __global__ __launch_bounds__(256) void beam_reorder_hist_kernel(const int32_t* __restrict__ src,
@@ -1160,19 +1034,6 @@ int decode_self_few(int set) {
   return v;
 }
 
-int decode_cross_wg(int set) {
-  // few-item cross attention in one workgroup per (item, head) (decode_cross_wg_kernel)
-  // instead of the split + combine pair: measured SLOWER (1-doc T5 9.7 vs 11.4 docs/s, BART
-  // 7.6 vs 8.7: one CU's address/L1 pipeline issues the 1024 scattered 128-B K rows of a
-  // head ~16x slower than the split grid spread over 192 CUs), so off unless ATPU_DEC_XWG=1
-  static int v = [] {
-    const char* f = std::getenv("ATPU_DEC_XWG");
-    return (f && f[0] == '1') ? 1 : 0;
-  }();
-  if (set == 0 || set == 1) v = set;
-  return v;
-}
-
 int decode_attention_splits(int rows, int group, int H, int seq_stride, bool cross) {
   // key chunks of the split cross attention, 0 = the per-(item, head) kernel: split while
   // the unsplit grid (items x heads) cannot cover the chip twice
@@ -1182,15 +1043,9 @@ int decode_attention_splits(int rows, int group, int H, int seq_stride, bool cro
   return (seq_stride + kSplitKeys - 1) / kSplitKeys;
 }
 
-// the split cross attention runs as decode_cross_wg_kernel (no workspace)
-static bool cross_in_one_wg(int rows, int group, int H, int seq_stride, int ns) {
-  const int nseq = (rows + group - 1) / group;
-  return ns > 0 && decode_cross_wg(-1) && seq_stride <= kWgMaxKeys && nseq * H <= num_cus() && group <= 8;
-}
-
 size_t decode_attention_ws_floats(int rows, int group, int H, int seq_stride, bool cross) {
   const int ns = decode_attention_splits(rows, group, H, seq_stride, cross);
-  return ns && !cross_in_one_wg(rows, group, H, seq_stride, ns) ? (size_t)rows * H * ns * kSplitRec : 0;
+  return ns ? (size_t)rows * H * ns * kSplitRec : 0;
 }
 
 void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int ldkv, int seq_stride, int group,
@@ -1247,21 +1102,6 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
   ATPU_CHECK(seq_stride <= kMaxKeys, "decode_attention: cache length above 2048");
   const int nseq = (rows + group - 1) / group;
   const int ns = decode_attention_splits(rows, group, H, seq_stride, lens != nullptr && !hist);
-  if (cross_in_one_wg(rows, group, H, seq_stride, ns)) {
-    ATPU_CHECK(ldq % 8 == 0 && (reinterpret_cast<uintptr_t>(q) & 15) == 0, "decode_attention: q needs 16-B rows");
-#define ATPU_DW(GM)                                                                                                \
-  hipLaunchKernelGGL((decode_cross_wg_kernel<GM>), dim3(nseq, H), dim3(kWgWaves * 64), 0, stream, q, ldq, k, v, ldkv, \
-                     seq_stride, group, rows, lens, bias_dist, bias_stride, out, ldo, scale)
-    if (group == 1)
-      ATPU_DW(1);
-    else if (group <= 4)
-      ATPU_DW(4);
-    else
-      ATPU_DW(8);
-#undef ATPU_DW
-    ATPU_HIP_CHECK(hipGetLastError());
-    return;
-  }
   if (ns > 0 && ws) {
     static_assert(kMaxSplits * kSplitKeys >= kMaxKeys, "combine kernel chunk count");
     ATPU_CHECK(ldq % 8 == 0 && (reinterpret_cast<uintptr_t>(q) & 15) == 0, "decode_attention: q needs 16-B rows");

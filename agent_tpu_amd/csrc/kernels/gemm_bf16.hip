@@ -37,16 +37,6 @@
 #ifndef ATPU_GEMM_SYNC_EPI
 #define ATPU_GEMM_SYNC_EPI 1
 #endif
-#ifndef ATPU_GEMM_EARLY_KT1
-#define ATPU_GEMM_EARLY_KT1 0
-#endif
-#ifndef ATPU_GEMM_DESYNC
-#define ATPU_GEMM_DESYNC 0
-#endif
-// persistent 256x256 kernel tile order: groups of this many tile rows (0 = row-major, N fastest)
-#ifndef ATPU_GEMM_GROUP
-#define ATPU_GEMM_GROUP 0
-#endif
 
 namespace atpu {
 namespace {
@@ -922,19 +912,12 @@ struct LnLds {
 // IN_ACC (InNorm): the caller started the accumulators at -mu*colsum (else the
 // epilogue applies -rstd*mu*colsum itself, from LDS colsum)
 // NOST (timing-only ablation, results WRONG): the output values are computed but not stored
-// EARLY: VMEM ops `early()` issues (the persistent kernel's next-tile K-tile-1 staging), called
-// after the residual loads are issued and BEFORE any store, so they are older than every
-// store; the counted residual waits see EARLY more younger ops
-struct NoEarly {
-  __device__ __forceinline__ void operator()() const {}
-};
-template <int EPI, bool NT, bool IN_ACC = true, int GM = 0, bool NOST = false, int EARLY = 0, typename F = NoEarly>
+template <int EPI, bool NT, bool IN_ACC = true, int GM = 0, bool NOST = false>
 __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int m0, int n0, int wm, int wn, int lane,
                                                   bf16* __restrict__ C, int ldc, const bf16* __restrict__ R, int ldr,
                                                   const float* lds_bias, char* scratch,
-                                                  const u32x4 (&pre)[2][2], LnLds ln = {}, F early = F{}) {
-  constexpr int kResWait = kLineResWait + EARLY;
-  static_assert(kResWait < 64, "vmcnt field is 6 bits on gfx950");
+                                                  const u32x4 (&pre)[2][2], LnLds ln = {}) {
+  constexpr int kResWait = kLineResWait;
   constexpr bool kIn = EPI & kEpiInNorm, kRes = EPI & kEpiResNorm, kSt = EPI & kEpiStatsOut;
   const int fr = lane & 15, fc = lane >> 4;
   // per-column LDS vectors (bias, colsum, gamma) at this lane's 4 columns of fragment j
@@ -981,11 +964,6 @@ __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int 
       res[i][0] = load16_untracked(rp);
       res[i][1] = load16_untracked(rp + 8 * (size_t)ldr);
     }
-  }
-  if constexpr (EARLY > 0) {
-    __builtin_amdgcn_sched_barrier(0);
-    early();  // after every load of the tail, before its first store (EARLY ops)
-    __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -1164,12 +1142,6 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
   const int wm = wave >> 2, wn = wave & 3;
   int v = blockIdx.x;
   if (v >= ntiles) return;
-#if ATPU_GEMM_DESYNC
-  // A/B experiment: every other CU of each XCD starts ATPU_GEMM_DESYNC x s_sleep(127) (~4 us
-  // each) late, so the CUs' tile epilogues (store bursts) stop coinciding
-  if ((blockIdx.x >> 3) & 1)
-    for (int i = 0; i < ATPU_GEMM_DESYNC; ++i) __builtin_amdgcn_s_sleep(127);
-#endif
 
   // staging rows of quarter q / instruction i (same map as 256p); the lane's
   // row is recomputed per tile (registers are the budget here), the LDS
@@ -1213,21 +1185,6 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
   // LDS, where the previous tile's last K-tile staged it) instead of adding it in the
   // epilogue: 16 fewer VGPRs and one op fewer per value pair on the epilogue chain
   constexpr bool kBiasAcc = (kRes || kSt) && (EPI & kEpiBias);
-  // Early K-tile-1 staging (ATPU_GEMM_EARLY_KT1, LN-folding variants; docs/PERF_NOTES.md round 4):
-  // vmcnt retires VMEM ops in issue order, so the wait that covers the next tile's K-tile-1
-  // quarters (staged during its K-tile 0) also waited for every epilogue store issued
-  // before them: the stores of a tile were exposed at K-tile 0 phase 2 of the next. Here
-  // the epilogue stages K-tile 1 of the next tile (into the buffer the last K-tile just
-  // freed) BEFORE its stores, K-tile 0 stages nothing, and its waits leave the stores in
-  // flight (they are the youngest ops); they are first retired at K-tile 1 phase 1,
-  // one and a half K-tiles after their issue. The last tile stages a dummy K-tile 1 of
-  // itself (same op counts), drained before the kernel exits.
-  constexpr bool kEarly = ATPU_GEMM_EARLY_KT1 && LINE && kPeel && DBG == 0 && !kInAcc;
-  constexpr int kEarlyOps = kEarly ? 8 : 0;  // 4 quarters x 2 DMA per wave
-  // VMEM ops issued at K-tile 0 phase 0 before its wait (this tile's bias -> LDS)
-  constexpr int kB0 = ((EPI & kEpiBias) && !kBiasAcc) ? 1 : 0;
-  // VMEM ops issued at K-tile 1 phase 0 before the staging: LN data staging (2), StatsOut flush (1)
-  constexpr int kLn1 = ((kRes || (kIn && !kInAcc)) ? 2 : 0) + (kSt ? 1 : 0);
   const bf16* src[4][2];
   uint32_t soff[4][2];
   auto set_src = [&](int tm0, int tn0) {
@@ -1330,7 +1287,7 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
   };
   int pm0 = 0, pn0 = 0;  // StatsOut: the tile whose row partials sit in LDS
 
-  int tile = group_tiles(xcd_remap(v, ntiles), ntm, ntn, ATPU_GEMM_GROUP);
+  int tile = xcd_remap(v, ntiles);
   int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 256;
   set_src(m0, n0);
   if constexpr (kBiasAcc) glds4(bias + n0 + (wave & 3) * 64, lds + kBiasOff + (wave & 3) * 256);
@@ -1405,15 +1362,13 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
       int kn = t + 1;  // K-tile staged during this one
       if (last && has_next) {
         // the stream runs on into K-tile 0 of the next tile
-        tile = group_tiles(xcd_remap(vn, ntiles), ntm, ntn, ATPU_GEMM_GROUP);
+        tile = xcd_remap(vn, ntiles);
         m0 = (tile / ntn) * 256;
         n0 = (tile % ntn) * 256;
         set_src(m0, n0);
         kn = 0;
       }
       const bool relax = is_t0 && !first;  // epilogue stores of the previous tile may be in flight
-      // kEarly: K-tile 1 was staged by the previous tile's epilogue (not for the first tile)
-      const bool pre_staged = kEarly && !first && (P == 0 || P == 1);
       // p0
       read_a(buf, 0);
       read_b(bl, buf, 0);
@@ -1439,80 +1394,33 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
           if (!first) ln_flush(pm0, pn0);
         }
       }
-      // kEarly, K-tile 0: outstanding (oldest first) Q2, Q3 of K-tile 0, the 8 K-tile-1 DMAs,
-      // the 16 stores, the bias DMA (kB0). Each wait retires the quarter read one phase
-      // later and leaves every younger op (stores included) in flight:
-      //   p0 -> Q2(0): 2 + 8 + 16 + kB0   p1 -> Q3(0): 8 + 16 + kB0
-      //   p2 -> Q0, Q1(1): 4 + 16 + kB0    p3 -> Q2(1): 2 + 16 + kB0
-      // K-tile 1, p0 -> Q3(1): 16 + kB0 + kLn1 + 2 (its own staging of K-tile 2); p1 -> nothing
-      // new (4 + 16 + kB0 + kLn1); the stores are retired at K-tile 1 p2 (vmcnt(4))
-      if constexpr (kEarly && P == 0) {
-        if (pre_staged) {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + 8 + kEpiOps + kB0) : "memory");
-        } else {
-          stage(0, kn, buf ^ 1);
-          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // first tile: no stores in flight
-        }
-      } else if (more) {
+      if (more) {
         stage(0, kn, buf ^ 1);
-        if constexpr (kEarly && P == 1) {
-          if (pre_staged) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kEpiOps + kB0 + kLn1 + 2) : "memory");
-          else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        } else {
-          if (relax) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + kEpiOps) : "memory");
-          else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        }
+        if (relax) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + kEpiOps) : "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
       }
       ATPU_PS_SYNC_MMA(bl, 0, 0);
       // p1
       read_b(br, buf, 1);
-      if constexpr (kEarly && P == 0) {
-        if (pre_staged) {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + kEpiOps + kB0) : "memory");
-        } else {
-          stage(1, kn, buf ^ 1);
-          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        }
-      } else if (more) {
+      if (more) {
         stage(1, kn, buf ^ 1);
-        if constexpr (kEarly && P == 1) {
-          // nothing older than the stores is still needed (Q3(1) retired at p0): the stores are
-          // first retired at p2, whose wait covers K-tile 2's Q0 (issued after them)
-          if (pre_staged) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + kEpiOps + kB0 + kLn1) : "memory");
-          else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        } else {
-          if (relax && !kEarly) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + kEpiOps) : "memory");
-          else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        }
+        if (relax) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + kEpiOps) : "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       ATPU_PS_SYNC_MMA(br, 0, 1);
       // p2
       read_a(buf, 1);
-      if constexpr (kEarly && P == 0) {
-        if (pre_staged) {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + kEpiOps + kB0) : "memory");
-        } else {
-          stage(2, kn, buf ^ 1);
-          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        }
-      } else if (more) {
+      if (more) {
         stage(2, kn, buf ^ 1);
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       }
       ATPU_PS_SYNC_MMA(br, 1, 1);
       // p3
-      if constexpr (kEarly && P == 0) {
-        if (pre_staged) {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + kEpiOps + kB0) : "memory");
-        } else {
-          stage(3, kn, buf ^ 1);
-          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        }
-      } else if (more) {
+      if (more) {
         stage(3, kn, buf ^ 1);
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       }
@@ -1572,20 +1480,12 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
       // tile-loop structure, the plain epilogue (no LN math, no statistics)
       constexpr int kEpiRun0 = kBiasAcc ? (EPI & ~kEpiBias) : EPI;
       constexpr int kEpiRun = (DBG & 8) ? (kEpiRun0 & ~(kEpiInNorm | kEpiResNorm | kEpiStatsOut)) : kEpiRun0;
-      // kEarly: the next tile's K-tile 1 into the buffer the last K-tile freed (buf ^ 1 after the
-      // flip; a dummy K-tile 1 of this tile when there is no next one: same op count)
-      const int ebuf = buf ^ 1;
-      auto early = [&] {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) stage(q, 1, ebuf);
-      };
       if constexpr (LINE)
-        epilogue_256_line<kEpiRun, NT, kInAcc, ((DBG >> 5) & 3), bool(DBG & 256), kEarlyOps>(
+        epilogue_256_line<kEpiRun, NT, kInAcc, ((DBG >> 5) & 3), bool(DBG & 256)>(
             acc, cm0, cn0, wm, wn, (kIn || kRes || kSt) ? opaque_lane() : lane, C, ldc, R, ldr,
             reinterpret_cast<const float*>(lds + kBiasOff) + tile_par * 256, lds + kEpiOff + wave * 2048, pre,
             LnLds{reinterpret_cast<const float*>(lds + kFinOff + (kInAcc ? tile_par * 2048 : 0)),
-                  reinterpret_cast<const float*>(lds + kColOff), reinterpret_cast<float*>(lds + kStOff)},
-            early);
+                  reinterpret_cast<const float*>(lds + kColOff), reinterpret_cast<float*>(lds + kStOff)});
       else
         epilogue_256<EPI, true, (DBG >> 1), NT>(acc, cm0, cn0, wm, wn, lane, C, ldc, bias, R, ldr, M,
                                             reinterpret_cast<const float*>(lds + kBiasOff) + tile_par * 256);
@@ -1603,8 +1503,6 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
   }
 #undef ATPU_PS_SYNC_MMA
   if (wm == 0) __builtin_amdgcn_s_barrier();  // close the stagger (equal barrier counts)
-  // kEarly: the last tile's dummy K-tile-1 DMAs land in LDS before the workgroup exits
-  if constexpr (kEarly) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr (kSt) {
     // the last tile's row partials: every wave's epilogue LDS writes done, then flushed
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -2303,14 +2201,7 @@ constexpr int gemv_u(int K) { return K <= 64 * 8 * 3 ? 3 : 6; }
 // Prefetch of the next GEMV's weight (PF): one extra wave per workgroup (l2_prefetch.h). A 4-row
 // GEMV on L2-resident weights ran 3.6-4.5 us against 4.9-7.5 us from HBM.
 using GemvPf = L2Pf;
-// A/B build switches (python -m agent_tpu_amd.csrc.build -D NAME=V --out ...)
-#ifndef ATPU_GEMV_BFLY
-#define ATPU_GEMV_BFLY 1  // butterfly reduction of the GEMV partials (0: 16 wave sums)
-#endif
-#ifndef ATPU_GEMV_EARLY
-#define ATPU_GEMV_EARLY 1  // epilogue operands loaded before the main loop: 0 never, 1 LN-folded, 2 all,
-                           // 3 LN-folded before, the rest right after the first round's loads
-#endif
+// tuning constants (python -m agent_tpu_amd.csrc.build -D NAME=V --out ...)
 #ifndef ATPU_GEMV_NWV
 #define ATPU_GEMV_NWV 4  // waves (4-column groups) per workgroup of the unsplit GEMVs but RowStats
 #endif
@@ -2321,18 +2212,11 @@ constexpr int kGemvNwv = ATPU_GEMV_NWV;
 #ifndef ATPU_GEMV_KS
 #define ATPU_GEMV_KS 2  // K slices of the split GEMV
 #endif
-#ifndef ATPU_GEMV_KS_STATS
-#define ATPU_GEMV_KS_STATS 0  // split the RowRms / RowLn GEMVs too (row statistics summed with the
-                              // partials): 1-doc BART / T5 within noise (profiles/gemv_ksplit_ab_r04.txt)
-#endif
 #ifndef ATPU_GEMV_KS_MINK
 #define ATPU_GEMV_KS_MINK 512  // split K above this
 #endif
 constexpr int kGemvKs = ATPU_GEMV_KS, kGemvKsU = 4096 / (512 * ATPU_GEMV_KS);  // K = 4096: one round
 constexpr int kKsNwv = ATPU_GEMV_KS_NWV;
-#ifndef ATPU_GEMV_PF_RS
-#define ATPU_GEMV_PF_RS 0  // L2 prefetch from RowStats GEMVs too
-#endif
 
 // BART's LayerNorm folding (RowLn / ResLn / RowStats, see LnDec): the row statistics come
 // from the <= 32 slab partials (lane = slab, wave sums); RowStats workgroups are 8 waves =
@@ -2373,12 +2257,9 @@ __global__ __launch_bounds__((NWV * KS + PF) * 64) void gemv_kernel(const bf16* 
   // are loaded before the main loop and arrive under it instead of as a dependent round trip
   // after the reductions: BART 1-doc 8.5 -> 8.8 docs/s; for the T5 epilogues (RowRms, ReLU,
   // residual, KV scatter) the same early loads measured slower (12.3 -> 11.7), so those load
-  // in the epilogue (profiles/summarize_1doc_gemv_early_loads_r04.txt)
-  constexpr bool kLn = (EPI & (kEpiRowLn | kEpiResLn)) != 0;
-  constexpr bool kEarly = ATPU_GEMV_EARLY == 2 || ((ATPU_GEMV_EARLY == 1 || ATPU_GEMV_EARLY == 3) && kLn);
-  // ATPU_GEMV_EARLY == 3: the other epilogues load theirs right after the first round's weight
-  // and A loads (younger than them, so the main loop's counted waits do not wait for them)
-  constexpr bool kMid = ATPU_GEMV_EARLY == 3 && !kLn;
+  // in the epilogue (profiles/summarize_1doc_gemv_early_loads_r04.txt; issued right after the
+  // first round's loads instead: also slower, profiles/summarize_1doc_gemv_mid_loads_ab_r04.txt)
+  constexpr bool kEarly = (EPI & (kEpiRowLn | kEpiResLn)) != 0;
   const int mo = lane >> 4, jo = (lane >> 2) & 3;  // the reduction's output lanes (below)
   const bool mine = mo < M && (lane & 3) == 0;
   const int om = min(mo, M - 1), n = n0 + jo;  // (clamped) output row
@@ -2424,9 +2305,6 @@ __global__ __launch_bounds__((NWV * KS + PF) * 64) void gemv_kernel(const bf16* 
       for (int m = 0; m < kGemvRows; ++m)
         av[u][m] = *reinterpret_cast<const bf16x8*>(A + (size_t)min(m, M - 1) * lda + c * 8);
     }
-    if constexpr (kMid) {
-      if (base == 0) epi_loads();
-    }
     // every load of the round is issued before the first use: left alone, the scheduler issued
     // them in groups of 8 with a full wait in between (U serialised memory latencies)
     __builtin_amdgcn_sched_barrier(0);
@@ -2456,21 +2334,7 @@ __global__ __launch_bounds__((NWV * KS + PF) * 64) void gemv_kernel(const bf16* 
   // step (two permlane swaps, then xor shuffles): 17 cross-lane ops instead of 16 x 6, and
   // lanes 4i..4i+3 end with output i = m*4 + j (RowRms: lanes 16m.. with row m's sum of squares)
   float v, rs = 0.f;
-  if constexpr (!ATPU_GEMV_BFLY) {  // A/B build: 16 (+4) independent wave sums
-    v = 0.f;
-#pragma unroll
-    for (int m = 0; m < kGemvRows; ++m) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float t = wave_sum(acc[m][j]);
-        v = (mo == m && jo == j) ? t : v;
-      }
-      if constexpr (EPI & kEpiRowRms) {
-        const float t = wave_sum(ssq[m]);
-        rs = mo == m ? t : rs;
-      }
-    }
-  } else {
+  {
     float a16[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) a16[i] = acc[i >> 2][i & 3];
@@ -2480,14 +2344,7 @@ __global__ __launch_bounds__((NWV * KS + PF) * 64) void gemv_kernel(const bf16* 
   // (sum, sum of squares) of A's rows (RowLn) or R's rows (ResLn), row mo
   float S = 0.f, Q = 0.f;
   if constexpr (EPI & (kEpiRowLn | kEpiResLn)) {
-    if constexpr (!ATPU_GEMV_BFLY) {
-#pragma unroll
-      for (int r = 0; r < kGemvRows; ++r) {
-        const float s0 = wave_sum(e_part[r].x), q0 = wave_sum(e_part[r].y);
-        S = mo == r ? s0 : S;
-        Q = mo == r ? q0 : Q;
-      }
-    } else {
+    {
       // the 8 sums (row r: S = 2r, Q = 2r + 1) by the same butterfly as the outputs: lane l
       // ends with sum l >> 3, i.e. row l >> 4 (= mo), its partner lane l ^ 8 the other one
       float a8[8];
@@ -2547,7 +2404,7 @@ __global__ __launch_bounds__((NWV * KS + PF) * 64) void gemv_kernel(const bf16* 
       }
     }
   }
-  if constexpr (!kEarly && !kMid) epi_loads();
+  if constexpr (!kEarly) epi_loads();
   float f = 0.f;  // RowStats: the stored (bf16-rounded) value
   if (mine) {
     if constexpr (EPI & kEpiRowRms) v *= __builtin_amdgcn_rsqf(rs * (1.f / K) + rms_eps);
@@ -2619,11 +2476,10 @@ void launch_gemv(const GemmArgs& g, hipStream_t s) {
     const char* f = std::getenv("ATPU_GEMV_PREFETCH");
     return !(f && f[0] == '0');
   }();
-  // not from RowStats GEMVs (A/B build ATPU_GEMV_PF_RS=1: their prefetch wave takes the slab
-  // barrier before draining its loads; with __syncthreads it drained them first, BART 1-doc
-  // 8.20 -> 7.98 docs/s): their 32 workgroups would stream the next weight alone, and the
-  // kernel ends only when the prefetch waves do
-  const bool pf = pf_on && g.pf_w && g.pf_n > 0 && g.pf_k > 0 && (ATPU_GEMV_PF_RS || !(g.epi & kEpiRowStats));
+  // not from RowStats GEMVs (measured: BART 1-doc 8.20 -> 7.98 docs/s with it, round 4): their
+  // 32 workgroups would stream the next weight alone, and the kernel ends only when the
+  // prefetch waves do
+  const bool pf = pf_on && g.pf_w && g.pf_n > 0 && g.pf_k > 0 && !(g.epi & kEpiRowStats);
   const GemvPf pfa{g.pf_w, g.pf_ld, g.pf_k, g.pf_n, g.pf_rpb > 0 ? g.pf_rpb : 16};
   const bool u6 = gemv_u(g.K) == 6;
   static const bool ks_on = [] {
@@ -2651,7 +2507,7 @@ void launch_gemv(const GemmArgs& g, hipStream_t s) {
   case E: {                                                                                                     \
     constexpr int nwv = ((E) & kEpiRowStats) ? 8 : kGemvNwv;                                                    \
     constexpr int kU6 = nwv < 8 ? 6 : 3;                                                                        \
-    constexpr bool kKs = !((E) & kEpiRowStats) && (ATPU_GEMV_KS_STATS || !((E) & (kEpiRowRms | kEpiRowLn)));    \
+    constexpr bool kKs = !((E) & (kEpiRowStats | kEpiRowRms | kEpiRowLn));                                      \
     if (kKs && ks2) {                                                                                           \
       if (pf) {                                                                                                 \
         if (ks_u1) ATPU_GEMV_GO_KS(E, 1, true);                                                                 \
@@ -2710,6 +2566,14 @@ bool gemv_has_case(int epi) {
 }
 
 }  // namespace
+
+bool gemv_selected(int M, int N, int epi) {
+  GemmArgs g;
+  g.M = M;
+  g.N = N;
+  g.epi = epi;
+  return gemv_ok(g) && gemv_has_case(epi);
+}
 
 void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
   ATPU_CHECK(g.M > 0 && g.N > 0 && g.K > 0, "gemm: empty problem");

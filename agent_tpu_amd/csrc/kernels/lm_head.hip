@@ -225,297 +225,6 @@ __global__ __launch_bounds__(BM / 32 * 64, (BM + kBN) * kRowB * NST <= 80 * 1024
   }
 }
 
-// ---------------------------------------------------------------------------
-// lm_head_wide_kernel: the same per-(row, slab) partials for step batches of many rows
-// (BART / T5 at 256 documents x 4 beams = 1024 rows), from 256 x 160 (rows x vocabulary)
-// tiles. The 128 x 128 kernel above runs 4 waves of 32 x 128: 10 fragment reads per 16
-// MFMAs, every wave re-reading the whole vocabulary slab, and two workgroups per CU
-// for latency; its mainloop holds ~0.6 PF. Here:
-//  * 4 waves (one per SIMD) of 64 rows x 160 vocabulary columns: 14 reads per 40 MFMAs,
-//    160 fp32 accumulators per lane (the 512-register file of a lone wave: AGPRs);
-//  * a 3-slot LDS ring of 64-deep K-tiles (3 x 52 KiB) fed by LDS-DMA two K-tiles ahead,
-//    one barrier per K-tile placed between the two 32-deep halves: the reads of the
-//    next K-tile's first half are issued under the MFMAs of this one's second half;
-//  * persistent: one workgroup per CU walks tiles b, b + G, ... and the DMA stream runs
-//    straight on into the next tile's K-tiles, so they load under this tile's epilogue;
-//    the M tiles of one vocabulary panel are consecutive under xcd_remap (one XCD, the
-//    panel read from HBM once); 1024 x 50264 makes 4 x 315 tiles, 4.9 per CU;
-//  * the epilogue is the 128 x 128 kernel's (per row: max, sum exp, ban / EOS masks,
-//    candidate set), with 160-column slabs; all of a row's columns of the tile sit in one
-//    wave, so there is no cross-wave step.
-// The MFMA order per output (K ascending, 32 at a time) and the RMS statistics are the
-// 128 x 128 kernel's: logits, tokens and scores are bit-identical to it.
-constexpr int kWM = 256, kWN = 160, kWNst = 3;
-constexpr int kWTN = kWN / 16;                // vocabulary fragments per wave
-constexpr int kWStage = (kWM + kWN) * kRowB;  // 53248 B
-constexpr int kWLps = (kWM + kWN) / 32;       // LDS-DMA instructions per wave per K-tile (8 rows each)
-constexpr int kWLpsA = kWM / 32;              // the first 8 of them stage A rows
-static_assert(kWNst * kWStage <= 160 * 1024, "LDS ring");
-
-template <int OFF>
-__device__ __forceinline__ bf16x8 lds_read128_off(unsigned a) {
-  bf16x8 r;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(OFF));
-  return r;
-}
-template <int OFF0, int STEP, int N, int... I>
-__device__ __forceinline__ void lds_read_frags(bf16x8 (&f)[N], unsigned a, std::integer_sequence<int, I...>) {
-  ((f[I] = lds_read128_off<OFF0 + I * STEP>(a)), ...);
-}
-// fragment F of a K-tile half: F < 4 the A rows, else vocabulary fragment F - 4
-template <int F>
-__device__ __forceinline__ void read_frag(unsigned xba, unsigned xbb, bf16x8 (&xa)[4], bf16x8 (&xb)[kWTN]) {
-  if constexpr (F < 4)
-    xa[F] = lds_read128_off<F * 16 * kRowB>(xba);
-  else
-    xb[F - 4] = lds_read128_off<(kWM + (F - 4) * 16) * kRowB>(xbb);
-}
-template <class Fn, int... I>
-__device__ __forceinline__ void static_for_impl(Fn&& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, class Fn>
-__device__ __forceinline__ void static_for(Fn&& f) {
-  static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
-// s_waitcnt lgkmcnt(N) that a fragment set passes through (its consumers cannot move above it)
-template <int N>
-__device__ __forceinline__ void lds_wait14(bf16x8 (&a)[4], bf16x8 (&b)[kWTN]) {
-  asm volatile("s_waitcnt lgkmcnt(%14)"
-               : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]),
-                 "+v"(b[4]), "+v"(b[5]), "+v"(b[6]), "+v"(b[7]), "+v"(b[8]), "+v"(b[9])
-               : "n"(N)
-               : "memory");
-}
-
-template <bool RMS, bool BIAS, bool BANS>
-__global__ __launch_bounds__(256, 1) void lm_head_wide_kernel(
-    const bf16* __restrict__ A, int lda, const bf16* __restrict__ W, int ldw, const float* __restrict__ bias,
-    float rms_eps, int M, int V, int K, const uint32_t* __restrict__ ban_bits, int ban_ld, int eos, int mask_eos,
-    float4* __restrict__ hdr, float2* __restrict__ cand) {
-  __shared__ __attribute__((aligned(16))) char lds[kWNst * kWStage];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int ntm = (M + kWM - 1) / kWM, ntn = (V + kWN - 1) / kWN, ntiles = ntm * ntn;
-  const int G = gridDim.x, b = blockIdx.x;  // G <= ntiles: every workgroup has a tile
-  const int nk = K / kBK;
-  const int ntl = (ntiles - b + G - 1) / G;
-  const int nstage = ntl * nk;  // this workgroup's K-tiles, all tiles in sequence
-
-  // staged row r = (i*4 + wave)*8 + srow (i < 8: A rows, else vocabulary rows r - 256);
-  // its swizzle (r >> 1) & 7 = (srow >> 1) + 4 (wave & 1) does not depend on i
-  const int srow = lane >> 3;
-  const int sw = ((lane & 7) ^ (((srow >> 1) + 4 * (wave & 1)) & 7)) * 8;
-  auto tile_of = [&](int t) { return xcd_remap(b + t * G, ntiles); };
-  // a K-tile's 13 LDS-DMAs, issued one at a time between MFMAs: lane row b0 + 32 i of the
-  // tile (clamped to the last row / vocabulary entry: branch-free tails), scalar tile / K bases
-  const int b0 = wave * 8 + srow;
-  struct StageP {
-    const char *a, *w;
-    char* l;
-    int lima, limw;
-    bool live;
-  };
-  auto plan = [&](int s) {  // wave-uniform s
-    StageP p{};
-    p.live = s < nstage;
-    if (!p.live) return p;
-    const int t = s / nk, kt = s - t * nk;
-    const int tile = tile_of(t);
-    const int m0 = (tile % ntm) * kWM, n0 = (tile / ntm) * kWN;
-    p.lima = M - 1 - m0;
-    p.limw = V - 1 - n0;
-    p.a = reinterpret_cast<const char*>(A + (size_t)m0 * lda + kt * kBK);
-    p.w = reinterpret_cast<const char*>(W + (size_t)n0 * ldw + kt * kBK);
-    p.l = lds + (s % kWNst) * kWStage + wave * 8 * kRowB;
-    return p;
-  };
-  auto dma = [&](const StageP& p, auto ic) {
-    constexpr int i = decltype(ic)::value;
-    if (!p.live) return;
-    if constexpr (i < kWLpsA) {
-      const unsigned r = min(b0 + 32 * i, p.lima);
-      glds16(p.a + (r * (unsigned)lda + sw) * 2u, p.l + i * 32 * kRowB);
-    } else {
-      const unsigned r = min(b0 + 32 * (i - kWLpsA), p.limw);
-      glds16(p.w + (r * (unsigned)ldw + sw) * 2u, p.l + i * 32 * kRowB);
-    }
-  };
-  auto stage = [&](int s) {
-    const StageP p = plan(s);
-    static_for<kWLps>([&](auto ic) { dma(p, ic); });
-  };
-
-  // fragment reads: A rows wave*64 + i*16 + fr, vocabulary rows 256 + j*16 + fr; swizzle fr >> 1
-  const int fr = lane & 15, fc = lane >> 4;
-  const int rdo = fr * kRowB;
-  const int sx = fr >> 1;
-  // by inline asm with counted waits (lds_wait14): for compiler-visible reads the waitcnt pass
-  // put an lgkmcnt(0) in front of the first MFMA, i.e. waited for the other half's 14 reads too
-  auto rd_base = [&](int s, int ks) {
-    return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)lds + (s % kWNst) * kWStage + rdo +
-           (((ks * 4 + fc) ^ sx) * 16);
-  };
-  auto rd = [&](int s, int ks, bf16x8 (&af)[4], bf16x8 (&bw)[kWTN]) {
-    const unsigned base = rd_base(s, ks);
-    const unsigned ba = base + wave * 64 * kRowB;
-    lds_read_frags<0, 16 * kRowB>(af, ba, std::make_integer_sequence<int, 4>{});
-    lds_read_frags<kWM * kRowB, 16 * kRowB>(bw, base, std::make_integer_sequence<int, kWTN>{});
-  };
-
-  f32x4 acc[4][kWTN];
-  float ssq[4];
-  bf16x8 xa[4], xb[kWTN], ya[4], yb[kWTN];
-  auto mma = [&](const bf16x8 (&af)[4], const bf16x8 (&bw)[kWTN]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if constexpr (RMS) ssq[i] = sumsq_chunk(af[i], ssq[i]);
-#pragma unroll
-      for (int j = 0; j < kWTN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af[i], acc[i][j], 0, 0, 0);
-    }
-  };
-
-  stage(0);
-  stage(1);
-  stage(2);
-  if (nstage >= 3)
-    wait_vm<2 * kWLps>();
-  else if (nstage == 2)
-    wait_vm<kWLps>();
-  else
-    wait_vm<0>();
-  asm volatile("s_barrier" ::: "memory");
-  rd(0, 0, xa, xb);
-  lds_wait14<0>(xa, xb);
-
-  int g = 0;  // K-tile of the stream
-  for (int t = 0; t < ntl; ++t) {
-    const int tile = tile_of(t);
-    const int m0 = (tile % ntm) * kWM, n0 = (tile / ntm) * kWN;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      ssq[i] = 0.f;
-#pragma unroll
-      for (int j = 0; j < kWTN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    for (int kt = 0; kt < nk; ++kt, ++g) {
-      rd(g, 1, ya, yb);
-      lds_wait14<14>(xa, xb);  // this half's reads, issued before the other half's
-      mma(xa, xb);
-      __builtin_amdgcn_sched_barrier(0);
-      // every wave's reads of slot g are done (its second half was read before the MFMAs
-      // above) and K-tile g+1 has landed: VMEM ops younger than its DMAs are K-tile g+2's,
-      // or, right after an epilogue, that epilogue's loads and stores (then drain all)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (kt == 0 && t > 0)
-        wait_vm<0>();
-      else if (g + 2 < nstage)
-        wait_vm<kWLps>();
-      else
-        wait_vm<0>();
-      asm volatile("s_barrier" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      // the second half's 40 MFMAs in 10 vocabulary-fragment groups; ahead of each group one
-      // or two of K-tile g+3's DMAs and of K-tile g+1's first-half reads, so the issue slots
-      // of the 13 DMAs (and their address math) and 14 reads hide under MFMAs
-      const StageP sp = plan(g + 3);
-      const bool more = g + 1 < nstage;
-      const unsigned xbb = more ? rd_base(g + 1, 0) : 0u, xba = xbb + wave * 64 * kRowB;
-      lds_wait14<14>(ya, yb);  // retired by the lgkmcnt(0) above; ties the registers
-      static_for<kWTN>([&](auto jc) {
-        constexpr int j = decltype(jc)::value;
-        if constexpr (j < 3) {
-          dma(sp, std::integral_constant<int, 2 * j>{});
-          dma(sp, std::integral_constant<int, 2 * j + 1>{});
-        } else {
-          dma(sp, std::integral_constant<int, j + 3>{});
-        }
-        if (more) {
-          if constexpr (j < 4) {
-            read_frag<2 * j>(xba, xbb, xa, xb);
-            read_frag<2 * j + 1>(xba, xbb, xa, xb);
-          } else {
-            read_frag<j + 4>(xba, xbb, xa, xb);
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if constexpr (RMS && j == 0) ssq[i] = sumsq_chunk(ya[i], ssq[i]);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(yb[j], ya[i], acc[i][j], 0, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      });
-    }
-
-    // ---------------------------------------------------------------- epilogue
-    // lane (fr, fc) holds rows m0 + wave*64 + i*16 + fr, columns n0 + j*16 + fc*4 + e
-    const int c0 = n0, slab = tile / ntm;
-    const bool tail = c0 + kWN > V;
-    const bool eos_here = mask_eos && eos >= c0 && eos < c0 + kWN;
-    f32x4 bv[kWTN];
-#pragma unroll
-    for (int j = 0; j < kWTN; ++j) {
-      const int n = c0 + j * 16 + fc * 4;
-      bv[j] = (BIAS && n < V) ? *reinterpret_cast<const f32x4*>(bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + wave * 64 + i * 16 + fr;
-      const bool live = m < M;
-      const float rs = RMS ? __builtin_amdgcn_rsqf(lane_rows_sum(ssq[i]) * (1.f / K) + rms_eps) : 1.f;
-      float v[kWTN][4];
-      float mx = -FLT_MAX;
-#pragma unroll
-      for (int j = 0; j < kWTN; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float x = acc[i][j][e];
-          if constexpr (RMS) x *= rs;
-          if constexpr (BIAS) x += bv[j][e];
-          if (tail && c0 + j * 16 + fc * 4 + e >= V) x = -FLT_MAX;
-          v[j][e] = x;
-          mx = fmaxf(mx, x);
-        }
-      const float rmax = lane_rows_max(mx);
-      const float mb = rmax * kLog2e;
-      float s = 0.f;
-#pragma unroll
-      for (int j = 0; j < kWTN; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) s += __builtin_amdgcn_exp2f(fmaf(v[j][e], kLog2e, -mb));
-      s = lane_rows_sum(s);
-      if constexpr (BANS) {
-        // the slab's 5 bitmap words of row m (word j >> 1 covers fragments j, j + 1)
-        uint32_t wd[kWN / 32];
-        const uint32_t* bp = ban_bits + (size_t)min(m, M - 1) * ban_ld + c0 / 32;
-        uint32_t any = 0u;
-#pragma unroll
-        for (int w = 0; w < kWN / 32; ++w) {
-          wd[w] = c0 + w * 32 < V ? bp[w] : 0u;  // words past the vocabulary are past the row
-          any |= wd[w];
-        }
-        if (__ballot(any != 0u)) {
-#pragma unroll
-          for (int j = 0; j < kWTN; ++j)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if ((wd[j >> 1] >> ((j & 1) * 16 + fc * 4 + e)) & 1u) v[j][e] = -FLT_MAX;
-        }
-      }
-      if (eos_here) {
-#pragma unroll
-        for (int j = 0; j < kWTN; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (c0 + j * 16 + fc * 4 + e == eos) v[j][e] = -FLT_MAX;
-      }
-      const size_t slot = (size_t)min(m, M - 1) * ntn + slab;
-      tile_row_emit<kWTN>(v, c0, fc, live, rmax, s, hdr + slot, cand + slot * kTileCand);
-    }
-  }
-}
-
 constexpr int kMergeThreads = 256;
 
 __global__ __launch_bounds__(kMergeThreads) void lm_head_merge_kernel(const float4* __restrict__ hdr,
@@ -679,19 +388,6 @@ int lm_head_stages(int set) {
 #endif
 }
 
-// 256 x 160 persistent kernel for step batches of >= kWideMinRows rows: ATPU_LM_WIDE=1 or
-// lm_head_wide(1) (default off until it beats the 128 x 128 kernel: docs/PERF_NOTES.md)
-constexpr int kWideMinRows = 512;
-
-int lm_head_wide(int set) {
-  static int v = [] {
-    const char* f = std::getenv("ATPU_LM_WIDE");
-    return (f && f[0] == '1') ? 1 : 0;
-  }();
-  if (set == 0 || set == 1) v = set;
-  return v;
-}
-
 // workspace: per-slab headers and candidates (slabs of 64 columns at the finest), the ban bitmap
 size_t lm_head_ws_bytes(int M, int V) {
   const size_t slabs = (size_t)M * ((V + 63) / 64);
@@ -713,8 +409,7 @@ void lm_head_topk(const bf16* A, int lda, const bf16* W, int ldw, const float* b
   ATPU_CHECK(nbmax >= 0 && (nbmax == 0 || bans), "lm_head_topk: ban list");
   ATPU_CHECK(ngram <= 0 || (seq && cur <= seq_stride), "lm_head_topk: n-gram bans need the token history [rows, >= cur]");
   const int cfg = lm_head_stages(-1);
-  const bool wide = lm_head_wide(-1) && M >= kWideMinRows;
-  const int wc = wide ? kWN : (cfg >= 4) ? 64 : 128;  // vocabulary columns per partial slab (the wave's columns)
+  const int wc = (cfg >= 4) ? 64 : 128;  // vocabulary columns per partial slab (the wave's columns)
   const int nslab = (V + wc - 1) / wc;
   const int ntn = (V + kBN - 1) / kBN;
   ATPU_CHECK((long long)((M + 127) / 128) * ntn < (1ll << 31), "lm_head_topk: grid too large");
@@ -730,7 +425,6 @@ void lm_head_topk(const bf16* A, int lda, const bf16* W, int ldw, const float* b
     hipLaunchKernelGGL(ban_bitmap_kernel, dim3(M), dim3(256), (size_t)ld * 4, stream, V, ld, bans, nbmax, seq,
                        seq_stride, cur, ngram, bits);
   }
-  const int ntiles_w = ((M + kWM - 1) / kWM) * ((V + kWN - 1) / kWN);
   const bool rms = rms_eps > 0.f, has_bias = bias != nullptr;
   ATPU_CHECK(!(rms && has_bias), "lm_head_topk: RMSNorm folding and a bias together are not instantiated");
 #define ATPU_LM(R, B, X, BM, N, WN)                                                                              \
@@ -758,32 +452,12 @@ void lm_head_topk(const bf16* A, int lda, const bf16* W, int ldw, const float* b
       ATPU_LM(R, B, X, 128, 2, 1);    \
   }
 #else
-  // one row tile (<= 128 rows: the 1-document step) with ATPU_LM_SMALL_RING=4: a 4-slot ring (one
-  // workgroup per CU, three K-tiles in flight). Measured (profiles/lm_head_small_ring_ab_r04.txt):
-  // T5 1-doc 14.52 -> 14.57 docs/s (noise), BART 11.07 -> 10.90 (its 393 vocabulary tiles take two
-  // rounds at one workgroup per CU): 2 slots stay the default
-  static const int small_ring = [] {
-    const char* f = std::getenv("ATPU_LM_SMALL_RING");
-    return (f && f[0] == '4') ? 4 : 2;
-  }();
-#define ATPU_LM_CFG(R, B, X)            \
-  if (M <= 128 && small_ring == 4) {    \
-    ATPU_LM(R, B, X, 128, 4, 1);        \
-  } else {                              \
-    ATPU_LM(R, B, X, 128, 2, 1);        \
-  }
+  // (a 4-slot ring for the one-row-tile step measured within noise for T5 and slower for BART,
+  // profiles/lm_head_small_ring_ab_r04.txt)
+#define ATPU_LM_CFG(R, B, X) ATPU_LM(R, B, X, 128, 2, 1);
 #endif
-#define ATPU_LM_WIDE(R, B, X)                                                                                    \
-  hipLaunchKernelGGL((lm_head_wide_kernel<R, B, X>), dim3(std::min(ntiles_w, num_cus())), dim3(256), 0, stream, A,    \
-                     lda, W, ldw, bias, rms_eps, M, V, K, bits, ld, eos, mask_eos, hdr, cand)
 #define ATPU_LM_BANS(R, B)        \
-  if (wide) {                     \
-    if (any_bans) {               \
-      ATPU_LM_WIDE(R, B, true);   \
-    } else {                      \
-      ATPU_LM_WIDE(R, B, false);  \
-    }                             \
-  } else if (any_bans) {          \
+  if (any_bans) {                 \
     ATPU_LM_CFG(R, B, true)       \
   } else {                        \
     ATPU_LM_CFG(R, B, false)      \
@@ -796,7 +470,6 @@ void lm_head_topk(const bf16* A, int lda, const bf16* W, int ldw, const float* b
     ATPU_LM_BANS(false, false)
   }
 #undef ATPU_LM_BANS
-#undef ATPU_LM_WIDE
 #undef ATPU_LM_CFG
 #undef ATPU_LM
   hipLaunchKernelGGL(lm_head_merge_kernel, dim3(M), dim3(kMergeThreads), 0, stream, hdr, cand, nslab, beam_scores,

@@ -25,21 +25,6 @@
 
 #include <algorithm>
 
-// timing-only ablations (A/B builds, results WRONG): 1 = no attention (images + barriers),
-// 2 = no softmax (P = raw scores), 4 = no context stores, 5 = no P.V (no V reads), 6 = no QK^T
-// (no K reads)
-#ifndef ATPU_QA_ABL
-#define ATPU_QA_ABL 0
-#endif
-// context stores non-temporal (A/B)
-// tile order: groups of this many 256-row blocks (0 = row-major, heads fastest)
-#ifndef ATPU_QA_GROUP
-#define ATPU_QA_GROUP 0
-#endif
-#ifndef ATPU_QA_NT
-#define ATPU_QA_NT 0
-#endif
-
 namespace atpu {
 namespace {
 
@@ -251,8 +236,7 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
 #pragma unroll
       for (int ds = 0; ds < 2; ++ds) {
         const int r = kt * 16 + fr;
-        if constexpr (ATPU_QA_ABL == 6) kf[kt][ds] = qf[ds][ds];
-        else kf[kt][ds] = ds_read128(ki + r * 128 + asw(r, ds * 4 + fc) * 16);
+        kf[kt][ds] = ds_read128(ki + r * 128 + asw(r, ds * 4 + fc) * 16);
       }
     // 20 reads in flight, retired in issue order: K-tile kt's MFMAs wait for lgkmcnt(14 - 2 kt).
     // Phase A: S(qp 0) = K.Q0^T, counted waits.
@@ -265,12 +249,8 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
       } else {
         lgkm_wait<14 - 2 * kt>(kf[kt][0], kf[kt][1]);
       }
-      if constexpr (ATPU_QA_ABL == 6) {
-        s[0][kt] = f32x4{(float)kf[kt][0][kt], (float)kf[kt][1][kt], 0.f, 1.f};
-      } else {
-        s[0][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][0], qf[0][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        s[0][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][1], qf[0][1], s[0][kt], 0, 0, 0);
-      }
+      s[0][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][0], qf[0][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      s[0][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][1], qf[0][1], s[0][kt], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);  // K-tile kt's MFMAs before the next wait
     };
     qk0(std::integral_constant<int, 0>{});
@@ -297,7 +277,7 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
       }
     };
     auto softmax = [&](int qp) {
-      if constexpr (ATPU_QA_ABL != 2) {
+      {
         float mx = -1e30f;
 #pragma unroll
         for (int kt = 0; kt < 8; ++kt)
@@ -324,12 +304,8 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
     // vector issue free for half its cycles)
 #pragma unroll
     for (int kt = 0; kt < 8; ++kt) {
-      if constexpr (ATPU_QA_ABL == 6) {
-        s[1][kt] = f32x4{(float)qf[1][0][kt], (float)qf[1][1][kt], 0.f, 1.f};
-      } else {
-        s[1][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][0], qf[1][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        s[1][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][1], qf[1][1], s[1][kt], 0, 0, 0);
-      }
+      s[1][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][0], qf[1][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      s[1][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][1], qf[1][1], s[1][kt], 0, 0, 0);
     }
     softmax(0);
 #pragma unroll
@@ -351,13 +327,8 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
           const int c = asw(k0, dt * 2 + (tp >> 1)) * 16;
-          if constexpr (ATPU_QA_ABL == 5) {
-            vlo[ks][dt] = bf16x4{(bf16)(float)c, (bf16)0.f, (bf16)0.f, (bf16)0.f};
-            vhi[ks][dt] = vlo[ks][dt];
-          } else {
-            vlo[ks][dt] = tr16(row + ks * 32 * 128 + c);
-            vhi[ks][dt] = tr16(row + (ks * 32 + 16) * 128 + c);
-          }
+          vlo[ks][dt] = tr16(row + ks * 32 * 128 + c);
+          vhi[ks][dt] = tr16(row + (ks * 32 + 16) * 128 + c);
         }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -390,10 +361,7 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
                                 "+v"(vhi[3][0]), "+v"(vhi[3][1]), "+v"(vhi[3][2]), "+v"(vhi[3][3])::"memory");
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
-        if constexpr (ATPU_QA_ABL == 5)
-          o[0][dt] = f32x4{(float)pf[0][ks][dt], (float)vfrag(ks, dt)[0], 0.f, ks ? o[0][dt][3] : 1.f};
-        else
-          o[0][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vfrag(ks, dt), pf[0][ks],
+        o[0][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vfrag(ks, dt), pf[0][ks],
                                                              ks ? o[0][dt] : f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
       o[0][4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[0][ks], ks ? o[0][4] : f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     }
@@ -414,10 +382,7 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
     for (int ks = 0; ks < 4; ++ks) {
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
-        if constexpr (ATPU_QA_ABL == 5)
-          o[1][dt] = f32x4{(float)pf[1][ks][dt], (float)vfrag(ks, dt)[0], 0.f, ks ? o[1][dt][3] : 1.f};
-        else
-          o[1][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vfrag(ks, dt), pf[1][ks],
+        o[1][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vfrag(ks, dt), pf[1][ks],
                                                              ks ? o[1][dt] : f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
       o[1][4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[1][ks], ks ? o[1][4] : f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     }
@@ -444,14 +409,12 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
       const int ro = hh * 8 + lr;
       const u32x4 val = *reinterpret_cast<const u32x4*>(ost + ro * 128 + asw(ro, lc8) * 16);
       u32x4* dst = reinterpret_cast<u32x4*>(obase + (size_t)(hh * 8) * ldc);
-      if constexpr (ATPU_QA_ABL == 4) asm volatile("" ::"v"(val), "v"(dst));
-      else if constexpr (ATPU_QA_NT) __builtin_nontemporal_store(val, dst);
-      else *dst = val;
+      *dst = val;
     }
   };
 
   const int nk = K / 64;
-  int tile = group_tiles(xcd_remap(v, ntiles), M / 256, ntn, ATPU_QA_GROUP);
+  int tile = xcd_remap(v, ntiles);
   int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 192;
   set_src(m0, n0);
 #pragma unroll
@@ -489,7 +452,7 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
       const bool more = !last || has_next;
       int kn = t + 1;
       if (last && has_next) {  // the stream runs on into K-tile 0 of the next tile
-        tile = group_tiles(xcd_remap(vn, ntiles), M / 256, ntn, ATPU_QA_GROUP);
+        tile = xcd_remap(vn, ntiles);
         m0 = (tile / ntn) * 256;
         n0 = (tile % ntn) * 192;
         set_src(m0, n0);
@@ -639,9 +602,7 @@ __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // the images of both sequences are complete
         __builtin_amdgcn_sched_barrier(0);
-#if ATPU_QA_ABL != 1
         attend(cm0, cn0 / 192, len);
-#endif
         // every wave's image reads are done before group 0 runs ahead into the next tile,
         // whose K-tile 1 is staged into operand buffer 1 (= part of the images)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

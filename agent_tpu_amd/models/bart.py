@@ -288,6 +288,19 @@ class BartModel:
                               p[q + "ln2_b"], cfg.eps)
         return ops.lm_head(x, p["shared"], p["final_logits_bias"], 0.0, logits)
 
+    def _gemv_path(self, rows: int) -> bool:
+        """The folded step's GEMMs all run on the <= 4-row GEMV (the library's own test, so
+        ATPU_GEMV / ATPU_GEMM_TILE / shape / epilogue cannot disagree with the folding plan)."""
+        from ..ops.linear import EPI_BIAS, EPI_GELU, EPI_KV_SCATTER, EPI_RES_LN, EPI_RESIDUAL, EPI_ROW_LN
+        from .._native import native
+
+        cfg, nat = self.cfg, native()
+        d, kv = cfg.d_model, (EPI_KV_SCATTER if self.kv_scatter else 0)
+        return (nat.gemv_selected(rows, 3 * d, EPI_ROW_LN | EPI_BIAS | kv)
+                and nat.gemv_selected(rows, d, EPI_ROW_LN | EPI_BIAS)
+                and nat.gemv_selected(rows, cfg.d_ff, EPI_ROW_LN | EPI_BIAS | EPI_GELU)
+                and nat.gemv_selected(rows, d, EPI_BIAS | EPI_RESIDUAL | EPI_RES_LN))
+
     def _step_folded(self, x, step, cache, T, ckv, src_lens, S, group, hist, logits=True):
         """:meth:`step` with the decoder LayerNorms folded into the GEMMs (only the last one
         runs as a pass). The GEMM producing a pre-LN row writes its partial (sum, sumsq) per
@@ -301,8 +314,7 @@ class BartModel:
         scale = (d // H) ** -0.5
         # partials of: the layer input (last FFN2 out), the self-attention block out, the cross block out
         px, p1, p2 = torch.empty((3, d // 32, x.shape[0], 2), dtype=torch.float32, device=x.device).unbind(0)
-        gemv = (x.is_cuda and x.shape[0] <= 4 and os.environ.get("ATPU_GEMV", "1") != "0"
-                and os.environ.get("ATPU_BART_SELF_STATS", "1") != "0")
+        gemv = x.is_cuda and os.environ.get("ATPU_BART_SELF_STATS", "1") != "0" and self._gemv_path(x.shape[0])
         so = (lambda t: None) if gemv else (lambda t: t)  # producer partials: not on the GEMV path
         ro = (lambda t: t) if gemv else (lambda t: None)  # row_ln consumer hands x's statistics on
         inp = (lambda t: None) if gemv else (lambda t: t)  # the GEMV row_ln reads none

@@ -102,7 +102,11 @@ def native_comm(dev: torch.device):
     if not (rccl.enabled() and is_dist() and dist.get_backend() == "nccl" and dev.type == "cuda"):
         return None
     if _NATIVE is not None and not _NATIVE.healthy():
-        _NATIVE = None  # aborted by a failed wait (or an async error): rebuilt collectively below
+        # aborted by a failed wait (or an async error) on THIS rank only: a local rebuild would
+        # be a collective its still-healthy peers never join (deadlock or mismatched
+        # collectives), so the group is lost and the launcher restarts it
+        _NATIVE = None
+        raise watchdog.RankLost(f"rank {dist.get_rank()}: native RCCL communicator aborted")
     if _NATIVE is None:
         with watchdog.collective("rccl communicator init"):
             _NATIVE = rccl.NativeComm.from_group(dev, group=_GROUP, ranks=members())

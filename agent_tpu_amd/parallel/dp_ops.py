@@ -413,16 +413,8 @@ def classify_batch_task(payload: Dict[str, Any]) -> Any:
 
 # ---------------------------------------------------------- risk_accumulate
 def _local_values(payload: Dict[str, Any], rank: int, ws: int) -> Tuple[torch.Tensor, int]:
-    """This rank's slice of the values, as fp64."""
-    if "source_uri" in payload:
-        table = _open_table(payload["source_uri"])
-        col = table.native.column_index(str(payload.get("field", "risk")))
-        if col < 0:
-            raise ValueError(f"field {payload.get('field', 'risk')!r} not in header {table.header}")
-        start = int(payload.get("start_row", 0))
-        total = max(0, min(int(payload.get("shard_size", table.num_rows)), table.num_rows - start))
-        s_r, n_r = split_range(start, total, ws, rank)
-        return torch.from_numpy(table.native.float_column(s_r, n_r, col)), total
+    """This rank's slice of a ``values`` / ``items`` payload, as fp64 (CSV payloads stream
+    through :func:`csv_stats` instead and are never materialised)."""
     from ops.risk_accumulate import gather_array  # same validation/messages as the CPU op (native parse)
 
     vals = gather_array(payload)

@@ -48,6 +48,11 @@ def ensure_rank_env(env: Optional[Dict[str, str]] = None) -> Dict[str, str]:
     target = os.environ if env is None else env
     for k, v in RANK_ENV_DEFAULTS.items():
         target.setdefault(k, v)
+    if env is None:
+        # this process is a rank: CPU affinity + host thread budget by its GPU's NUMA node
+        from .placement import place_rank
+
+        place_rank()
     return target
 
 
@@ -114,8 +119,7 @@ def self_launch(script: str, argv: Sequence[str], nproc: int, env: Optional[Dict
     child_env = dict(os.environ)
     child_env.update(env or {})
     child_env[RESULT_ENV] = res_path
-    ensure_rank_env(child_env)
-    child_env.setdefault("OMP_NUM_THREADS", "4")
+    ensure_rank_env(child_env)  # each rank sizes OMP / host threads by its NUMA share (placement.py)
     objs: List[Dict[str, Any]] = []
     proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=None, env=child_env, text=True, bufsize=1)
     try:

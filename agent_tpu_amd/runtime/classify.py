@@ -298,7 +298,7 @@ class ClassifyEngine:
             self._stager = native().HostStager(self.n_slots, self.B * self.max_row_bytes, self.B)
         return self._stager
 
-    def classify_table(self, table, start: int, n: int, col: int, host_threads: int = 8,
+    def classify_table(self, table, start: int, n: int, col: int, host_threads: Optional[int] = None,
                        out_idx: Optional[torch.Tensor] = None, out_score: Optional[torch.Tensor] = None,
                        stage_timing: bool = False) -> Tuple[torch.Tensor, torch.Tensor, RunStats]:
         """Pipelined classification of CSV rows ``[start, start+n)``.
@@ -313,6 +313,10 @@ class ClassifyEngine:
         and ``device_span_ms`` (see :class:`DeviceStages`).
         """
         assert self.device.type == "cuda", "classify_table needs a ROCm device"
+        if host_threads is None:
+            from ..parallel.placement import host_threads as budget
+
+            host_threads = budget(8)  # this rank's NUMA share (placement.py), at most the tuned 8
         n = max(0, min(int(n), table.num_rows - int(start)))
         dev = self.device
         out_idx = torch.empty((n, self.k), dtype=torch.int32, device=dev) if out_idx is None else out_idx

@@ -34,7 +34,18 @@ _LOCK = threading.Lock()
 
 
 def _threads() -> int:
-    return max(1, int(os.getenv("RISK_HOST_THREADS", str(min(16, os.cpu_count() or 4)))))
+    from ..parallel.placement import host_threads
+
+    # this rank's share of its NUMA node (parallel/placement.py), not the whole machine
+    return max(1, int(os.getenv("RISK_HOST_THREADS", "0") or 0) or host_threads(16))
+
+
+def gpu_min_rows() -> int:
+    """Shards below this many rows reduce on the host (``RISK_GPU_MIN_VALUES``; ``RISK_DEVICE=gpu``
+    forces the device)."""
+    if os.getenv("RISK_DEVICE", "auto").strip().lower() == "gpu":
+        return 0
+    return int(os.getenv("RISK_GPU_MIN_VALUES", "1000000"))
 
 
 def chunk_rows(device: Optional[torch.device] = None) -> int:
@@ -89,7 +100,13 @@ def column_stats(table, start: int, n: int, col: int, device: Optional[torch.dev
     ``[start, start+n)``, plus ``{"device", "chunks", "bytes", "host_rows"}`` details.
     Empty input gives ``[0, 0, inf, -inf]``. Raises ValueError on a non-numeric field."""
     n = max(0, min(int(n), table.num_rows - int(start)))
+    if device is not None and n < gpu_min_rows():
+        device = None  # a small shard: the host parse beats the stream's setup and DMA round trips
     rows = int(rows or chunk_rows(device))
+    if device is not None:
+        # slots sized to the shard (a power of two >= 64 Ki rows, so the cache of streams stays
+        # small) instead of always the HBM-sized chunk
+        rows = min(rows, 1 << max(16, (n - 1).bit_length()))
     info: Dict[str, Any] = {"device": "cpu", "chunks": 0, "bytes": 0, "host_rows": 0}
     if device is None or device.type != "cuda" or n == 0:
         st = _host_chunks(table, start, n, col, rows) if n else {"count": 0, "sum": 0.0, "min": float("inf"),

@@ -785,9 +785,25 @@ class Agent:
                     lz.finished()
         finally:
             lz.stop()
-            leased = lz.take_ahead()  # a lease taken before the stop is still ours: run it
+            leased = lz.take_ahead()
             if leased is not None:
-                self.run_tasks(*leased)
+                if self.exit_code == EXIT_RANK_LOST:
+                    # the DP group just lost a rank: its collectives would hang until
+                    # DP_COLLECTIVE_TIMEOUT, so fail the jobs now (as on_rank_lost does)
+                    self.fail_lease(*leased, {"type": "RankLost", "trace": "",
+                                              "message": "DP rank lost before this lease started"})
+                else:
+                    self.run_tasks(*leased)  # shutdown: a lease taken before the stop is still ours
+
+    def fail_lease(self, lease_id: str, tasks: List[Any], err: Dict[str, Any]) -> None:
+        """Post ``failed`` for every well-formed task of a lease that will not run."""
+        for task in tasks:
+            try:
+                job_id, op, _, epoch = extract_task(task)
+            except Exception:
+                continue
+            self._begin(lease_id, [(job_id, op, None, epoch)])
+            self._finish(lease_id, job_id, op, epoch, None, err, 0.0)
 
 
 def _on_signal(signum: int, _frame: Any) -> None:

@@ -150,7 +150,8 @@ def risk_accumulate(payload: Dict[str, Any]) -> Dict[str, Any]:
         from agent_tpu_amd.ops.reduce import stats_dict
         from agent_tpu_amd.parallel.dp_ops import csv_stats, risk_device
 
-        dev = risk_device() if _use_gpu(GPU_MIN_VALUES) else None
+        dev = risk_device()
+        # the device is used for shards of >= RISK_GPU_MIN_VALUES rows (runtime.risk.column_stats)
         st, info = csv_stats(payload, 0, 1, dev)
         stats = stats_dict(st.tolist())
         if info["device"] == "gpu":

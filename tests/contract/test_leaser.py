@@ -70,3 +70,39 @@ def test_stop_hands_back_the_lease_taken_ahead(leaser):
     leaser.finished()
     leaser.stop()
     assert leaser.take_ahead()[0] == "L1" and leaser.take_ahead() is None
+
+
+def test_rank_lost_fails_the_lease_taken_ahead(monkeypatch):
+    """a job raising RankLost ends the loop; the lease the helper took ahead is
+    posted ``failed`` (RankLost) instead of being run on the broken DP group."""
+    import app
+    from agent_tpu_amd.parallel.watchdog import RankLost
+
+    posted, ran = [], []
+
+    class Ctl(FakeCtl):
+        def result(self, lease_id, job_id, epoch, status, result, error):
+            posted.append((lease_id, job_id, epoch, status, error and error["type"]))
+
+    monkeypatch.setattr(app, "Controller", Ctl)
+    monkeypatch.setattr(app, "IDLE_SLEEP_SEC", 0.0)
+    monkeypatch.setattr(app, "_running", True)
+    monkeypatch.setenv("LEASE_PREFETCH_AFTER_MS", "5")
+    FakeCtl.log = []
+    FakeCtl.queue = [("L0", [{"id": "a", "op": "boom", "job_epoch": 1}]),
+                     ("L1", [{"id": "b", "op": "boom", "job_epoch": 2}, {"id": "c", "op": "boom"}])]
+
+    def boom(payload):
+        ran.append(payload)
+        time.sleep(0.1)  # long enough for the helper to lease L1 ahead
+        raise RankLost("rank 1: lost")
+
+    agent = object.__new__(app.Agent)
+    agent.handlers, agent.caps, agent.profile = {"boom": boom}, ["boom"], {}
+    agent.ctl, agent.health, agent.exit_code = Ctl(), None, 0
+    agent._inflight, agent._inflight_lock = {}, threading.Lock()
+    agent._poster, agent._leaser = None, None
+    agent._loop_prefetch()
+    assert agent.exit_code == app.EXIT_RANK_LOST and len(ran) == 1
+    assert posted == [("L0", "a", 1, "failed", "RankLost"), ("L1", "b", 2, "failed", "RankLost"),
+                      ("L1", "c", None, "failed", "RankLost")]

@@ -120,3 +120,22 @@ def test_peak_host_memory_independent_of_shard_size(tmp_path):
     assert small["count"] == 400_000 and big["count"] == 3_200_000
     # a one-pass parse would add 8 B x 2.8 M = 22 MB of values plus ~50 MB of mapped file
     assert big["delta"] - small["delta"] < 8 << 20, (small, big)
+
+
+def test_small_shard_stays_on_host(tmp_path, monkeypatch):
+    """a shard below RISK_GPU_MIN_VALUES rows is reduced on the host even when a
+    device is passed (no pinned stream is built for it)."""
+    import torch
+
+    from agent_tpu_amd._native import native
+    from agent_tpu_amd.runtime import risk
+
+    path = tmp_path / "s.csv"
+    path.write_text("id,risk\n" + "".join(f"{i},{i * 0.5}\n" for i in range(100)))
+    t = native().CsvTable(str(path))
+    monkeypatch.delenv("RISK_DEVICE", raising=False)
+    monkeypatch.setenv("RISK_GPU_MIN_VALUES", "1000")
+    n0 = len(risk._STREAMS)
+    st, info = risk.column_stats(t, 0, 100, t.column_index("risk"), torch.device("cuda", 0))
+    assert info["device"] == "cpu" and len(risk._STREAMS) == n0
+    assert st.tolist() == [100.0, sum(i * 0.5 for i in range(100)), 0.0, 49.5]

@@ -34,39 +34,25 @@ def test_decode_attention_cross(gpu, rows, group, S, H):
 @pytest.mark.parametrize("lens,group,S,H,scale", [([1, 63, 64, 65, 128, 1024], 4, 1024, 12, 1.0),
                                                    ([1000], 4, 1024, 12, 0.125), ([130, 7], 1, 130, 16, 1.0),
                                                    ([700, 3, 640], 8, 704, 12, 1.0), ([200, 199], 3, 256, 12, 1.0)])
-@pytest.mark.parametrize("wg", [1, 0])
-def test_decode_cross_split_keys(gpu, lens, group, S, H, scale, wg):
-    # few items: the keys are split into 64-key chunks (flash decoding) and combined, in one
-    # 16-wave workgroup per (item, head) (wg=1, the default) or over workgroups plus a combine
-    # kernel (wg=0); chunks past an item's length, a 1-key item, partial last chunks, 1-8 beams
+def test_decode_cross_split_keys(gpu, lens, group, S, H, scale):
+    # few items: the keys are split into 64-key chunks (flash decoding) over workgroups and
+    # combined by a second kernel; chunks past an item's length, a 1-key item, partial last
+    # chunks, 1-8 beams
     from agent_tpu_amd._native import native
 
     nat = native()
     nseq = len(lens)
     rows = nseq * group - (1 if group > 2 else 0)  # a short last item
-    prev = nat.decode_cross_wg(-1)
-    nat.decode_cross_wg(wg)
-    try:
-        assert (nat.decode_attention_ws_floats(rows, group, H, S, True) > 0) == (wg == 0)
-        q = _r((rows, 3 * H * 64), gpu, seed=41)[:, :H * 64]  # strided like the fused QKV output
-        kv = _r((nseq * S, 2 * H * 64), gpu, seed=42)
-        lt = torch.tensor(lens, dtype=torch.int32)
-        outs = []
-        for bias in (None, _r((H, S), gpu, 1.0, torch.float32, seed=43)):
-            out = ops.decode_attention(q, kv[:, :H * 64], kv[:, H * 64:], H, S, group, lens=lt.to(gpu),
-                                       bias_dist=bias, scale=scale)
-            ref = _decode_attention_ref(q.cpu(), kv.cpu()[:, :H * 64], kv.cpu()[:, H * 64:], H, S, group, lt, None,
-                                        None if bias is None else bias.cpu(), scale, None)
-            assert _rel(out, ref) < 2e-2
-            outs.append(out)
-        if wg:  # the same per-chunk math as the split kernels: within an fp32 summation order
-            nat.decode_cross_wg(0)
-            for bias, out in zip((None, _r((H, S), gpu, 1.0, torch.float32, seed=43)), outs):
-                other = ops.decode_attention(q, kv[:, :H * 64], kv[:, H * 64:], H, S, group, lens=lt.to(gpu),
-                                             bias_dist=bias, scale=scale)
-                assert (out.float() - other.float()).abs().max().item() <= 2 ** -7 * other.float().abs().max().item()
-    finally:
-        nat.decode_cross_wg(prev)
+    assert nat.decode_attention_ws_floats(rows, group, H, S, True) > 0
+    q = _r((rows, 3 * H * 64), gpu, seed=41)[:, :H * 64]  # strided like the fused QKV output
+    kv = _r((nseq * S, 2 * H * 64), gpu, seed=42)
+    lt = torch.tensor(lens, dtype=torch.int32)
+    for bias in (None, _r((H, S), gpu, 1.0, torch.float32, seed=43)):
+        out = ops.decode_attention(q, kv[:, :H * 64], kv[:, H * 64:], H, S, group, lens=lt.to(gpu),
+                                   bias_dist=bias, scale=scale)
+        ref = _decode_attention_ref(q.cpu(), kv.cpu()[:, :H * 64], kv.cpu()[:, H * 64:], H, S, group, lt, None,
+                                    None if bias is None else bias.cpu(), scale, None)
+        assert _rel(out, ref) < 2e-2
 
 
 @pytest.mark.parametrize("rows,H,T,t", [(4, 12, 130, 70), (1, 12, 130, 0), (8, 16, 300, 299)])
@@ -338,38 +324,6 @@ def test_lm_head_topk_matches_logits_path(gpu, cfg, R, V, d, rms, bias, k, mask)
     torch.testing.assert_close(sc.cpu(), rsc.cpu(), atol=1e-4, rtol=1e-5)
     if mask:
         assert not (idx == 1).any()
-
-
-@pytest.mark.parametrize("R,V,d,rms,bias,k,mask,ngram", [(1024, 50264, 1024, False, True, 8, True, 3),
-                                                         (1024, 32128, 768, True, False, 8, False, 0),
-                                                         (600, 50264, 1024, False, True, 8, False, 0),
-                                                         (1300, 4100, 128, False, True, 5, True, 2),
-                                                         (512, 1000, 64, True, False, 8, True, 0)])
-def test_lm_head_wide_matches_128_kernel(gpu, R, V, d, rms, bias, k, mask, ngram):
-    # the 256 x 160 persistent kernel (>= 512 rows) against the 128 x 128 one: same MFMA
-    # order and RMS statistics -> identical logits, so identical tokens (row and vocabulary tails,
-    # K = 64, device n-gram bans, EOS mask); both against the fp32-logit path
-    nat = __import__("agent_tpu_amd._native", fromlist=["native"]).native()
-    head, bs = _lm_case(R, V, d, rms, bias, gpu, seed=R + d)
-    ng = None
-    if ngram:
-        g = torch.Generator().manual_seed(R)
-        seq = torch.randint(0, 8, (R, 40), generator=g, dtype=torch.int32).to(gpu)
-        ng = (seq, 40, ngram)
-    prev = nat.lm_head_wide(-1)
-    try:
-        nat.lm_head_wide(1)
-        sc, idx = head.topk(bs, k, eos=1, mask_eos=mask, ngram=ng)
-        nat.lm_head_wide(0)
-        sc0, idx0 = head.topk(bs, k, eos=1, mask_eos=mask, ngram=ng)
-    finally:
-        nat.lm_head_wide(prev)
-    assert torch.equal(idx, idx0)
-    # the log-softmax normaliser is summed over 160- instead of 128-column partials
-    torch.testing.assert_close(sc, sc0, atol=2e-5, rtol=1e-6)
-    rsc, ridx = ops.beam_topk_rows(head.logits(), bs, k, eos=1, mask_eos=mask, ngram=ng)
-    assert torch.equal(idx.cpu(), ridx.cpu())
-    torch.testing.assert_close(sc.cpu(), rsc.cpu(), atol=1e-4, rtol=1e-5)
 
 
 def test_lm_head_topk_matches_cpu(gpu):
@@ -767,6 +721,34 @@ def test_bart_step_ln_fold_matches_unfolded(gpu):
         assert _rel(lf, lc) < 5e-2 and _rel(lp, lc) < 5e-2, t
         assert _rel(lf, lp) < 3e-2, t
         tok = lc.argmax(-1).to(torch.int32)
+
+
+def test_bart_step_folded_with_forced_tile(gpu):
+    """with ATPU_GEMM_TILE forcing a tile kernel, <= 4-row folded BART steps must
+    plan for the tile kernels (producer partials), not the GEMV (which would throw)."""
+    from agent_tpu_amd._native import native
+    from agent_tpu_amd.models.bart import BartModel, config_for, init_random
+
+    cfg = config_for("bart-tiny")
+    gp = init_random(cfg, seed=2, std=0.1).to(gpu)
+    m = BartModel(cfg, gp)
+    g = torch.Generator().manual_seed(5)
+    B, S, T = 3, 16, 8
+    ids = torch.randint(3, cfg.vocab_size, (B, S), generator=g, dtype=torch.int32).to(gpu)
+    lens = torch.tensor([16, 9, 12], dtype=torch.int32).to(gpu)
+    _, kg = m.encode(ids, lens)
+    tok = torch.randint(3, cfg.vocab_size, (B,), generator=g, dtype=torch.int32).to(gpu)
+    step = torch.zeros(1, dtype=torch.int32, device=gpu)
+    outs = []
+    prev = native().gemm_force_tile(-1)
+    for tile in (0, 128):
+        native().gemm_force_tile(tile)
+        try:
+            assert m._gemv_path(B) == (tile == 0)
+            outs.append(m.step(tok, step, m.new_cache(B, T), T, kg, lens, S, 1))
+        finally:
+            native().gemm_force_tile(prev)
+    assert _rel(outs[1], outs[0]) < 3e-2
 
 
 @pytest.mark.parametrize("M,d,rms", [(1024, 768, True), (256, 1024, False), (4096, 768, True), (77, 256, False)])

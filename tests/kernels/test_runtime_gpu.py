@@ -174,6 +174,7 @@ def test_risk_stream_gpu_parse_and_chunks(gpu, tmp_path, monkeypatch):
     from agent_tpu_amd._native import native
     from agent_tpu_amd.runtime import risk
 
+    monkeypatch.setenv("RISK_DEVICE", "gpu")  # small shards too (default: >= RISK_GPU_MIN_VALUES rows)
     rng = np.random.default_rng(3)
     vals = [f"{v:.6f}" for v in rng.uniform(-1000, 1000, 250_003)]
     t = native().CsvTable(_risk_csv(tmp_path / "r.csv", vals))
@@ -201,6 +202,7 @@ def test_risk_stream_gpu_fallbacks_match_host(gpu, tmp_path, monkeypatch):
     from agent_tpu_amd._native import native
     from agent_tpu_amd.runtime import risk
 
+    monkeypatch.setenv("RISK_DEVICE", "gpu")
     odd = ["1e5", "-2.5E-3", " 3.5 ", "+7", ".5", "5.", "-0", "0.1234567890123456789012", '"42.5"', "inf",
            "1e400", "123456789012345678901", "9007199254740993", "1e-30", "0.000001", "00012.50"]
     vals = [odd[i % len(odd)] if i % 3 == 0 else f"{(i % 1000) / 8:.3f}" for i in range(30_000)]

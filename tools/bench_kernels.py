@@ -105,16 +105,7 @@ def main():
             bsc = torch.zeros(R_, device=dev)
             cases[name] = (lambda h=head, b=bsc: h.topk(b, 8, 2, False),
                            lambda h=head, b=bsc: ops.beam_topk_rows(h.logits(), b, 8, 2, False), 2 * R_ * V_ * d_)
-            def with_wide(wide, h=head, b=bsc):  # 128 x 128 (0) or 256 x 160 persistent (1) kernel
-                prev = nat.lm_head_wide(-1)
-                nat.lm_head_wide(wide)
-                try:
-                    return h.topk(b, 8, 2, False)
-                finally:
-                    nat.lm_head_wide(prev)
-
-            extra[name] = {"gemm_only": lambda h=head: h.logits(), "lm128": lambda f=with_wide: f(0),
-                           "lm_wide": lambda f=with_wide: f(1)}
+            extra[name] = {"gemm_only": lambda h=head: h.logits()}
     gam, bet = r(H, dtype=torch.float32), r(H, dtype=torch.float32)
     cases["layernorm"] = (lambda: ops.layernorm(x768, gam, bet, 1e-12),
                           lambda: torch.nn.functional.layer_norm(x768, (H,), gam.bfloat16(), bet.bfloat16(), 1e-12),
