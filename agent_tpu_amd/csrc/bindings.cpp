@@ -144,6 +144,21 @@ PYBIND11_MODULE(_atpu, m) {
   m.def("trace_pop", &trace_pop);
   m.def("trace_mark", [](const std::string& n) { trace_mark(n.c_str()); });
   m.def("gemm_splitk_splits", &gemm_splitk_splits, "split-K factor chosen for an [M,N,K] GEMM");
+  m.def(
+      "rand_fill",
+      [](uintptr_t dst, int64_t n, bool f32, uint64_t seed, uint64_t sid, float scale0, int64_t n0, float scale1,
+         uintptr_t stream) { rand_fill(P<void>(dst), n, f32, seed, sid, scale0, n0, scale1, S(stream)); },
+      py::arg("dst"), py::arg("n"), py::arg("f32"), py::arg("seed"), py::arg("sid"), py::arg("scale0"), py::arg("n0"),
+      py::arg("scale1"), py::arg("stream"), "seeded random init of a device tensor (atpu/rand.h)");
+  m.def(
+      "rand_fill_host",
+      [](uintptr_t dst, int64_t n, bool f32, uint64_t seed, uint64_t sid, float scale0, int64_t n0, float scale1,
+         int threads) {
+        py::gil_scoped_release nogil;
+        rand_fill_host(P<void>(dst), n, f32, seed, sid, scale0, n0, scale1, threads);
+      },
+      py::arg("dst"), py::arg("n"), py::arg("f32"), py::arg("seed"), py::arg("sid"), py::arg("scale0"), py::arg("n0"),
+      py::arg("scale1"), py::arg("threads") = 8, "CPU twin of rand_fill (bit-identical values)");
   m.def("gemv_selected", &gemv_selected, py::arg("M"), py::arg("N"), py::arg("epi"),
         "true when gemm_bf16 runs this [M, N] problem / epilogue on the <= 4-row GEMV");
   m.def("gemm_force_tile", &gemm_force_tile, py::arg("set") = -1, "GEMM kernel family override: 0 auto, 64, 128, 256");

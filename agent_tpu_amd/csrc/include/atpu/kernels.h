@@ -11,6 +11,12 @@ namespace atpu {
 
 typedef __bf16 bf16;
 
+// ---------------------------------------------------------------- random init (atpu/rand.h)
+// dst[i] = Irwin-Hall(4) value of (seed, sid, i) x (i < n0 ? scale0 : scale1), bf16 (RNE) or fp32;
+// bit-identical to rand_fill_host (runtime.h)
+void rand_fill(void* dst, int64_t n, bool f32, uint64_t seed, uint64_t sid, float scale0, int64_t n0, float scale1,
+               hipStream_t stream);
+
 // ---------------------------------------------------------------- GEMM (K3/K5/K6)
 enum GemmEpilogue : int {
   kEpiBias = 1,

@@ -115,6 +115,10 @@ class HostStager {
 
 // roctx ranges (MI355X_TRACE=1; no-ops otherwise), see runtime/trace.cpp
 bool trace_enabled();
+// CPU twin of rand_fill (kernels.h): the same values, on `threads` host threads
+void rand_fill_host(void* dst, int64_t n, bool f32, uint64_t seed, uint64_t sid, float scale0, int64_t n0,
+                    float scale1, int threads);
+
 void trace_push(const char* name);
 void trace_pop();
 void trace_mark(const char* name);

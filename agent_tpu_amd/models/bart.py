@@ -30,7 +30,7 @@ from typing import Dict, Optional
 import torch
 
 from .. import ops
-from .params import ParamPack
+from .params import ParamPack, rand_fill
 
 POS_OFFSET = 2  # BartLearnedPositionalEmbedding offset
 
@@ -113,19 +113,19 @@ def param_specs(cfg: BartConfig):
     yield "dec.ckv_b", (cfg.dec_layers * 2 * d,), f32
 
 
-def init_random(cfg: BartConfig, seed: int = 0, std: float = 0.02) -> ParamPack:
-    """Seeded random init (HF BART scheme: N(0, init_std) weights, zero biases, LN = 1/0)."""
-    pack = ParamPack(param_specs(cfg))
-    g = torch.Generator().manual_seed(int(seed))
+def init_random(cfg: BartConfig, seed: int = 0, std: float = 0.02, device="cpu") -> ParamPack:
+    """Seeded random init (HF BART scheme: N(0, init_std)-like weights, zero biases, LN = 1/0),
+    built on ``device`` with the same bits everywhere (``params.rand_fill``)."""
+    pack = ParamPack(param_specs(cfg), device=device)
     for name in pack.names():
         t = pack[name]
         base = name.split(".")[-1]
         if base.endswith("_g"):
             t.fill_(1.0)
         elif base.endswith("_b") or name == "final_logits_bias":
-            t.zero_()
+            pass  # zeros
         else:
-            t.copy_((torch.randn(t.shape, generator=g) * std).to(t.dtype))
+            rand_fill(t, seed, name, std)
     return pack
 
 

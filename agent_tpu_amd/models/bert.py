@@ -26,7 +26,7 @@ from typing import Dict, Optional, Tuple
 import torch
 
 from .. import ops
-from .params import ParamPack
+from .params import ParamPack, rand_fill
 
 
 @dataclass(frozen=True)
@@ -111,27 +111,27 @@ def param_specs(cfg: BertConfig):
     yield "cls_b", (C,), f32
 
 
-def init_random(cfg: BertConfig, seed: int = 0, std: float = 0.02, bias_std: float = 0.0) -> ParamPack:
-    """Seeded random init on the CPU (bit-identical on every host/rank).
+def init_random(cfg: BertConfig, seed: int = 0, std: float = 0.02, bias_std: float = 0.0,
+                device="cpu") -> ParamPack:
+    """Seeded random init, built where it will live: on a GPU by the ``rand_fill`` kernel
+    (no host pass, no H2D copy), on the CPU by its native twin; the bits are the same on
+    every device, host and rank (``params.rand_fill``).
 
-    Matches HF's BERT init scheme (N(0, 0.02) weights, LN γ=1/β=0, zero biases)
-    unless ``bias_std`` > 0, which tests use to exercise the bias epilogues.
+    HF's BERT init scheme (N(0, 0.02)-like weights, LN γ=1/β=0, zero biases) unless
+    ``bias_std`` > 0, which tests use to exercise the bias epilogues.
     """
-    pack = ParamPack(param_specs(cfg))
-    g = torch.Generator().manual_seed(int(seed))
+    pack = ParamPack(param_specs(cfg), device=device)
     for name in pack.names():
         t = pack[name]
         if name.endswith("ln_g") or name.endswith("ln1_g") or name.endswith("ln2_g"):
             t.fill_(1.0)
         elif name.endswith("ln_b") or name.endswith("ln1_b") or name.endswith("ln2_b"):
-            t.zero_()
+            pass  # zeros
         elif name.endswith("_b"):
             if bias_std > 0:
-                t.copy_(torch.randn(t.shape, generator=g) * bias_std)
-            else:
-                t.zero_()
+                rand_fill(t, seed, name, bias_std)
         else:
-            t.copy_((torch.randn(t.shape, generator=g) * std).to(t.dtype))
+            rand_fill(t, seed, name, std)
     return pack
 
 

@@ -62,8 +62,11 @@ class ParamPack:
     def to(self, device) -> "ParamPack":
         out = ParamPack.__new__(ParamPack)
         out.specs, out.layout, out.nbytes = self.specs, self.layout, self.nbytes
-        # a pageable host -> HBM copy runs at ~56 GB/s on MI355X (tools/probe_h2d.py: as fast as
-        # from pinned memory; two-slot pinned staging measured 40 GB/s), so no staging here
+        # pageable host -> HBM (a checkpoint load; random init is built on the device instead,
+        # params.rand_fill). bench/cold_load.py --h2d: the FIRST copy of a process pays ~140 ms
+        # of one-time HIP copy-path setup (a 4 KiB copy takes it all) and a never-copied source
+        # buffer ~6-15 ms of page registration; a repeat copy of a 219 MB buffer runs at 56 GB/s
+        # (as fast as from pinned memory; two-slot pinned staging measured 40 GB/s)
         out.buffer = self.buffer.to(device)
         out._views = out._make_views()
         return out
@@ -71,3 +74,32 @@ class ParamPack:
     def with_dtype(self, float_dtype: torch.dtype) -> Dict[str, torch.Tensor]:
         """Plain dict of copies with floating params cast (CPU oracle uses fp32)."""
         return {k: (v.to(float_dtype) if v.is_floating_point() else v.clone()) for k, v in self._views.items()}
+
+
+def _sid(name: str) -> int:
+    """Stream id of a parameter: FNV-1a-64 of its name (adding a tensor shifts no other)."""
+    h = 0xCBF29CE484222325
+    for b in name.encode():
+        h = ((h ^ b) * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def rand_fill(t: torch.Tensor, seed: int, name: str, std: float, n0: int = -1, std1: float = 0.0) -> None:
+    """Seeded N(0, std^2)-like init of ``t`` in place (Irwin-Hall(4), ``csrc/include/atpu/rand.h``):
+    on a GPU tensor the ``rand_fill`` kernel writes it where it lives, on a CPU tensor the native
+    twin does; both give the same bits. Elements ``[n0, numel)`` take ``std1`` when ``n0 >= 0``."""
+    from .._native import native
+
+    assert t.is_contiguous() and t.dtype in (torch.bfloat16, torch.float32), (t.dtype, t.shape)
+    nat = native()
+    n = t.numel()
+    norm = 2.6428997921303014e-05  # atpu::rnd::kIh4Norm
+    s0 = float(std * norm)
+    s1 = float(std1 * norm) if n0 >= 0 else s0
+    n0 = n if n0 < 0 else n0
+    args = (t.data_ptr(), n, t.dtype == torch.float32, int(seed) & 0xFFFFFFFFFFFFFFFF, _sid(name), s0, n0, s1)
+    if t.is_cuda:
+        with torch.cuda.device(t.device):
+            nat.rand_fill(*args, torch.cuda.current_stream(t.device).cuda_stream)
+    else:
+        nat.rand_fill_host(*args, max(1, min(8, torch.get_num_threads())))

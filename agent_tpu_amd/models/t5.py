@@ -31,7 +31,7 @@ from typing import Dict, Optional
 import torch
 
 from .. import ops
-from .params import ParamPack
+from .params import ParamPack, rand_fill
 
 
 @dataclass(frozen=True)
@@ -101,10 +101,10 @@ def param_specs(cfg: T5Config):
     yield "lm", (cfg.vocab_size, d), bf
 
 
-def init_random(cfg: T5Config, seed: int = 0) -> ParamPack:
-    """Seeded random init (HF T5 scheme: factor 1.0 normal with fan-in scaling)."""
-    pack = ParamPack(param_specs(cfg))
-    g = torch.Generator().manual_seed(int(seed))
+def init_random(cfg: T5Config, seed: int = 0, device="cpu") -> ParamPack:
+    """Seeded random init (HF T5 scheme: factor 1.0 normal-like with fan-in scaling), built on
+    ``device`` with the same bits everywhere (``params.rand_fill``)."""
+    pack = ParamPack(param_specs(cfg), device=device)
     d, f = cfg.d_model, cfg.d_ff
     for name in pack.names():
         t = pack[name]
@@ -112,19 +112,18 @@ def init_random(cfg: T5Config, seed: int = 0) -> ParamPack:
         if base.startswith("ln"):
             t.fill_(1.0)
         elif base == "rel":
-            t.copy_(torch.randn(t.shape, generator=g) * d ** -0.5)
+            rand_fill(t, seed, name, d ** -0.5)
         elif name == "shared":
-            t.copy_(torch.randn(t.shape, generator=g).to(t.dtype))
+            rand_fill(t, seed, name, 1.0)
         elif base in ("wo",):
-            t.copy_((torch.randn(t.shape, generator=g) * f ** -0.5).to(t.dtype))
+            rand_fill(t, seed, name, f ** -0.5)
         elif base == "qkv":
-            w = torch.randn(t.shape, generator=g) * d ** -0.5
-            w[:d] *= cfg.d_kv ** -0.5  # T5 folds the 1/sqrt(d_kv) attention scale into q
-            t.copy_(w.to(t.dtype))
+            # T5 folds the 1/sqrt(d_kv) attention scale into the q rows (the first d rows)
+            rand_fill(t, seed, name, d ** -0.5 * cfg.d_kv ** -0.5, n0=d * t.shape[1], std1=d ** -0.5)
         elif base == "cq":
-            t.copy_((torch.randn(t.shape, generator=g) * d ** -0.5 * cfg.d_kv ** -0.5).to(t.dtype))
+            rand_fill(t, seed, name, d ** -0.5 * cfg.d_kv ** -0.5)
         else:
-            t.copy_((torch.randn(t.shape, generator=g) * d ** -0.5).to(t.dtype))
+            rand_fill(t, seed, name, d ** -0.5)
     if cfg.tie_embeddings:
         pack["lm"].copy_((pack["shared"].float() * d ** -0.5).to(torch.bfloat16))
     return pack

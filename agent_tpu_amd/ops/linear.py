@@ -298,7 +298,9 @@ def fold_ln_into_linear(w: torch.Tensor, b: torch.Tensor, gamma: torch.Tensor, b
     ``colsum`` is taken over the (bf16-rounded) ``w_f`` the GEMM multiplies with."""
     wf = (w.float() * gamma.float().unsqueeze(0)).to(w.dtype)
     colsum = wf.float().sum(1).contiguous()
-    bf = (b.float() + w.float() @ beta.float()).contiguous()
+    # w @ beta as a broadcast product + row sum, not a GEMV: a torch matmul here was the
+    # first rocBLAS call of the process (~100 ms of library initialisation on a cold load)
+    bf = (b.float() + (w.float() * beta.float().unsqueeze(0)).sum(1)).contiguous()
     return wf.contiguous(), colsum, bf
 
 

@@ -322,6 +322,9 @@ def classify_csv_task(payload: Dict[str, Any]) -> Any:
     # model load is itself collective (C1 broadcast, errors exchanged before it), on every rank
     with span("load_ms", timing):
         h = get_gpu_handle(get_model_path(payload.get("model_path")))
+    if getattr(h, "fresh", False):  # an LRU miss: this job paid the cold load (phases)
+        h.fresh = False
+        timing["cold_load"] = {k: (round(v, 2) if isinstance(v, float) else v) for k, v in h.load_ms.items()}
     err, idx, sc, meta = "", None, None, {}
     try:
         start = int(payload.get("start_row", 0))

@@ -114,11 +114,12 @@ class ClassifyEngine:
 
     def _graph_step(self, slot: int):
         if slot not in self._graphs:
-            s = torch.cuda.Stream(self.device)
-            s.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(s):  # warm up allocator + code objects off-graph
-                self._step(slot, self.B)
-            torch.cuda.current_stream(self.device).wait_stream(s)
+            if not self._graphs:  # once per engine: the other slots' steps take the same kernels
+                s = torch.cuda.Stream(self.device)
+                s.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(s):  # warm up allocator + code objects off-graph
+                    self._step(slot, self.B)
+                torch.cuda.current_stream(self.device).wait_stream(s)
             g, outs = capture_graph(lambda: self._step(slot, self.B))
             self._graphs[slot] = (g, outs)
         g, outs = self._graphs[slot]

@@ -320,6 +320,8 @@ def _generate_body(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
     fused = pin and gen.device_select and K2 <= ops.LM_HEAD_MAX_K and LM_FUSED
     ngram_dev = pin and bool(gen.device_select) and bool(gen.no_repeat_ngram_size)
     t0 = time.perf_counter()
+    # device-side stage clocks (hipEvent pairs on this search's stream): encoder, decode loop
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if pin else None
 
     # graph cache: the source is padded to a length bucket (keys past src_lens are masked
     # in the encoder and the cross attention), the buffers of a previous search of this
@@ -344,11 +346,15 @@ def _generate_body(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
             new_slot.bufs["lens"] = src_lens.to(torch.int32).clone()
         src_lens = (slot or new_slot).bufs["lens"]
 
+    if evs:
+        evs[0].record()  # after the host-side source prep: the window holds the encoder only
     with span("encode"):
         if slot is not None:
             _, ckv = model.encode(src_ids, src_lens, ckv_out=slot.bufs["ckv"])
         else:
             _, ckv = model.encode(src_ids, src_lens)
+    if evs:
+        evs[1].record()
     t_enc = time.perf_counter()
     if slot is not None:
         b = slot.bufs
@@ -607,21 +613,42 @@ def _generate_body(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
     t_dec = time.perf_counter()
     seqs = [fin_seq[b, 0, :int(fin_len[b, 0])].tolist() for b in range(B)]
     scores = [float(fin_scores[b, 0]) for b in range(B)]
-    return GenResult(seqs, scores, steps, {"encode_ms": (t_enc - t0) * 1e3, "decode_ms": (t_dec - t_enc) * 1e3})
+    # encode_ms / decode_ms: GPU time between hipEvents (encoder kernels; encoder end -> the
+    # last decode step's work); host_*: the host clock of the enqueue / the search loop
+    tm = {"host_encode_enqueue_ms": (t_enc - t0) * 1e3, "host_decode_loop_ms": (t_dec - t_enc) * 1e3}
+    if evs:
+        evs[2].record()
+        evs[2].synchronize()
+        tm["encode_ms"] = evs[0].elapsed_time(evs[1])
+        tm["decode_ms"] = evs[1].elapsed_time(evs[2])
+    else:
+        tm["encode_ms"], tm["decode_ms"] = tm["host_encode_enqueue_ms"], tm["host_decode_loop_ms"]
+    return GenResult(seqs, scores, steps, tm)
 
 
 def build_model(name: str, pack=None, device: Optional[torch.device] = None, seed: int = 0, fp32: bool = False,
                 broadcast: bool = False):
     """``t5-*`` / ``bart-*`` preset name -> (model, pack); random init when no pack.
 
-    ``broadcast``: inside a DP group, rank 0 initialises the weights and every
-    rank receives them in ONE RCCL broadcast of the flat ParamPack (C1)."""
+    Random init is built on ``device`` itself (``params.rand_fill``: a kernel, no host pass or
+    H2D copy) and is bit-identical on every rank, so a DP group needs no broadcast for it.
+    ``broadcast`` with a given ``pack``: rank 0's weights reach every rank in ONE RCCL
+    broadcast of the flat ParamPack (C1)."""
     from ..models import bart, t5
 
     fam = family_of(name)
     mod = bart if fam == "bart" else t5
     cfg = mod.config_for(name)
-    if broadcast:
+    if pack is None:
+        dev = device if device is not None else torch.device("cpu")
+        if broadcast:
+            from ..parallel.dp_ops import load_collectively
+
+            # every rank builds the same bits; the exchange fails the job on all ranks together
+            pack = load_collectively(lambda: mod.init_random(cfg, seed=seed, device=dev), lambda p: p)
+        else:
+            pack = mod.init_random(cfg, seed=seed, device=dev)
+    elif broadcast:
         from ..models.params import ParamPack
         from ..parallel.dp import broadcast_pack, world
         from ..parallel.dp_ops import load_collectively
@@ -629,14 +656,12 @@ def build_model(name: str, pack=None, device: Optional[torch.device] = None, see
         dev = device if device is not None else torch.device("cpu")
         src = pack
 
-        def local():  # rank 0: seeded init + H2D; others: the destination buffer (either may OOM)
+        def local():  # rank 0: its pack on the device; others: the destination buffer (either may OOM)
             if world()[0] == 0:
-                p = src if src is not None else mod.init_random(cfg, seed=seed)
-                return p if p.buffer.device == dev else p.to(dev)
+                return src if src.buffer.device == dev else src.to(dev)
             return ParamPack(mod.param_specs(cfg), device=dev)
 
         pack = load_collectively(local, lambda p: broadcast_pack(p, cfg, dev, builder=mod.param_specs))
-    pack = pack if pack is not None else mod.init_random(cfg, seed=seed)
     if device is not None and pack.buffer.device != device:
         pack = pack.to(device)
     cls = bart.BartModel if fam == "bart" else t5.T5Model
@@ -778,9 +803,11 @@ class SummarizeEngine:
         t0 = time.perf_counter()
         outs = generate_concurrent(self.model, parts, gen)
         wall = (time.perf_counter() - t0) * 1e3
-        enc = max(o.timing_ms["encode_ms"] for o in outs)
+        # the parts run side by side: each stage is as long as its longest part
+        tm = {k: max(o.timing_ms[k] for o in outs) for k in outs[0].timing_ms}
+        tm["host_search_wall_ms"] = wall
         return GenResult([s for o in outs for s in o.sequences], [s for o in outs for s in o.scores],
-                         max(o.steps for o in outs), {"encode_ms": enc, "decode_ms": wall - enc})
+                         max(o.steps for o in outs), tm)
 
     def generate_ids(self, texts: Sequence[str], gen: GenConfig) -> GenResult:
         """Token sequences only (a DP rank's shard; rank 0 detokenizes)."""
@@ -791,7 +818,9 @@ class SummarizeEngine:
         return [self.detokenize(s, m) for s, m in zip(seqs, self.word_maps(texts))]
 
     def summarize(self, texts: Sequence[str], gen: GenConfig) -> Tuple[List[str], GenResult]:
+        t0 = time.perf_counter()
         ids, lens, _ = self.encode_texts(texts, with_maps=False)
+        t_prep = (time.perf_counter() - t0) * 1e3
         if self.device.type == "cuda" and os.getenv("ATPU_SUMM_MAPS_OVERLAP", "1") not in ("0", "false", "no"):
             # the detokenization maps are built on a worker thread while the GPU decodes
             # (the native part releases the GIL; the decode loop mostly waits on events)
@@ -801,7 +830,11 @@ class SummarizeEngine:
         else:
             res = self.run(ids, lens, gen)
             maps = self.word_maps(texts)
-        return [self.detokenize(s, m) for s, m in zip(res.sequences, maps)], res
+        t1 = time.perf_counter()
+        out = [self.detokenize(s, m) for s, m in zip(res.sequences, maps)]
+        res.timing_ms["host_prepare_ms"] = t_prep  # host tokenization + source staging
+        res.timing_ms["host_detokenize_ms"] = (time.perf_counter() - t1) * 1e3
+        return out, res
 
 
 _POOL = None

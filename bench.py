@@ -46,7 +46,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch-rows", type=int, default=int(os.environ.get("BENCH_BATCH_ROWS", "1024")))
+    # default: the batch the agent serves this model with (worker_sizing.classify_batch_rows, the
+    # number the worker profile advertises), so engine, advertised and benched batch agree
+    ap.add_argument("--batch-rows", type=int, default=int(os.environ.get("BENCH_BATCH_ROWS", "0")))
     ap.add_argument("--seq-len", type=int, default=128)
     ap.add_argument("--model", default="bert-base")
     ap.add_argument("--topk", type=int, default=5)
@@ -62,6 +64,12 @@ def parse():
                     help="data-plane collectives: torch.distributed (ProcessGroupNCCL) or the native RcclComm")
     a = ap.parse_args()
     os.environ["ATPU_COMM"] = a.comm
+    if a.batch_rows <= 0:
+        from worker_sizing import classify_batch_rows, probe_kfd
+
+        devs = probe_kfd()  # sysfs: no HIP context before the launcher has forked the ranks
+        hbm = devs[0]["total_memory_bytes"] if devs else 288 * 1024 ** 3
+        a.batch_rows = classify_batch_rows(hbm, a.model, a.seq_len)
     return a
 
 
@@ -132,21 +140,23 @@ def main() -> int:
     table = nat.CsvTable(csv_path)
     col = table.column_index("text")
 
-    # weights: rank 0 initialises on the host and uploads them (pinned staging), then one
-    # RCCL broadcast gives every rank a copy (C1). The HIP context exists before either
-    # clock starts, so the two timings are the copy and the collective only.
+    # weights: rank 0 builds the seeded random init on its GPU (params.rand_fill: a kernel
+    # writing the ParamPack in place, no host pass or H2D copy), then one RCCL broadcast gives
+    # every rank a copy (C1, the path a checkpoint load takes). The HIP context exists before
+    # either clock starts, so the two timings are the init and the collective only.
     torch.empty(1, device=dev)
     torch.cuda.synchronize(dev)
-    pack = init_random(cfg, seed=0) if rank == 0 else None
-    h2d_ms, bcast_ms = None, None
+    init_ms, bcast_ms = None, None
     if rank == 0:
-        dst = torch.empty_like(pack.buffer, device=dev)  # allocation outside the clock
-        torch.cuda.synchronize(dev)
         t_b = time.perf_counter()
-        dst.copy_(pack.buffer)
+        pack = init_random(cfg, seed=0, device=dev)
         torch.cuda.synchronize(dev)
-        h2d_ms = (time.perf_counter() - t_b) * 1000.0
-        pack = pack.adopt(dst)
+        init_ms = (time.perf_counter() - t_b) * 1000.0
+    else:
+        from agent_tpu_amd.models.bert import param_specs
+        from agent_tpu_amd.models.params import ParamPack
+
+        pack = ParamPack(param_specs(cfg), device=dev)
     if world > 1:
         dist.barrier()
         t_b = time.perf_counter()
@@ -216,8 +226,8 @@ def main() -> int:
                 "topk": min(a.topk, cfg.num_labels),
                 "hipgraph": not a.no_graph,
                 "concurrent_batches": a.slots if eng.concurrent else 1, "cu_split": bool(eng.cu_split),
-                # rank 0's pinned-staged host -> HBM upload, and the C1 RCCL broadcast (N > 1 only)
-                "weight_h2d_ms": round(h2d_ms, 2) if h2d_ms is not None else None,
+                # rank 0's seeded init on the device, and the C1 RCCL broadcast (N > 1 only)
+                "weight_init_ms": round(init_ms, 2) if init_ms is not None else None,
                 "weight_broadcast_ms": round(bcast_ms, 2) if bcast_ms is not None else None,
                 "weight_bytes": int(pack.nbytes),
                 "last_layer_cls_only": cls_only,

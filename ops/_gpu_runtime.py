@@ -72,6 +72,8 @@ class GpuHandle:
         self.model_path = spec.path
         self.cfg = cfg
         self.engine = engine
+        self.load_ms: Dict[str, Any] = {}  # cold-load phases (set by _build_handle)
+        self.fresh = True  # built by this call (the first job reports load_ms as its cold load)
 
 
 def _load_host_pack(spec: ModelSpec, cfg):
@@ -97,10 +99,12 @@ def _load_host_pack(spec: ModelSpec, cfg):
 def _build_handle(model_path: str, device) -> GpuHandle:
     """Load a model on this rank, or on every rank of the DP group together.
 
-    Under a process group the load follows ``dp_ops.load_collectively``: rank 0
-    builds the weights on the host and copies them to its GPU, the other ranks
-    allocate the destination, errors are exchanged, and only then does the C1
-    broadcast run (all ranks or none); the engine build is exchanged again.
+    Random-init specs are built on the device by every rank (``params.rand_fill``: the
+    same bits everywhere, no host init, no H2D copy, no broadcast). A ``.safetensors``
+    spec follows ``dp_ops.load_collectively``: rank 0 loads it on the host and copies it
+    to its GPU, the other ranks allocate the destination, errors are exchanged, and only
+    then does the C1 broadcast run (all ranks or none); the engine build is exchanged
+    again. ``handle.load_ms`` records the phases (weights, engine).
     """
     from agent_tpu_amd.models.bert import config_for, param_specs
     from agent_tpu_amd.models.params import ParamPack
@@ -108,26 +112,46 @@ def _build_handle(model_path: str, device) -> GpuHandle:
     from agent_tpu_amd.parallel.dp_ops import load_collectively
     from agent_tpu_amd.runtime.classify import ClassifyEngine
 
+    import time
+
+    from agent_tpu_amd.models.bert import init_random
+
     dist_on = is_dist()
-    box = {}
+    box = {"t0": time.perf_counter()}
+
+    def sync():
+        if getattr(device, "type", "cpu") == "cuda":
+            import torch
+
+            torch.cuda.synchronize(device)
 
     def local():
         spec = parse_spec(model_path)
         cfg = config_for(spec.preset, num_labels=spec.labels)
         box.update(spec=spec, cfg=cfg)
+        if not spec.file:
+            return init_random(cfg, seed=spec.seed, device=device)
         if dist_on and world()[0] != 0:
             return ParamPack(param_specs(cfg), device=device)
         return _load_host_pack(spec, cfg).to(device)
 
     def collective(pack):
-        return broadcast_pack(pack, box["cfg"], device) if dist_on else pack
+        out = broadcast_pack(pack, box["cfg"], device) if dist_on and box["spec"].file else pack
+        sync()
+        box["t1"] = time.perf_counter()
+        return out
 
     def post(pack):
         spec, cfg = box["spec"], box["cfg"]
         batch = spec.batch_rows or _auto_batch_rows(spec.preset, spec.seq_len)
         eng = ClassifyEngine(cfg, pack, device, batch_rows=batch, seq_len=spec.seq_len,
                              topk=min(cfg.num_labels, 64))
-        return GpuHandle(spec, cfg, eng)
+        sync()
+        h = GpuHandle(spec, cfg, eng)
+        t2 = time.perf_counter()
+        h.load_ms = {"weights_ms": (box["t1"] - box["t0"]) * 1e3, "engine_ms": (t2 - box["t1"]) * 1e3,
+                     "total_ms": (t2 - box["t0"]) * 1e3, "source": "file" if spec.file else "device_rand"}
+        return h
 
     return load_collectively(local, collective, post)
 

@@ -73,8 +73,8 @@ def test_batch_rows_from_small_hbm(monkeypatch):
     for v in ("CLASSIFY_BATCH_ROWS", "CLASSIFY_SEQ_LEN", "HBM_RESERVE_GB", "MODEL_LRU_GB", "CLASSIFY_BATCH_ROWS_CAP"):
         monkeypatch.delenv(v, raising=False)
     assert ws.classify_batch_rows(288 * GIB) == 1024
-    # 12 GiB: 8 reserved, 3 for the model LRU -> 1 GiB of activations / 3.95 MB per row -> 272 -> 256
-    assert ws.classify_batch_rows(12 * GIB) == 256
+    # 12 GiB: 8 reserved, 3 for the model LRU -> 1 GiB of activations / 3.16 MB per row -> 339 -> 320
+    assert ws.classify_batch_rows(12 * GIB) == 320
     assert ws.classify_batch_rows(10 * GIB) == 1  # nothing left after reserve + LRU: one row at a time
 
 
@@ -105,8 +105,8 @@ def test_model_aware_capacity_288gb(kfd, monkeypatch):
         monkeypatch.delenv(v, raising=False)
     cap = ws.detect_gpu()["capacity"]
     # per-row bytes: slots x (text staging + ids + S*2*(6H + I) activations + LN statistics)
-    assert ws.classify_row_bytes("bert-base", 128) == 3_947_536
-    assert ws.classify_row_bytes("bert-large", 128) == 5_258_256
+    assert ws.classify_row_bytes("bert-base", 128) == 3_161_104
+    assert ws.classify_row_bytes("bert-large", 128) == 4_209_680
     assert cap["classify_batch_rows"] == {"bert-base": 1024, "bert-large": 1024}  # token target binds at 288 GB
     assert cap["classify_seq_len"] == 128
     # per-document bytes of a beam search at the reference's settings (src 1024, 4 beams, max 130)

@@ -239,3 +239,49 @@ def test_risk_op_csv_streams_on_gpu(gpu, tmp_path, monkeypatch):
     ref = risk_accumulate({"values": [float(v) for v in vals[1:99_991]]})
     assert out["device"] == "gpu" and out["stream"]["chunks"] == 5 and out["count"] == 99_990
     assert out["min"] == ref["min"] and out["max"] == ref["max"] and abs(out["sum"] - ref["sum"]) < 1e-6
+
+
+def test_rand_fill_gpu_matches_host(gpu):
+    """The rand_fill kernel and its CPU twin give the same bits (bf16 / fp32, ragged tails,
+    split scale), and a BERT pack built on the GPU equals the host-built one."""
+    from agent_tpu_amd.models.bert import config_for, init_random
+    from agent_tpu_amd.models.params import rand_fill
+
+    for n, dt, n0 in ((1, torch.bfloat16, -1), (1000003, torch.bfloat16, 12345), (77777, torch.float32, -1),
+                      (4096, torch.float32, 100)):
+        h = torch.empty(n, dtype=dt)
+        g = torch.empty(n, dtype=dt, device=gpu)
+        rand_fill(h, 11, "t", 0.05, n0=n0, std1=0.3)
+        rand_fill(g, 11, "t", 0.05, n0=n0, std1=0.3)
+        assert torch.equal(g.cpu().view(torch.int16 if dt == torch.bfloat16 else torch.int32),
+                           h.view(torch.int16 if dt == torch.bfloat16 else torch.int32)), (n, dt)
+    cfg = config_for("bert-base", num_labels=2)
+    pg = init_random(cfg, seed=5, device=gpu)
+    ph = init_random(cfg, seed=5)
+    assert torch.equal(pg.buffer.cpu(), ph.buffer)
+
+
+def test_classify_row_bytes_covers_the_engine(gpu):
+    """worker_sizing.classify_row_bytes (what the worker profile's batch is sized by) against
+    the device memory a ClassifyEngine step really takes beyond its weights: an upper bound
+    that is not loose by more than 2x (bert-base, S = 128, both staging slots)."""
+    from agent_tpu_amd.models.bert import config_for, init_random
+    from agent_tpu_amd.runtime.classify import ClassifyEngine
+    from worker_sizing import classify_row_bytes
+
+    cfg = config_for("bert-base", num_labels=2)
+    pack = init_random(cfg, seed=0, device=gpu)
+    torch.cuda.synchronize()
+    B = 256
+    base = torch.cuda.memory_allocated(gpu)
+    torch.cuda.reset_peak_memory_stats(gpu)
+    eng = ClassifyEngine(cfg, pack, gpu, batch_rows=B, seq_len=128, topk=2)
+    folded = eng.memory_bytes() - pack.nbytes - sum(t.numel() for t in eng.text) \
+        - sum(t.numel() * 4 for t in eng.ids_s) - sum(t.numel() * 4 for t in eng.offs)
+    texts = ["word " * 200] * B
+    for slot in range(2):
+        eng.classify_texts(texts)
+    torch.cuda.synchronize()
+    used = torch.cuda.max_memory_allocated(gpu) - base - folded
+    est = B * classify_row_bytes("bert-base", 128, 2)
+    assert used <= est and used >= est // 2, (used, est)

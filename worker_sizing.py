@@ -259,12 +259,13 @@ def _activation_budget(hbm_bytes: int) -> int:
 def classify_row_bytes(model: str = "bert-base", seq_len: int = 128, slots: int = 2) -> int:
     """Device bytes one batch row costs the ClassifyEngine (agent_tpu_amd/runtime/classify.py):
     per staging slot (``slots`` batches in flight, each with its own graph pool) the text
-    staging, ids/lengths and the encoder's activations: two hidden-state buffers, the packed
-    QKV, the attention context and the FFN intermediate (bf16), plus per-row LayerNorm
-    statistics (fp32 partials of up to 4 column tiles and the finalized pair)."""
+    staging, ids/lengths and the LayerNorm-folded encoder's live activations (bf16): the
+    layer input, the attention context (the fused QKV + attention kernel never writes the
+    [S, 3H] QKV), the out-proj sum, the FFN intermediate and the FFN2 sum, plus per-row
+    LayerNorm statistics (fp32 partials of up to 4 column tiles and the finalized pair)."""
     H, I, _, _, _ = CLASSIFY_DIMS[model]
     S = int(seq_len)
-    act = S * 2 * (2 * H + 3 * H + H + I) + S * 4 * (2 * 4 + 2)
+    act = S * 2 * (4 * H + I) + S * 4 * (2 * 4 + 2)
     return slots * (CLASSIFY_MAX_ROW_BYTES + 4 + S * 4 + 4 + act)
 
 
