@@ -296,6 +296,18 @@ def health_task(payload: Dict[str, Any]) -> Any:
         res = health.check(probe=bool(payload.get("probe", True)), only=[torch.cuda.current_device()])
     else:
         res = {"ok": False, "devices": [], "healthy": [], "unhealthy": {}, "error": "no ROCm device visible"}
+    from .placement import current_plan, host_threads
+
+    plan = current_plan()
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        ncpu = os.cpu_count() or 0
+    # this rank's row of the node's rank table: its device and host placement (placement.py)
+    res["rank_info"] = {"rank": dist.get_rank() if is_dist() else 0, "local_rank": int(os.getenv("LOCAL_RANK", "0")),
+                        "device": torch.cuda.current_device() if torch.cuda.is_available() else None,
+                        "numa": plan["numa"] if plan else None, "ncpus": ncpu, "host_threads": host_threads(),
+                        "placement": plan["source"] if plan else "unplaced"}
     parts = [res]
     if is_dist():
         parts = [None] * world()[1]

@@ -204,8 +204,19 @@ def verify_ranks(expected: int, backend: str, dev) -> List[Dict[str, Any]]:
     ws = dist.get_world_size() if dist.is_initialized() else 1
     if ws != expected:
         raise LaunchError(f"WORLD_SIZE {ws} != --gpus {expected}")
+    from .placement import current_plan, host_threads
+
     me = {"rank": dist.get_rank() if dist.is_initialized() else 0, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
           "device": str(dev), "device_id": _device_id(dev), "pid": os.getpid()}
+    plan = current_plan()
+    try:
+        aff = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = []
+    # host placement (placement.py): NUMA node, the cpuset this rank runs on, its thread budget
+    me["host"] = {"numa": plan["numa"] if plan else None, "source": plan["source"] if plan else "unplaced",
+                  "cpus": (f"{aff[0]}-{aff[-1]}" if aff and aff[-1] - aff[0] + 1 == len(aff) else str(len(aff)))
+                  if aff else None, "ncpus": len(aff), "threads": host_threads()}
     table: List[Dict[str, Any]] = [me]
     if dist.is_initialized() and ws > 1:
         table = [None] * ws  # type: ignore[list-item]

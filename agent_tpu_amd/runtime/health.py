@@ -99,6 +99,9 @@ def merge(parts: List[Dict[str, Any]]) -> Dict[str, Any]:
         out["unhealthy"].update(p.get("unhealthy", {}))
         if p.get("error"):
             errs.append(p["error"])
+    ranks = [p["rank_info"] for p in parts if p.get("rank_info")]
+    if ranks:
+        out["ranks"] = sorted(ranks, key=lambda r: r["rank"])
     out["devices"].sort(key=lambda d: d["index"])
     out["healthy"] = sorted(set(out["healthy"]) - set(out["unhealthy"]))
     out["ok"] = bool(out["healthy"])

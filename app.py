@@ -242,6 +242,8 @@ def worker_profile(health: Optional[Dict[str, Any]] = None, caps: Optional[List[
     if health is not None and prof.get("gpu", {}).get("gpu_present"):
         prof["gpu"]["health"] = {"ok": health.get("ok", False), "healthy": health.get("healthy", []),
                                  "unhealthy": {str(k): v for k, v in health.get("unhealthy", {}).items()}}
+        if health.get("ranks"):  # DP: one row per rank (device, NUMA node, cpuset size, thread budget)
+            prof["gpu"]["health"]["ranks"] = health["ranks"]
         if "healthy" in health:
             # advertise only devices that passed (reduced capacity after a fault)
             prof["gpu"]["gpu_count"] = len(health["healthy"])

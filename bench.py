@@ -220,6 +220,7 @@ def main() -> int:
                 "rccl_world_size": rccl_world if a.dist_backend == "nccl" or world == 1 else None,
                 "pg_world_size": rccl_world,
                 "rank_devices": [t["device"] for t in rank_table],
+                "rank_hosts": [t.get("host") for t in rank_table],
                 "distinct_devices": len({t["device_id"] for t in rank_table}) == len(rank_table),
                 "rows_per_gpu_per_step": B,
                 "num_labels": cfg.num_labels,

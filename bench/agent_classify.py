@@ -79,6 +79,8 @@ def main() -> int:
         print(json.dumps({"error": "timeout" if not ok else "failed jobs", "results": len(ctl.results),
                           "first_bad": bad[:1]}, default=str)[:2000])
         return 1
+    prof = (ctl.lease_requests[0].get("worker_profile") or {}) if ctl.lease_requests else {}
+    rank_table = ((prof.get("gpu") or {}).get("health") or {}).get("ranks")
     first = ctl.results[0]["result"]  # the warm-up job: it paid the model's cold load
     ftm = first.get("timing_ms") or {}
     first_job = {"elapsed_ms": first.get("elapsed_ms"), "load_ms": ftm.get("load_ms"), "cold_load": ftm.get("cold_load")}
@@ -95,7 +97,7 @@ def main() -> int:
                                  "dp_ranks": a.dp, "dp_backend": a.dp_backend if a.dp > 1 else None,
                                  "median_op_rows_per_sec": round(engine_rps, 1),
                                  "median_op_elapsed_ms": op_ms, "median_op_timing_ms": timing,
-                                 "first_job_cold_model": first_job,
+                                 "first_job_cold_model": first_job, "rank_table": rank_table,
                                  "transport": "HTTP/1.1 keep-alive, loopback mock controller",
                                  "data": "synthetic CSV rows, random-init weights"}}), flush=True)
     return 0
