@@ -84,6 +84,10 @@ RESULT_POST_ASYNC = os.getenv("RESULT_POST_ASYNC", "1").strip().lower() in ("1",
 LEASE_PREFETCH = os.getenv("LEASE_PREFETCH", "1").strip().lower() in ("1", "true", "yes", "on")
 # lease size this agent can batch well; advertised in worker_profile.limits (MAX_TASKS stays the request)
 MAX_BATCH_TASKS = int(os.getenv("MAX_BATCH_TASKS", "1024"))
+# with RESULT_POST_ASYNC: results that queue up while the poster is busy go out pipelined on one
+# keep-alive connection (PipelinedPoster); 0 = one request / response round trip per result
+RESULT_PIPELINE = os.getenv("RESULT_PIPELINE", "1").strip().lower() in ("1", "true", "yes", "on")
+METRICS_REFRESH_SEC = float(os.getenv("METRICS_REFRESH_SEC", "0.25"))
 FAIL_ON_NOT_OK = os.getenv("FAIL_ON_NOT_OK", "0").strip().lower() in ("1", "true", "yes")
 
 _running = True
@@ -134,6 +138,8 @@ class Metrics:
         self.jobs_failed = 0
         self._rows: List[Tuple[float, int]] = []
         self._lock = threading.Lock()
+        self._sampled: Optional[Dict[str, Any]] = None
+        self._sampled_at = 0.0
 
     def job_done(self, ok: bool, result: Any) -> None:
         with self._lock:
@@ -155,14 +161,22 @@ class Metrics:
             return sum(n for _, n in self._rows) / span
 
     def snapshot(self) -> Dict[str, Any]:
-        out: Dict[str, Any] = {}
-        if psutil is not None:
-            try:
-                out["cpu_util"] = float(psutil.cpu_percent(interval=None)) / 100.0
-                out["ram_mb"] = float(psutil.virtual_memory().used) / (1024 * 1024)
-            except Exception:
-                out = {}
-        out.update(gpu_metrics())
+        """The lease's ``metrics``. The host / GPU sampling (procfs and sysfs reads, ~1 ms per
+        lease in this container: the cost of a 1-task echo lease) is refreshed at most every
+        METRICS_REFRESH_SEC (default 0.25 s, the reference's idle poll); the job counters and
+        rows/s are always current."""
+        now = time.monotonic()
+        if self._sampled is None or now - self._sampled_at >= METRICS_REFRESH_SEC:
+            out: Dict[str, Any] = {}
+            if psutil is not None:
+                try:
+                    out["cpu_util"] = float(psutil.cpu_percent(interval=None)) / 100.0
+                    out["ram_mb"] = float(psutil.virtual_memory().used) / (1024 * 1024)
+                except Exception:
+                    out = {}
+            out.update(gpu_metrics())
+            self._sampled, self._sampled_at = out, now
+        out = dict(self._sampled)
         out["jobs_completed"] = self.jobs_completed
         out["jobs_failed"] = self.jobs_failed
         out["rows_per_sec"] = round(self.rows_per_sec(), 2)
@@ -190,9 +204,10 @@ def gpu_metrics() -> Dict[str, Any]:
             out.update({"hbm_used_gb": [round(u / 2**30, 2) for u, _ in vram],
                         "hbm_total_gb": [round(t / 2**30, 2) for _, t in vram]})
             return out
-        import torch
-
-        if not torch.cuda.is_available() or not torch.cuda.is_initialized():
+        torch = sys.modules.get("torch")
+        # only a process that already runs on its GPU (a CPU-only agent never imports torch for
+        # this; torch.cuda.is_available() re-probes the runtime, ~20 ms per lease without a GPU)
+        if torch is None or not torch.cuda.is_initialized():
             return out
         # no sysfs: this process's OWN device only (never a peer rank's GPU)
         i = torch.cuda.current_device()
@@ -367,10 +382,17 @@ class Controller:
             return None
         return lease_id, tasks
 
-    def result(self, lease_id: str, job_id: str, epoch: Any, status: str, result: Any, error: Any) -> None:
+    def result(self, lease_id: str, job_id: str, epoch: Any, status: str, result: Any, error: Any,
+               attempts_done: int = 0) -> None:
+        """``attempts_done``: attempts already made elsewhere (a pipelined post answered 5xx);
+        at most RESULT_RETRIES + 1 attempts in all, backing off before each retry."""
         body = {"lease_id": lease_id, "job_id": job_id, "job_epoch": epoch, "status": status,
                 "result": result, "error": error}
-        for attempt in range(RESULT_RETRIES + 1):
+        if attempts_done > RESULT_RETRIES:
+            raise RuntimeError(f"result failed after {attempts_done} attempts")
+        if attempts_done:
+            time.sleep(min(2.0, 0.1 * 2 ** (attempts_done - 1)))
+        for attempt in range(attempts_done, RESULT_RETRIES + 1):
             code, resp = self.post("/v1/results", body)
             if 0 < code < 400:
                 return
@@ -380,6 +402,116 @@ class Controller:
                     raise RuntimeError(f"result failed: {resp}")
                 raise RuntimeError(f"result HTTP {code}: {resp}")
             time.sleep(min(2.0, 0.1 * 2**attempt))
+
+
+class PipelinedPoster:
+    """Result posts pipelined on ONE keep-alive connection (HTTP/1.1 request pipelining): the
+    queued results go out back to back in one ``sendall`` and their responses are read in
+    order afterwards, so the agent's encoding of result i+1 overlaps the controller's handling
+    of result i and no post waits a round trip for the one before it. The controller still
+    sees one ``POST /v1/results`` per job, in FIFO order (ref ``app.py:198-218``).
+
+    A result whose answer is retryable (transport error, 5xx) or that the server never
+    answered (it closed the connection mid-batch) is handed back to the caller, which posts
+    it through the serial, retrying :meth:`Controller.result`; 4xx answers are final (logged).
+    Plain ``http://`` only (``https`` controllers use the serial path)."""
+
+    MAX_BATCH = 64
+
+    def __init__(self, base: str, timeout: float) -> None:
+        import urllib.parse
+
+        u = urllib.parse.urlsplit(base)
+        self.ok = u.scheme == "http"
+        self.host, self.port = u.hostname or "localhost", u.port or 80
+        self.path = (u.path.rstrip("/") + "/v1/results").encode()
+        self.timeout = timeout
+        self.sock = None
+        self.buf = b""
+
+    def _connect(self):
+        if self.sock is None:
+            self.sock = socket.create_connection((self.host, self.port), timeout=self.timeout)
+            self.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            self.buf = b""
+        return self.sock
+
+    def close(self) -> None:
+        if self.sock is not None:
+            try:
+                self.sock.close()
+            except OSError:
+                pass
+        self.sock, self.buf = None, b""
+
+    def _read_until(self, sep: bytes) -> bytes:
+        while sep not in self.buf:
+            chunk = self.sock.recv(65536)
+            if not chunk:
+                raise ConnectionResetError("controller closed the connection")
+            self.buf += chunk
+        i = self.buf.index(sep) + len(sep)
+        out, self.buf = self.buf[:i], self.buf[i:]
+        return out
+
+    def _read_n(self, n: int) -> bytes:
+        while len(self.buf) < n:
+            chunk = self.sock.recv(max(65536, n - len(self.buf)))
+            if not chunk:
+                raise ConnectionResetError("controller closed the connection")
+            self.buf += chunk
+        out, self.buf = self.buf[:n], self.buf[n:]
+        return out
+
+    def _response(self) -> Tuple[int, bool]:
+        """(status, server will close) of the next response; its body is read and dropped."""
+        head = self._read_until(b"\r\n\r\n").decode("latin-1").split("\r\n")
+        code = int(head[0].split(" ", 2)[1])
+        hdr = {}
+        for line in head[1:]:
+            k, _, v = line.partition(":")
+            hdr[k.strip().lower()] = v.strip().lower()
+        if hdr.get("transfer-encoding", "") == "chunked":
+            while True:
+                n = int(self._read_until(b"\r\n").split(b";")[0], 16)
+                self._read_n(n + 2)
+                if n == 0:
+                    break
+        elif code != 204 and code >= 200:
+            self._read_n(int(hdr.get("content-length", "0") or 0))
+        return code, hdr.get("connection", "") == "close"
+
+    def post_many(self, items: List[Any]) -> List[Tuple[Any, int]]:
+        """Post ``items`` ((lease_id, job_id, epoch, status, result, error) tuples) pipelined;
+        returns ``(item, attempts made)`` for those that still need a (serial, retrying) post."""
+        if not items:
+            return []
+        reqs = []
+        for lease_id, job_id, epoch, status, result, error in items:
+            data = _dumps({"lease_id": lease_id, "job_id": job_id, "job_epoch": epoch, "status": status,
+                           "result": result, "error": error})
+            reqs.append(b"POST " + self.path + b" HTTP/1.1\r\nHost: " + self.host.encode() +
+                        b"\r\nContent-Type: application/json\r\nContent-Length: " + str(len(data)).encode() +
+                        b"\r\n\r\n" + data)
+        done = 0
+        redo: List[Tuple[Any, int]] = []
+        try:
+            sock = self._connect()
+            sock.sendall(b"".join(reqs))
+            for it in items:
+                code, close = self._response()
+                done += 1
+                if code >= 500:
+                    redo.append((it, 1))
+                elif code >= 400:
+                    log_every("result", f"{LOG} post result error: result HTTP {code} (job {it[1]})")
+                if close:
+                    self.close()
+                    break
+        except (OSError, ValueError, IndexError) as exc:
+            log_every("result", f"{LOG} pipelined post: {exc}; falling back to serial posts")
+            self.close()
+        return redo + [(it, 0) for it in items[done:]]
 
 
 class Leaser:
@@ -493,9 +625,12 @@ class Leaser:
         self.thread.join(timeout=HTTP_TIMEOUT_SEC + 5)
 
 
+_TRACE = os.getenv("MI355X_TRACE", "0").strip().lower() in ("1", "true")
+
+
 def _op_span(op: str):
     """roctx range around a job under MI355X_TRACE=1 (no import cost otherwise)."""
-    if os.getenv("MI355X_TRACE", "0").strip().lower() not in ("1", "true"):
+    if not _TRACE:
         import contextlib
 
         return contextlib.nullcontext()
@@ -544,7 +679,8 @@ class Agent:
         if RESULT_POST_ASYNC:
             import queue
 
-            self._poster = queue.Queue(maxsize=4)  # bounded: backpressure on a slow controller
+            # bounded: backpressure on a slow controller (a whole lease of 1-row results may queue)
+            self._poster = queue.Queue(maxsize=max(4, 2 * PipelinedPoster.MAX_BATCH if RESULT_PIPELINE else 4))
             threading.Thread(target=self._poster_loop, name="atpu-result-poster", daemon=True).start()
 
     # ---------------------------------------------------- lost-rank handling
@@ -599,7 +735,8 @@ class Agent:
             return
         self._run_one(lease_id, job)
 
-    def _run_one(self, lease_id: str, job: Tuple[str, str, Dict[str, Any], Any]) -> None:
+    def _run_one(self, lease_id: str, job: Tuple[str, str, Dict[str, Any], Any],
+                 defer: Optional[Tuple[List[Any], List[str]]] = None) -> None:
         job_id, op, payload, epoch = job
         self._begin(lease_id, [job])
         t0 = time.time()
@@ -616,41 +753,82 @@ class Agent:
             err = {"type": type(exc).__name__, "message": str(exc), "trace": traceback.format_exc(limit=12)}
             self._note_device_fault(str(exc))
             self._note_rank_lost(exc)
-        self._finish(lease_id, job_id, op, epoch, out, err, (time.time() - t0) * 1000.0)
+        self._finish(lease_id, job_id, op, epoch, out, err, (time.time() - t0) * 1000.0, defer)
 
     def _finish(self, lease_id: str, job_id: str, op: str, epoch: Any, out: Any, err: Optional[Dict[str, Any]],
-                ms: float) -> None:
+                ms: float, defer: Optional[Tuple[List[Any], List[str]]] = None) -> None:
+        """Claim, count and post one job's result and log it (the reference's ``ok job=`` line).
+        ``defer`` = (items, lines): collect the post and the log line instead (a batch hands
+        its results to the poster as ONE queue entry and writes its lines in one call)."""
         if not self._claim(job_id):
             return  # already failed by the DP watchdog
         ok = err is None
         METRICS.job_done(ok, out)
         item = (lease_id, job_id, epoch, "succeeded" if ok else "failed", out if ok else None, None if ok else err)
-        if self._poster is not None:
+        if defer is not None:
+            defer[0].append(item)
+        elif self._poster is not None:
             self._poster.put(item)
         else:
             self._post(self.ctl, item)
         if ok:
-            print(f"{LOG} ok job={job_id} op={op} ms={ms:.1f}", flush=True)
+            line = f"{LOG} ok job={job_id} op={op} ms={ms:.1f}"
+            if defer is not None:
+                defer[1].append(line)
+            else:
+                print(line, flush=True)
         else:
             log_every("exec", f"{LOG} FAIL job={job_id} op={op} ms={ms:.1f} err={err}")
 
+    def _flush_deferred(self, items: List[Any], lines: List[str]) -> None:
+        if items:
+            if self._poster is not None:
+                self._poster.put(items)  # one entry: the poster pipelines the whole batch
+            else:
+                for it in items:
+                    self._post(self.ctl, it)
+        if lines:
+            sys.stdout.write("\n".join(lines) + "\n")
+            sys.stdout.flush()
+
     @staticmethod
-    def _post(ctl: "Controller", item) -> None:
+    def _post(ctl: "Controller", item, attempts_done: int = 0) -> None:
         try:
-            ctl.result(*item)
+            ctl.result(*item, attempts_done=attempts_done)
         except Exception as exc:
             log_every("result", f"{LOG} post result error: {exc}")
 
     def _poster_loop(self) -> None:
         ctl = Controller(CONTROLLER_URL, HTTP_TIMEOUT_SEC)  # own keep-alive session (not shared across threads)
+        pipe = PipelinedPoster(CONTROLLER_URL, HTTP_TIMEOUT_SEC) if RESULT_PIPELINE else None
+        if pipe is not None and not pipe.ok:
+            pipe = None
+        import queue as _q
+
         while True:
-            item = self._poster.get()
+            # queue entries: one result tuple, a list of them (a batch's results), or None (stop)
+            entries = [self._poster.get()]
+            if pipe is not None:  # everything already queued goes out in pipelined batches
+                while entries[-1] is not None:
+                    try:
+                        entries.append(self._poster.get_nowait())
+                    except _q.Empty:
+                        break
+            stop = entries[-1] is None
+            batch = [it for e in entries if e is not None for it in (e if isinstance(e, list) else [e])]
             try:
-                if item is None:
-                    return
-                self._post(ctl, item)
+                for b0 in range(0, len(batch), PipelinedPoster.MAX_BATCH):
+                    part = batch[b0:b0 + PipelinedPoster.MAX_BATCH]
+                    rest = pipe.post_many(part) if pipe is not None and len(part) > 1 else [(it, 0) for it in part]
+                    for it, tried in rest:
+                        self._post(ctl, it, tried)
             finally:
-                self._poster.task_done()
+                for _ in entries:
+                    self._poster.task_done()
+            if stop:
+                if pipe is not None:
+                    pipe.close()
+                return
 
     def flush_results(self) -> None:
         """Wait until every queued result is posted (shutdown / tests)."""
@@ -678,6 +856,7 @@ class Agent:
             self._note_rank_lost(exc)
             outs = [("err", exc, tr)] * len(jobs)
         ms = (time.time() - t0) * 1000.0
+        defer: Tuple[List[Any], List[str]] = ([], [])
         for (job_id, _, _, epoch), res in zip(jobs, outs):
             out, err = None, None
             if res[0] == "ok":
@@ -690,7 +869,8 @@ class Agent:
                 tr = res[2] if len(res) > 2 else "".join(
                     traceback.format_exception(type(exc), exc, exc.__traceback__, limit=12))
                 err = {"type": type(exc).__name__, "message": str(exc), "trace": tr}
-            self._finish(lease_id, job_id, op, epoch, out, err, ms)
+            self._finish(lease_id, job_id, op, epoch, out, err, ms, defer)
+        self._flush_deferred(*defer)
 
     def run_tasks(self, lease_id: str, tasks: List[Any]) -> None:
         """Every task of the lease, in order; with LEASE_BATCH, same-op jobs of a
@@ -710,14 +890,24 @@ class Agent:
                     groups.setdefault(j[1], []).append(j)
             groups = {op: js for op, js in groups.items() if len(js) > 1}
         done: set = set()
+        # the results of consecutive single jobs go to the poster (and their log lines to stdout)
+        # in groups: flushed every 64 jobs, after 2 ms, before a batch and at the end of the lease
+        defer: Tuple[List[Any], List[str]] = ([], [])
+        t_flush = time.monotonic()
         for j in jobs:
             op = j[1]
             if op in groups:
+                self._flush_deferred(*defer)
+                defer = ([], [])
                 if op not in done:
                     done.add(op)
                     self._run_batch(lease_id, groups[op])
                 continue
-            self._run_one(lease_id, j)
+            self._run_one(lease_id, j, defer)
+            if len(defer[0]) >= 64 or time.monotonic() - t_flush >= 0.002:
+                self._flush_deferred(*defer)
+                defer, t_flush = ([], []), time.monotonic()
+        self._flush_deferred(*defer)
 
     def _note_rank_lost(self, exc: BaseException) -> None:
         """A job that lost a DP rank ends the loop after its result: exit non-zero."""

@@ -36,6 +36,9 @@ def main() -> int:
     ap.add_argument("--batch", default="1", help="LEASE_BATCH")
     ap.add_argument("--dp", type=int, default=1,
                     help="agent ranks (torch.distributed.run, one process per GPU; rank 0 leases)")
+    ap.add_argument("--controller", default="fast", choices=["fast", "mock"],
+                    help="input form: the asyncio stand-in (bench/fast_controller.py) or the test mock "
+                         "(ThreadingHTTPServer, itself the ceiling at ~6-7k results/s)")
     ap.add_argument("--dp-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse N ranks on fewer GPUs (ranks share a card)")
     a = ap.parse_args()
@@ -115,7 +118,15 @@ def input_form(a) -> int:
         n = int(rng.integers(16, S - 2))
         return [101] + [int(x) for x in rng.integers(1000, 30000, n)] + [102] + [0] * (S - n - 2)
 
-    ctl = MockController().start()
+    if a.controller == "fast":
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from fast_controller import FastController
+
+        ctl = FastController().start()
+        count = lambda c: c.n_results()  # noqa: E731
+    else:
+        ctl = MockController().start()
+        count = lambda c: len(c.results)  # noqa: E731
 
     def job(i):
         return {"id": f"j{i}", "op": "map_classify", "job_epoch": i,
@@ -128,11 +139,11 @@ def input_form(a) -> int:
     p = subprocess.Popen([sys.executable, "app.py"], cwd=REPO, env=env, stdout=subprocess.DEVNULL,
                          stderr=subprocess.DEVNULL)
     try:
-        ok = ctl.wait(lambda c: len(c.results) >= nwarm, 600)
+        ok = ctl.wait(lambda c: count(c) >= nwarm, 600)
         for b0 in range(0, a.jobs, a.max_tasks):
             ctl.lease(*[job(i) for i in range(b0, min(a.jobs, b0 + a.max_tasks))], lease_id=f"L{b0}")
         t0 = time.perf_counter()
-        ok = ok and ctl.wait(lambda c: len(c.results) >= nwarm + a.jobs, 1200)
+        ok = ok and ctl.wait(lambda c: count(c) >= nwarm + a.jobs, 1200)
         el = time.perf_counter() - t0
     finally:
         p.send_signal(signal.SIGTERM)
@@ -147,7 +158,9 @@ def input_form(a) -> int:
     print(json.dumps({"metric": f"classified rows/sec end to end through the agent, 1-row input jobs ({a.model}, 1 GPU)",
                       "value": round(a.jobs / el, 1), "unit": "rows/s", "higher_is_better": True,
                       "config": {"jobs": a.jobs, "max_tasks": a.max_tasks, "lease_batch": a.batch, "seq_len": S,
+                                 "jobs_per_lease": a.max_tasks, "leases_per_sec": round(a.jobs / a.max_tasks / el, 1),
                                  "result_keys": sorted(res[0]["result"]),
+                                 "controller": a.controller,
                                  "transport": "HTTP/1.1 keep-alive, loopback mock controller",
                                  "data": "synthetic token ids, random-init weights"}}), flush=True)
     return 0

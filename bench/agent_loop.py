@@ -29,8 +29,16 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=5000)
     ap.add_argument("--max-tasks", type=int, default=1)
+    ap.add_argument("--controller", default="mock", choices=["mock", "fast"],
+                    help="fast: the asyncio stand-in (bench/fast_controller.py) instead of the test mock")
     a = ap.parse_args()
-    ctl = MockController().start()
+    if a.controller == "fast":
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from fast_controller import FastController
+
+        ctl = FastController().start()
+    else:
+        ctl = MockController().start()
     k = max(1, a.max_tasks)
     for i in range(0, a.jobs, k):
         ctl.lease(*[{"id": f"j{j}", "op": "echo", "payload": {"i": j}} for j in range(i, min(a.jobs, i + k))],
@@ -42,7 +50,8 @@ def main() -> int:
     try:
         ok = ctl.wait(lambda c: len(c.lease_requests) >= 1, 120)
         t0 = time.perf_counter()
-        ok = ok and ctl.wait(lambda c: len(c.results) >= a.jobs, 600)
+        count = (lambda c: c.n_results()) if a.controller == "fast" else (lambda c: len(c.results))
+        ok = ok and ctl.wait(lambda c: count(c) >= a.jobs, 600)
         el = time.perf_counter() - t0
     finally:
         p.send_signal(signal.SIGTERM)
@@ -54,7 +63,8 @@ def main() -> int:
     v = a.jobs / el
     print(json.dumps({"metric": "echo jobs/sec end to end (agent loop vs mock controller)", "value": round(v, 1),
                       "unit": "jobs/s", "higher_is_better": True, "vs_baseline": round(v / BASELINE_JOBS_PER_SEC, 2),
-                      "config": {"jobs": a.jobs, "max_tasks": k, "transport": "HTTP/1.1 keep-alive, loopback"}}))
+                      "config": {"jobs": a.jobs, "max_tasks": k, "controller": a.controller,
+                                 "transport": "HTTP/1.1 keep-alive, loopback"}}))
     return 0
 
 

@@ -81,7 +81,7 @@ def test_rank_lost_fails_the_lease_taken_ahead(monkeypatch):
     posted, ran = [], []
 
     class Ctl(FakeCtl):
-        def result(self, lease_id, job_id, epoch, status, result, error):
+        def result(self, lease_id, job_id, epoch, status, result, error, attempts_done=0):
             posted.append((lease_id, job_id, epoch, status, error and error["type"]))
 
     monkeypatch.setattr(app, "Controller", Ctl)

@@ -171,7 +171,11 @@ def test_async_result_poster_keeps_every_result(ctl):
         code, out = stop_agent(p)
     assert code == 0, out
     got = [(r["job_id"], r["job_epoch"], r["result"]["echo"]["i"]) for r in ctl.results]
-    assert got == [(f"a{i}", i, i) for i in range(12)]
+    # every result exactly once with its epoch, FIFO except the retried one (with RESULT_PIPELINE
+    # the results queued behind it were already on the wire when its 500 came back)
+    assert sorted(got) == sorted((f"a{i}", i, i) for i in range(12))
+    assert [g for g in got if g[0] != "a3"] == [(f"a{i}", i, i) for i in range(12) if i != 3]
+    assert ctl.result_attempts["a3"] == 2
 
 
 def _order(ctl):
