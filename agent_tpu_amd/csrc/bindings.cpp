@@ -159,6 +159,17 @@ PYBIND11_MODULE(_atpu, m) {
       },
       py::arg("dst"), py::arg("n"), py::arg("f32"), py::arg("seed"), py::arg("sid"), py::arg("scale0"), py::arg("n0"),
       py::arg("scale1"), py::arg("threads") = 8, "CPU twin of rand_fill (bit-identical values)");
+  m.def(
+      "t5_ffn_fused",
+      [](uintptr_t x, uintptr_t wi, uintptr_t wo, uintptr_t y, int M, int d, int f, float eps, uintptr_t h_ws,
+         uintptr_t sync, uintptr_t stream) {
+        t5_ffn_fused(P<const bf16>(x), P<const bf16>(wi), P<const bf16>(wo), P<bf16>(y), M, d, f, eps, P<bf16>(h_ws),
+                     P<unsigned>(sync), S(stream));
+      },
+      py::arg("x"), py::arg("wi"), py::arg("wo"), py::arg("y"), py::arg("M"), py::arg("d"), py::arg("f"),
+      py::arg("eps"), py::arg("h_ws"), py::arg("sync"), py::arg("stream"),
+      "persistent-launch prototype: the T5-base decode FFN block (<= 4 rows) in one launch");
+  m.def("t5_ffn_fused_ws_bytes", &t5_ffn_fused_ws_bytes);
   m.def("gemv_selected", &gemv_selected, py::arg("M"), py::arg("N"), py::arg("epi"),
         "true when gemm_bf16 runs this [M, N] problem / epilogue on the <= 4-row GEMV");
   m.def("gemm_force_tile", &gemm_force_tile, py::arg("set") = -1, "GEMM kernel family override: 0 auto, 64, 128, 256");

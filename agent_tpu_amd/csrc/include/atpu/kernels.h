@@ -17,6 +17,14 @@ typedef __bf16 bf16;
 void rand_fill(void* dst, int64_t n, bool f32, uint64_t seed, uint64_t sid, float scale0, int64_t n0, float scale1,
                hipStream_t stream);
 
+// ---------------------------------------------------------------- persistent decode FFN (prototype)
+// y = x + relu(rsqrt(mean(x^2) + eps) * x . wi^T) . wo^T for <= 4 rows of the T5-base FFN (d 768,
+// d_ff 3072) in ONE launch with one in-launch grid barrier (kernels/decode_ffn.hip). h_ws: bf16
+// [4, 3072]; sync: 3 uint32 words zeroed once at allocation, one set per concurrent stream.
+size_t t5_ffn_fused_ws_bytes();
+void t5_ffn_fused(const bf16* x, const bf16* wi, const bf16* wo, bf16* y, int M, int d, int f, float eps, bf16* h_ws,
+                  unsigned* sync, hipStream_t stream);
+
 // ---------------------------------------------------------------- GEMM (K3/K5/K6)
 enum GemmEpilogue : int {
   kEpiBias = 1,

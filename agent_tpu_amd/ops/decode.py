@@ -373,3 +373,22 @@ def beam_select(sc: torch.Tensor, tk: torch.Tensor, nb: int, V: int, eos: int, h
     same_device(sc, tk, stage, rec)
     native().beam_select(ptr(sc), ptr(tk), B, nb, K2, int(V), int(eos), int(bool(hit_all)), float(neg), ptr(stage),
                          ptr(rec), launch_stream(sc))
+
+
+def t5_ffn_fused(x: torch.Tensor, wi: torch.Tensor, wo: torch.Tensor, eps: float,
+                 sync: torch.Tensor, out: Optional[torch.Tensor] = None,
+                 h_ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Persistent-launch prototype (``csrc/kernels/decode_ffn.hip``): the T5-base decode FFN block
+    ``x + relu(rms(x) . wi^T) . wo^T`` for <= 4 rows in ONE launch (``wi`` with the RMSNorm
+    gamma folded in). ``sync``: int32 [>= 3], zeroed once, one per concurrent stream."""
+    check_bf16_dev(x, "x")
+    check(x.dim() == 2 and x.is_contiguous() and wi.is_contiguous() and wo.is_contiguous(), "contiguous operands")
+    check(sync.dtype == torch.int32 and sync.numel() >= 3 and sync.is_cuda, "sync: int32 [3] on the device")
+    M, d = x.shape
+    f = wi.shape[0]
+    out = torch.empty_like(x) if out is None else out
+    if h_ws is None:
+        h_ws = torch.empty(native().t5_ffn_fused_ws_bytes() // 2, dtype=torch.bfloat16, device=x.device)
+    native().t5_ffn_fused(ptr(x), ptr(wi), ptr(wo), ptr(out), M, d, f, float(eps), ptr(h_ws), ptr(sync),
+                          launch_stream(x))
+    return out

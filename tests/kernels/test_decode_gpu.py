@@ -1009,3 +1009,24 @@ def test_decode_advance_matches_reorder_path(gpu, rows, T, with_seq):
             t2 = min(step + 1, T - 1)
             assert torch.equal(sd.cpu()[:, :t2 + 1], s_ref[:, :t2 + 1]), step
         assert torch.equal(tokens.cpu(), tok) and int(std.item()) == step + 1
+
+
+@pytest.mark.parametrize("M", [1, 4])
+def test_t5_ffn_fused_matches_launches(gpu, M):
+    """Persistent-launch prototype (one grid barrier): the fused T5-base FFN block against the
+    two GEMV launches and the fp32 math, twice (the barrier words persist across launches)."""
+    from agent_tpu_amd.ops.decode import t5_ffn_fused
+
+    g = torch.Generator().manual_seed(M)
+    d, f, eps = 768, 3072, 1e-6
+    x = torch.randn(M, d, generator=g).to(torch.bfloat16).to(gpu)
+    wi = (torch.randn(f, d, generator=g) * d ** -0.5).to(torch.bfloat16).to(gpu)
+    wo = (torch.randn(d, f, generator=g) * f ** -0.5).to(torch.bfloat16).to(gpu)
+    sync = torch.zeros(3, dtype=torch.int32, device=gpu)
+    ref = ops.linear(ops.linear(x, wi, act="relu", rms_eps=eps), wo, residual=x)
+    for _ in range(2):
+        out = t5_ffn_fused(x, wi, wo, eps, sync)
+        torch.cuda.synchronize()
+        assert sync[2].item() == 0 and sync[0].item() == 0  # no give-up; the counter is back at 0
+        assert (out.float() - ref.float()).abs().max().item() <= 2e-2 * ref.float().abs().max().item()
+    assert sync[1].item() == 2  # one generation per launch
