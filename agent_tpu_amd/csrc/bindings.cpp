@@ -133,6 +133,23 @@ PYBIND11_MODULE(_atpu, m) {
       py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("in_fin"), py::arg("colsum"),
       py::arg("lens"), py::arg("scale"), py::arg("stream"));
   m.def(
+      "qkv_attention_ws",
+      [](uintptr_t A, int lda, uintptr_t Bt, int ldb, uintptr_t C, int ldc, uintptr_t bias, int M, int N, int K,
+         int epi, uintptr_t in_fin, uintptr_t colsum, uintptr_t lens, float scale, int mode, uintptr_t stream) {
+        GemmArgs g;
+        g.A = P<const bf16>(A); g.lda = lda; g.Bt = P<const bf16>(Bt); g.ldb = ldb; g.C = P<bf16>(C); g.ldc = ldc;
+        g.bias = P<const float>(bias); g.M = M; g.N = N; g.K = K; g.epi = epi;
+        g.in_fin = P<const float>(in_fin); g.colsum = P<const float>(colsum);
+        qkv_attention_ws(g, mode, P<const int32_t>(lens), scale, S(stream));
+      },
+      "wave-specialised QKV + attention (128 x 192 tiles); mode 0 stores Q|K|V, 1 timing only, 2 attention",
+      py::arg("A"), py::arg("lda"), py::arg("Bt"), py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("bias"),
+      py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("in_fin"), py::arg("colsum"),
+      py::arg("lens"), py::arg("scale"), py::arg("mode"), py::arg("stream"));
+  m.def("ws_variant", &ws_variant, "experiment knob of the wave-specialised QKV kernel; -1 reads", py::arg("set"));
+  m.def("qkv_attention_ws_ok", &qkv_attention_ws_ok, "shapes the wave-specialised QKV + attention kernel takes",
+        py::arg("M"), py::arg("N"), py::arg("K"));
+  m.def(
       "ln_stats_finalize",
       [](uintptr_t part, int slots, int M, int K, float eps, uintptr_t fin, uintptr_t stream) {
         ln_stats_finalize(P<const float>(part), slots, M, K, eps, P<float>(fin), S(stream));

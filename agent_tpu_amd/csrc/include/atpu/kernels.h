@@ -110,6 +110,12 @@ void gemm256h(const GemmArgs& g, int mode, hipStream_t stream);
 // Bt = the QKV weight with rows in [head][Q 64 | K 64 | V 64] order (bias / colsum likewise),
 // g.C = the context [M, N / 3] (row stride g.ldc), lens[M / 128] the sequence lengths
 void qkv_attention(const GemmArgs& g, const int32_t* lens, float scale, hipStream_t stream);
+// wave-specialised form (qkv_attn_ws.hip): 128 x 192 tiles (one sequence x one head), 4 MFMA
+// waves on the main loop while 4 waves stage operands and run the previous tile's attention.
+// mode 0 stores Q|K|V ([M, N], head order) to g.C, 1 timing only, 2 attention (as qkv_attention)
+bool qkv_attention_ws_ok(int M, int N, int K);
+int ws_variant(int set);  // experiment knob of the ws kernel (benchmarks); -1 reads
+void qkv_attention_ws(const GemmArgs& g, int mode, const int32_t* lens, float scale, hipStream_t stream);
 int attention_persist_mode(int set);  // packed BERT attention: 1 persistent (default), 0 per-item
 int num_cus();                        // CUs a persistent grid is sized for (device count, or the budget below)
 int cu_budget(int set);               // >0: size persistent grids for this many CUs (CU-masked streams)

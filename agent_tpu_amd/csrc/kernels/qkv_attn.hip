@@ -22,6 +22,7 @@
 // >= 1 consumes LN2 of the previous layer folded into the weights, as gemm256s).
 #include "atpu/common.h"
 #include "atpu/kernels.h"
+#include "atpu/lds_ops.h"
 
 #include <algorithm>
 
@@ -32,8 +33,6 @@ constexpr int kHImgA = 256 * 128;             // A image: 256 rows x 128 B
 constexpr int kHImgB = 192 * 128;             // B image: 192 rows x 128 B
 constexpr int kHBuf = kHImgA + kHImgB;        // one K-tile
 constexpr int kHStores = 24;                  // MODE 0 epilogue stores per wave (8 row x 3 col fragments)
-
-__device__ __forceinline__ int hsw(int r, int c) { return c ^ ((r >> 1) & 7); }
 
 // image row of staging round i (of the quarter) for the wave's 8-row group g8 = (i*8 + wave)*8
 __device__ __forceinline__ int hq_row(int q, int ql) {
@@ -46,51 +45,7 @@ __device__ __forceinline__ int hq_row(int q, int ql) {
 }
 constexpr int hq_rounds(int q) { return q == 2 ? 1 : 2; }
 
-// attention images (MODE 2): per sequence s of the tile, Q, K, V of the head as [128][128 B]
-// bf16 images, 16-B chunk c of row r at slot c ^ (r & 7). One swizzle is bank-conflict-free
-// for all three access patterns (checked by simulation, tools/lds_banks_qkv_attn.py): the
-// 16-B image writes (8-lane groups = 8 consecutive rows of one chunk, mod 32 banks), the
-// ds_read_b128 fragment reads of Q and K, and the transposed ds_read_b64_tr_b16 reads of V
-// (32-lane groups = 8 rows x 2 chunks, mod 64 banks). The operand-image swizzle c ^ ((r>>1)&7)
-// was 2-way on the writes and, for V, 2-way on the transposed reads.
-constexpr int kAImg = 128 * 128;
-__device__ __forceinline__ int asw(int r, int c) { return c ^ (r & 7); }
-
-// v_permlane16_swap: lane rows (16-lane groups) 1 and 3 of x trade places with rows 0 and 2
-// of y. On the two packed halves of MFMA fragments of row blocks i (x) and i+1 (y) it leaves
-// lane row G holding 8 consecutive columns (G >> 1: which 8 of the 16) of block i + (G & 1):
-// one 16-B LDS write per lane instead of two 8-B writes. The s_nop covers the VALU-write ->
-// permlane-read hazard.
-__device__ __forceinline__ void swap16(unsigned& x, unsigned& y) {
-  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
-}
-
-// ds_read_b128 by inline asm, waited for by lgkm_wait below: for the compiler-visible form the
-// waitcnt pass put one lgkmcnt(0) after all 20 Q/K reads of the attention instead of counted
-// waits, so the first QK^T MFMA waited for the last K fragment
-__device__ __forceinline__ bf16x8 ds_read128(const char* p) {
-  bf16x8 r;
-  const unsigned a = (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
-  return r;
-}
-// s_waitcnt lgkmcnt(N) that the two registers it retires pass through (so their consumers
-// cannot be scheduled above it)
-template <int N>
-__device__ __forceinline__ void lgkm_wait(bf16x8& a, bf16x8& b) {
-  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
-}
-
-typedef short hv4s __attribute__((vector_size(8)));
-// ds_read_b64_tr_b16 (per 16-lane group: lane 4q+p addresses row q, elements 4p..4p+3 of a
-// 4 x 16 block; lane i receives column i of the 4 rows). Inline asm: the builtin makes the
-// waitcnt pass drain the LDS-DMA stream in flight to the other operand buffer.
-__device__ __forceinline__ bf16x4 tr16(const char* p) {
-  hv4s r;
-  const unsigned a = (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
-  return __builtin_bit_cast(bf16x4, r);
-}
+constexpr int kAImg = kAttnImg;  // attention images (MODE 2): lds_ops.h
 
 template <int EPI, int MODE>
 __global__ __launch_bounds__(512, 1) void gemm256h_kernel(const bf16* __restrict__ A, int lda,
