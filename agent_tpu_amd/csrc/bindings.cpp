@@ -146,6 +146,7 @@ PYBIND11_MODULE(_atpu, m) {
       py::arg("A"), py::arg("lda"), py::arg("Bt"), py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("bias"),
       py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("in_fin"), py::arg("colsum"),
       py::arg("lens"), py::arg("scale"), py::arg("mode"), py::arg("stream"));
+  m.def("ws_stamps", &ws_stamps, "cycle stamps of the last ws launch (diagnostic build only)", py::arg("nblocks"));
   m.def("ws_variant", &ws_variant, "experiment knob of the wave-specialised QKV kernel; -1 reads", py::arg("set"));
   m.def("qkv_attention_ws_ok", &qkv_attention_ws_ok, "shapes the wave-specialised QKV + attention kernel takes",
         py::arg("M"), py::arg("N"), py::arg("K"));

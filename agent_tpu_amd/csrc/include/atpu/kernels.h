@@ -2,6 +2,7 @@
 // All launchers are asynchronous on the given stream and graph-capturable
 // (no allocation, no synchronisation inside).
 #pragma once
+#include <vector>
 
 #include <hip/hip_runtime.h>
 
@@ -115,6 +116,8 @@ void qkv_attention(const GemmArgs& g, const int32_t* lens, float scale, hipStrea
 // mode 0 stores Q|K|V ([M, N], head order) to g.C, 1 timing only, 2 attention (as qkv_attention)
 bool qkv_attention_ws_ok(int M, int N, int K);
 int ws_variant(int set);  // experiment knob of the ws kernel (benchmarks); -1 reads
+// per-workgroup cycle stamps of the last ws launch (diagnostic build -DATPU_WS_STAMPS; else empty)
+std::vector<unsigned long long> ws_stamps(int nblocks);
 void qkv_attention_ws(const GemmArgs& g, int mode, const int32_t* lens, float scale, hipStream_t stream);
 int attention_persist_mode(int set);  // packed BERT attention: 1 persistent (default), 0 per-item
 int num_cus();                        // CUs a persistent grid is sized for (device count, or the budget below)

@@ -1,5 +1,9 @@
 // BERT QKV projection + self-attention, wave-specialised ("give the
-// attention to one wave group while the other runs the next tile").
+// attention to one wave group while the other runs the next tile"), and the same structure
+// as a GEMM whose epilogue leaves through dedicated waves ("dedicated epilogue waves").
+// DEV BUILD ONLY (-DATPU_DEV_BUILD, build.py --dev): measured slower than the release kernels
+// (QKV+attention 489 vs 479 us, FFN1 693 vs 592 us at the bench shape; docs/PERF_NOTES.md
+// "Wave-specialised kernels"), kept as the recorded experiment; the release .so has stubs.
 //
 // qkv_attn.hip runs the attention of a tile in its epilogue with all 8 waves, so the MFMA
 // pipes idle for the image writes, the softmax and the context stores (~35 % of that kernel).
@@ -12,29 +16,34 @@
 //    LDS-DMA issue on these waves. After the last K-tile: bias (+ InNorm) -> bf16 Q, K, V
 //    images of the sequence in LDS, barrier, next tile.
 //  * loader/attention waves 4-7: between two barriers ("slots") they issue the LDS-DMA of the
-//    K-tile two ahead into the operand stage the barrier just freed, run one chunk of the
-//    PREVIOUS tile's attention (each wave 32 queries, the schedule of qkv_attn.hip's attend()),
-//    and wait for their DMA before arriving at the next barrier.
-// Barriers per tile: one per K-tile (KB_t: stage of K-tile t free, K-tile t+1 landed) and one
-// after the image writes (EB). Slots of the loader waves, tile T (NK K-tiles):
-//   slot -1 (EB(T-1) .. KB_0): vectors (bias, colsum, fin) of T; attention chunk 1 of T-1
-//   slot s  (KB_s .. KB_s+1), s = 0..NK-2: DMA of K-tile s+2 (s = NK-2: K-tile 0 of T+1);
-//           chunks 2, 3, 4+5 of T-1 in slots 0-2, its context stores in slot 3
-//   slot NK-1 (KB_NK-1 .. EB(T)): DMA of K-tile 1 of T+1
-// The attention of T-1 is over (its LDS reads retired) before KB_NK-1 of T, after which the
-// MMA waves overwrite the images. The last tile's attention runs after the final barrier.
+//    K-tiles ahead into the ring slots the barrier just freed, run one piece of the PREVIOUS
+//    tile's attention (each wave 32 queries; the math of qkv_attn.hip's attend()), and wait
+//    for their DMA before arriving at the next barrier.
+// Barriers per tile: one per K-tile (KB_t: K-tile t's ring slots free, K-tile t+1 landed) and
+// one after the image writes (EB). Slots of the loader waves, tile T (NK K-tiles):
+//   slot -1 (EB(T-1) .. KB_0): vectors (bias, colsum, fin) of T; attention piece 1 of T-1
+//   slot s  (KB_s .. KB_s+1 / EB): DMA of B K-tile s+2 and A K-tile s+AS (past NK: the next
+//           tile's); pieces 2-10 of T-1 in slots 0-8, its context stores in slot 9
+// The A operand ring is AS deep (2, or 3 with ws_variant bit 3 at K = 768: the activation
+// tiles, first touched in HBM, get two slots of latency), the B (weight) ring 2 deep. The
+// attention of T-1 is over (its LDS reads retired) before KB_NK-1 of T, after which the MMA
+// waves overwrite the images. The last tile's attention runs after the final barrier.
 //
-// LDS: 2 operand stages x 40 KiB (A 128 x 128 B + B 192 x 128 B), 3 attention images
-// (48 KiB), bias / colsum / fin (2.5 KiB): 130.5 KiB, one workgroup per CU.
+// LDS: A ring AS x 16 KiB, B ring 2 x 24 KiB, 3 attention images (48 KiB), bias / colsum / fin
+// (2.5 KiB): 130.5 / 146.5 KiB, one workgroup per CU.
 // MODE 0 stores Q|K|V (bf16, head order) instead of attention (exactness of the GEMM part);
-// MODE 1 is timing-only (no epilogue). NK = K / 64: 12 (BERT-base), 16 (BERT-large).
+// MODE 1 is timing-only (no epilogue). MODE 3 / 4: a plain GEMM (N % 192) whose output
+// leaves through the loader waves (MODE 3 with GELU: BERT's FFN1), the MMA waves' epilogue
+// only the bias / InNorm image. NK = K / 64: 12 (BERT-base), 16 (BERT-large).
 #include "atpu/common.h"
 #include "atpu/kernels.h"
 #include "atpu/lds_ops.h"
 
 #include <algorithm>
+#include <vector>
 
 namespace atpu {
+#ifdef ATPU_DEV_BUILD
 namespace {
 
 constexpr int kWImgA = 128 * 128;  // A operand image: 128 rows x 128 B
@@ -51,6 +60,27 @@ struct WsLds {
   static_assert(kSize <= 160 * 1024, "LDS budget");
 };
 
+// Diagnostic build only (-DATPU_WS_STAMPS, a separate .so; the release kernel has no stamps):
+// s_memtime cycle sums per workgroup, written with vector stores to a buffer of their own that
+// no output reads. MMA wave 0: [0] K-tile barrier waits, [1] image-barrier waits, [2] image
+// writes, [3] total, [4] tiles; loader wave 4: [5] barrier waits, [6] DMA waits, [7] total,
+// [16 + c] attention piece c (1..11). 32 words per workgroup.
+#ifdef ATPU_WS_STAMPS
+__device__ unsigned long long g_ws_stamps[1024 * 32];
+#define WS_NOW() __builtin_amdgcn_s_memtime()
+#define WS_T(v)                         \
+  __builtin_amdgcn_sched_barrier(0);    \
+  const uint64_t v = WS_NOW();          \
+  __builtin_amdgcn_sched_barrier(0)
+#define WS_ACC(i, t0)                   \
+  __builtin_amdgcn_sched_barrier(0);    \
+  st[i] += WS_NOW() - (t0);             \
+  __builtin_amdgcn_sched_barrier(0)
+#else
+#define WS_T(v)
+#define WS_ACC(i, t0)
+#endif
+
 template <int EPI, int MODE, int NK, int AS>
 __global__ __launch_bounds__(512, 1) void qkv_ws_kernel(const bf16* __restrict__ A, int lda,
                                                         const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C,
@@ -58,8 +88,8 @@ __global__ __launch_bounds__(512, 1) void qkv_ws_kernel(const bf16* __restrict__
                                                         const float* __restrict__ in_fin,
                                                         const float* __restrict__ colsum, int M, int N,
                                                         const int32_t* __restrict__ lens, float scale, int var) {
-  static_assert(NK % 2 == 0 && NK % AS == 0 && NK >= 8,
-                "K-tiles: whole rings per tile (every tile starts in stage 0), >= 8 (attention slots)");
+  static_assert(NK % 2 == 0 && NK % AS == 0 && NK >= 11,
+                "K-tiles: whole rings per tile (every tile starts in stage 0), 11 attention slots");
   constexpr bool kIn = EPI & kEpiInNorm;
   using L = WsLds<AS>;
   constexpr int kWAttn = L::kAttn, kWBias = L::kBias, kWCol = L::kCol, kWFin = L::kFin;
@@ -70,10 +100,17 @@ __global__ __launch_bounds__(512, 1) void qkv_ws_kernel(const bf16* __restrict__
   const int G = gridDim.x;
   int v = blockIdx.x;
   if (v >= ntiles) return;
+  // tile order: consecutive tiles (one XCD's concurrent set, xcd_remap) walk groups of GM
+  // row blocks x all column tiles, the GM row blocks fastest (var bits 5-6: GM = 1, 2, 4, 8).
+  // GM = 1 is the column-fastest order; with GM = 4 an XCD's 32 concurrent tiles need 4 A and
+  // 8 B panels (3.2 MB at K = 768) instead of every B panel (4.7 MB for FFN1's N = 3072).
+  const int mt = M / 128, gm_log = (var >> 5) & 3;
   auto tile_of = [&](int vv, int& m0, int& n0) {
     const int t = xcd_remap(vv, ntiles);
-    m0 = (t / ntn) * 128;
-    n0 = (t % ntn) * 192;
+    const int gsz = ntn << gm_log, g = t / gsz, r = t - g * gsz;
+    const int gm = min(1 << gm_log, mt - (g << gm_log));
+    m0 = ((g << gm_log) + r % gm) * 128;
+    n0 = (r / gm) * 192;
   };
   auto opaque_lane = [] {
     int l = __lane_id();
@@ -81,6 +118,15 @@ __global__ __launch_bounds__(512, 1) void qkv_ws_kernel(const bf16* __restrict__
     return l;
   };
   const int fr = lane & 15, fc = lane >> 4;
+#ifdef ATPU_WS_STAMPS
+  uint64_t st[32] = {};
+  const uint64_t st_start = WS_NOW();
+  auto st_flush = [&](int lo, int hi) {
+    st[lo == 0 ? 3 : 7] = WS_NOW() - st_start;
+    if (lane == 0)
+      for (int i = lo; i < hi; ++i) g_ws_stamps[blockIdx.x * 32 + i] = st[i];
+  };
+#endif
 
   if (wave < 4) {
     // =============================== MMA waves ===============================
@@ -127,14 +173,17 @@ __global__ __launch_bounds__(512, 1) void qkv_ws_kernel(const bf16* __restrict__
         __builtin_amdgcn_sched_barrier(0);
         mma(a0, b0);
         __builtin_amdgcn_sched_barrier(0);
+        WS_T(t_kb);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // KB_t
+        WS_ACC(0, t_kb);
         __builtin_amdgcn_sched_barrier(0);
         if (t + 1 < NK) read_ks(t + 1, 0, a0, b0);
         __builtin_amdgcn_sched_barrier(0);
         mma(a1, b1);
         __builtin_amdgcn_sched_barrier(0);
       }
+      WS_T(t_epi);
       if constexpr (MODE == 1) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -208,16 +257,26 @@ __global__ __launch_bounds__(512, 1) void qkv_ws_kernel(const bf16* __restrict__
       }
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      WS_ACC(2, t_epi);
+      WS_T(t_eb);
       __builtin_amdgcn_s_barrier();  // EB: the images are complete
+      WS_ACC(1, t_eb);
       __builtin_amdgcn_sched_barrier(0);
+#ifdef ATPU_WS_STAMPS
+      st[4] += 1;
+#endif
       v += G;
       if (v >= ntiles) break;
     }
+#ifdef ATPU_WS_STAMPS
+    if (wave == 0) st_flush(0, 5);
+#endif
     return;
   }
 
   // ============================ loader / attention waves ============================
   const int l = wave - 4;
+  if (var & 16) __builtin_amdgcn_s_setprio(1);
   // LDS-DMA: this wave stages A rows l*32..+32 (4 x 8 rows) and B rows l*48..+48 (6 x 8 rows)
   // of a K-tile; the lane's 32-bit source offsets carry the swizzle (the DMA writes lane-linear)
   uint32_t soffA[4], soffB[6];
@@ -267,18 +326,16 @@ __global__ __launch_bounds__(512, 1) void qkv_ws_kernel(const bf16* __restrict__
   auto slot_end = [&](auto fly_c) {
     constexpr int fly = decltype(fly_c)::value;
     __builtin_amdgcn_sched_barrier(0);
+    WS_T(t_vm);
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(fly) : "memory");
+    WS_ACC(6, t_vm);
+    WS_T(t_bar);
     __builtin_amdgcn_s_barrier();
+    WS_ACC(5, t_bar);
     __builtin_amdgcn_sched_barrier(0);
   };
   using Fly0 = std::integral_constant<int, 0>;
   using FlyA = std::integral_constant<int, AS == 3 ? 4 : 0>;
-  // the DMA of slot s (s >= 0): B of K-tile s + 2, A of K-tile s + AS (runtime s: this tile)
-  auto slot_dma = [&](int sl) {
-    stageB(sl + 2, sl & 1);
-    stageA(sl + AS, (sl + AS) % AS);
-  };
-
   int m0, n0;
   tile_of(v, m0, n0);
   set_srcA(m0);
@@ -288,17 +345,17 @@ __global__ __launch_bounds__(512, 1) void qkv_ws_kernel(const bf16* __restrict__
 #pragma unroll
   for (int k = 0; k < AS; ++k) stageA(k, k);
   slot_end(Fly0{});  // the first tile's B K-tiles 0-1 and A K-tiles 0..AS-1 landed
-  int pm0 = 0, ph = 0;
+  int pm0 = 0, ph = 0, pn0 = 0;
   // one tile of the loader waves; ATT: the previous tile's attention runs in its slots (a
-  // compile-time flag - a runtime `if (pending)` around every chunk made the attention state
+  // compile-time flag - a runtime `if (pending)` around every piece made the attention state
   // of both paths live at each join: ~100 VGPRs of spills). Returns false after the last tile.
   auto tile_body = [&](auto att_c) -> bool {
-    constexpr bool pending = decltype(att_c)::value && MODE == 2;
+    constexpr bool pending = decltype(att_c)::value && MODE >= 2;
     const int vn = v + G;
     const bool has_next = vn < ntiles;
     int nm0 = 0, nn0 = 0;
     if (has_next) tile_of(vn, nm0, nn0);
-    // ---- attention of the previous tile (pm0, head ph), queries l*32..+32, in chunks; the
+    // ---- attention of the previous tile (pm0, head ph), queries l*32..+32, in pieces; the
     // state is local to one tile (declared outside the tile loop it was loop-carried: spills)
     const char* qi = lds + kWAttn;
     const char* ki = qi + kAttnImg;
@@ -352,70 +409,94 @@ __global__ __launch_bounds__(512, 1) void qkv_ws_kernel(const bf16* __restrict__
       }
       return vf;
     };
-    // chunk 1: the sequence length (scalar load, consumed before any counted LDS wait), Q and K
-    // fragment reads, S(qp 0) = K.Q0^T with counted waits, mask
-    // LDS addresses from an opaque lane id inside each chunk: from `lane` they are loop-invariant,
-    // and hoisted out of the tile loop they held ~60 VGPRs for its whole length (spills)
-    auto chunk1 = [&]() {
-      len = min(lens[pm0 >> 7], 128);
-      asm volatile("" : "+s"(len));
-      const int ln = opaque_lane(), fr = ln & 15, fc = ln >> 4;
-  #pragma unroll
-      for (int qp = 0; qp < 2; ++qp)
-  #pragma unroll
-        for (int ds = 0; ds < 2; ++ds) {
-          const int r = l * 32 + qp * 16 + fr;
-          qf[qp][ds] = ds_read128(qi + r * 128 + asw(r, ds * 4 + fc) * 16);
-        }
-  #pragma unroll
-      for (int kt = 0; kt < 8; ++kt)
-  #pragma unroll
-        for (int ds = 0; ds < 2; ++ds) {
-          const int r = kt * 16 + fr;
-          kf[kt][ds] = ds_read128(ki + r * 128 + asw(r, ds * 4 + fc) * 16);
-        }
-      auto qk0 = [&](auto kt_c) {
-        constexpr int kt = decltype(kt_c)::value;
-        if constexpr (kt == 0) {
-          lgkm_wait<14>(qf[0][0], qf[0][1]);
-          asm volatile("" : "+v"(qf[1][0]), "+v"(qf[1][1]), "+v"(kf[0][0]), "+v"(kf[0][1]));
-        } else {
-          lgkm_wait<14 - 2 * kt>(kf[kt][0], kf[kt][1]);
-        }
-        s[0][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][0], qf[0][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        s[0][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][1], qf[0][1], s[0][kt], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      };
-      qk0(std::integral_constant<int, 0>{});
-      qk0(std::integral_constant<int, 1>{});
-      qk0(std::integral_constant<int, 2>{});
-      qk0(std::integral_constant<int, 3>{});
-      qk0(std::integral_constant<int, 4>{});
-      qk0(std::integral_constant<int, 5>{});
-      qk0(std::integral_constant<int, 6>{});
-      qk0(std::integral_constant<int, 7>{});
-      mask(0);
-    };
-    // chunk 2: S(qp 1) MFMAs beside softmax(qp 0)
-    auto chunk2 = [&]() {
-  #pragma unroll
-      for (int kt = 0; kt < 8; ++kt) {
-        s[1][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][0], qf[1][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        s[1][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][1], qf[1][1], s[1][kt], 0, 0, 0);
+    // The attention in 11 pieces, one per slot (slots -1 .. 9), each well under the MMA waves'
+    // K-tile: the measured (stamped) chunks of a 5- and an 8-way split ran 550-1300 cycles under
+    // the main loop's LDS and MFMA traffic, and every one longer than the MMA waves' ~1170-cycle
+    // K-tile held them at the next barrier (29 % of their cycles).
+    //  1: len (scalar load, consumed before any counted LDS wait), Q and K fragment reads,
+    //     S(qp 0) of key tiles 0-3 with counted waits;  2: key tiles 4-7, mask;
+    //  3: S(qp 1);  4: softmax(qp 0), mask(qp 1);  5: the 32 transposed V reads, softmax(qp 1);
+    //  6, 7: P0.V (key steps 0-1, 2-3);  8, 9: the qp 0 context packed, P1.V;
+    //  10: context -> this wave's 32 Q rows (free once read) and back as whole 128-B rows;
+    //  11: the global stores (issued at the start of slot 9, before its DMA).
+    // LDS addresses come from an opaque lane id inside each piece: from `lane` they are
+    // loop-invariant, and hoisted out of the tile loop they held ~60 VGPRs (spills).
+    u32x4 cval[4];
+    auto qk0 = [&](auto kt_c) {
+      constexpr int kt = decltype(kt_c)::value;
+      if constexpr (kt == 0) {
+        lgkm_wait<14>(qf[0][0], qf[0][1]);
+        asm volatile("" : "+v"(qf[1][0]), "+v"(qf[1][1]), "+v"(kf[0][0]), "+v"(kf[0][1]));
+      } else if constexpr (kt < 4) {
+        lgkm_wait<14 - 2 * kt>(kf[kt][0], kf[kt][1]);
+      } else {
+        lgkm_wait<0>(kf[kt][0], kf[kt][1]);  // landed at the slot end: pins only
       }
-      softmax(0);
+      s[0][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][0], qf[0][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      s[0][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][1], qf[0][1], s[0][kt], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    // the V reads retired (slot end, or here for the last tile) and their registers pinned
+    // after the wait: the tr16 asm outputs look available to the compiler at issue
+    auto v_landed = [&]() {
   #pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+      for (int ks = 0; ks < 4; ++ks)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vlo[ks][0]), "+v"(vlo[ks][1]), "+v"(vlo[ks][2]), "+v"(vlo[ks][3]),
+                     "+v"(vhi[ks][0]), "+v"(vhi[ks][1]), "+v"(vhi[ks][2]), "+v"(vhi[ks][3])::"memory");
+    };
+    auto pv = [&](int qp, int ks0) {
+  #pragma unroll
+      for (int ks = ks0; ks < ks0 + 2; ++ks) {
+  #pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          o[qp][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vfrag(ks, dt), pf[qp][ks],
+                                                              ks ? o[qp][dt] : f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        o[qp][4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qp][ks], ks ? o[qp][4] : f32x4{0.f, 0.f, 0.f, 0.f},
+                                                           0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
-      mask(1);
     };
-    // chunk 3: all 32 transposed V reads, P0.V beside softmax(qp 1); key step ks waits for its
-    // 8 V reads (the lgkmcnt field holds at most 15: steps 0-1 wait for 17 of the 32)
-    auto chunk3 = [&]() {
-      {
+    // 1 / (row sum of the bf16 P): v_rcp_f32 (1 ulp) before the bf16 rounding of the context
+    auto inv_sum = [&](int qp) { return len > 0 && o[qp][4][0] > 0.f ? __builtin_amdgcn_rcpf(o[qp][4][0]) : 0.f; };
+    auto piece_impl = [&](int c) {
+      if (c == 1) {
+        len = min(lens[pm0 >> 7], 128);
+        asm volatile("" : "+s"(len));
+        const int ln = opaque_lane(), fr = ln & 15, fc = ln >> 4;
+  #pragma unroll
+        for (int qp = 0; qp < 2; ++qp)
+  #pragma unroll
+          for (int ds = 0; ds < 2; ++ds) {
+            const int r = l * 32 + qp * 16 + fr;
+            qf[qp][ds] = ds_read128(qi + r * 128 + asw(r, ds * 4 + fc) * 16);
+          }
+  #pragma unroll
+        for (int kt = 0; kt < 8; ++kt)
+  #pragma unroll
+          for (int ds = 0; ds < 2; ++ds) {
+            const int r = kt * 16 + fr;
+            kf[kt][ds] = ds_read128(ki + r * 128 + asw(r, ds * 4 + fc) * 16);
+          }
+        qk0(std::integral_constant<int, 0>{});
+        qk0(std::integral_constant<int, 1>{});
+        qk0(std::integral_constant<int, 2>{});
+        qk0(std::integral_constant<int, 3>{});
+      } else if (c == 2) {
+        qk0(std::integral_constant<int, 4>{});
+        qk0(std::integral_constant<int, 5>{});
+        qk0(std::integral_constant<int, 6>{});
+        qk0(std::integral_constant<int, 7>{});
+        mask(0);
+      } else if (c == 3) {
+  #pragma unroll
+        for (int kt = 0; kt < 8; ++kt) {
+          s[1][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][0], qf[1][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          s[1][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][1], qf[1][1], s[1][kt], 0, 0, 0);
+        }
+      } else if (c == 4) {
+        softmax(0);
+        mask(1);
+      } else if (c == 5) {
         const int ln = opaque_lane();
         const int tq = (ln >> 2) & 3, tp = ln & 3;
         const int k0 = (ln >> 4) * 4 + tq;
@@ -424,133 +505,116 @@ __global__ __launch_bounds__(512, 1) void qkv_ws_kernel(const bf16* __restrict__
         for (int ks = 0; ks < 4; ++ks)
   #pragma unroll
           for (int dt = 0; dt < 4; ++dt) {
-            const int c = asw(k0, dt * 2 + (tp >> 1)) * 16;
-            vlo[ks][dt] = tr16(row + ks * 32 * 128 + c);
-            vhi[ks][dt] = tr16(row + (ks * 32 + 16) * 128 + c);
+            const int cc = asw(k0, dt * 2 + (tp >> 1)) * 16;
+            vlo[ks][dt] = tr16(row + ks * 32 * 128 + cc);
+            vhi[ks][dt] = tr16(row + (ks * 32 + 16) * 128 + cc);
           }
+        __builtin_amdgcn_sched_barrier(0);
+        softmax(1);
+      } else if (c == 6) {
+        v_landed();
+        pv(0, 0);
+      } else if (c == 7) {
+        pv(0, 2);
+      } else if (c == 8) {
+        const float inv0 = inv_sum(0);
+  #pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          xw[dt][0] = pack_bf16x2(o[0][dt][0] * inv0, o[0][dt][1] * inv0);
+          xw[dt][1] = pack_bf16x2(o[0][dt][2] * inv0, o[0][dt][3] * inv0);
+        }
+        pv(1, 0);
+      } else if (c == 9) {
+        pv(1, 2);
+      } else if (c == 10) {
+        const int ln = opaque_lane(), fr = ln & 15, fc = ln >> 4;
+        char* ost = const_cast<char*>(qi) + l * 32 * 128;
+        const float inv1 = inv_sum(1);
+  #pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          unsigned x0 = xw[dt][0], x1 = xw[dt][1];
+          unsigned y0 = pack_bf16x2(o[1][dt][0] * inv1, o[1][dt][1] * inv1);
+          unsigned y1 = pack_bf16x2(o[1][dt][2] * inv1, o[1][dt][3] * inv1);
+          swap16(x0, y0);
+          swap16(x1, y1);
+          const int ro = (fc & 1) * 16 + fr, ch = dt * 2 + (fc >> 1);
+          ds_write128(ost + ro * 128 + asw(ro, ch) * 16, u32x4{x0, x1, y0, y1});
+        }
+        const int lr = ln >> 3, lc8 = ln & 7;
+  #pragma unroll
+        for (int hh = 0; hh < 4; ++hh) {
+          const int ro = hh * 8 + lr;
+          cval[hh] = ds_read128u(ost + ro * 128 + asw(ro, lc8) * 16);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cval[0]), "+v"(cval[1]), "+v"(cval[2]), "+v"(cval[3])::"memory");
+      } else if (c == 11) {
+        const int ln = opaque_lane();
+        const int lr = ln >> 3, lc8 = ln & 7;
+        bf16* obase = C + (size_t)(pm0 + l * 32 + lr) * ldc + ph * 64 + lc8 * 8;
+  #pragma unroll
+        for (int hh = 0; hh < 4; ++hh) *reinterpret_cast<u32x4*>(obase + (size_t)(hh * 8) * ldc) = cval[hh];
       }
       __builtin_amdgcn_sched_barrier(0);
-      softmax(1);
+    };
+    // MODE 3 / 4 (a GEMM whose output leaves through the loader waves): piece c = 1..6 takes
+    // 16 rows (two 8-row blocks) of image (c - 1) >> 1 of this wave's 32 rows, applies GELU
+    // (MODE 3, on the bf16-rounded pre-activation, as the bf16 model's gelu(linear(x))) and
+    // stores whole 128-B rows, non-temporal
+    auto store_piece = [&](int c) {
+      const int typ = (c - 1) >> 1, rb = (c - 1) & 1;
+      const int ln = opaque_lane(), ch = ln & 7;
+      u32x4 v[2];
+      int row[2];
   #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        if (ks == 0) asm volatile("s_waitcnt lgkmcnt(15)" : "+v"(vlo[0][0]), "+v"(vlo[0][1]), "+v"(vlo[0][2]), "+v"(vlo[0][3]),
-                                  "+v"(vhi[0][0]), "+v"(vhi[0][1]), "+v"(vhi[0][2]), "+v"(vhi[0][3])::"memory");
-        if (ks == 1) asm volatile("s_waitcnt lgkmcnt(15)" : "+v"(vlo[1][0]), "+v"(vlo[1][1]), "+v"(vlo[1][2]), "+v"(vlo[1][3]),
-                                  "+v"(vhi[1][0]), "+v"(vhi[1][1]), "+v"(vhi[1][2]), "+v"(vhi[1][3])::"memory");
-        if (ks == 2) asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(vlo[2][0]), "+v"(vlo[2][1]), "+v"(vlo[2][2]), "+v"(vlo[2][3]),
-                                  "+v"(vhi[2][0]), "+v"(vhi[2][1]), "+v"(vhi[2][2]), "+v"(vhi[2][3])::"memory");
-        if (ks == 3) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vlo[3][0]), "+v"(vlo[3][1]), "+v"(vlo[3][2]), "+v"(vlo[3][3]),
-                                  "+v"(vhi[3][0]), "+v"(vhi[3][1]), "+v"(vhi[3][2]), "+v"(vhi[3][3])::"memory");
+      for (int h = 0; h < 2; ++h) {
+        row[h] = l * 32 + rb * 16 + h * 8 + (ln >> 3);
+        v[h] = ds_read128u(qi + typ * kAttnImg + row[h] * 128 + asw(row[h], ch) * 16);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1])::"memory");
+      if constexpr (MODE == 3) {
+        float f[16];
   #pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-          o[0][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vfrag(ks, dt), pf[0][ks],
-                                                             ks ? o[0][dt] : f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        o[0][4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[0][ks], ks ? o[0][4] : f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        for (int h = 0; h < 2; ++h)
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            f[h * 8 + 2 * e] = __uint_as_float(v[h][e] << 16);
+            f[h * 8 + 2 * e + 1] = __uint_as_float(v[h][e] & 0xffff0000u);
+          }
+        gelu_poly16_v<1>(f);  // scalar FMAs: packed ones beside the MMA waves' MFMAs cost ~3x (MICROARCH)
+  #pragma unroll
+        for (int h = 0; h < 2; ++h)
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) v[h][e] = pack_bf16x2(f[h * 8 + 2 * e], f[h * 8 + 2 * e + 1]);
       }
   #pragma unroll
-      for (int g = 0; g < 20; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-        __builtin_amdgcn_sched_group_barrier(0x002, 5, 1);
-      }
+      for (int h = 0; h < 2; ++h)
+        __builtin_nontemporal_store(v[h], reinterpret_cast<u32x4*>(C + (size_t)(pm0 + row[h]) * ldc + pn0 + typ * 64 +
+                                                                   ch * 8));
       __builtin_amdgcn_sched_barrier(0);
     };
-    // chunk 4: P1.V MFMAs beside the scaling / packing of the qp 0 context
-    auto chunk4 = [&]() {
-      const float inv0 = len > 0 && o[0][4][0] > 0.f ? 1.f / o[0][4][0] : 0.f;
-  #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        xw[dt][0] = pack_bf16x2(o[0][dt][0] * inv0, o[0][dt][1] * inv0);
-        xw[dt][1] = pack_bf16x2(o[0][dt][2] * inv0, o[0][dt][3] * inv0);
-      }
-  #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-  #pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-          o[1][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vfrag(ks, dt), pf[1][ks],
-                                                             ks ? o[1][dt] : f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        o[1][4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[1][ks], ks ? o[1][4] : f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
+    auto piece = [&](int c) {
+      WS_T(t_c);
+      if constexpr (MODE == 2) piece_impl(c);
+      if constexpr (MODE >= 3) store_piece(c);
+#ifdef ATPU_WS_STAMPS
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      st[16 + c] += WS_NOW() - t_c;
+#endif
     };
-    // chunk 5: context -> this wave's 32 Q rows (free once read) and back as whole 128-B rows
-    // (cval); chunk 6: the global stores, issued at the start of the next slot before its DMA
-    u32x4 cval[4];
-    auto chunk5 = [&]() {
-      const int ln = opaque_lane(), fr = ln & 15, fc = ln >> 4;
-      char* ost = const_cast<char*>(qi) + l * 32 * 128;
-      const float inv1 = len > 0 && o[1][4][0] > 0.f ? 1.f / o[1][4][0] : 0.f;
-  #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        unsigned x0 = xw[dt][0], x1 = xw[dt][1];
-        unsigned y0 = pack_bf16x2(o[1][dt][0] * inv1, o[1][dt][1] * inv1);
-        unsigned y1 = pack_bf16x2(o[1][dt][2] * inv1, o[1][dt][3] * inv1);
-        swap16(x0, y0);
-        swap16(x1, y1);
-        const int ro = (fc & 1) * 16 + fr, ch = dt * 2 + (fc >> 1);
-        ds_write128(ost + ro * 128 + asw(ro, ch) * 16, u32x4{x0, x1, y0, y1});
-      }
-      const int l2 = opaque_lane();
-      const int lr = l2 >> 3, lc8 = l2 & 7;
-  #pragma unroll
-      for (int hh = 0; hh < 4; ++hh) {
-        const int ro = hh * 8 + lr;
-        cval[hh] = ds_read128u(ost + ro * 128 + asw(ro, lc8) * 16);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cval[0]), "+v"(cval[1]), "+v"(cval[2]), "+v"(cval[3])::"memory");
-    };
-    auto chunk6 = [&]() {
-      const int l2 = opaque_lane();
-      const int lr = l2 >> 3, lc8 = l2 & 7;
-      bf16* obase = C + (size_t)(pm0 + l * 32 + lr) * ldc + ph * 64 + lc8 * 8;
-  #pragma unroll
-      for (int hh = 0; hh < 4; ++hh) *reinterpret_cast<u32x4*>(obase + (size_t)(hh * 8) * ldc) = cval[hh];
-    };
-    auto chunk = [&](int c) {
-      if constexpr (MODE == 2) {
-        if (c == 1) chunk1();
-        if (c == 2) chunk2();
-        if (c == 3) chunk3();
-        if (c == 4) chunk4();
-        if (c == 5) chunk5();
-        if (c == 6) chunk6();
-      }
-    };
-    // slots -1 .. 3: the previous tile's attention beside the DMA of K-tiles 2 .. 5 (+1 for
-    // A with AS = 3); the context stores go out at the start of slot 3, before its DMA
+    // slot -1: the tile's epilogue vectors, piece 1
     stage_vec(m0, n0);
-    if constexpr (pending) chunk(1);
-    slot_end(Fly0{});  // KB_0
-    slot_dma(0);
-    if constexpr (pending) chunk(2);
-    slot_end(FlyA{});
-    slot_dma(1);
-    if constexpr (pending) chunk(3);
-    slot_end(FlyA{});
-    slot_dma(2);
-    if constexpr (pending) {
-      chunk(4);
-      chunk(5);
-    }
-    slot_end(FlyA{});
-    if constexpr (pending) chunk(6);
-    slot_dma(3);
-    slot_end(FlyA{});  // KB_4
-#pragma unroll 1
-    for (int sl = 4; sl + AS < NK; ++sl) {
-      slot_dma(sl);
-      if (var & 4) {  // diagnostic (results wrong): no DMA wait in these slots (drained later)
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-      } else {
-        slot_end(FlyA{});
-      }
-    }
-    // the last AS slots run into the next tile: B of K-tile s + 2 and A of K-tile s + AS, past
-    // NK taken from the next tile (its offsets switched at its K-tile 0)
+    if constexpr (pending) piece(1);
+    if constexpr (pending && MODE >= 3) slot_end(std::integral_constant<int, 2>{});  // KB_0; stores fly
+    else slot_end(Fly0{});  // KB_0
+    // slots 0 .. NK-1: the DMA of B K-tile s + 2 and A K-tile s + AS (past NK: the next tile's,
+    // its offsets switched at its K-tile 0). MODE 2: pieces 2-10 in slots 0-8, the stores in
+    // slot 9; MODE 3 / 4: pieces 2-6 in slots 0-4, after the DMA
+    constexpr int kLast = MODE == 2 ? 10 : 6;
 #pragma unroll
-    for (int sl = NK - AS; sl < NK; ++sl) {
+    for (int sl = 0; sl < NK; ++sl) {
+      if (sl == 9 && MODE == 2) {
+        if constexpr (pending) piece(11);
+      }
       const int kb = sl + 2, ka = sl + AS;
       if (kb < NK) {
         stageB(kb, kb & 1);
@@ -564,19 +628,45 @@ __global__ __launch_bounds__(512, 1) void qkv_ws_kernel(const bf16* __restrict__
         if (ka == NK) set_srcA(nm0);
         stageA(ka - NK, ka % AS);
       }
-      if (has_next) slot_end(FlyA{});  // KB_sl+1, or EB after the last slot
-      else slot_end(Fly0{});
+      if (sl + 2 <= kLast) {
+        if constexpr (pending) piece(sl + 2);
+      }
+      // MODE 3 / 4: the piece's 2 stores, issued after the DMA, may fly one slot longer
+      constexpr bool st2 = MODE >= 3 && pending;
+      if (st2 && sl + 2 <= kLast) {
+        if (ka < NK || has_next) slot_end(std::integral_constant<int, FlyA::value + 2>{});
+        else slot_end(std::integral_constant<int, 2>{});
+      } else {
+        if (ka < NK || has_next) slot_end(FlyA{});  // KB_sl+1, or EB after the last slot
+        else slot_end(Fly0{});
+      }
     }
     pm0 = m0;
     ph = n0 / 192;
+    pn0 = n0;
     if (!has_next) {
       // the last tile's attention, after the final barrier
-      chunk(1);
-      chunk(2);
-      chunk(3);
-      chunk(4);
-      chunk(5);
-      chunk(6);
+      if constexpr (MODE >= 3) {
+        piece(1);
+        piece(2);
+        piece(3);
+        piece(4);
+        piece(5);
+        piece(6);
+      }
+      if constexpr (MODE == 2) {
+        piece(1);
+        piece(2);
+        piece(3);
+        piece(4);
+        piece(5);
+        piece(6);
+        piece(7);
+        piece(8);
+        piece(9);
+        piece(10);
+        piece(11);
+      }
       return false;
     }
     v = vn;
@@ -584,16 +674,30 @@ __global__ __launch_bounds__(512, 1) void qkv_ws_kernel(const bf16* __restrict__
     n0 = nn0;
     return true;
   };
-  if (!tile_body(std::false_type{})) return;
-  while (tile_body(std::true_type{})) {
-  }
+  if (tile_body(std::false_type{}))
+    while (tile_body(std::true_type{})) {
+    }
+#ifdef ATPU_WS_STAMPS
+  if (wave == 4) st_flush(5, 32);
+#endif
 }
 
 }  // namespace
 
+#ifdef ATPU_WS_STAMPS
+std::vector<unsigned long long> ws_stamps(int nblocks) {
+  std::vector<unsigned long long> out((size_t)nblocks * 32);
+  ATPU_HIP_CHECK(hipMemcpyFromSymbol(out.data(), HIP_SYMBOL(g_ws_stamps), out.size() * 8, 0, hipMemcpyDeviceToHost));
+  return out;
+}
+#else
+std::vector<unsigned long long> ws_stamps(int) { return {}; }
+#endif
+
 static int g_ws_variant = 0;
-// experiment knob (benchmarks): bit 0 = MMA waves at s_setprio 2; bit 2 = diagnostic, no DMA wait in
-// the middle slots (results wrong); bit 3 = a 3-deep A ring (K = 768); set >= 0 switches
+// experiment knob (benchmarks): bit 0 = MMA waves at s_setprio 2; bit 3 = a 3-deep A ring
+// (K = 768); bit 4 = loader waves at s_setprio 1; bits 5-6 = log2 of the row blocks per tile
+// group (tile_of); set >= 0 switches, returns the current
 int ws_variant(int set) {
   if (set >= 0) g_ws_variant = set;
   return g_ws_variant;
@@ -611,7 +715,8 @@ void qkv_attention_ws(const GemmArgs& g, int mode, const int32_t* lens, float sc
   ATPU_CHECK(!(g.epi & kEpiInNorm) || (g.in_fin && g.colsum), "qkv_attention_ws: InNorm needs in_fin and colsum");
   ATPU_CHECK(g.bias && g.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(g.C) & 15) == 0,
              "qkv_attention_ws: bias, 16-B aligned output rows");
-  ATPU_CHECK(mode >= 0 && mode <= 2, "qkv_attention_ws: mode 0 (store QKV), 1 (timing only) or 2 (attention)");
+  ATPU_CHECK(mode >= 0 && mode <= 4,
+             "qkv_attention_ws: mode 0 (store QKV), 1 (timing only), 2 (attention), 3 (GELU GEMM), 4 (GEMM)");
   ATPU_CHECK(mode != 2 || lens, "qkv_attention_ws: lens");
   const int tiles = (g.M / 128) * (g.N / 192);
   int nb = std::min(tiles, num_cus());
@@ -627,7 +732,9 @@ void qkv_attention_ws(const GemmArgs& g, int mode, const int32_t* lens, float sc
 #define ATPU_WS_MODE(E)                \
   if (mode == 0) { ATPU_WS_NK(E, 0); } \
   else if (mode == 1) { ATPU_WS_NK(E, 1); } \
-  else { ATPU_WS_NK(E, 2); }
+  else if (mode == 2) { ATPU_WS_NK(E, 2); } \
+  else if (mode == 3) { ATPU_WS_NK(E, 3); } \
+  else { ATPU_WS_NK(E, 4); }
   if (g.epi & kEpiInNorm) {
     ATPU_WS_MODE(kEpiBias | kEpiInNorm);
   } else {
@@ -638,5 +745,14 @@ void qkv_attention_ws(const GemmArgs& g, int mode, const int32_t* lens, float sc
 #undef ATPU_WS
   ATPU_HIP_CHECK(hipGetLastError());
 }
+
+#else  // release build: the measured-slower experiment is not compiled (docs/PERF_NOTES.md)
+std::vector<unsigned long long> ws_stamps(int) { return {}; }
+int ws_variant(int) { return 0; }
+bool qkv_attention_ws_ok(int, int, int) { return false; }
+void qkv_attention_ws(const GemmArgs&, int, const int32_t*, float, hipStream_t) {
+  ATPU_CHECK(false, "qkv_attention_ws: wave-specialised kernels are in the dev build only (build.py --dev)");
+}
+#endif  // ATPU_DEV_BUILD
 
 }  // namespace atpu

@@ -9,7 +9,8 @@ projection and attention as separate framework ops).
 Two kernels: ``256h`` (the attention in the tile epilogue, all 8 waves) and ``ws``
 (``csrc/kernels/qkv_attn_ws.hip``: 128 x 192 tiles, 4 MFMA waves on the main loop while 4
 waves stage operands and run the previous tile's attention). ``ATPU_QKV_WS=1`` selects ``ws``
-where its shapes allow (hidden 768 / 1024).
+where its shapes allow (hidden 768 / 1024) in a dev build of the extension; it measured ~2 %
+slower than ``256h`` and is not in the release build.
 
 The kernels want the QKV weight rows (and bias / colsum) in head order, ``[h][Q 64 | K 64 |
 V 64]``; :func:`qkv_head_order` is that permutation of the usual ``[Q | K | V]`` layout.
@@ -46,8 +47,10 @@ def qkv_attention_ok(M: int, N: int, K: int, S: int) -> bool:
 
 
 def ws_ok(M: int, N: int, K: int) -> bool:
-    """Shapes of the wave-specialised kernel: whole 128-row sequences, hidden 768 or 1024."""
-    return M % SEQ == 0 and N % 192 == 0 and K in (768, 1024) and M * K * 2 < (1 << 32) and N * K * 2 < (1 << 32)
+    """Shapes of the wave-specialised kernel: whole 128-row sequences, hidden 768 or 1024; a
+    dev build of the extension only (the kernel measured slower: docs/PERF_NOTES.md)."""
+    return (M % SEQ == 0 and N % 192 == 0 and K in (768, 1024) and M * K * 2 < (1 << 32) and N * K * 2 < (1 << 32)
+            and bool(native().qkv_attention_ws_ok(M, N, K)))
 
 
 def ws_default() -> bool:

@@ -16,6 +16,14 @@ from agent_tpu_amd.ops.attention import attention_ref
 H, D, K = 12, 64, 768
 
 
+def _need_ws(kernel):
+    if kernel == "ws":
+        from agent_tpu_amd._native import native
+
+        if not native().DEV_BUILD:
+            pytest.skip("wave-specialised kernel: dev build of the extension only (build.py --dev)")
+
+
 def _case(B, seed, innorm):
     g = torch.Generator().manual_seed(seed)
     dev = torch.device("cuda", 0)
@@ -50,6 +58,7 @@ def _ref(x, w, b, lens, fin, col, B):
 @pytest.mark.parametrize("kernel", ["256h", "ws"])
 @pytest.mark.parametrize("B,innorm", [(2, False), (2, True), (32, True), (130, False), (258, True)])
 def test_fused_matches_fp32_reference(B, innorm, kernel):
+    _need_ws(kernel)
     dev, M, x, w, b, lens, fin, col = _case(B, 10 + B, innorm)
     p = ops.qkv_head_order(H)
     w_h, b_h = w[p].contiguous(), b[p].contiguous()
@@ -69,6 +78,7 @@ def test_fused_matches_fp32_reference(B, innorm, kernel):
 @pytest.mark.parametrize("kernel", ["256h", "ws"])
 @pytest.mark.parametrize("innorm", [False, True])
 def test_fused_matches_unfused_kernels(innorm, kernel):
+    _need_ws(kernel)
     B = 64
     dev, M, x, w, b, lens, fin, col = _case(B, 3, innorm)
     xd, wd, bd, ld = x.to(dev), w.to(dev), b.to(dev), lens.to(dev)
@@ -103,6 +113,7 @@ def test_cpu_reference_path_matches_unfused():
 @pytest.mark.gpu
 @pytest.mark.parametrize("kernel", ["256h", "ws"])
 def test_fused_bert_large_shape(kernel):
+    _need_ws(kernel)
     """16 heads, hidden 1024 (K / 64 = 16): the bert-large encoder runs the fused kernel too."""
     Hl, Kl, B = 16, 1024, 34
     g = torch.Generator().manual_seed(21)
@@ -154,6 +165,7 @@ def test_gemm256h_store_mode_exact():
 def test_ws_store_mode_exact(B, innorm, k):
     """Mode 0 of the wave-specialised kernel (the GEMM part: Q|K|V stored instead of attended)
     against fp32, with odd sequence counts (several tiles per CU at B = 129 x 12 heads)."""
+    _need_ws("ws")
     dev = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(B)
     M, N = B * 128, 2304 if k == 768 else 3072
@@ -183,6 +195,7 @@ def test_ws_store_mode_exact(B, innorm, k):
 @pytest.mark.parametrize("B", [1, 3, 21, 257])
 def test_ws_odd_sequence_counts(B):
     """ws takes any number of 128-token sequences (the 256h kernel needs an even count)."""
+    _need_ws("ws")
     dev, M, x, w, b, lens, fin, col = _case(B, 40 + B, True)
     p = ops.qkv_head_order(H)
     got = ops.qkv_attention(x.to(dev), w[p].contiguous().to(dev), b[p].contiguous().to(dev), lens.to(dev), H,
@@ -194,10 +207,11 @@ def test_ws_odd_sequence_counts(B):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("var", [1, 8, 9])
+@pytest.mark.parametrize("var", [1, 8, 9, 24])
 def test_ws_schedule_variants_exact(var):
     """The ws kernel's schedule variants (MMA-wave priority, 3-deep A ring) give the same
     attention as the default schedule, bit for bit (same math, same order)."""
+    _need_ws("ws")
     from agent_tpu_amd._native import native
 
     B = 67
