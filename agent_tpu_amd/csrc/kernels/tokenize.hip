@@ -11,11 +11,16 @@
 //   ids = [CLS=101] + first S-2 tokens + [SEP=102] + [PAD=0]...; len = n + 2.
 //
 // One 64-wide wave per row. The row is staged into LDS, then scanned 64 bytes
-// per step: each lane classifies its byte, token starts are found against the
-// left neighbour (shfl_up; chunk-carry through lane 63), the lane at a word
-// start walks its word in LDS to count/hash pieces, and an inclusive wave scan
-// of piece counts gives every token its output slot. The scan stops as soon
-// as S-2 tokens exist, so long rows cost only the bytes that are used.
+// per step: each lane classifies its byte (and the byte 64 further on), token
+// starts are found against the left neighbour (shfl_up; chunk-carry through lane
+// 63), a word's length is the run of word bytes from its start in the 128-bit
+// ballot of the two chunks (one ctz; words of 64+ bytes fall back to a walk), and
+// an inclusive wave scan of piece counts gives every token its output slot. The
+// lane at a token start hashes its piece from 7 aligned dwords of LDS realigned
+// with v_alignbyte (no dependent byte loads; the byte loop runs to the longest
+// piece of the step). The scan stops as soon as S-2 tokens exist, so long rows
+// cost only the bytes that are used. (The byte-walking form spent ~90 us on a
+// 1024-row batch, latency-bound on dependent LDS reads.)
 #include "atpu/common.h"
 #include "atpu/kernels.h"
 
@@ -53,7 +58,9 @@ __global__ __launch_bounds__(256) void tokenize_kernel(const uint8_t* __restrict
                                                        const int32_t* __restrict__ offsets, int32_t* __restrict__ ids,
                                                        int32_t* __restrict__ lens, int B, int S, int vocab,
                                                        int max_row_bytes, long long text_bytes) {
-  __shared__ __attribute__((aligned(16))) uint8_t rowbuf[4][kMaxRowBytes + 16];
+  // + 16: the row starts up to 15 bytes into its first 16-B piece; + 32: a piece hash reads
+  // 7 dwords from its aligned start (at most 28 bytes past a byte of the row)
+  __shared__ __attribute__((aligned(16))) uint8_t rowbuf[4][kMaxRowBytes + 48];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int row = blockIdx.x * 4 + w;
   if (row >= B) return;
@@ -83,9 +90,12 @@ __global__ __launch_bounds__(256) void tokenize_kernel(const uint8_t* __restrict
   int32_t* out = ids + (size_t)row * S;
   int ntok = 0;
   int carry = 0;
+  const uint8_t* rb = rowbuf[w];
   for (int base = 0; base < n && ntok < cap; base += 64) {
     const int i = base + lane;
     const int cls = i < n ? byte_class(buf[i]) : 0;
+    const int cls2 = i + 64 < n ? byte_class(buf[i + 64]) : 0;
+    const uint64_t W = __ballot(cls == 2), W2 = __ballot(cls2 == 2);
     int prev = __shfl_up(cls, 1, 64);
     if (lane == 0) prev = carry;
     const bool st = cls == 1 || (cls == 2 && prev != 2);
@@ -93,29 +103,47 @@ __global__ __launch_bounds__(256) void tokenize_kernel(const uint8_t* __restrict
     if (st) {
       if (cls == 1) {
         npieces = 1;
+        wlen = 1;
       } else {
-        int j = i;
-        while (j < n && byte_class(buf[j]) == 2) ++j;
-        wlen = j - i;
+        // word bytes from i on: bits lane..63 of W, then W2
+        const uint64_t x = lane == 0 ? W : ((W >> lane) | (W2 << (64 - lane)));
+        if (~x != 0) {
+          wlen = __builtin_ctzll(~x);
+        } else {  // 64+ word bytes: walk the rest
+          int j = i + 64;
+          while (j < n && byte_class(buf[j]) == 2) ++j;
+          wlen = j - i;
+        }
         npieces = (wlen + kPiece - 1) / kPiece;
       }
     }
     const int incl = wave_inclusive_scan(npieces, lane);
     const int excl = incl - npieces;
-    if (st) {
-      for (int p = 0; p < npieces; ++p) {
-        const int pos = ntok + excl + p;
-        if (pos >= cap) break;
-        uint32_t h;
-        if (cls == 1) {
-          h = fnv_step(kFnvBasis, buf[i]);
-        } else {
-          h = p == 0 ? kFnvBasis : cont_basis;
-          const int b0 = i + p * kPiece, b1 = min(i + (p + 1) * kPiece, i + wlen);
-          for (int j = b0; j < b1; ++j) h = fnv_step(h, buf[j]);
-        }
-        out[1 + pos] = (int32_t)(1000u + h % mod);
+    for (int p = 0;; ++p) {
+      const bool act = st && p < npieces && ntok + excl + p < cap;
+      if (__ballot(act) == 0) break;
+      const int b0 = p * kPiece, len = min(wlen - b0, kPiece);  // this lane's piece: bytes [i+b0, +len)
+      int lmax = act ? len : 0;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) lmax = max(lmax, __shfl_xor(lmax, o, 64));
+      // 7 aligned dwords cover the piece (<= 24 bytes at offset <= 3); v_alignbyte drops the offset
+      const int abs0 = sh + i + b0;
+      const uint32_t* dp = reinterpret_cast<const uint32_t*>(rb + (act ? (abs0 & ~3) : 0));
+      const uint32_t sft = (uint32_t)(abs0 & 3) * 8u;
+      uint32_t d[7], e[6];
+#pragma unroll
+      for (int k = 0; k < 7; ++k) d[k] = dp[k];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) e[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sft >> 3);
+      uint32_t h = (cls == 1 || p == 0) ? kFnvBasis : cont_basis;
+#pragma unroll
+      for (int k = 0; k < kPiece; ++k) {
+        if (k >= lmax) break;
+        const uint32_t cb = (e[k >> 2] >> ((k & 3) * 8)) & 0xffu;
+        const uint32_t hn = fnv_step(h, cb);
+        h = k < len ? hn : h;
       }
+      if (act) out[1 + ntok + excl + p] = (int32_t)(1000u + h % mod);
     }
     ntok += __shfl(incl, 63, 64);
     carry = __shfl(cls, 63, 64);

@@ -282,6 +282,14 @@ def test_tokenizer_gpu_matches_python_and_host(gpu, nat):
 
     rows = make_text_rows(300, words_per_row=40, seed=3)
     rows += ["", "   ", "Hello, WORLD!!", "x" * 100, "naïve café — 東京 ok", "a\tb\nc\x01d", "(" * 300]
+    # words of every length 1..130 at every offset mod 64 (the 128-bit ballot window, the 64+
+    # byte walk, 24-byte pieces), upper case, and rows of random bytes
+    rng = np.random.default_rng(7)
+    for L in list(range(1, 72)) + [95, 96, 97, 127, 128, 129, 130]:
+        for off in (0, 1, 3, 23, 40, 61, 62, 63):
+            rows.append(" " * off + "".join(chr(65 + (k * 7 + L) % 26) for k in range(L)) + ",ab " + "Q" * (L % 30))
+    for _ in range(40):
+        rows.append(bytes(rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8)).decode("latin-1"))
     text, offs = T.pack_rows(rows)
     for S in (8, 128):
         ids_py, lens_py = T.tokenize_rows([r.encode() for r in rows], S, 30522, 2048)
