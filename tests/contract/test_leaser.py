@@ -54,6 +54,28 @@ def test_long_batch_gets_its_next_lease_ahead(leaser):
     assert leaser.pending() == [("L2", [{"id": "2"}])]  # one ahead per batch, never more
 
 
+def test_lease_ahead_waits_for_the_expected_end_of_long_batches(leaser, monkeypatch):
+    """the ahead lease is taken ~LEASE_PREFETCH_LEAD_MS before a batch's
+    expected end (moving average of batch durations), not 2 ms in, so its tasks do not sit
+    out a long batch."""
+    leaser.lead = 0.05
+    leaser.next()
+    leaser.started()
+    time.sleep(0.3)  # first batch: no history, the helper leases after LEASE_PREFETCH_AFTER_MS
+    leaser.finished()
+    t_first = FakeCtl.log[1][1]
+    assert leaser.next()[0] == "L1"
+    leaser.started()
+    t0 = time.monotonic()
+    assert t_first - (t0 - 0.3) < 0.1
+    time.sleep(0.35)
+    leaser.finished()
+    assert [n for n, _ in FakeCtl.log] == ["MainThread", "atpu-leaser", "atpu-leaser"]
+    lag = FakeCtl.log[2][1] - t0  # the second batch's lease ahead: ~0.3 - 0.05 s in
+    assert 0.2 < lag < 0.32, lag
+    assert leaser.pending() == [("L2", [{"id": "2"}])]
+
+
 def test_short_batches_stay_serial(leaser):
     for i in range(3):
         assert leaser.next()[0] == f"L{i}"
