@@ -293,12 +293,21 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   wait_vmcnt0();
   __syncthreads();  // Q fragments, distance table and chunk 0 are in place
 
-  float m_run = -1e30f, l_run = 0.f;
-  f32x4 o[4];
+  // VALU per score (the kernel was VALU-bound, MFMA busy 18 %: profiles/pmc_flash_attention_t5_src1024.txt):
+  // the distance bias comes from ONE per-lane LDS base per chunk with immediate offsets (no
+  // per-value index math or clamp: entries past the table's used part are only read for keys
+  // >= Skv, which the tail mask drops), scale and bias are one FMA, and the row sums come from
+  // the MFMA (P times a ones block, o[4]) instead of VALU adds and a cross-lane sum -- the sum
+  // of the same bf16-rounded P the context is made of.
+  float m_run = -1e30f;
+  f32x4 o[5];
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int dt = 0; dt < 5; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int q = qw + fr;
   const int qc = min(q, Sq - 1);
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.0f;
 
   for (int c = 0; c < nch; ++c) {
     const int kc = c * kKC;
@@ -326,23 +335,29 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     }
 
     const bool tail = kc + kKC > len;
+    // this lane's scores: keys kc + kt*16 + fg*4 + r -> distance-table entry
+    // kc + kt*16 + fg*4 + r - qc + Sq - 1 = tb[kt*16 + r]
+    const float* tb = tab + (kc + fg * 4 - qc + Sq - 1);
     float cmax = -1e30f;
 #pragma unroll
     for (int kt = 0; kt < 8; ++kt) {
-      const int key0 = kc + kt * 16 + fg * 4;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float x = s[kt][r] * scale_log2;
-        if constexpr (DIST) x += tab[min(key0 + r - qc + Sq - 1, ntab - 1)];
-        if (tail) x = key0 + r >= len ? -1e30f : x;
+        float x;
+        if constexpr (DIST) x = fmaf(s[kt][r], scale_log2, tb[kt * 16 + r]);
+        else x = s[kt][r] * scale_log2;
         s[kt][r] = x;
-        cmax = fmaxf(cmax, x);
       }
+      if (tail) {
+        const int key0 = kc + kt * 16 + fg * 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[kt][r] = key0 + r >= len ? -1e30f : s[kt][r];
+      }
+      cmax = fmaxf(cmax, fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3])));
     }
     cmax = lane_rows_max(cmax);  // l, l^16, l^32, l^48 by permlane swaps
     const float m_new = fmaxf(m_run, cmax);
     const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-    float psum = 0.f;
 #pragma unroll
     for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
@@ -351,13 +366,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         float p = __builtin_amdgcn_exp2f(x - m_new);
         if (tail) p = x <= -1e29f ? 0.f : p;
         s[kt][r] = p;
-        psum += p;
       }
-    psum = lane_rows_sum(psum);
-    l_run = l_run * alpha + psum;
     m_run = m_new;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+    for (int dt = 0; dt < 5; ++dt) o[dt] *= alpha;
 
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -382,11 +394,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         }
         o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[dt], 0, 0, 0);
       }
+      o[4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf, o[4], 0, 0, 0);  // row sums
     }
     __syncthreads();  // every wave is done with buffer buf before chunk c+2 is staged into it
   }
 
   if (q < Sq) {
+    const float l_run = o[4][0];  // every element of the ones block holds the query's row sum
     const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
     bf16* orow = O + ((size_t)b * Sq + q) * ldo + h * kD;
 #pragma unroll
