@@ -4,7 +4,7 @@ interleaved timing of
   * 256s  : ops.linear_ln (the production QKV GEMM, bias | InNorm, full-line nt epilogue)
   * 256h  : gemm256h mode 0 (same math, fragment-layout stores)
   * 256h-noepi : gemm256h mode 1 (main loop only, timing only)
-  * ws_*  : the wave-specialised kernel (qkv_attn_ws.hip): attention, main loop only, Q|K|V store
+  * ws_*  : the wave-specialised kernel (qkv_attn_ws.hip; dev build only): attention, main loop only, Q|K|V store
 Prints one JSON line per configuration. Usage: python tools/bench_256h.py [--rows 131072]
 """
 from __future__ import annotations
@@ -102,11 +102,14 @@ def main() -> int:
         "256h_innorm": lambda: run_h(nat, x, w, b, out, fin, col, 0),
         "256h_noepi": lambda: run_h(nat, x, w, b, out, fin, col, 1),
         "256h_bias": lambda: run_h(nat, x, w, b, out, None, None, 0),
-        "ws_qkv_attn": lambda: ops.qkv_attention(x, w_h, b_h, lens, N // 192, in_fin=fin, colsum_h=col_h, out=ctx,
-                                                 kernel="ws"),
-        "ws_noepi": lambda: qkv_ws(x, w_h, b_h, out, 1, in_fin=fin, colsum_h=col_h),
-        "ws_store": lambda: qkv_ws(x, w_h, b_h, out, 0, in_fin=fin, colsum_h=col_h),
     }
+    if nat.DEV_BUILD:  # the wave-specialised kernel is compiled in the dev build only
+        cands.update({
+            "ws_qkv_attn": lambda: ops.qkv_attention(x, w_h, b_h, lens, N // 192, in_fin=fin, colsum_h=col_h, out=ctx,
+                                                     kernel="ws"),
+            "ws_noepi": lambda: qkv_ws(x, w_h, b_h, out, 1, in_fin=fin, colsum_h=col_h),
+            "ws_store": lambda: qkv_ws(x, w_h, b_h, out, 0, in_fin=fin, colsum_h=col_h),
+        })
     if a.only:
         cands = {k: f for k, f in cands.items() if k in a.only.split(",")}
     if a.ws_variants:

@@ -2,7 +2,8 @@
 """BERT-base FFN1 (M x 768 -> 3072, LN-folded input, bias, GELU): the 256 x 256 production
 kernel (ops.linear_ln) against the wave-specialised kernel (ops.linear.gemm_ws), interleaved
 rounds on random data; also the ws main loop alone (timing only) and the plain (no GELU) form.
-One JSON line per configuration. Usage: python tools/bench_ffn1_ws.py [--rows 131072] [--variants 8,24]
+One JSON line per configuration. Needs a dev build of the extension (build.py --dev: the ws kernels
+are not in the release build). Usage: python tools/bench_ffn1_ws.py [--rows 131072] [--variants 8,24]
 """
 from __future__ import annotations
 
