@@ -197,6 +197,11 @@ class BartModel:
         self.ln_fold = (self.device.type == "cuda" and not fp32
                         and os.getenv("ATPU_DEC_LN_FOLD", "1") not in ("0", "false", "no"))
         self._lfold: Optional[Dict[str, torch.Tensor]] = None
+        # encoder: the post-LN LayerNorms folded into the GEMMs around them, as BERT's encoder
+        # (BertClassifier.encode_folded): 24 fewer full passes over [B*S, d] per encode
+        self.enc_ln_fold = (self.device.type == "cuda" and not fp32
+                            and os.getenv("ATPU_ENC_LN_FOLD", "1") not in ("0", "false", "no"))
+        self._efold: Optional[Dict[str, torch.Tensor]] = None
 
     def ln_folded(self) -> Dict[str, torch.Tensor]:
         """Decoder weights with each LayerNorm folded into its consumers (built once).
@@ -220,6 +225,69 @@ class BartModel:
             self._lfold = f
         return self._lfold
 
+    def enc_folded(self) -> Dict[str, torch.Tensor]:
+        """Encoder weights with each post-LN LayerNorm folded into its consumers (built once,
+        then the device is synchronised: concurrent encodes on other streams read them).
+
+        QKV of layer i >= 1 consumes LN2 of layer i-1 and FFN1 consumes LN1: gamma into the
+        weight, beta into the bias, plus column sums (:func:`ops.fold_ln_into_linear`); the
+        out-proj / FFN2 residual is that LayerNorm's output: its beta goes into their bias."""
+        if self._efold is None:
+            p, f = self.p, {}
+            for i in range(self.cfg.enc_layers):
+                q, prev = f"enc.l{i}.", f"enc.l{i - 1}."
+                if i > 0:
+                    g2, b2 = p[prev + "ln2_g"], p[prev + "ln2_b"]
+                    f[q + "qkv_w"], f[q + "qkv_c"], f[q + "qkv_b"] = ops.fold_ln_into_linear(
+                        p[q + "qkv_w"], p[q + "qkv_b"], g2, b2)
+                    f[q + "o_b"] = (p[q + "o_b"].float() + b2.float()).contiguous()
+                f[q + "f1_w"], f[q + "f1_c"], f[q + "f1_b"] = ops.fold_ln_into_linear(
+                    p[q + "f1_w"], p[q + "f1_b"], p[q + "ln1_g"], p[q + "ln1_b"])
+                f[q + "f2_b"] = (p[q + "f2_b"].float() + p[q + "ln1_b"].float()).contiguous()
+            torch.cuda.synchronize(self.device)
+            self._efold = f
+        return self._efold
+
+    def _enc_fold_ok(self, M: int) -> bool:
+        d, ff = self.cfg.d_model, self.cfg.d_ff
+        return (self.enc_ln_fold and self.cfg.enc_layers >= 2 and ops.fold_ok(M, 3 * d, d) and ops.fold_ok(M, ff, d)
+                and ops.fold_ok(M, d, ff))
+
+    def _encode_folded(self, ids: torch.Tensor, lens: torch.Tensor, ckv_out: Optional[torch.Tensor] = None):
+        """:meth:`encode` with the LayerNorms folded (BERT's scheme, bert.py ``encode_folded``):
+        the residual stream stays raw (pre-LN sums); out-proj / FFN2 emit per-row (sum, sumsq)
+        partials of their output, ``ln_finalize`` turns them into (rstd, rstd*mu), which the
+        next FFN1 / QKV apply to the folded weights' product and the next FFN2 / out-proj to
+        their residual. Only the last LayerNorm runs (its output feeds the cross K|V)."""
+        cfg, p, f = self.cfg, self.p, self.enc_folded()
+        B, S = ids.shape
+        d, H, M, eps = cfg.d_model, cfg.heads, B * S, cfg.eps
+        h0 = ops.embed_layernorm(ids, p["shared"], p["enc.pos"][POS_OFFSET:], self._type0, p["enc.ln_emb_g"],
+                                 p["enc.ln_emb_b"], eps)
+        part = torch.empty((d // 256, M, 2), dtype=torch.float32, device=ids.device)  # raw rows' partials
+        fin = torch.empty((M, 2), dtype=torch.float32, device=ids.device)             # (rstd, rstd*mu)
+        g = h0
+        for i in range(cfg.enc_layers):
+            q, prev = f"enc.l{i}.", f"enc.l{i - 1}."
+            if i == 0:
+                qkv = ops.linear(h0, p[q + "qkv_w"], p[q + "qkv_b"])
+            else:  # consumes LN2_{i-1}(g); fin = its statistics (also the out-proj residual's)
+                qkv = ops.linear_ln(g, f[q + "qkv_w"], f[q + "qkv_b"], in_fin=fin, colsum=f[q + "qkv_c"])
+            ctx = ops.attention_packed(qkv, lens, B, S, H)
+            if i == 0:
+                a = ops.linear_ln(ctx, p[q + "o_w"], p[q + "o_b"], residual=h0, part_out=part)
+            else:
+                a = ops.linear_ln(ctx, p[q + "o_w"], f[q + "o_b"], residual=g, res_fin=fin,
+                                  res_gamma=p[prev + "ln2_g"], part_out=part)
+            ops.ln_finalize(part, d, eps, out=fin)  # LN1 statistics of a
+            ff = ops.linear_ln(a, f[q + "f1_w"], f[q + "f1_b"], act="gelu", in_fin=fin, colsum=f[q + "f1_c"])
+            g = ops.linear_ln(ff, p[q + "f2_w"], f[q + "f2_b"], residual=a, res_fin=fin, res_gamma=p[q + "ln1_g"],
+                              part_out=part)
+            ops.ln_finalize(part, d, eps, out=fin)  # LN2 statistics of g
+        last = f"enc.l{cfg.enc_layers - 1}."
+        h = ops.layernorm(g, p[last + "ln2_g"], p[last + "ln2_b"], eps)
+        return h, ops.linear(h, p["dec.ckv_w"], p["dec.ckv_b"], out=ckv_out)
+
     def prepare_decode(self, S: int, T: int) -> None:
         """Build the lazily folded decoder weights before concurrent decode streams fork."""
         if self.ln_fold:
@@ -235,6 +303,8 @@ class BartModel:
         cfg, p = self.cfg, self.p
         B, S = ids.shape
         H = cfg.heads
+        if ids.is_cuda and self._enc_fold_ok(B * S):
+            return self._encode_folded(ids, lens, ckv_out)
         h = ops.embed_layernorm(ids, p["shared"], p["enc.pos"][POS_OFFSET:], self._type0, p["enc.ln_emb_g"],
                                 p["enc.ln_emb_b"], cfg.eps)
         for i in range(cfg.enc_layers):

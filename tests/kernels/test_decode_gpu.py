@@ -496,6 +496,33 @@ def test_encoder_long_source_matches_cpu(gpu, family, S):
         assert _rel(kg[b * S:b * S + n], kc[b * S:b * S + n]) < 3e-2
 
 
+def test_bart_encoder_ln_fold_matches_unfolded(gpu):
+    """The LN-folded BART encoder (BartModel._encode_folded: BERT's fold scheme, StatsOut
+    partials + InNorm / ResNorm GEMMs) against the LayerNorm-pass encoder and the fp32 CPU
+    oracle, at a width the folding GEMMs take (d = 256, d_ff = 1024, 2 x 1024 tokens)."""
+    import dataclasses
+
+    from agent_tpu_amd.models.bart import BartModel, config_for, init_random
+
+    cfg = dataclasses.replace(config_for("bart-tiny"), d_model=256, heads=4, d_ff=1024, enc_layers=3,
+                              max_positions=1024)
+    pack = init_random(cfg, seed=5)
+    cpu_m, gpu_m = BartModel(cfg, pack, fp32=True), BartModel(cfg, pack.to(gpu))
+    B, S = 2, 1024
+    g = torch.Generator().manual_seed(6)
+    ids = torch.randint(5, cfg.vocab_size, (B, S), generator=g, dtype=torch.int32)
+    lens = torch.tensor([S, S - 301], dtype=torch.int32)
+    assert gpu_m._enc_fold_ok(B * S)
+    ef, kf = gpu_m.encode(ids.to(gpu), lens.to(gpu))
+    gpu_m.enc_ln_fold = False
+    eu, ku = gpu_m.encode(ids.to(gpu), lens.to(gpu))
+    ec, kc = cpu_m.encode(ids, lens)
+    for b in range(B):
+        r = slice(b * S, b * S + int(lens[b]))
+        assert _rel(ef[r], eu[r]) < 2e-2 and _rel(kf[r], ku[r]) < 2e-2
+        assert _rel(ef[r], ec[r]) < 3e-2 and _rel(kf[r], kc[r]) < 3e-2
+
+
 def test_map_summarize_op_gpu(gpu, monkeypatch):
     import importlib
 
