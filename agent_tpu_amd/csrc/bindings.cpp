@@ -332,6 +332,13 @@ PYBIND11_MODULE(_atpu, m) {
                            uintptr_t stream) {
     embed_gather(P<const int32_t>(ids), P<const bf16>(table), P<bf16>(out), tokens, N, vocab, S(stream));
   });
+  m.def("embed_pos_layernorm", [](uintptr_t ids, uintptr_t table, uintptr_t pos, uintptr_t step, int pos_off, int npos,
+                                  uintptr_t gamma, uintptr_t beta, uintptr_t out, int rows, int N, int vocab, float eps,
+                                  uintptr_t stream) {
+    embed_pos_layernorm(P<const int32_t>(ids), P<const bf16>(table), P<const bf16>(pos), P<const int32_t>(step),
+                        pos_off, npos, P<const float>(gamma), P<const float>(beta), P<bf16>(out), rows, N, vocab, eps,
+                        S(stream));
+  });
   m.def("tokenize", [](uintptr_t text, uintptr_t offsets, uintptr_t ids, uintptr_t lens, int B, int Sq, int vocab,
                        int max_row_bytes, uintptr_t stream, long long text_bytes) {
     tokenize_hash(P<const uint8_t>(text), P<const int32_t>(offsets), P<int32_t>(ids), P<int32_t>(lens), B, Sq, vocab,

@@ -199,6 +199,11 @@ void embed_layernorm(const int32_t* ids, const int32_t* type_ids, const bf16* wo
 // partials part[slots][M][2] (sum, sumsq), slots summed in order (deterministic)
 void ln_stats_finalize(const float* part, int slots, int M, int K, float eps, float* fin, hipStream_t stream);
 // Plain embedding gather (T5 encoder/decoder input): out[t] = table[ids[t]] * scale
+// LN(table[ids[r]] + pos[*step + pos_off]) per row (decoder input of a learned-position model at a
+// device-side step; the layernorm_bf16 math, bit for bit)
+void embed_pos_layernorm(const int32_t* ids, const bf16* table, const bf16* pos, const int32_t* step, int pos_off,
+                         int npos, const float* gamma, const float* beta, bf16* out, int rows, int N, int vocab,
+                         float eps, hipStream_t stream);
 void embed_gather(const int32_t* ids, const bf16* table, bf16* out, int tokens, int N, int vocab,
                   hipStream_t stream);
 

@@ -85,17 +85,13 @@ __device__ __forceinline__ float half_sum(float v) {
 // 512-byte row segments instead of one 512-byte segment with 8-byte accesses.
 // Half the memory instructions of layernorm_kernel for the same bytes; the
 // statistics stay fp32 two-pass, reduced over the half wave.
+// one row of the half-wave LayerNorm: LN(x_row (+ res_row)) -> out_row (rows of N = 256 NG)
 template <int NG, bool NTL>
-__global__ __launch_bounds__(256) void layernorm_hw_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
-                                                           const float* __restrict__ gamma,
-                                                           const float* __restrict__ beta, bf16* __restrict__ out,
-                                                           int rows, float eps) {
-  const int hl = threadIdx.x & 31;
-  const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
-  const bool live = row < rows;
-  const int r = live ? row : rows - 1;  // dead half-waves read a valid row, never store
+__device__ __forceinline__ void ln_hw_row(const bf16* __restrict__ xrow, const bf16* __restrict__ rrow,
+                                          const float* __restrict__ gamma, const float* __restrict__ beta,
+                                          bf16* __restrict__ orow_base, bool live, float eps, int hl) {
   constexpr int N = NG * 256;
-  const bf16* xr = x + (size_t)r * N + hl * 8;
+  const bf16* xr = xrow + hl * 8;
   float v[NG * 8];
   bf16x8 xv[NG];
 #pragma unroll
@@ -104,8 +100,8 @@ __global__ __launch_bounds__(256) void layernorm_hw_kernel(const bf16* __restric
     if constexpr (NTL) xv[g] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(xr + g * 256));
     else xv[g] = *reinterpret_cast<const bf16x8*>(xr + g * 256);
   }
-  if (res) {
-    const bf16* rr = res + (size_t)r * N + hl * 8;
+  if (rrow) {
+    const bf16* rr = rrow + hl * 8;
     bf16x8 rv[NG];
 #pragma unroll
     for (int g = 0; g < NG; ++g) rv[g] = *reinterpret_cast<const bf16x8*>(rr + g * 256);
@@ -131,7 +127,7 @@ __global__ __launch_bounds__(256) void layernorm_hw_kernel(const bf16* __restric
   }
   const float rstd = rsqrtf(half_sum(q) * (1.0f / N) + eps);
   if (!live) return;
-  bf16* orow = out + (size_t)row * N + hl * 8;
+  bf16* orow = orow_base + hl * 8;
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
     const int c = g * 256 + hl * 8;
@@ -147,6 +143,45 @@ __global__ __launch_bounds__(256) void layernorm_hw_kernel(const bf16* __restric
     }
     *reinterpret_cast<bf16x8*>(orow + g * 256) = o;
   }
+}
+
+template <int NG, bool NTL>
+__global__ __launch_bounds__(256) void layernorm_hw_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, bf16* __restrict__ out,
+                                                           int rows, float eps) {
+  const int hl = threadIdx.x & 31;
+  const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
+  const bool live = row < rows;
+  const int r = live ? row : rows - 1;  // dead half-waves read a valid row, never store
+  constexpr int N = NG * 256;
+  ln_hw_row<NG, NTL>(x + (size_t)r * N, res ? res + (size_t)r * N : nullptr, gamma, beta, out + (size_t)row * N,
+                     live, eps, hl);
+}
+
+// Decoder input of a learned-position model at one device-side step (BART): LN(table[ids[r]] +
+// pos[*step + pos_off]) per row, the layernorm_hw math on the gathered rows, so the output equals
+// embed_gather + the position row + layernorm_bf16(residual=) bit for bit in one launch (the
+// position index never leaves the device: no host sync, graph-capturable).
+template <int NG>
+__global__ __launch_bounds__(256) void embed_pos_ln_kernel(const int32_t* __restrict__ ids,
+                                                           const bf16* __restrict__ table,
+                                                           const bf16* __restrict__ pos,
+                                                           const int32_t* __restrict__ step, int pos_off, int npos,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, bf16* __restrict__ out,
+                                                           int rows, int vocab, float eps) {
+  const int hl = threadIdx.x & 31;
+  const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
+  const bool live = row < rows;
+  const int r = live ? row : rows - 1;
+  constexpr int N = NG * 256;
+  int id = ids[r];
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+  int pi = *step + pos_off;
+  pi = pi < 0 ? 0 : (pi >= npos ? npos - 1 : pi);
+  ln_hw_row<NG, false>(table + (size_t)id * N, pos + (size_t)pi * N, gamma, beta, out + (size_t)row * N, live, eps,
+                       hl);
 }
 
 template <int NG>
@@ -295,6 +330,18 @@ void ln_stats_finalize(const float* part, int slots, int M, int K, float eps, fl
   if (M <= 0) return;
   hipLaunchKernelGGL(ln_stats_finalize_kernel, dim3((M + 255) / 256), dim3(256), 0, stream, part, slots, M,
                      1.0f / static_cast<float>(K), eps, fin);
+  ATPU_HIP_CHECK(hipGetLastError());
+}
+
+void embed_pos_layernorm(const int32_t* ids, const bf16* table, const bf16* pos, const int32_t* step, int pos_off,
+                         int npos, const float* gamma, const float* beta, bf16* out, int rows, int N, int vocab,
+                         float eps, hipStream_t stream) {
+  check_width(N);
+  ATPU_CHECK(vocab > 0 && npos > 0 && step, "embed_pos_layernorm: empty table or no step");
+  if (rows <= 0) return;
+  const dim3 grid((rows + 7) / 8);
+  ATPU_NG_DISPATCH(N, hipLaunchKernelGGL(embed_pos_ln_kernel<NG>, grid, dim3(256), 0, stream, ids, table, pos, step,
+                                         pos_off, npos, gamma, beta, out, rows, vocab, eps));
   ATPU_HIP_CHECK(hipGetLastError());
 }
 

@@ -188,7 +188,6 @@ class BartModel:
         self.device = pack.buffer.device
         dt = self.p["shared"].dtype
         self._type0 = torch.zeros((2, cfg.d_model), dtype=dt, device=self.device)
-        self._pos_off = torch.tensor([POS_OFFSET], dtype=torch.int64, device=self.device)
         # decode QKV GEMM writes K|V straight into the KV cache (no kv_append pass)
         self.kv_scatter = (self.device.type == "cuda" and not fp32
                            and os.getenv("ATPU_KV_SCATTER", "1") not in ("0", "false", "no"))
@@ -330,10 +329,9 @@ class BartModel:
         cfg, p = self.cfg, self.p
         d, H = cfg.d_model, cfg.heads
         scale = (d // H) ** -0.5
-        x = ops.embed_gather(tokens, p["shared"])
-        pos = p["dec.pos"].index_select(0, step.reshape(1).long() + self._pos_off)
-        x = ops.layernorm(x, p["dec.ln_emb_g"], p["dec.ln_emb_b"], cfg.eps,
-                          residual=pos.expand(x.shape[0], d).contiguous())
+        # token + learned position (device-side step) + LayerNorm in one launch
+        x = ops.embed_pos_layernorm(tokens, p["shared"], p["dec.pos"], step, POS_OFFSET, p["dec.ln_emb_g"],
+                                    p["dec.ln_emb_b"], cfg.eps)
         if self.ln_fold:
             return self._step_folded(x, step, cache, T, ckv, src_lens, S, group, hist, logits)
         for i in range(cfg.dec_layers):

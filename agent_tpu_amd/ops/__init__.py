@@ -13,7 +13,7 @@ from .decode import decode_advance, decode_advance_ok  # noqa: F401
 from .decode import beam_select, beam_select_ref, ngram_bans, lm_head_topk, lm_head, LmHead, LM_HEAD_MAX_K  # noqa: F401
 from .attention import attention_packed, attention  # noqa: F401
 from .qkv_attention import qkv_attention, qkv_attention_ok, qkv_head_order  # noqa: F401
-from .norm import layernorm, rmsnorm, embed_layernorm, embed_gather  # noqa: F401
+from .norm import layernorm, rmsnorm, embed_layernorm, embed_gather, embed_pos_layernorm  # noqa: F401
 from .tokenize import tokenize  # noqa: F401
 from .head import classify_head_topk  # noqa: F401
 from .reduce import risk_stats, reduce_stats_tensor  # noqa: F401

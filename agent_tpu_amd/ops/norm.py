@@ -109,3 +109,35 @@ def embed_gather(ids: torch.Tensor, table: torch.Tensor, out: Optional[torch.Ten
         _check_out(out, (flat.numel(), N), table)
     native().embed_gather(ptr(flat), ptr(table), ptr(out), flat.numel(), N, V, launch_stream(table))
     return out
+
+
+def embed_pos_layernorm(ids: torch.Tensor, table: torch.Tensor, pos: torch.Tensor, step: torch.Tensor, pos_off: int,
+                        gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-5,
+                        out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``LN(table[ids[r]] + pos[step + pos_off])`` for every row r of ``ids`` -> ``[rows, N]``.
+
+    The decoder input of a learned-position model (BART) at one device-side step: one launch,
+    bit for bit ``layernorm(embed_gather(ids, table), residual=pos[step + pos_off])`` and the
+    position index stays on the device (graph-capturable, no host sync)."""
+    V, N = table.shape
+    flat = ids.reshape(-1)
+    rows = flat.numel()
+    if not ids.is_cuda:
+        pi = (step.reshape(-1)[:1].long() + pos_off).clamp(0, pos.shape[0] - 1)
+        x = table[flat.long().clamp(0, V - 1)]
+        y = layernorm(x, gamma, beta, eps, residual=pos.index_select(0, pi).expand(rows, N).contiguous())
+        return out.copy_(y) if out is not None else y
+    check(flat.dtype == torch.int32 and flat.is_contiguous(), "ids must be contiguous int32")
+    check(step.dtype == torch.int32 and step.is_cuda and step.numel() >= 1, "step must be a device int32 tensor")
+    check_bf16_dev(table, "table")
+    check_bf16_dev(pos, "pos")
+    check(pos.is_contiguous() and tuple(pos.shape[1:]) == (N,) and pos.shape[0] > 0, "pos must be [P, N]")
+    _f32(gamma, N, "gamma")
+    _f32(beta, N, "beta")
+    if out is None:
+        out = torch.empty((rows, N), dtype=torch.bfloat16, device=ids.device)
+    else:
+        _check_out(out, (rows, N), table)
+    native().embed_pos_layernorm(ptr(flat), ptr(table), ptr(pos), ptr(step), int(pos_off), pos.shape[0], ptr(gamma),
+                                 ptr(beta), ptr(out), rows, N, V, float(eps), launch_stream(table))
+    return out

@@ -275,6 +275,26 @@ def test_embed_layernorm_and_gather(gpu):
     assert torch.equal(e.cpu(), word.cpu()[ids.view(-1).long()])
 
 
+@pytest.mark.parametrize("N,rows,off", [(1024, 4, 2), (768, 13, 0), (1024, 64, 2)])
+def test_embed_pos_layernorm_matches_the_three_op_path(gpu, N, rows, off):
+    # BART's decoder input: one launch == embed_gather + position row + layernorm(residual=), bit for bit,
+    # with the position index read on the device (step past the table end clamps)
+    V, P = 3000, 140
+    table, pos = _rand((V, N), gpu, seed=41), _rand((P, N), gpu, seed=42)
+    g = _rand((N,), gpu, 1.0, torch.float32, seed=43)
+    b = _rand((N,), gpu, 1.0, torch.float32, seed=44)
+    ids = torch.randint(0, V, (rows,), dtype=torch.int32).to(gpu)
+    ids[0] = V + 5  # clamped like embed_gather
+    for st in (0, 7, P - off - 1, P + 3):
+        step = torch.tensor([st], dtype=torch.int32, device=gpu)
+        y = ops.embed_pos_layernorm(ids, table, pos, step, off, g, b, 1e-5)
+        pr = pos[min(st + off, P - 1)].view(1, N).expand(rows, N).contiguous()
+        ref = ops.layernorm(ops.embed_gather(ids, table), g, b, 1e-5, residual=pr)
+        assert torch.equal(y, ref), st
+        cpu = ops.embed_pos_layernorm(ids.cpu(), table.cpu(), pos.cpu(), step.cpu(), off, g.cpu(), b.cpu(), 1e-5)
+        assert _rel_err(y, cpu.float()) < 1e-2
+
+
 # -------------------------------------------------------------- tokenizer
 def test_tokenizer_gpu_matches_python_and_host(gpu, nat):
     from agent_tpu_amd import tokenizer as T
