@@ -335,6 +335,98 @@ __global__ __launch_bounds__(kMergeThreads) void lm_head_merge_kernel(const floa
   }
 }
 
+// Few rows (a 1-document step: 4-32 rows, one workgroup each on an idle chip): the merge above
+// is a dependent chain per thread (16-32 candidate insertions of 8 compare-selects, then two
+// 8-round wave arg-max passes at one wave per SIMD) -- 14.6-16.3 us per call. Here 16 waves
+// per row and 4 threads per tile, each inserting its tile's 4 candidate slots: the
+// insertion chain is 4 long; the per-wave passes run side by side; wave 0 merges the 16
+// waves' top kTileSel (two per lane). Same selection (value desc, token asc) and output.
+constexpr int kMergeFewThreads = 1024;
+constexpr int kMergeFewRows = 32;  // rows up to which lm_head_topk merges with it
+
+__global__ __launch_bounds__(kMergeFewThreads) void lm_head_merge_few_kernel(const float4* __restrict__ hdr,
+                                                                              const float2* __restrict__ cand, int ntn,
+                                                                              const float* __restrict__ beam_scores,
+                                                                              int K, float* __restrict__ out_score,
+                                                                              int32_t* __restrict__ out_token) {
+  constexpr int NW = kMergeFewThreads / 64;
+  constexpr int kPart = kTileCand / 4;  // candidate slots per thread
+  static_assert(NW * kTileSel == 128, "wave 0 merges two per lane");
+  __shared__ float wm[NW], wsum[NW];
+  __shared__ float cv[NW * kTileSel];
+  __shared__ int ci[NW * kTileSel];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int part = tid & 3;
+  const float4* h = hdr + (size_t)row * ntn;
+  const float4* c4 = reinterpret_cast<const float4*>(cand + (size_t)row * ntn * kTileCand);
+  float mx = -FLT_MAX, sm = 0.f;
+  float tv[kTileSel];
+  int ti[kTileSel];
+#pragma unroll
+  for (int r = 0; r < kTileSel; ++r) {
+    tv[r] = -FLT_MAX;
+    ti[r] = 0x7fffffff;
+  }
+  for (int t = tid >> 2; t < ntn; t += kMergeFewThreads / 4) {
+    const float4 p = h[t];
+    // slots part*4 .. part*4+3: two 16-B loads, issued with the header's
+    const float4 e0 = c4[(size_t)t * (kTileCand / 2) + part * 2];
+    const float4 e1 = c4[(size_t)t * (kTileCand / 2) + part * 2 + 1];
+    const int n = __float_as_int(p.z);
+    if (part == 0) {
+      if (p.x > mx) {
+        sm = sm * __expf(mx - p.x) + p.y;
+        mx = p.x;
+      } else if (p.x > -FLT_MAX) {
+        sm += p.y * __expf(p.x - mx);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kPart; ++q) {
+      const float4 e = q < 2 ? e0 : e1;
+      const float x = (q & 1) ? e.z : e.x;
+      const int id = __float_as_int((q & 1) ? e.w : e.y);
+      if (part * kPart + q < n && better(x, id, tv[kTileSel - 1], ti[kTileSel - 1])) list_insert<kTileSel>(tv, ti, x, id);
+    }
+  }
+  const float gm0 = wave_max(mx);
+  float sa = (mx == -FLT_MAX) ? 0.f : sm * __expf(mx - gm0);
+  sa = wave_sum(sa);
+  float rv;
+  int ri;
+  wave_topk<kTileSel>(tv, ti, rv, ri);
+  if (lane == 0) {
+    wm[w] = gm0;
+    wsum[w] = sa;
+  }
+  if (lane < kTileSel) {
+    cv[w * kTileSel + lane] = rv;
+    ci[w * kTileSel + lane] = ri;
+  }
+  __syncthreads();
+  if (w == 0) {
+    float gm = -FLT_MAX;
+#pragma unroll
+    for (int x = 0; x < NW; ++x) gm = fmaxf(gm, wm[x]);
+    float gs = 0.f;
+#pragma unroll
+    for (int x = 0; x < NW; ++x) gs += wsum[x] * __expf(wm[x] - gm);
+    const float shift = beam_scores[row] - gm - __logf(gs);
+#pragma unroll
+    for (int r = 0; r < kTileSel; ++r) {
+      tv[r] = -FLT_MAX;
+      ti[r] = 0x7fffffff;
+    }
+    list_insert<kTileSel>(tv, ti, cv[lane], ci[lane]);
+    list_insert<kTileSel>(tv, ti, cv[lane + 64], ci[lane + 64]);
+    wave_topk<kTileSel>(tv, ti, rv, ri);
+    if (lane < K) {
+      out_score[(size_t)row * K + lane] = rv == -FLT_MAX ? -FLT_MAX : rv + shift;
+      out_token[(size_t)row * K + lane] = ri;
+    }
+  }
+}
+
 // Per-row ban bitmap (bit t of row r set = token t banned): the explicit ban list
 // (-1 padded) and/or the no-repeat-n-gram bans of the device token history, built
 // in LDS and written out whole (rows of ban_ld words, zero past V).
@@ -472,8 +564,12 @@ void lm_head_topk(const bf16* A, int lda, const bf16* W, int ldw, const float* b
 #undef ATPU_LM_BANS
 #undef ATPU_LM_CFG
 #undef ATPU_LM
-  hipLaunchKernelGGL(lm_head_merge_kernel, dim3(M), dim3(kMergeThreads), 0, stream, hdr, cand, nslab, beam_scores,
-                     topk, out_score, out_token);
+  if (M <= kMergeFewRows)
+    hipLaunchKernelGGL(lm_head_merge_few_kernel, dim3(M), dim3(kMergeFewThreads), 0, stream, hdr, cand, nslab,
+                       beam_scores, topk, out_score, out_token);
+  else
+    hipLaunchKernelGGL(lm_head_merge_kernel, dim3(M), dim3(kMergeThreads), 0, stream, hdr, cand, nslab, beam_scores,
+                       topk, out_score, out_token);
   ATPU_HIP_CHECK(hipGetLastError());
 }
 
