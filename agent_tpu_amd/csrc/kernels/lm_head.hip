@@ -63,6 +63,85 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// Epilogue of one 16-row fragment of a wave's WC = 16 TN vocabulary columns (lane (frow,
+// fchunk): row m, columns c0 + j*16 + fchunk*4 + e): RMS scale / bias, the row's max and
+// sum exp over every column, bans / EOS mask / past-V columns out of the candidates, then
+// the slab's header and candidate set (tile_row_emit).
+template <bool RMS, bool BIAS, bool BANS, int TN>
+__device__ __forceinline__ void lm_row_emit(const f32x4 (&acc)[TN], float ssq, int m, int fchunk, int c0, int M, int V,
+                                            int K, const float* __restrict__ bias, float rms_eps,
+                                            const uint32_t* __restrict__ ban_bits, int ban_ld, int eos, int mask_eos,
+                                            int nslab, float4* __restrict__ hdr, float2* __restrict__ cand) {
+  constexpr int WC = TN * 16;
+  const int slab = c0 / WC;
+  const bool tail = c0 + WC > V;
+  const bool eos_here = mask_eos && eos >= c0 && eos < c0 + WC;
+  f32x4 bv[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = c0 + j * 16 + fchunk * 4;
+    bv[j] = (BIAS && n < V) ? *reinterpret_cast<const f32x4*>(bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  {
+    const bool live = m < M;
+    const float rs = RMS ? __builtin_amdgcn_rsqf(lane_rows_sum(ssq) * (1.f / K) + rms_eps) : 1.f;
+    float v[TN][4];
+    float mx = -FLT_MAX;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x = acc[j][e];
+        if constexpr (RMS) x *= rs;
+        if constexpr (BIAS) x += bv[j][e];
+        if (tail && c0 + j * 16 + fchunk * 4 + e >= V) x = -FLT_MAX;
+        v[j][e] = x;
+        mx = fmaxf(mx, x);
+      }
+    const float rmax = lane_rows_max(mx);
+    const float mb = rmax * kLog2e;
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s += __builtin_amdgcn_exp2f(fmaf(v[j][e], kLog2e, -mb));
+    s = lane_rows_sum(s);
+
+    // selection values: banned / masked EOS / past-V columns -> -FLT_MAX
+    if constexpr (BANS) {
+      // the slab's WC / 32 bitmap words of row m (16-B rows, 8-B aligned slabs)
+      uint32_t wd[WC / 32];
+      const uint32_t* bp = ban_bits + (size_t)min(m, M - 1) * ban_ld + c0 / 32;
+      if constexpr (WC == 128) {
+        const uint4 q = *reinterpret_cast<const uint4*>(bp);
+        wd[0] = q.x, wd[1] = q.y, wd[2] = q.z, wd[3] = q.w;
+      } else {
+        const uint2 q = *reinterpret_cast<const uint2*>(bp);
+        wd[0] = q.x, wd[1] = q.y;
+      }
+      uint32_t any = 0u;
+#pragma unroll
+      for (int w = 0; w < WC / 32; ++w) any |= wd[w];
+      if (__ballot(any != 0u)) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if ((wd[j >> 1] >> ((j & 1) * 16 + fchunk * 4 + e)) & 1u) v[j][e] = -FLT_MAX;
+      }
+    }
+    if (eos_here) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (c0 + j * 16 + fchunk * 4 + e == eos) v[j][e] = -FLT_MAX;
+    }
+    const size_t slot = (size_t)m * nslab + slab;
+    tile_row_emit<TN>(v, c0, fchunk, live, rmax, s, hdr + slot, cand + slot * kTileCand);
+  }
+}
+
 template <bool RMS, bool BIAS, bool BANS, int BM, int NST, int WN>
 __global__ __launch_bounds__(BM / 32 * 64, (BM + kBN) * kRowB * NST <= 80 * 1024 ? 2 : 1) void lm_head_topk_kernel(
     const bf16* __restrict__ A, int lda, const bf16* __restrict__ W, int ldw, const float* __restrict__ bias,
@@ -154,75 +233,81 @@ __global__ __launch_bounds__(BM / 32 * 64, (BM + kBN) * kRowB * NST <= 80 * 1024
   // lane (frow, fchunk) holds rows wm*WR + i*16 + frow, columns c0 + j*16 + fchunk*4 + e
   const int c0 = n0 + wn * WC;  // this wave's slab
   if (c0 >= V) return;          // wholly past the vocabulary (wave-uniform)
-  const int slab = c0 / WC;
-  const bool tail = c0 + WC > V;
-  const bool eos_here = mask_eos && eos >= c0 && eos < c0 + WC;
-  f32x4 bv[TN];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = c0 + j * 16 + fchunk * 4;
-    bv[j] = (BIAS && n < V) ? *reinterpret_cast<const f32x4*>(bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = m0 + wm * WR + i * 16 + frow;
-    const bool live = m < M;
-    const float rs = RMS ? __builtin_amdgcn_rsqf(lane_rows_sum(ssq[i]) * (1.f / K) + rms_eps) : 1.f;
-    float v[TN][4];
-    float mx = -FLT_MAX;
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float x = acc[i][j][e];
-        if constexpr (RMS) x *= rs;
-        if constexpr (BIAS) x += bv[j][e];
-        if (tail && c0 + j * 16 + fchunk * 4 + e >= V) x = -FLT_MAX;
-        v[j][e] = x;
-        mx = fmaxf(mx, x);
-      }
-    const float rmax = lane_rows_max(mx);
-    const float mb = rmax * kLog2e;
-    float s = 0.f;
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) s += __builtin_amdgcn_exp2f(fmaf(v[j][e], kLog2e, -mb));
-    s = lane_rows_sum(s);
+  for (int i = 0; i < TM; ++i)
+    lm_row_emit<RMS, BIAS, BANS, TN>(acc[i], ssq[i], m0 + wm * WR + i * 16 + frow, fchunk, c0, M, V, K, bias, rms_eps,
+                                     ban_bits, ban_ld, eos, mask_eos, nslab, hdr, cand);
+}
 
-    // selection values: banned / masked EOS / past-V columns -> -FLT_MAX
-    if constexpr (BANS) {
-      // the slab's WC / 32 bitmap words of row m (16-B rows, 8-B aligned slabs)
-      uint32_t wd[WC / 32];
-      const uint32_t* bp = ban_bits + (size_t)min(m, M - 1) * ban_ld + c0 / 32;
-      if constexpr (WC == 128) {
-        const uint4 q = *reinterpret_cast<const uint4*>(bp);
-        wd[0] = q.x, wd[1] = q.y, wd[2] = q.z, wd[3] = q.w;
-      } else {
-        const uint2 q = *reinterpret_cast<const uint2*>(bp);
-        wd[0] = q.x, wd[1] = q.y;
-      }
-      uint32_t any = 0u;
+// Few rows (<= 16: a 1-document decode step) and <= one panel per CU: lm_head_topk_kernel streams each 128-column
+// panel through a 2-slot LDS ring, one 64-deep K-tile per barrier, with the A tile's 128
+// staged rows mostly copies of the 4 real ones -- 20 us per T5 step for 49 MB of weights.
+// Here 8 waves split K (K / 8 = 96 or 128 per wave) and every lane issues ALL its operand
+// loads at once, straight from global memory into MFMA fragment registers (no LDS, no
+// barrier in the loop): 16-B weight chunks of the panel's 128 rows, the A rows from L2.
+// Each wave's [16 rows x 128 columns] partial goes through LDS, wave w sums column block w
+// over the 8 waves (fixed order), and wave 0 runs the same epilogue (lm_row_emit) on the
+// one 16-row fragment: the same slab format, so lm_head_merge* take it unchanged.
+constexpr int kFewRows = 16, kFewWaves = 8, kFewKs = 4;  // rows, waves (K split), max k-steps of 32 per wave
+
+template <bool RMS, bool BIAS, bool BANS>
+__global__ __launch_bounds__(kFewWaves * 64) void lm_head_few_kernel(
+    const bf16* __restrict__ A, int lda, const bf16* __restrict__ W, int ldw, const float* __restrict__ bias,
+    float rms_eps, int M, int V, int K, const uint32_t* __restrict__ ban_bits, int ban_ld, int eos, int mask_eos,
+    float4* __restrict__ hdr, float2* __restrict__ cand) {
+  constexpr int TN = kBN / 16;
+  __shared__ f32x4 red[kFewWaves][TN][64];  // 64 KiB
+  __shared__ float rsq[kFewWaves][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int frow = lane & 15, fchunk = lane >> 4;
+  const int n0 = blockIdx.x * kBN;
+  const int kw = K / kFewWaves;  // host: K % (32 * kFewWaves) == 0, kw <= 32 * kFewKs
+  const int k0 = wave * kw + fchunk * 8;
+  const bf16* ar = A + (size_t)min(frow, M - 1) * lda + k0;
+  bf16x8 af[kFewKs], bw[kFewKs][TN];
 #pragma unroll
-      for (int w = 0; w < WC / 32; ++w) any |= wd[w];
-      if (__ballot(any != 0u)) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if ((wd[j >> 1] >> ((j & 1) * 16 + fchunk * 4 + e)) & 1u) v[j][e] = -FLT_MAX;
-      }
-    }
-    if (eos_here) {
+  for (int ks = 0; ks < kFewKs; ++ks) {
+    if (ks * 32 < kw) {  // wave-uniform
+      af[ks] = *reinterpret_cast<const bf16x8*>(ar + ks * 32);
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (c0 + j * 16 + fchunk * 4 + e == eos) v[j][e] = -FLT_MAX;
+        bw[ks][j] = *reinterpret_cast<const bf16x8*>(W + (size_t)min(n0 + j * 16 + frow, V - 1) * ldw + k0 + ks * 32);
     }
-    const size_t slot = (size_t)m * nslab + slab;
-    tile_row_emit<TN>(v, c0, fchunk, live, rmax, s, hdr + slot, cand + slot * kTileCand);
   }
+  f32x4 acc[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ssq = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < kFewKs; ++ks) {
+    if (ks * 32 < kw) {
+      if constexpr (RMS) ssq = sumsq_chunk(af[ks], ssq);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[ks][j], af[ks], acc[j], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) red[wave][j][lane] = acc[j];
+  if constexpr (RMS) rsq[wave][lane] = ssq;
+  __syncthreads();
+  {  // column block j = wave, summed over the waves in order
+    f32x4 t = red[0][wave][lane];
+#pragma unroll
+    for (int x = 1; x < kFewWaves; ++x) t += red[x][wave][lane];
+    red[0][wave][lane] = t;
+  }
+  __syncthreads();
+  if (wave != 0 || n0 >= V) return;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) acc[j] = red[0][j][lane];
+  if constexpr (RMS) {
+    ssq = rsq[0][lane];
+#pragma unroll
+    for (int x = 1; x < kFewWaves; ++x) ssq += rsq[x][lane];
+  }
+  lm_row_emit<RMS, BIAS, BANS, TN>(acc, ssq, frow, fchunk, n0, M, V, K, bias, rms_eps, ban_bits, ban_ld, eos, mask_eos,
+                                   (V + kBN - 1) / kBN, hdr, cand);
 }
 
 constexpr int kMergeThreads = 256;
@@ -519,6 +604,23 @@ void lm_head_topk(const bf16* A, int lda, const bf16* W, int ldw, const float* b
   }
   const bool rms = rms_eps > 0.f, has_bias = bias != nullptr;
   ATPU_CHECK(!(rms && has_bias), "lm_head_topk: RMSNorm folding and a bias together are not instantiated");
+  // few rows, and one workgroup per CU covers the vocabulary (T5's 251 panels; BART's 393 would
+  // run in two rounds at one 8-wave workgroup per CU: 44 vs 40 us per call, measured)
+  const bool few = M <= kFewRows && K % (32 * kFewWaves) == 0 && K <= 32 * kFewWaves * kFewKs && wc == kBN &&
+                   ntn <= num_cus();
+  if (few) {
+#define ATPU_LMF(R, B, X)                                                                                             \
+  hipLaunchKernelGGL((lm_head_few_kernel<R, B, X>), dim3(ntn), dim3(kFewWaves * 64), 0, stream, A, lda, W, ldw, bias, \
+                     rms_eps, M, V, K, bits, ld, eos, mask_eos, hdr, cand)
+    if (rms) {
+      if (any_bans) ATPU_LMF(true, false, true); else ATPU_LMF(true, false, false);
+    } else if (has_bias) {
+      if (any_bans) ATPU_LMF(false, true, true); else ATPU_LMF(false, true, false);
+    } else {
+      if (any_bans) ATPU_LMF(false, false, true); else ATPU_LMF(false, false, false);
+    }
+#undef ATPU_LMF
+  } else {
 #define ATPU_LM(R, B, X, BM, N, WN)                                                                              \
   hipLaunchKernelGGL((lm_head_topk_kernel<R, B, X, BM, N, WN>), dim3(((M + BM - 1) / BM) * ntn), dim3(BM / 32 * 64), \
                      0, stream, A, lda, W, ldw, bias, rms_eps, M, V, K, bits, ld, eos, mask_eos, hdr, cand)
@@ -564,6 +666,7 @@ void lm_head_topk(const bf16* A, int lda, const bf16* W, int ldw, const float* b
 #undef ATPU_LM_BANS
 #undef ATPU_LM_CFG
 #undef ATPU_LM
+  }
   if (M <= kMergeFewRows)
     hipLaunchKernelGGL(lm_head_merge_few_kernel, dim3(M), dim3(kMergeFewThreads), 0, stream, hdr, cand, nslab,
                        beam_scores, topk, out_score, out_token);

@@ -306,7 +306,10 @@ def _lm_case(R, V, d, rms, bias, gpu, seed, scale=1.0):
 @pytest.mark.parametrize("R,V,d,rms,bias,k,mask", [(12, 32128, 768, True, False, 8, True), (300, 50264, 1024, False, True, 8, False),
                                                    (4, 1000, 64, False, False, 2, True), (1024, 32128, 768, True, False, 8, False),
                                                    (130, 4100, 128, False, True, 5, True), (512, 50264, 1024, False, True, 8, True),
-                                                   (256, 1000, 128, True, False, 8, False)])
+                                                   (256, 1000, 128, True, False, 8, False),
+                                                   # <= 16 rows, <= one 128-column panel per CU: lm_head_few_kernel
+                                                   (8, 20000, 1024, False, True, 8, True), (16, 32128, 768, True, False, 8, False),
+                                                   (1, 32128, 768, True, False, 8, True)])
 def test_lm_head_topk_matches_logits_path(gpu, cfg, R, V, d, rms, bias, k, mask):
     # fused LM head + top-k == fp32-logit GEMM + beam_topk_rows: the same MFMA accumulation
     # order gives bit-identical logits, so the tokens match exactly; the normaliser is summed
@@ -365,9 +368,9 @@ def test_lm_head_topk_device_ngram(gpu, n, cur, R):
     torch.testing.assert_close(sc.cpu(), rsc.cpu(), atol=1e-4, rtol=1e-5)
 
 
-@pytest.mark.parametrize("R", [16, 256])
-def test_lm_head_topk_ban_list(gpu, R):
-    V, d, nb = 50264, 256, 12
+@pytest.mark.parametrize("R,V", [(16, 50264), (256, 50264), (4, 20000)])  # (4, 20000): the few-row kernel
+def test_lm_head_topk_ban_list(gpu, R, V):
+    d, nb = 256, 12
     head, bs = _lm_case(R, V, d, False, True, gpu, seed=70)
     logits = head.logits()
     g = torch.Generator().manual_seed(71)
