@@ -235,6 +235,8 @@ PYBIND11_MODULE(_atpu, m) {
   m.def("decode_attention_ws_floats", [](int rows, int group, int H, int seq_stride, bool cross) {
     return decode_attention_ws_floats(rows, group, H, seq_stride, cross);
   });
+  m.def("host_device_ptr", &host_device_ptr, "device address of a pinned host buffer (checked)", py::arg("host"),
+        py::arg("bytes"));
   m.def("beam_select", [](uintptr_t sc, uintptr_t tk, int B, int nb, int K2, int V, int eos, int hit_all, float neg,
                           uintptr_t stage, uintptr_t rec, uintptr_t stream) {
     beam_select(P<const float>(sc), P<const int32_t>(tk), B, nb, K2, V, eos, hit_all, neg, P<int32_t>(stage),
@@ -243,13 +245,27 @@ PYBIND11_MODULE(_atpu, m) {
   m.def(
       "decode_advance",
       [](uintptr_t hist, uintptr_t seq, int rows, int stride, uintptr_t par, uintptr_t tok, uintptr_t tokens,
-         uintptr_t step_dev, uintptr_t stream) {
+         uintptr_t step_dev, uintptr_t stream, uintptr_t emb, int vocab, int N, uintptr_t pos, int pos_off, int npos,
+         uintptr_t gamma, uintptr_t beta, float eps, uintptr_t out) {
+        DecEmbed em;
+        em.table = P<const bf16>(emb);
+        em.vocab = vocab;
+        em.pos = P<const bf16>(pos);
+        em.pos_off = pos_off;
+        em.npos = npos;
+        em.gamma = P<const float>(gamma);
+        em.beta = P<const float>(beta);
+        em.eps = eps;
+        em.out = P<bf16>(out);
         decode_advance(P<int32_t>(hist), P<int32_t>(seq), rows, stride, P<const int32_t>(par), P<const int32_t>(tok),
-                       P<int32_t>(tokens), P<int32_t>(step_dev), S(stream));
+                       P<int32_t>(tokens), P<int32_t>(step_dev), S(stream), em, N);
       },
-      "one-workgroup beam state advance: hist/seq reordered in place, tokens = tok, step += 1", py::arg("hist"),
-      py::arg("seq"), py::arg("rows"), py::arg("stride"), py::arg("par"), py::arg("tok"), py::arg("tokens"),
-      py::arg("step"), py::arg("stream"));
+      "one-workgroup beam state advance: hist/seq reordered in place, tokens = tok, step += 1 (emb: the new "
+      "tokens' decoder input into out, LayerNorm with gamma)",
+      py::arg("hist"), py::arg("seq"), py::arg("rows"), py::arg("stride"), py::arg("par"), py::arg("tok"),
+      py::arg("tokens"), py::arg("step"), py::arg("stream"), py::arg("emb") = 0, py::arg("vocab") = 0,
+      py::arg("N") = 0, py::arg("pos") = 0, py::arg("pos_off") = 0, py::arg("npos") = 0, py::arg("gamma") = 0,
+      py::arg("beta") = 0, py::arg("eps") = 0.f, py::arg("out") = 0);
   m.def("decode_advance_lds", &decode_advance_lds, py::arg("rows"), py::arg("stride"), py::arg("seq"));
   m.def(
       "beam_reorder_hist",

@@ -147,11 +147,26 @@ int decode_xattn_prefetch(int set);  // 1: few-item attention kernels prefetch a
 // hist / seq reordered in place by par (as beam_reorder_hist, seq with last = tok, off 1),
 // tokens = tok, *step_dev += 1
 size_t decode_advance_lds(int rows, int stride, bool seq);
+// decoder input of the new tokens, written by decode_advance (table == nullptr: none):
+// out[r] = table[tok[r]], or with gamma LN(table[tok[r]] + pos[step + 1 + pos_off])
+struct DecEmbed {
+  const bf16* table = nullptr;
+  int vocab = 0;
+  const bf16* pos = nullptr;
+  int pos_off = 0, npos = 0;
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+  float eps = 0.f;
+  bf16* out = nullptr;
+};
 void decode_advance(int32_t* hist, int32_t* seq, int rows, int stride, const int32_t* par, const int32_t* tok,
-                    int32_t* tokens, int32_t* step_dev, hipStream_t stream);
+                    int32_t* tokens, int32_t* step_dev, hipStream_t stream, const DecEmbed& em = DecEmbed{},
+                    int N = 0);
 // dst[r][j] = src[parent[r]][j] (j < t), dst[r][t] = last ? last[r] : parent[r]; t = *step_dev + off
 // device beam selection (runtime/summarize.py): item top-K2 over its beams' candidates, hits,
 // next running beams -> stage [parents | tokens | score bits] and a host record per item
+// device address of a pinned host buffer of `bytes` (checked with hipPointerGetAttributes)
+uintptr_t host_device_ptr(uintptr_t host, size_t bytes);
 void beam_select(const float* sc, const int32_t* tk, int B, int nb, int K2, int V, int eos, int hit_all, float neg,
                  int32_t* stage, int32_t* rec, hipStream_t stream);
 void beam_reorder_hist(const int32_t* src, int32_t* dst, const int32_t* parent, int rows, int stride,

@@ -27,6 +27,7 @@
 #include "atpu/common.h"
 #include "atpu/kernels.h"
 #include "atpu/l2_prefetch.h"
+#include "atpu/ln_row.h"
 #include "atpu/topk.h"
 
 #include <cfloat>
@@ -611,10 +612,15 @@ __global__ __launch_bounds__(256) void beam_reorder_hist_kernel(const int32_t* _
 //   seq[r][:t+1] = seq[par[r]][:t+1], seq[r][t+1] = tok[r]   (optional, n-gram bans)
 //   tokens[r] = tok[r];  step += 1
 // in place: every row is gathered into LDS before any is written back.
+// NG > 0: also the decoder input of the new tokens, rows of N = 256 NG (the next step's first
+// launch folded in): xout[r] = emb[tok[r]] (T5), or with gamma LN(emb[tok[r]] + pos[step + 1 +
+// pos_off]) (BART: embed_pos_ln_kernel's math, ln_hw_row), one half wave per row.
+template <int NG>
 __global__ __launch_bounds__(256) void decode_advance_kernel(int32_t* __restrict__ hist, int32_t* __restrict__ seq,
                                                              int rows, int stride, const int32_t* __restrict__ par,
                                                              const int32_t* __restrict__ tok,
-                                                             int32_t* __restrict__ tokens, int32_t* step_dev) {
+                                                             int32_t* __restrict__ tokens, int32_t* step_dev,
+                                                             DecEmbed em) {
   extern __shared__ int32_t adv_sh[];  // [rows][stride] hist, then [rows][stride] seq
   const int tid = threadIdx.x;
   const int step = *step_dev;
@@ -640,6 +646,26 @@ __global__ __launch_bounds__(256) void decode_advance_kernel(int32_t* __restrict
     }
   for (int r = tid; r < rows; r += blockDim.x) tokens[r] = tok[r];
   if (tid == 0) *step_dev = step + 1;
+  if constexpr (NG > 0) {
+    constexpr int N = NG * 256;
+    const int hl = tid & 31;
+    for (int r = tid >> 5; r < rows; r += 8) {  // 8 half waves
+      int id = tok[r];
+      id = id < 0 ? 0 : (id >= em.vocab ? em.vocab - 1 : id);
+      const bf16* er = em.table + (size_t)id * N;
+      if (em.gamma) {
+        int pi = step + 1 + em.pos_off;
+        pi = pi < 0 ? 0 : (pi >= em.npos ? em.npos - 1 : pi);
+        ln_hw_row<NG, false>(er, em.pos ? em.pos + (size_t)pi * N : nullptr, em.gamma, em.beta, em.out + (size_t)r * N,
+                             true, em.eps, hl);
+      } else {
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+          *reinterpret_cast<bf16x8*>(em.out + (size_t)r * N + g * 256 + hl * 8) =
+              *reinterpret_cast<const bf16x8*>(er + g * 256 + hl * 8);
+      }
+    }
+  }
 }
 
 // cache[row][t][0:ncols] = src[row][col0 : col0+ncols]
@@ -1152,12 +1178,37 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
 size_t decode_advance_lds(int rows, int stride, bool seq) { return (size_t)rows * stride * (seq ? 2 : 1) * 4; }
 
 void decode_advance(int32_t* hist, int32_t* seq, int rows, int stride, const int32_t* par, const int32_t* tok,
-                    int32_t* tokens, int32_t* step_dev, hipStream_t stream) {
+                    int32_t* tokens, int32_t* step_dev, hipStream_t stream, const DecEmbed& em, int N) {
   ATPU_CHECK(rows > 0 && stride > 0 && hist && par && tok && tokens && step_dev, "decode_advance: bad arguments");
   const size_t lds = decode_advance_lds(rows, stride, seq != nullptr);
   ATPU_CHECK(lds <= 64 * 1024, "decode_advance: rows x stride too large for one workgroup (use beam_reorder_hist)");
-  hipLaunchKernelGGL(decode_advance_kernel, dim3(1), dim3(256), lds, stream, hist, seq, rows, stride, par, tok, tokens,
-                     step_dev);
+  if (!em.table) {
+    hipLaunchKernelGGL(decode_advance_kernel<0>, dim3(1), dim3(256), lds, stream, hist, seq, rows, stride, par, tok,
+                       tokens, step_dev, em);
+  } else {
+    ATPU_CHECK(em.out && em.vocab > 0 && (!em.gamma || (em.beta && (!em.pos || em.npos > 0))),
+               "decode_advance: embedding needs table, out, vocab (and beta / positions with gamma)");
+    ATPU_CHECK((reinterpret_cast<uintptr_t>(em.table) & 15) == 0 && (reinterpret_cast<uintptr_t>(em.out) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(em.pos) & 15) == 0 && (reinterpret_cast<uintptr_t>(em.gamma) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(em.beta) & 15) == 0,
+               "decode_advance: embedding operands must be 16-byte aligned");
+    switch (N) {
+      case 512:
+        hipLaunchKernelGGL(decode_advance_kernel<2>, dim3(1), dim3(256), lds, stream, hist, seq, rows, stride, par, tok,
+                           tokens, step_dev, em);
+        break;
+      case 768:
+        hipLaunchKernelGGL(decode_advance_kernel<3>, dim3(1), dim3(256), lds, stream, hist, seq, rows, stride, par, tok,
+                           tokens, step_dev, em);
+        break;
+      case 1024:
+        hipLaunchKernelGGL(decode_advance_kernel<4>, dim3(1), dim3(256), lds, stream, hist, seq, rows, stride, par, tok,
+                           tokens, step_dev, em);
+        break;
+      default:
+        throw std::invalid_argument("decode_advance: embedding width must be 512, 768 or 1024");
+    }
+  }
   ATPU_HIP_CHECK(hipGetLastError());
 }
 
@@ -1216,6 +1267,23 @@ void beam_topk_rows(const float* logits, int rows, int V, const float* beam_scor
   }
 #undef ATPU_TK
   ATPU_HIP_CHECK(hipGetLastError());
+}
+
+uintptr_t host_device_ptr(uintptr_t host, size_t bytes) {
+  // the device address of a pinned (hipHostMalloc'd / registered) host buffer, checked on the
+  // host before any kernel writes there: an unmapped address would fault the GPU
+  hipPointerAttribute_t a{};
+  ATPU_HIP_CHECK(hipPointerGetAttributes(&a, reinterpret_cast<void*>(host)));
+  ATPU_CHECK(a.type == hipMemoryTypeHost && a.devicePointer != nullptr,
+             "host_device_ptr: not a device-mapped pinned host buffer");
+  // the whole range must lie in the same mapping
+  hipPointerAttribute_t b{};
+  ATPU_HIP_CHECK(hipPointerGetAttributes(&b, reinterpret_cast<void*>(host + (bytes ? bytes - 1 : 0))));
+  ATPU_CHECK(b.type == hipMemoryTypeHost && b.devicePointer != nullptr &&
+                 reinterpret_cast<uintptr_t>(b.devicePointer) - reinterpret_cast<uintptr_t>(a.devicePointer) ==
+                     (bytes ? bytes - 1 : 0),
+             "host_device_ptr: the range is not one pinned mapping");
+  return reinterpret_cast<uintptr_t>(a.devicePointer);
 }
 
 void beam_select(const float* sc, const int32_t* tk, int B, int nb, int K2, int V, int eos, int hit_all, float neg,

@@ -323,15 +323,25 @@ class BartModel:
         dt = self.p["dec.l0.qkv_w"].dtype
         return torch.zeros((self.cfg.dec_layers, rows * T, 2 * self.cfg.d_model), dtype=dt, device=self.device)
 
+    def dec_embed(self) -> Optional["ops.DecEmbed"]:
+        """The decoder input ``LN(shared[tok] + pos[step + 2])`` for ops.decode_advance to write
+        (device bf16 model; None: the step embeds its tokens itself)."""
+        p = self.p
+        if not (p["shared"].is_cuda and p["shared"].dtype == torch.bfloat16 and self.cfg.d_model in (512, 768, 1024)):
+            return None
+        return ops.DecEmbed(p["shared"], p["dec.pos"], POS_OFFSET, p["dec.ln_emb_g"], p["dec.ln_emb_b"], self.cfg.eps)
+
     def step(self, tokens: torch.Tensor, step: torch.Tensor, cache: torch.Tensor, T: int, ckv: torch.Tensor,
-             src_lens: torch.Tensor, S: int, group: int, hist: Optional[torch.Tensor] = None, logits: bool = True):
+             src_lens: torch.Tensor, S: int, group: int, hist: Optional[torch.Tensor] = None, logits: bool = True,
+             x0: Optional[torch.Tensor] = None):
         """One decoder position for ``rows`` sequences -> fp32 logits [rows, V] (see T5Model.step)."""
         cfg, p = self.cfg, self.p
         d, H = cfg.d_model, cfg.heads
         scale = (d // H) ** -0.5
-        # token + learned position (device-side step) + LayerNorm in one launch
-        x = ops.embed_pos_layernorm(tokens, p["shared"], p["dec.pos"], step, POS_OFFSET, p["dec.ln_emb_g"],
-                                    p["dec.ln_emb_b"], cfg.eps)
+        # token + learned position (device-side step) + LayerNorm in one launch; x0: the input
+        # ops.decode_advance already wrote (dec_embed)
+        x = x0 if x0 is not None else ops.embed_pos_layernorm(tokens, p["shared"], p["dec.pos"], step, POS_OFFSET,
+                                                              p["dec.ln_emb_g"], p["dec.ln_emb_b"], cfg.eps)
         if self.ln_fold:
             return self._step_folded(x, step, cache, T, ckv, src_lens, S, group, hist, logits)
         for i in range(cfg.dec_layers):

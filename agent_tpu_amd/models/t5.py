@@ -279,8 +279,16 @@ class T5Model:
         dt = self.p["dec.l0.qkv"].dtype
         return torch.zeros((self.cfg.dec_layers, rows * T, 2 * self.cfg.d_model), dtype=dt, device=self.device)
 
+    def dec_embed(self) -> Optional["ops.DecEmbed"]:
+        """The decoder input (``shared[tok]``) for ops.decode_advance to write, on the device
+        bf16 model (None: the step embeds its tokens itself)."""
+        t = self.p["shared"]
+        ok = t.is_cuda and t.dtype == torch.bfloat16 and self.cfg.d_model in (512, 768, 1024)
+        return ops.DecEmbed(t) if ok else None
+
     def step(self, tokens: torch.Tensor, step: torch.Tensor, cache: torch.Tensor, T: int, ckv: torch.Tensor,
-             src_lens: torch.Tensor, S: int, group: int, hist: Optional[torch.Tensor] = None, logits: bool = True):
+             src_lens: torch.Tensor, S: int, group: int, hist: Optional[torch.Tensor] = None, logits: bool = True,
+             x0: Optional[torch.Tensor] = None):
         """One decoder position for ``rows`` sequences -> fp32 logits [rows, V]
         (``logits=False``: the :class:`ops.LmHead` input for the fused LM head + top-k).
 
@@ -293,7 +301,8 @@ class T5Model:
         cfg, p = self.cfg, self.p
         d, H = cfg.d_model, cfg.heads
         dbias = self.dec_bias(T)
-        x = ops.embed_gather(tokens, p["shared"])
+        # x0: the input ops.decode_advance already embedded (dec_embed)
+        x = x0 if x0 is not None else ops.embed_gather(tokens, p["shared"])
         if x.dtype != p["dec.l0.qkv"].dtype:
             x = x.to(p["dec.l0.qkv"].dtype)
         if self.rms_fold:

@@ -132,10 +132,16 @@ def decode_advance_ok(rows: int, T: int, seq: bool) -> bool:
 
 
 def decode_advance(hist: torch.Tensor, seq: Optional[torch.Tensor], parent: torch.Tensor, tok: torch.Tensor,
-                   tokens: torch.Tensor, step: torch.Tensor) -> None:
+                   tokens: torch.Tensor, step: torch.Tensor, embed: Optional[DecEmbed] = None,
+                   out: Optional[torch.Tensor] = None) -> None:
     """A small beam search's per-step state advance in ONE launch, in place: ``hist`` reordered
     by ``parent`` (:func:`beam_reorder_hist`, t = step), ``seq`` likewise with the new tokens
-    (off 1), ``tokens = tok``, ``step += 1`` (replaces 2 reorders, 3 copies and an add)."""
+    (off 1), ``tokens = tok``, ``step += 1`` (replaces 2 reorders, 3 copies and an add).
+
+    ``embed`` (a model's :class:`DecEmbed`) with ``out`` [rows, d]: the same launch also writes
+    the new tokens' decoder input into ``out`` (the next step's embedding launch folded in):
+    ``table[tok]`` or, with a LayerNorm, ``LN(table[tok] + pos[step + pos_off])`` at the
+    advanced step -- bit for bit :func:`embed_gather` / :func:`embed_pos_layernorm`."""
     R, T = hist.shape
     if not hist.is_cuda:
         alt = torch.empty_like(hist)
@@ -147,14 +153,51 @@ def decode_advance(hist: torch.Tensor, seq: Optional[torch.Tensor], parent: torc
             seq.copy_(alt)
         tokens.copy_(tok)
         step.add_(1)
+        if embed is not None:
+            out.copy_(embed.apply(tokens, step))
         return
     for t, n in ((hist, "hist"), (parent, "parent"), (tok, "tok"), (tokens, "tokens"), (step, "step")):
         check(t.dtype == torch.int32 and t.is_cuda and t.is_contiguous(), f"decode_advance: {n} must be int32 on device")
     check(seq is None or (seq.dtype == torch.int32 and tuple(seq.shape) == (R, T) and seq.is_contiguous()),
           "decode_advance: seq must be int32 [R, T]")
     check(decode_advance_ok(R, T, seq is not None), "decode_advance: batch too large for one workgroup")
+    if embed is None:
+        native().decode_advance(ptr(hist), ptr(seq), R, T, ptr(parent), ptr(tok), ptr(tokens), ptr(step),
+                                launch_stream(hist))
+        return
+    V, d = embed.table.shape
+    check(embed.table.is_cuda and embed.table.dtype == torch.bfloat16 and embed.table.is_contiguous(),
+          "decode_advance: embedding table must be contiguous bf16 on device")
+    check(out is not None and tuple(out.shape) == (R, d) and out.dtype == torch.bfloat16 and out.is_contiguous(),
+          f"decode_advance: out must be bf16 [{R}, {d}]")
+    check(d in (512, 768, 1024), "decode_advance: embedding width 512 / 768 / 1024")
+    if embed.gamma is not None:
+        check(embed.gamma.dtype == torch.float32 and embed.gamma.numel() == d and embed.beta is not None
+              and embed.beta.numel() == d, "decode_advance: fp32 gamma / beta [d]")
+    if embed.pos is not None:
+        check(embed.pos.dtype == torch.bfloat16 and embed.pos.is_contiguous() and embed.pos.shape[1] == d,
+              "decode_advance: positions bf16 [P, d]")
     native().decode_advance(ptr(hist), ptr(seq), R, T, ptr(parent), ptr(tok), ptr(tokens), ptr(step),
-                            launch_stream(hist))
+                            launch_stream(hist), ptr(embed.table), V, d, ptr(embed.pos), int(embed.pos_off),
+                            embed.pos.shape[0] if embed.pos is not None else 0, ptr(embed.gamma), ptr(embed.beta),
+                            float(embed.eps), ptr(out))
+
+
+class DecEmbed:
+    """A decoder's input embedding, for :func:`decode_advance` to produce the next step's input:
+    ``table[tok]`` (T5), or ``LN(table[tok] + pos[step + pos_off])`` with ``gamma`` (BART)."""
+
+    def __init__(self, table: torch.Tensor, pos: Optional[torch.Tensor] = None, pos_off: int = 0,
+                 gamma: Optional[torch.Tensor] = None, beta: Optional[torch.Tensor] = None, eps: float = 0.0):
+        self.table, self.pos, self.pos_off, self.gamma, self.beta, self.eps = table, pos, pos_off, gamma, beta, eps
+
+    def apply(self, tokens: torch.Tensor, step: torch.Tensor) -> torch.Tensor:
+        """The same input through the stand-alone ops (the models' own path)."""
+        from .norm import embed_gather, embed_pos_layernorm
+
+        if self.gamma is None:
+            return embed_gather(tokens, self.table)
+        return embed_pos_layernorm(tokens, self.table, self.pos, step, self.pos_off, self.gamma, self.beta, self.eps)
 
 
 def gather_rows(src: torch.Tensor, dst: torch.Tensor, parent: torch.Tensor, nrows: int, seq_stride: int,
@@ -370,9 +413,17 @@ def beam_select(sc: torch.Tensor, tk: torch.Tensor, nb: int, V: int, eos: int, h
         return
     check(sc.dtype == torch.float32 and tk.dtype == torch.int32 and sc.is_contiguous() and tk.is_contiguous(),
           "beam_select: sc fp32 / tk int32, contiguous")
-    same_device(sc, tk, stage, rec)
+    if rec.device.type == "cpu":
+        # the record straight into pinned host memory (no device buffer + D2H copy launch): the
+        # host reads it after an event recorded behind this kernel
+        check(rec.is_pinned(), "beam_select: a host rec must be pinned")
+        same_device(sc, tk, stage)
+        rec_p = native().host_device_ptr(ptr(rec), rec.numel() * 4)
+    else:
+        same_device(sc, tk, stage, rec)
+        rec_p = ptr(rec)
     native().beam_select(ptr(sc), ptr(tk), B, nb, K2, int(V), int(eos), int(bool(hit_all)), float(neg), ptr(stage),
-                         ptr(rec), launch_stream(sc))
+                         rec_p, launch_stream(sc))
 
 
 def t5_ffn_fused(x: torch.Tensor, wi: torch.Tensor, wo: torch.Tensor, eps: float,

@@ -44,6 +44,12 @@ from ..tokenizer import pack_rows
 from ..utils.trace import span
 
 NEG = -1.0e9
+# the device beam selection writes each step's record straight into the pinned host slot the
+# search loop reads (no device record + D2H copy launch per step); ATPU_REC_ZERO_COPY=0: copy
+REC_ZERO_COPY = os.environ.get("ATPU_REC_ZERO_COPY", "1") != "0"
+# a small search's state advance also writes the next step's decoder input (one launch fewer
+# per step); ATPU_ADVANCE_EMBED=0: the step embeds its tokens itself
+ADVANCE_EMBED = os.environ.get("ATPU_ADVANCE_EMBED", "1") != "0"
 # host-side step timing (tools/host_prof_summ.py): a dict to accumulate into, or None
 HOST_PROF: Optional[Dict[str, float]] = None
 # device selection runs the fused LM head + top-k (ops.lm_head_topk, csrc/kernels/lm_head.hip)
@@ -417,12 +423,25 @@ def _generate_body(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
     graph, g_logits = (slot.graph, slot.out) if slot is not None else (None, None)
 
     small = dev.type == "cuda" and ops.decode_advance_ok(rows, T, seq_dev is not None)
+    # the same launch also embeds the new tokens (the step's first launch folded in)
+    emb = model.dec_embed() if small and ADVANCE_EMBED and hasattr(model, "dec_embed") else None
+    x0 = None
+    if emb is not None:
+        if slot is not None and "x0" in slot.bufs:
+            x0 = slot.bufs["x0"]
+        else:
+            x0 = torch.empty((rows, emb.table.shape[1]), dtype=torch.bfloat16, device=dev)
+            if new_slot is not None:
+                new_slot.bufs["x0"] = x0
 
     def advance() -> torch.Tensor:
         """Histories follow their parent beams (backpointers, no KV copy), new tokens in,
         position + 1, decoder step -> logits. Static buffers only (graph-capturable)."""
         if small:  # one launch for the whole state advance (1-document searches)
-            ops.decode_advance(hist, seq_dev, par_dev, tok_dev, tokens, step_dev)
+            ops.decode_advance(hist, seq_dev, par_dev, tok_dev, tokens, step_dev, embed=emb, out=x0)
+            if x0 is not None:
+                return model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist, logits=not fused,
+                                  x0=x0)
         else:
             ops.beam_reorder_hist(hist, hist_alt, par_dev, step_dev)
             hist.copy_(hist_alt)  # keep the captured buffer address
@@ -552,8 +571,11 @@ def _generate_body(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
             tp0 = time.perf_counter()
             with span("beam_select"):
                 sc_d, tk_d = select_dev(cur)
-                ops.beam_select(sc_d, tk_d, nb, V, cfg.eos_id, cur + 1 >= T, NEG, stage_dev, rec_dev)
-                rec_host[slot].copy_(rec_dev, non_blocking=True)
+                if REC_ZERO_COPY:  # the kernel writes the pinned record itself
+                    ops.beam_select(sc_d, tk_d, nb, V, cfg.eos_id, cur + 1 >= T, NEG, stage_dev, rec_host[slot])
+                else:
+                    ops.beam_select(sc_d, tk_d, nb, V, cfg.eos_id, cur + 1 >= T, NEG, stage_dev, rec_dev)
+                    rec_host[slot].copy_(rec_dev, non_blocking=True)
                 rec_ev[slot].record()
             if cur + 1 < T:
                 logits = launch_next()

@@ -816,6 +816,45 @@ def test_beam_select_kernel(gpu, B, nb, K2):
         rec_c = torch.zeros((B, 3 * K2 + nb), dtype=torch.int32)
         ops.beam_select(sc, tk, nb, V, eos, hit_all, -1e9, st_c, rec_c)
         assert torch.equal(rec_g.cpu(), rec_c) and torch.equal(st_g.cpu(), st_c)
+        # the record written by the kernel straight into pinned host memory (the search loop's form)
+        rec_h = torch.full((B, 3 * K2 + nb), -7, dtype=torch.int32).pin_memory()
+        ops.beam_select(sc.to(gpu), tk.to(gpu), nb, V, eos, hit_all, -1e9, st_g, rec_h)
+        ev = torch.cuda.Event()
+        ev.record()
+        ev.synchronize()
+        assert torch.equal(rec_h, rec_c)
+
+
+@pytest.mark.parametrize("d,ln,rows", [(768, False, 4), (1024, True, 4), (1024, True, 20), (512, False, 9)])
+def test_decode_advance_embeds_the_new_tokens(gpu, d, ln, rows):
+    # the state advance's embedding == the stand-alone embed op at the advanced step, bit for bit
+    T, V, P = 40, 3000, 140
+    g = torch.Generator().manual_seed(d + rows)
+    table = (torch.randn(V, d, generator=g) * 0.1).to(gpu, torch.bfloat16)
+    pos = (torch.randn(P, d, generator=g) * 0.1).to(gpu, torch.bfloat16) if ln else None
+    gam = (1 + 0.1 * torch.randn(d, generator=g)).to(gpu) if ln else None
+    bet = (0.1 * torch.randn(d, generator=g)).to(gpu) if ln else None
+    emb = ops.DecEmbed(table, pos, 2, gam, bet, 1e-5)
+    hist = torch.randint(0, rows, (rows, T), generator=g, dtype=torch.int32).to(gpu)
+    par = torch.randint(0, rows, (rows,), generator=g, dtype=torch.int32).to(gpu)
+    tok = torch.randint(0, V, (rows,), generator=g, dtype=torch.int32).to(gpu)
+    tok[0] = V + 3  # clamped
+    tokens = torch.zeros(rows, dtype=torch.int32, device=gpu)
+    step = torch.tensor([7], dtype=torch.int32, device=gpu)
+    h2, t2, s2 = hist.clone(), tokens.clone(), step.clone()
+    out = torch.empty((rows, d), dtype=torch.bfloat16, device=gpu)
+    ops.decode_advance(hist, None, par, tok, tokens, step, embed=emb, out=out)
+    ops.decode_advance(h2, None, par, tok, t2, s2)
+    assert torch.equal(hist, h2) and torch.equal(tokens, t2) and int(step) == 8 == int(s2)
+    assert torch.equal(out, emb.apply(tokens, step))
+
+
+def test_beam_select_host_record_must_be_pinned(gpu):
+    sc = torch.zeros((4, 8), device=gpu)
+    tk = torch.zeros((4, 8), dtype=torch.int32, device=gpu)
+    st = torch.zeros(12, dtype=torch.int32, device=gpu)
+    with pytest.raises(ValueError, match="pinned"):
+        ops.beam_select(sc, tk, 4, 100, 1, False, -1e9, st, torch.zeros((1, 28), dtype=torch.int32))
 
 
 @pytest.mark.parametrize("family", ["t5-tiny", "bart-tiny"])
