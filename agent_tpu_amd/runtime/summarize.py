@@ -801,11 +801,12 @@ class SummarizeEngine:
         """Beam search over a tokenized batch. On a GPU with device selection the batch is
         split into ``ATPU_SUMM_STREAMS`` (default 3) contiguous parts searched concurrently
         on their own streams (:func:`generate_concurrent`), each part >= ``ATPU_SUMM_PART_MIN``
-        (default 300). Two parts ran bimodally (T5, 1024 docs: 708 / 989 / 987 and 575 / 645 docs/s in
+        (default 128). Two parts ran bimodally (T5, 1024 docs: 708 / 989 / 987 and 575 / 645 docs/s in
         separate processes), three held 980-990 (tools/gpu_summ_streams.sh).
-        One host thread runs every part's bookkeeping, so the
-        split only pays once a part's GPU step outlasts the other parts' host work
-        (T5-base, MI355X: 1024 docs 819 -> 845 docs/s; 256 docs as 2x128: 668 -> 654)."""
+        One host thread runs every part's bookkeeping, so the split pays once a part's GPU step
+        outlasts the other parts' host work: at the reference's 1024-token sources 256 docs as
+        2 x 128 beat one search (T5-base 568 -> 576-583, BART-large-CNN 411 -> 423-428 docs/s;
+        3 x 85 no better, docs/PERF_NOTES.md "Summarize: two searches at 256 documents")."""
         B = int(ids.shape[0])
         cap = self.max_batch_docs
         if cap and B > cap:  # HBM-sized device batches, searched one after another
@@ -817,7 +818,7 @@ class SummarizeEngine:
             return GenResult([s for o in outs for s in o.sequences], [s for o in outs for s in o.scores],
                              max(o.steps for o in outs), timing)
         n = int(os.getenv("ATPU_SUMM_STREAMS", "3"))
-        n = max(1, min(n, B // max(1, int(os.getenv("ATPU_SUMM_PART_MIN", "300")))))
+        n = max(1, min(n, B // max(1, int(os.getenv("ATPU_SUMM_PART_MIN", "128")))))
         if n < 2 or self.device.type != "cuda" or not gen.device_select:
             return generate(self.model, ids, lens, gen)
         cuts = [B * i // n for i in range(n + 1)]
