@@ -2154,9 +2154,11 @@ bool big_fills(int M, int N) { return 2 * ((M + 255) / 256) * (N / 256) > num_cu
 
 int gemm_splitk_splits(int M, int N, int K) {
   // Skinny problems (decode: M = beams x docs) leave most of the 256 CUs idle.
-  // dec kernel: split K only when even 64x64 tiles give < 128 blocks AND the
+  // dec kernel: split K only when even 64x64 tiles give < 64 blocks AND the
   // K loop is long (>= 32 K-tiles): the reduce launch costs ~4 us, which a
-  // 12-16 K-tile loop does not win back (measured, tools/bench_decode_gemm.py).
+  // 12-16 K-tile loop does not win back (measured, tools/bench_decode_gemm.py);
+  // at 96-192 blocks (512-1024 rows) unsplit measured faster too (round 5:
+  // tools/bench_dec_splitk.py at 1024 rows, T5 256-doc summarize at 2 x 512 rows).
   // 128x128 kernel: split so the grid reaches ~2 blocks per CU, >= 2 K-tiles per split.
   static const int forced = [] {
     const char* f = std::getenv("ATPU_GEMM_SPLITK");
@@ -2166,7 +2168,7 @@ int gemm_splitk_splits(int M, int N, int K) {
   int want;
   if (gemm_dec_mode(-1) == 1 && skinny(M, N)) {
     const int tiles = ((M + 63) / 64) * ((N + 63) / 64);
-    want = forced >= 0 ? forced : (tiles >= 128 || nk < 32 ? 1 : (256 + tiles - 1) / tiles);
+    want = forced >= 0 ? forced : (tiles >= 64 || nk < 32 ? 1 : (256 + tiles - 1) / tiles);
     want = std::max(1, std::min({want, nk / 8, 16}));
   } else {
     const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
