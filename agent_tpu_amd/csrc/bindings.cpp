@@ -133,24 +133,6 @@ PYBIND11_MODULE(_atpu, m) {
       py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("in_fin"), py::arg("colsum"),
       py::arg("lens"), py::arg("scale"), py::arg("stream"));
   m.def(
-      "qkv_attention_ws",
-      [](uintptr_t A, int lda, uintptr_t Bt, int ldb, uintptr_t C, int ldc, uintptr_t bias, int M, int N, int K,
-         int epi, uintptr_t in_fin, uintptr_t colsum, uintptr_t lens, float scale, int mode, uintptr_t stream) {
-        GemmArgs g;
-        g.A = P<const bf16>(A); g.lda = lda; g.Bt = P<const bf16>(Bt); g.ldb = ldb; g.C = P<bf16>(C); g.ldc = ldc;
-        g.bias = P<const float>(bias); g.M = M; g.N = N; g.K = K; g.epi = epi;
-        g.in_fin = P<const float>(in_fin); g.colsum = P<const float>(colsum);
-        qkv_attention_ws(g, mode, P<const int32_t>(lens), scale, S(stream));
-      },
-      "wave-specialised QKV + attention (128 x 192 tiles); mode 0 stores Q|K|V, 1 timing only, 2 attention",
-      py::arg("A"), py::arg("lda"), py::arg("Bt"), py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("bias"),
-      py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("in_fin"), py::arg("colsum"),
-      py::arg("lens"), py::arg("scale"), py::arg("mode"), py::arg("stream"));
-  m.def("ws_stamps", &ws_stamps, "cycle stamps of the last ws launch (diagnostic build only)", py::arg("nblocks"));
-  m.def("ws_variant", &ws_variant, "experiment knob of the wave-specialised QKV kernel; -1 reads", py::arg("set"));
-  m.def("qkv_attention_ws_ok", &qkv_attention_ws_ok, "shapes the wave-specialised QKV + attention kernel takes",
-        py::arg("M"), py::arg("N"), py::arg("K"));
-  m.def(
       "ln_stats_finalize",
       [](uintptr_t part, int slots, int M, int K, float eps, uintptr_t fin, uintptr_t stream) {
         ln_stats_finalize(P<const float>(part), slots, M, K, eps, P<float>(fin), S(stream));
@@ -177,33 +159,14 @@ PYBIND11_MODULE(_atpu, m) {
       },
       py::arg("dst"), py::arg("n"), py::arg("f32"), py::arg("seed"), py::arg("sid"), py::arg("scale0"), py::arg("n0"),
       py::arg("scale1"), py::arg("threads") = 8, "CPU twin of rand_fill (bit-identical values)");
-  m.def(
-      "t5_ffn_fused",
-      [](uintptr_t x, uintptr_t wi, uintptr_t wo, uintptr_t y, int M, int d, int f, float eps, uintptr_t h_ws,
-         uintptr_t sync, uintptr_t stream) {
-        t5_ffn_fused(P<const bf16>(x), P<const bf16>(wi), P<const bf16>(wo), P<bf16>(y), M, d, f, eps, P<bf16>(h_ws),
-                     P<unsigned>(sync), S(stream));
-      },
-      py::arg("x"), py::arg("wi"), py::arg("wo"), py::arg("y"), py::arg("M"), py::arg("d"), py::arg("f"),
-      py::arg("eps"), py::arg("h_ws"), py::arg("sync"), py::arg("stream"),
-      "persistent-launch prototype: the T5-base decode FFN block (<= 4 rows) in one launch");
-  m.def("t5_ffn_fused_ws_bytes", &t5_ffn_fused_ws_bytes);
   m.def("gemv_selected", &gemv_selected, py::arg("M"), py::arg("N"), py::arg("epi"),
         "true when gemm_bf16 runs this [M, N] problem / epilogue on the <= 4-row GEMV");
   m.def("gemm_force_tile", &gemm_force_tile, py::arg("set") = -1, "GEMM kernel family override: 0 auto, 64, 128, 256");
   m.def("gemm_dec_mode", &gemm_dec_mode, py::arg("set") = -1,
         "skinny-M GEMM path: 1 = 64x64 multi-stage dec kernel, 0 = 128x128 split-K; returns the current");
-#ifdef ATPU_DEV_BUILD
-  m.attr("DEV_BUILD") = true;
-#else
-  m.attr("DEV_BUILD") = false;
-#endif
   m.def("gemm_256_variant", &gemm_256_variant, py::arg("set") = -1,
-        "256x256 GEMM schedule: 0 = 256b, 1 = 256p ping-pong, 2 = 256s persistent, 3 = 256l full-line "
-        "epilogue, 4 = 256n full-line + nt stores (default); set >= 0 switches, returns the current");
-  m.def("gemm_ablate", &gemm_ablate, py::arg("set") = -1,
-        "timing-only ablations of the persistent 256x256 GEMM (results WRONG): 4 no epilogue, 5 no stores, "
-        "6 no VALU, 7 LN-folding structure with the plain epilogue; 0 off; returns the current");
+        "256x256 GEMM schedule: 1 = 256p ping-pong, 3 = 256l persistent full-line epilogue, "
+        "4 = 256n full-line + nt stores (default); set >= 0 switches, returns the current");
   m.def("cu_budget", &cu_budget, py::arg("set") = -1,
         "get/set the CU count persistent grids are sized for (0 = the device's; set it to the CU share of "
         "CU-masked streams)");
@@ -222,16 +185,13 @@ PYBIND11_MODULE(_atpu, m) {
   m.def("decode_attention", [](uintptr_t q, int ldq, uintptr_t k, uintptr_t v, int ldkv, int seq_stride, int group,
                                uintptr_t lens, uintptr_t step_dev, uintptr_t hist, int hist_stride, uintptr_t bias,
                                int bias_stride, uintptr_t out, int ldo, int rows, int H, float scale, uintptr_t stream,
-                               uintptr_t ws, uintptr_t pf_w, int pf_ld, int pf_k, int pf_n, int pf_rpb) {
-    const L2Pf pf{P<const bf16>(pf_w), pf_ld, pf_k, pf_n, pf_rpb > 0 ? pf_rpb : 16};
+                               uintptr_t ws) {
     decode_attention(P<const bf16>(q), ldq, P<const bf16>(k), P<const bf16>(v), ldkv, seq_stride, group,
                      P<const int32_t>(lens), P<const int32_t>(step_dev), P<const int32_t>(hist), hist_stride,
-                     P<const float>(bias), bias_stride, P<bf16>(out), ldo, rows, H, scale, S(stream), P<float>(ws),
-                     pf_w ? &pf : nullptr);
+                     P<const float>(bias), bias_stride, P<bf16>(out), ldo, rows, H, scale, S(stream), P<float>(ws));
   }, py::arg("q"), py::arg("ldq"), py::arg("k"), py::arg("v"), py::arg("ldkv"), py::arg("seq_stride"), py::arg("group"),
      py::arg("lens"), py::arg("step_dev"), py::arg("hist"), py::arg("hist_stride"), py::arg("bias"), py::arg("bias_stride"),
-     py::arg("out"), py::arg("ldo"), py::arg("rows"), py::arg("H"), py::arg("scale"), py::arg("stream"), py::arg("ws") = 0,
-     py::arg("pf_w") = 0, py::arg("pf_ld") = 0, py::arg("pf_k") = 0, py::arg("pf_n") = 0, py::arg("pf_rpb") = 16);
+     py::arg("out"), py::arg("ldo"), py::arg("rows"), py::arg("H"), py::arg("scale"), py::arg("stream"), py::arg("ws") = 0);
   m.def("decode_attention_ws_floats", [](int rows, int group, int H, int seq_stride, bool cross) {
     return decode_attention_ws_floats(rows, group, H, seq_stride, cross);
   });
@@ -301,7 +261,6 @@ PYBIND11_MODULE(_atpu, m) {
   m.def("lm_head_ws_bytes", &lm_head_ws_bytes);
   m.def("lm_head_stages", &lm_head_stages, py::arg("set") = -1);
   m.def("decode_self_few", &decode_self_few, py::arg("set") = -1);
-  m.def("decode_xattn_prefetch", &decode_xattn_prefetch, py::arg("set") = -1);
   m.def(
       "lm_head_topk",
       [](uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t bias, float rms_eps, int M, int V, int K, int topk,

@@ -6,7 +6,7 @@ Every ``kernels/*.hip``, ``runtime/*.cpp`` and ``comm/*.cpp`` translation unit p
 rebuilt when its source or any header is newer). No hipify, no torch headers:
 kernels take raw device pointers and a hipStream_t from torch.
 
-Usage: ``python -m agent_tpu_amd.csrc.build [--force] [--debug] [--asan-host] [--dev]``
+Usage: ``python -m agent_tpu_amd.csrc.build [--force] [--debug] [--asan-host]``
 """
 from __future__ import annotations
 
@@ -74,24 +74,16 @@ def _compile(src: Path, flags: List[str], force: bool) -> Path:
 
 
 def build(force: bool = False, debug: bool = False, asan_host: bool = False, jobs: int = 0, verbose: bool = False,
-          dev: bool = False, defines: Sequence[str] = (), out: Optional[Path] = None) -> Path:
-    """``dev`` (or ATPU_DEV_BUILD=1) compiles in the timing-only GEMM ablations and the
-    retired 256b / 256s schedules (tools/gemm_ablate.py, tools/bench_gelu.py,
-    tools/bench_fold.py); a release build has none of them. The objects of the two
-    flavours live in separate directories.
-
-    ``defines`` + ``out``: an A/B variant of the extension (e.g. ``ATPU_GEMM_SYNC_EPI=1``)
+          defines: Sequence[str] = (), out: Optional[Path] = None) -> Path:
+    """``defines`` + ``out``: an A/B variant of the extension (e.g. ``ATPU_GEMM_SYNC_EPI=1``)
     linked to ``out`` (load it with ``ATPU_NATIVE_PATH``), objects in their own directory."""
-    dev = dev or os.environ.get("ATPU_DEV_BUILD", "0") == "1"
     global BUILD
     tag = ("_" + "_".join(d.replace("=", "") for d in defines)) if defines else ""
-    BUILD = REPO / "build" / (("obj_dev" if dev else "obj") + tag)
+    BUILD = REPO / "build" / ("obj" + tag)
     BUILD.mkdir(parents=True, exist_ok=True)
     flags = [f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result",
              "-Wno-unused-function", "-fvisibility=hidden"]
     flags += ["-O0", "-g"] if debug else ["-O3", "-DNDEBUG"]
-    if dev:
-        flags += ["-DATPU_DEV_BUILD"]
     flags += [f"-D{d}" for d in defines]
     if asan_host:
         # host-only sanitizer: GPU ASan/xnack+ is not available on this pool
@@ -104,7 +96,7 @@ def build(force: bool = False, debug: bool = False, asan_host: bool = False, job
     out = Path(out) if out is not None else ext_path()
     newest = max(o.stat().st_mtime for o in objs)
     stamp = REPO / "build" / ("linked_flavour" + tag)
-    flavour = ("dev" if dev else "release") + ("-debug" if debug else "") + ("-asan" if asan_host else "") + tag + str(out)
+    flavour = "release" + ("-debug" if debug else "") + ("-asan" if asan_host else "") + tag + str(out)
     same = stamp.exists() and stamp.read_text() == flavour
     if force or not same or not out.exists() or out.stat().st_mtime < newest:
         # librccl.so.1: at run time the copy torch already loaded (same SONAME) serves it
@@ -127,14 +119,13 @@ def main(argv=None) -> int:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--asan-host", action="store_true")
-    ap.add_argument("--dev", action="store_true", help="compile in timing-only ablations / retired schedules")
     ap.add_argument("-j", "--jobs", type=int, default=0)
     ap.add_argument("-D", "--define", action="append", default=[], help="A/B variant: extra -D (needs --out)")
     ap.add_argument("--out", default=None, help="A/B variant: link the extension here instead of in-tree")
     a = ap.parse_args(argv)
     if a.define and not a.out:
         ap.error("--define builds an A/B variant: give --out")
-    build(force=a.force, debug=a.debug, asan_host=a.asan_host, jobs=a.jobs, verbose=True, dev=a.dev,
+    build(force=a.force, debug=a.debug, asan_host=a.asan_host, jobs=a.jobs, verbose=True,
           defines=a.define, out=a.out)
     return 0
 

@@ -18,14 +18,6 @@ typedef __bf16 bf16;
 void rand_fill(void* dst, int64_t n, bool f32, uint64_t seed, uint64_t sid, float scale0, int64_t n0, float scale1,
                hipStream_t stream);
 
-// ---------------------------------------------------------------- persistent decode FFN (prototype)
-// y = x + relu(rsqrt(mean(x^2) + eps) * x . wi^T) . wo^T for <= 4 rows of the T5-base FFN (d 768,
-// d_ff 3072) in ONE launch with one in-launch grid barrier (kernels/decode_ffn.hip). h_ws: bf16
-// [4, 3072]; sync: 3 uint32 words zeroed once at allocation, one set per concurrent stream.
-size_t t5_ffn_fused_ws_bytes();
-void t5_ffn_fused(const bf16* x, const bf16* wi, const bf16* wo, bf16* y, int M, int d, int f, float eps, bf16* h_ws,
-                  unsigned* sync, hipStream_t stream);
-
 // ---------------------------------------------------------------- GEMM (K3/K5/K6)
 enum GemmEpilogue : int {
   kEpiBias = 1,
@@ -103,7 +95,6 @@ int gemm_dec_mode(int set);
 int gemm_force_tile(int set);
 // 256x256 schedule selector (benchmarks): set >= 0 switches; returns the current
 int gemm_256_variant(int set);
-int gemm_ablate(int set);  // timing-only ablations of the persistent 256x256 kernel (results wrong); -1 reads
 // persistent 256 x 192 GEMM (qkv_attn.hip; one BERT head's Q|K|V per tile): epi = Bias or
 // Bias|InNorm; mode 0 stores C, 1 = timing only (no epilogue, C untouched)
 void gemm256h(const GemmArgs& g, int mode, hipStream_t stream);
@@ -111,14 +102,6 @@ void gemm256h(const GemmArgs& g, int mode, hipStream_t stream);
 // Bt = the QKV weight with rows in [head][Q 64 | K 64 | V 64] order (bias / colsum likewise),
 // g.C = the context [M, N / 3] (row stride g.ldc), lens[M / 128] the sequence lengths
 void qkv_attention(const GemmArgs& g, const int32_t* lens, float scale, hipStream_t stream);
-// wave-specialised form (qkv_attn_ws.hip): 128 x 192 tiles (one sequence x one head), 4 MFMA
-// waves on the main loop while 4 waves stage operands and run the previous tile's attention.
-// mode 0 stores Q|K|V ([M, N], head order) to g.C, 1 timing only, 2 attention (as qkv_attention)
-bool qkv_attention_ws_ok(int M, int N, int K);
-int ws_variant(int set);  // experiment knob of the ws kernel (benchmarks); -1 reads
-// per-workgroup cycle stamps of the last ws launch (diagnostic build -DATPU_WS_STAMPS; else empty)
-std::vector<unsigned long long> ws_stamps(int nblocks);
-void qkv_attention_ws(const GemmArgs& g, int mode, const int32_t* lens, float scale, hipStream_t stream);
 int attention_persist_mode(int set);  // packed BERT attention: 1 persistent (default), 0 per-item
 int num_cus();                        // CUs a persistent grid is sized for (device count, or the budget below)
 int cu_budget(int set);               // >0: size persistent grids for this many CUs (CU-masked streams)
@@ -132,17 +115,15 @@ int64_t make_cu_mask_stream(int first_bit, int nbits);  // hipStream_t over CU-m
 // of row r lives in physical row hist[r * hist_stride + j] when hist is given
 // (beam backpointers), else in row r. bias_dist (fp32 [H, bias_stride]) adds
 // bias_dist[h][len-1-j] (T5 decoder relative position bias).
-struct L2Pf;  // l2_prefetch.h: a later kernel's weight rows to pull into L2 (split cross attention only)
 void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int ldkv, int seq_stride, int group,
                       const int32_t* lens, const int32_t* step_dev, const int32_t* hist, int hist_stride,
                       const float* bias_dist, int bias_stride, bf16* out, int ldo, int rows, int H, float scale,
-                      hipStream_t stream, float* ws = nullptr, const L2Pf* pf = nullptr);
+                      hipStream_t stream, float* ws = nullptr);
 // Cross attention (lens) over a grid of few items splits the keys into 64-key chunks
 // (flash decoding) when given a workspace of this many floats (0: no split for the shape).
 int decode_attention_splits(int rows, int group, int H, int seq_stride, bool cross);
 size_t decode_attention_ws_floats(int rows, int group, int H, int seq_stride, bool cross);
 int decode_self_few(int set);  // 1: few-row self attention one wave per (row, head), T <= 192 (default); -1 reads
-int decode_xattn_prefetch(int set);  // 1: few-item attention kernels prefetch a later GEMV weight (default 0); -1 reads
 // one-workgroup state advance of a small beam search (rows x stride x 4 B x (seq ? 2 : 1) <= 64 KiB):
 // hist / seq reordered in place by par (as beam_reorder_hist, seq with last = tok, off 1),
 // tokens = tok, *step_dev += 1

@@ -333,23 +333,13 @@ __global__ __launch_bounds__(NW * 64) void decode_self_attention_kernel(
 constexpr int kSplitKeys = 64;
 constexpr int kSplitRec = 2 + kD;  // floats per (row, head, chunk): max, sum, o[64]
 
-// PF: a second wave pulls a later decoder kernel's weight rows into L2 (l2_prefetch.h; BART's
-// fc1, whose predecessor, a RowStats GEMV, cannot prefetch), taking the workgroup's two barriers
-template <int GM, bool PF>
-__global__ __launch_bounds__(64 * (1 + PF)) void decode_cross_split_kernel(
+template <int GM>
+__global__ __launch_bounds__(64) void decode_cross_split_kernel(
     const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k, const bf16* __restrict__ v, int ldkv,
     int seq_stride, int group, int nrows, const int32_t* __restrict__ lens, const float* __restrict__ bias_dist,
-    int bias_stride, float* __restrict__ ws, int H, float scale, L2Pf pf) {
+    int bias_stride, float* __restrict__ ws, int H, float scale) {
   typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
   __shared__ float pl[GM][kSplitKeys];
-  if constexpr (PF) {
-    __shared__ __attribute__((aligned(16))) char pf_scratch[256];
-    if (threadIdx.x >= 64) {
-      const int bid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-      l2_prefetch_rows<2>(pf, threadIdx.x & 63, pf_scratch, bid, gridDim.x * gridDim.y * gridDim.z);
-      return;
-    }
-  }
   const int seq = blockIdx.x, h = blockIdx.y, c = blockIdx.z, NS = gridDim.z;
   const int lane = threadIdx.x;
   const int G = min(group, nrows - seq * group);
@@ -361,10 +351,6 @@ __global__ __launch_bounds__(64 * (1 + PF)) void decode_cross_split_kernel(
     for (int i = lane; i < G * kSplitRec; i += 64) {
       const int g = i / kSplitRec, e = i % kSplitRec;
       rec(g)[e] = e == 0 ? -FLT_MAX : 0.f;
-    }
-    if constexpr (PF) {  // the prefetch wave's two barriers still need this wave's
-      __syncthreads();
-      __syncthreads();
     }
     return;
   }
@@ -482,25 +468,15 @@ __global__ __launch_bounds__(64) void decode_attn_combine_kernel(const float* __
 // issued before the first use. decode_self_attention_kernel walks the same keys in up to
 // 3 + 5 dependent load rounds per head (6.3 us per call at 4 rows x 12 heads).
 // ----------------------------------------------------------------------------
-// PF: a second wave pulls a later decoder kernel's weight rows into L2 (l2_prefetch.h; BART's
-// cross-attention query projection, whose predecessor, a RowStats GEMV, cannot prefetch)
-template <int KC, bool PF>
-__global__ __launch_bounds__(64 * (1 + PF)) void decode_self_few_kernel(
+template <int KC>
+__global__ __launch_bounds__(64) void decode_self_few_kernel(
     const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k, const bf16* __restrict__ v, int ldkv,
     int seq_stride, const int32_t* __restrict__ step_dev, const int32_t* __restrict__ hist, int hist_stride,
-    const float* __restrict__ bias_dist, int bias_stride, bf16* __restrict__ out, int ldo, float scale, L2Pf pf) {
+    const float* __restrict__ bias_dist, int bias_stride, bf16* __restrict__ out, int ldo, float scale) {
   typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
   constexpr int NK = KC * 64, NV = NK / 8;
   __shared__ int prow[NK];
   __shared__ float pw[NK];
-  if constexpr (PF) {
-    __shared__ __attribute__((aligned(16))) char pf_scratch[256];
-    if (threadIdx.x >= 64) {
-      l2_prefetch_rows<1>(pf, threadIdx.x & 63, pf_scratch, blockIdx.x + gridDim.x * blockIdx.y,
-                          gridDim.x * gridDim.y);
-      return;
-    }
-  }
   const int seq = xcd_remap(blockIdx.x, gridDim.x), h = blockIdx.y, lane = threadIdx.x;
   const int ksub = lane >> 3, dc = (lane & 7) * 8;
   // round 1
@@ -1036,19 +1012,6 @@ __global__ __launch_bounds__(kSelMax) void beam_select_kernel(const float* __res
 
 }  // namespace
 
-// L2 prefetch of a later GEMV's weight from the few-item attention kernels (BART's fc1 and cross
-// query weights, whose predecessors are RowStats GEMVs). Measured within noise (1-doc BART
-// 10.49 vs 10.47 docs/s, profiles/xattn_prefetch_ab_r04.txt): off unless ATPU_XATTN_PREFETCH=1
-int decode_xattn_prefetch(int set) {
-  static int on = [] {
-    const char* f = std::getenv("ATPU_XATTN_PREFETCH");
-    return (f && f[0] == '1') ? 1 : 0;
-  }();
-  if (set == 0 || set == 1) on = set;
-  return on;
-}
-static bool xattn_prefetch() { return decode_xattn_prefetch(-1) != 0; }
-
 int decode_self_few(int set) {
   // few-row self attention: one wave per (row, head), all loads in two rounds
   // (decode_self_few_kernel); ATPU_DEC_SELF_FEW=0 or decode_self_few(0) turns it off
@@ -1077,7 +1040,7 @@ size_t decode_attention_ws_floats(int rows, int group, int H, int seq_stride, bo
 void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int ldkv, int seq_stride, int group,
                       const int32_t* lens, const int32_t* step_dev, const int32_t* hist, int hist_stride,
                       const float* bias_dist, int bias_stride, bf16* out, int ldo, int rows, int H, float scale,
-                      hipStream_t stream, float* ws, const L2Pf* pf) {
+                      hipStream_t stream, float* ws) {
   ATPU_CHECK(rows > 0 && H > 0 && group >= 1, "decode_attention: bad shape");
   ATPU_CHECK(lens || step_dev, "decode_attention: need lens or a device step");
   ATPU_CHECK(!hist || (step_dev && group == 1), "decode_attention: hist is for self attention (group 1)");
@@ -1094,24 +1057,16 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
     ATPU_CHECK(ldo % 8 == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 && (reinterpret_cast<uintptr_t>(q) & 15) == 0,
                "decode_attention: q / out need 16-B rows");
     if (rows * H <= num_cus() && seq_stride <= 192 && decode_self_few(-1)) {
-      const bool pfon = xattn_prefetch() && pf && pf->w && pf->n > 0 && pf->k > 0 && (rows * H) % 8 == 0;
-      const L2Pf pfa = pfon ? *pf : L2Pf{nullptr, 0, 0, 0, 16};
-#define ATPU_SF(KC, P)                                                                                              \
-  hipLaunchKernelGGL((decode_self_few_kernel<KC, P>), dim3(rows, H), dim3(64 * (1 + P)), 0, stream, q, ldq, k, v,      \
-                     ldkv, seq_stride, step_dev, hist, hist_stride, bias_dist, bias_stride, out, ldo, scale, pfa)
-#define ATPU_SFP(KC)   \
-  if (pfon)            \
-    ATPU_SF(KC, true); \
-  else                 \
-    ATPU_SF(KC, false);
+#define ATPU_SF(KC)                                                                                                \
+  hipLaunchKernelGGL((decode_self_few_kernel<KC>), dim3(rows, H), dim3(64), 0, stream, q, ldq, k, v, ldkv, seq_stride, \
+                     step_dev, hist, hist_stride, bias_dist, bias_stride, out, ldo, scale)
       if (seq_stride <= 64) {
-        ATPU_SFP(1)
+        ATPU_SF(1);
       } else if (seq_stride <= 128) {
-        ATPU_SFP(2)
+        ATPU_SF(2);
       } else {
-        ATPU_SFP(3)
+        ATPU_SF(3);
       }
-#undef ATPU_SFP
 #undef ATPU_SF
       ATPU_HIP_CHECK(hipGetLastError());
       return;
@@ -1132,26 +1087,16 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
     static_assert(kMaxSplits * kSplitKeys >= kMaxKeys, "combine kernel chunk count");
     ATPU_CHECK(ldq % 8 == 0 && (reinterpret_cast<uintptr_t>(q) & 15) == 0, "decode_attention: q needs 16-B rows");
     ATPU_CHECK((reinterpret_cast<uintptr_t>(ws) & 15) == 0, "decode_attention: ws must be 16-byte aligned");
-    // with a prefetch target and a grid of whole XCD rounds (the prefetched lines must land in
-    // the L2 of the XCD whose workgroup reads them)
-    const bool pfon = xattn_prefetch() && pf && pf->w && pf->n > 0 && pf->k > 0 && (nseq * H * ns) % 8 == 0;
-    const L2Pf pfa = pfon ? *pf : L2Pf{nullptr, 0, 0, 0, 16};
-#define ATPU_DS(GM, P)                                                                                          \
-  hipLaunchKernelGGL((decode_cross_split_kernel<GM, P>), dim3(nseq, H, ns), dim3(64 * (1 + P)), 0, stream, q, ldq, \
-                     k, v, ldkv, seq_stride, group, rows, lens, bias_dist, bias_stride, ws, H, scale, pfa)
-#define ATPU_DSP(GM)   \
-  if (pfon)            \
-    ATPU_DS(GM, true); \
-  else                 \
-    ATPU_DS(GM, false);
+#define ATPU_DS(GM)                                                                                               \
+  hipLaunchKernelGGL((decode_cross_split_kernel<GM>), dim3(nseq, H, ns), dim3(64), 0, stream, q, ldq, k, v, ldkv, \
+                     seq_stride, group, rows, lens, bias_dist, bias_stride, ws, H, scale)
     if (group == 1) {
-      ATPU_DSP(1)
+      ATPU_DS(1);
     } else if (group <= 4) {
-      ATPU_DSP(4)
+      ATPU_DS(4);
     } else {
-      ATPU_DSP(8)
+      ATPU_DS(8);
     }
-#undef ATPU_DSP
 #undef ATPU_DS
     ATPU_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(decode_attn_combine_kernel, dim3(rows, H), dim3(64), 0, stream, ws, ns, H, out, ldo);

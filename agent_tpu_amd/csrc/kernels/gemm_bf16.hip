@@ -353,8 +353,8 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
 }
 
 // ============================================================================
-// 256x256 tile, 8 waves, FULL-LINE staging (kernel "256b"; retired: dev builds only,
-// python -m agent_tpu_amd.csrc.build --dev). Its staging constants (g2) are shared.
+// 256x256 tile, 8 waves, FULL-LINE staging (the retired "256b" schedule, git history;
+// docs/PERF_NOTES.md). Its staging constants (g2) are shared by the kernels below.
 //
 // The ablation of the ring kernel showed the LDS-DMA instructions themselves
 // costing ~40 % of the MFMA rate; its k-half chunks had 64-byte rows, so every
@@ -376,165 +376,6 @@ constexpr int kTile = 4 * kChunk;
 __device__ __forceinline__ int sw(int r, int c) { return c ^ ((r >> 1) & 7); }
 }  // namespace g2
 
-#ifdef ATPU_DEV_BUILD
-
-// DBG: timing-only ablation builds (results are WRONG): 1 = no vmcnt/barrier
-// waits, 2 = no global->LDS DMA. See docs/PERF_NOTES.md.
-template <int EPI, int DBG = 0>
-__global__ __launch_bounds__(512, 2) void gemm256b_kernel(
-    const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C, int ldc,
-    const float* __restrict__ bias, const bf16* __restrict__ R, int ldr, int M, int N, int K) {
-  using namespace g2;
-  __shared__ __attribute__((aligned(16))) char lds[2 * kTile];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int ntn = N / 256, ntm = (M + 255) / 256;
-  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
-  const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 256;
-
-  // staging: chunk q (0..3) = (A|B) x (row half); this wave issues
-  // instructions i = wave, wave + 8 of each chunk (8 rows x 128 B each)
-  const int srow = lane >> 3, spos = lane & 7;
-  const int lr0 = wave * 8 + srow, lr1 = (wave + 8) * 8 + srow;  // local rows 0..127
-  const bf16* src[4][2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    src[h][0] = A + (size_t)min(m0 + h * 128 + lr0, M - 1) * lda + sw(lr0, spos) * 8;
-    src[h][1] = A + (size_t)min(m0 + h * 128 + lr1, M - 1) * lda + sw(lr1, spos) * 8;
-    src[2 + h][0] = Bt + (size_t)(n0 + h * 128 + lr0) * ldb + sw(lr0, spos) * 8;
-    src[2 + h][1] = Bt + (size_t)(n0 + h * 128 + lr1) * ldb + sw(lr1, spos) * 8;
-  }
-  auto issue_tile = [&](int kt, int buf) {
-    if constexpr (DBG & 2) return;
-    char* base = lds + buf * kTile;
-    const int koff = kt * 64;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      glds16(src[q][0] + koff, base + q * kChunk + wave * 1024);
-      glds16(src[q][1] + koff, base + q * kChunk + (wave + 8) * 1024);
-    }
-  };
-
-  const int wm = wave >> 2, wn = wave & 3;
-  const int fr = lane & 15, fc = lane >> 4;
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto load_b = [&](bf16x8 (&f)[4], int buf, int ks) {
-    const char* img = lds + buf * kTile + (2 + (wn >> 1)) * kChunk;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int r = (wn & 1) * 64 + j * 16 + fr;
-      f[j] = *reinterpret_cast<const bf16x8*>(img + r * 128 + sw(r, ks * 4 + fc) * 16);
-    }
-  };
-  auto load_a = [&](bf16x8 (&f)[4], int buf, int ks, int qm) {
-    const char* img = lds + buf * kTile + wm * kChunk;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = qm * 64 + i * 16 + fr;
-      f[i] = *reinterpret_cast<const bf16x8*>(img + r * 128 + sw(r, ks * 4 + fc) * 16);
-    }
-  };
-  auto mma = [&](const bf16x8 (&bfr)[4], const bf16x8 (&afr)[4], int qm) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[qm * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], afr[i], acc[qm * 4 + i][j], 0, 0, 0);
-  };
-#define ATPU_INTERLEAVE(NREAD)                                           \
-  _Pragma("unroll") for (int q = 0; q < (NREAD); ++q) {                  \
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                   \
-    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                   \
-  }                                                                      \
-  __builtin_amdgcn_sched_group_barrier(0x008, 16 - (NREAD), 0)
-
-  const int nk = K / 64;
-  bf16x8 b0[4], b1[4], a00[4], a01[4], a10[4], a11[4];
-  issue_tile(0, 0);
-  for (int t = 0; t < nk; ++t) {
-    const int cur = t & 1;
-    if constexpr (!(DBG & 1)) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    load_b(b0, cur, 0);
-    load_a(a00, cur, 0, 0);
-    if (t + 1 < nk) issue_tile(t + 1, cur ^ 1);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(b0, a00, 0);
-    load_a(a01, cur, 0, 1);
-    ATPU_INTERLEAVE(4);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(b0, a01, 1);
-    load_b(b1, cur, 1);
-    load_a(a10, cur, 1, 0);
-    ATPU_INTERLEAVE(8);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(b1, a10, 0);
-    load_a(a11, cur, 1, 1);
-    ATPU_INTERLEAVE(4);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(b1, a11, 1);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-#undef ATPU_INTERLEAVE
-
-  f32x4 bv[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = n0 + wn * 64 + j * 16 + fc * 4;
-    if constexpr (EPI & kEpiBias) bv[j] = *reinterpret_cast<const f32x4*>(bias + n);
-    else bv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-#pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    bf16x4 res[4][4];
-    if constexpr (EPI & kEpiResidual) {
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii) {
-        const int m = min(m0 + wm * 128 + (half * 4 + ii) * 16 + fr, M - 1);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          res[ii][j] = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + n0 + wn * 64 + j * 16 + fc * 4);
-      }
-    }
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii) {
-      const int i = half * 4 + ii;
-      const int m = m0 + wm * 128 + i * 16 + fr;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wn * 64 + j * 16 + fc * 4;
-        f32x4 v = acc[i][j] + bv[j];
-        if constexpr (EPI & kEpiGelu) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = gelu_fast(v[e]);
-        }
-        if constexpr (EPI & kEpiTanh) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
-        }
-        if constexpr (EPI & kEpiRelu) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-        }
-        if constexpr (EPI & kEpiResidual) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += bf2f(res[ii][j][e]);
-        }
-        bf16x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
-        if (m < M) *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
-      }
-    }
-  }
-}
-
-#endif  // ATPU_DEV_BUILD (256b)
 
 // ============================================================================
 // 256x256 tile, 8 waves, PING-PONG schedule (kernel "256p").
@@ -820,13 +661,6 @@ __global__ __launch_bounds__(512, 1) void gemm256p_kernel(
 
 void launch_256p(const GemmArgs& g, hipStream_t s) {
   const int nb = ((g.M + 255) / 256) * (g.N / 256);
-#ifdef ATPU_DEV_BUILD
-  if (gemm_ablate(-1) == 4) {  // no epilogue (timing only, results wrong)
-    hipLaunchKernelGGL((gemm256p_kernel<kEpiBias, 1>), dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C,
-                       g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K);
-    return;
-  }
-#endif
 #define ATPU_G256P(E)                                                                                     \
   case E:                                                                                                 \
     hipLaunchKernelGGL((gemm256p_kernel<E>), dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, \
@@ -1543,23 +1377,6 @@ int64_t make_cu_mask_stream(int first_bit, int nbits) {
   return reinterpret_cast<int64_t>(s);
 }
 
-int gemm_ablate(int set) {
-#ifdef ATPU_DEV_BUILD
-  // timing-only ablations of the persistent kernel (results WRONG): ATPU_GEMM_ABLATE=4|5|6|7,
-  // and A/B schedules 8-11. Compiled into dev builds only.
-  static int v = [] {
-    const char* f = std::getenv("ATPU_GEMM_ABLATE");
-    return f ? std::atoi(f) : 0;
-  }();
-  if (set >= 0) v = set;
-  return v;
-#else
-  // release build: no ablation exists; ATPU_GEMM_ABLATE and set() are ignored
-  (void)set;
-  return 0;
-#endif
-}
-
 namespace {
 
 template <bool NT, bool LINE = false>
@@ -1569,76 +1386,12 @@ void launch_256s(const GemmArgs& g, hipStream_t s) {
   int nb = std::min(tiles, num_cus());
   if (nb >= 8) nb &= ~7;
   const LnFold lf{g.in_fin, g.colsum, g.res_fin, g.gamma, g.part_out};
-#ifdef ATPU_DEV_BUILD
-  const int ablate = gemm_ablate(-1);
-  if (ablate == 4 || ablate == 5 || ablate == 6) {  // timing only: no epilogue / no stores / no VALU
-    auto k = ablate == 4 ? gemm256s_kernel<kEpiBias, 1> : ablate == 5 ? gemm256s_kernel<kEpiBias, 2>
-                                                                       : gemm256s_kernel<kEpiBias, 4>;
-    hipLaunchKernelGGL(k, dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M,
-                       g.N, g.K, lf);
-    return;
-  }
-#endif
 #define ATPU_G256S(E)                                                                                          \
   case E:                                                                                                      \
     hipLaunchKernelGGL((gemm256s_kernel<E, 0, NT, LINE>), dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, \
                        g.bias, g.R, g.ldr, g.M, g.N, g.K, lf);                                                 \
     break;
   if constexpr (LINE) {
-#ifdef ATPU_DEV_BUILD
-    if (ablate == 8 && (g.epi & kEpiInNorm)) {  // A/B: InNorm with the accumulators started at -mu*colsum
-      if (g.epi & kEpiGelu)
-        hipLaunchKernelGGL((gemm256s_kernel<kEpiBias | kEpiInNorm | kEpiGelu, 16, NT, LINE>), dim3(nb), dim3(512), 0, s,
-                           g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, lf);
-      else
-        hipLaunchKernelGGL((gemm256s_kernel<kEpiBias | kEpiInNorm, 16, NT, LINE>), dim3(nb), dim3(512), 0, s, g.A,
-                           g.lda, g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, lf);
-      return;
-    }
-    if (ablate >= 9 && ablate <= 11 && g.epi == (kEpiBias | kEpiInNorm | kEpiGelu)) {
-      // A/B of the GELU evaluation (gelu_poly16_v): 9 scalar, 10 packed degree 8, 11 scalar degree 8
-      auto k = ablate == 9 ? gemm256s_kernel<kEpiBias | kEpiInNorm | kEpiGelu, 32, NT, LINE>
-               : ablate == 10 ? gemm256s_kernel<kEpiBias | kEpiInNorm | kEpiGelu, 64, NT, LINE>
-                              : gemm256s_kernel<kEpiBias | kEpiInNorm | kEpiGelu, 96, NT, LINE>;
-      hipLaunchKernelGGL(k, dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M,
-                         g.N, g.K, lf);
-      return;
-    }
-    if (ablate == 12 || ablate == 13) {
-      // timing only: 12 = the LN-folding epilogues without their global stores, 13 = no epilogue
-#define ATPU_G256S_N(E)                                                                                        \
-  case E:                                                                                                      \
-    hipLaunchKernelGGL((ablate == 12 ? gemm256s_kernel<E, 256, NT, LINE> : gemm256s_kernel<E, 1, NT, LINE>),   \
-                       dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, \
-                       g.K, lf);                                                                               \
-    return;
-      switch (g.epi) {
-        ATPU_G256S_N(kEpiBias | kEpiInNorm)
-        ATPU_G256S_N(kEpiBias | kEpiInNorm | kEpiGelu)
-        ATPU_G256S_N(kEpiBias | kEpiResidual | kEpiStatsOut)
-        ATPU_G256S_N(kEpiBias | kEpiResidual | kEpiResNorm | kEpiStatsOut)
-        default:
-          break;
-      }
-#undef ATPU_G256S_N
-    }
-    if (ablate == 7) {  // timing only: LN-folding structure without its epilogue math
-#define ATPU_G256S_A(E)                                                                                        \
-  case E:                                                                                                      \
-    hipLaunchKernelGGL((gemm256s_kernel<E, 8, NT, LINE>), dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, \
-                       g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, lf);                                          \
-    return;
-      switch (g.epi) {
-        ATPU_G256S_A(kEpiBias | kEpiInNorm)
-        ATPU_G256S_A(kEpiBias | kEpiInNorm | kEpiGelu)
-        ATPU_G256S_A(kEpiBias | kEpiResidual | kEpiStatsOut)
-        ATPU_G256S_A(kEpiBias | kEpiResidual | kEpiResNorm | kEpiStatsOut)
-        default:
-          break;
-      }
-#undef ATPU_G256S_A
-    }
-#endif  // ATPU_DEV_BUILD
     switch (g.epi) {
       ATPU_G256S(kEpiBias | kEpiInNorm)
       ATPU_G256S(kEpiBias | kEpiInNorm | kEpiGelu)
@@ -1664,45 +1417,6 @@ void launch_256s(const GemmArgs& g, hipStream_t s) {
 #undef ATPU_G256S
 }
 
-#ifdef ATPU_DEV_BUILD
-void launch_256b(const GemmArgs& g, hipStream_t s) {
-  const int nb = ((g.M + 255) / 256) * (g.N / 256);
-  static const int ablate = [] {
-    const char* f = std::getenv("ATPU_GEMM_ABLATE");
-    return f ? std::atoi(f) : 0;
-  }();
-  if (ablate && g.epi == (kEpiBias | kEpiResidual)) {
-#define ATPU_ABL(D)                                                                                              \
-  case D:                                                                                                        \
-    hipLaunchKernelGGL((gemm256b_kernel<kEpiBias | kEpiResidual, D>), dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, \
-                       g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K);                                   \
-    return;
-    switch (ablate) {
-      ATPU_ABL(1) ATPU_ABL(2) ATPU_ABL(3)
-      default: break;
-    }
-#undef ATPU_ABL
-  }
-#define ATPU_G256B(E)                                                                                     \
-  case E:                                                                                                 \
-    hipLaunchKernelGGL((gemm256b_kernel<E>), dim3(nb), dim3(512), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, \
-                       g.bias, g.R, g.ldr, g.M, g.N, g.K);                                                \
-    break;
-  switch (g.epi) {
-    ATPU_G256B(0)
-    ATPU_G256B(kEpiBias)
-    ATPU_G256B(kEpiBias | kEpiGelu)
-    ATPU_G256B(kEpiBias | kEpiTanh)
-    ATPU_G256B(kEpiBias | kEpiResidual)
-    ATPU_G256B(kEpiResidual)
-    ATPU_G256B(kEpiGelu)
-    ATPU_G256B(kEpiRelu)
-    default:
-      throw std::invalid_argument("atpu: unsupported GEMM epilogue " + std::to_string(g.epi));
-  }
-#undef ATPU_G256B
-}
-#endif  // ATPU_DEV_BUILD
 
 
 
@@ -2093,29 +1807,22 @@ void launch_tile(const GemmArgs& g, hipStream_t s) {
 }  // namespace
 
 int gemm_256_variant(int set) {
-  // 256x256 schedule (ATPU_GEMM_256=b|p|s|l|n):
-  //   0 "256b" one K-tile per barrier pair   1 "256p" ping-pong, one launch per tile
-  //   2 "256s" persistent ping-pong, permlane epilogue
+  // 256x256 schedule (ATPU_GEMM_256=p|l|n):
+  //   1 "256p" ping-pong, one launch per tile
   //   3 "256l" persistent, full-line LDS-transposed epilogue
   //   4 "256n" = 256l with non-temporal stores (default; docs/PERF_NOTES.md)
-  //   0 and 2 are retired schedules, compiled into dev builds only
+  //   (0 "256b" and 2 "256s" with the permlane epilogue are retired: git history)
   static int v = [] {
     const char* f = std::getenv("ATPU_GEMM_256");
     if (!f) return 4;
     switch (f[0]) {
-#ifdef ATPU_DEV_BUILD
-      case 'b': return 0;
-      case 's': return 2;
-#endif
       case 'p': return 1;
       case 'l': return 3;
       default: return 4;
     }
   }();
   if (set >= 0) {
-#ifndef ATPU_DEV_BUILD
-    ATPU_CHECK(set == 1 || set == 3 || set == 4, "gemm_256_variant: schedules 0 (256b) and 2 (256s) need a dev build");
-#endif
+    ATPU_CHECK(set == 1 || set == 3 || set == 4, "gemm_256_variant: schedules 1 (256p), 3 (256l), 4 (256n)");
     v = set;
   }
   return v;
@@ -2678,18 +2385,10 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
   // 256s counts its epilogue's stores in the next tile's waits: whole row tiles only
   const bool persistent_ok = g.M % 256 == 0;
   if (use_big && persistent_ok && kernel256 >= 2) {
-#ifdef ATPU_DEV_BUILD
-    if (kernel256 == 2) launch_256s<false, false>(g, stream);
-    else
-#endif
     if (kernel256 == 3) launch_256s<false, true>(g, stream);
     else launch_256s<true, true>(g, stream);
   } else if (use_big && kernel256 != 0)
     launch_256p(g, stream);  // M % 256 != 0 (or the per-tile schedule forced)
-#ifdef ATPU_DEV_BUILD
-  else if (use_big)
-    launch_256b(g, stream);
-#endif
   else if ((forced == 64 || (!forced && gemm_dec_mode(-1) == 1 && skinny(g.M, g.N))))
     launch_dec(g, stream);
   else

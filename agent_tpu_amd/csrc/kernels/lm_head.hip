@@ -552,17 +552,8 @@ int lm_head_stages(int set) {
   //   1: 128x128, 4 slots (128 KiB)   2: 256x128, 2 slots (96 KiB)   3: 256x128, 3 slots (144 KiB)
   //   4: as 0 with 2x2 waves of 64 x 64 (fewer LDS fragment reads per MFMA; 64-column slabs)
   //   5: as 2 with 4x2 waves of 64 x 64
-#ifdef ATPU_DEV_BUILD
-  static int v = [] {
-    const char* f = std::getenv("ATPU_LM_CFG");
-    return (f && f[0] >= '0' && f[0] <= '5') ? f[0] - '0' : 0;
-  }();
-  if (set >= 0 && set <= 5) v = set;
-  return v;
-#else
   (void)set;
   return 0;
-#endif
 }
 
 // workspace: per-slab headers and candidates (slabs of 64 columns at the finest), the ban bitmap
@@ -624,32 +615,9 @@ void lm_head_topk(const bf16* A, int lda, const bf16* W, int ldw, const float* b
 #define ATPU_LM(R, B, X, BM, N, WN)                                                                              \
   hipLaunchKernelGGL((lm_head_topk_kernel<R, B, X, BM, N, WN>), dim3(((M + BM - 1) / BM) * ntn), dim3(BM / 32 * 64), \
                      0, stream, A, lda, W, ldw, bias, rms_eps, M, V, K, bits, ld, eos, mask_eos, hdr, cand)
-#ifdef ATPU_DEV_BUILD
-#define ATPU_LM_CFG(R, B, X)          \
-  switch (cfg) {                      \
-    case 1:                           \
-      ATPU_LM(R, B, X, 128, 4, 1);    \
-      break;                          \
-    case 2:                           \
-      ATPU_LM(R, B, X, 256, 2, 1);    \
-      break;                          \
-    case 3:                           \
-      ATPU_LM(R, B, X, 256, 3, 1);    \
-      break;                          \
-    case 4:                           \
-      ATPU_LM(R, B, X, 128, 2, 2);    \
-      break;                          \
-    case 5:                           \
-      ATPU_LM(R, B, X, 256, 2, 2);    \
-      break;                          \
-    default:                          \
-      ATPU_LM(R, B, X, 128, 2, 1);    \
-  }
-#else
   // (a 4-slot ring for the one-row-tile step measured within noise for T5 and slower for BART,
   // profiles/lm_head_small_ring_ab_r04.txt)
 #define ATPU_LM_CFG(R, B, X) ATPU_LM(R, B, X, 128, 2, 1);
-#endif
 #define ATPU_LM_BANS(R, B)        \
   if (any_bans) {                 \
     ATPU_LM_CFG(R, B, true)       \

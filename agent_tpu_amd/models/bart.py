@@ -413,10 +413,8 @@ class BartModel:
                 qkv = ops.linear(x, w, b, row_ln=rl, row_ln_out=rlo, prefetch=(p[q + "o_w"], rpb))
                 ops.kv_append(qkv, d, 2 * d, c, T, step)
                 qh = qkv[:, :d]
-            # the cross query projection's weight: prefetched by the o GEMV on the GEMV path, by
-            # the self attention (ATPU_XATTN_PREFETCH) when o is a RowStats producer
-            ctx = ops.decode_attention(qh, c[:, :d], c[:, d:], H, T, 1, step=step, scale=scale, hist=hist,
-                                       prefetch=f[q + "cq_w"])
+            # the cross query projection's weight: prefetched by the o GEMV on the GEMV path
+            ctx = ops.decode_attention(qh, c[:, :d], c[:, d:], H, T, 1, step=step, scale=scale, hist=hist)
             if i == 0:
                 x1 = ops.linear(ctx, p[q + "o_w"], p[q + "o_b"], residual=x, stats_out=so(p1), prefetch=f[q + "cq_w"])
             else:
@@ -425,8 +423,7 @@ class BartModel:
             cq = ops.linear(x1, f[q + "cq_w"], f[q + "cq_b"], row_ln=(eps, f[q + "cq_c"], inp(p1)), row_ln_out=ro(p1),
                             prefetch=(p[q + "co_w"], rpb))
             kv = ckv[:, i * 2 * d:(i + 1) * 2 * d]
-            ctx = ops.decode_attention(cq, kv[:, :d], kv[:, d:], H, S, group, lens=src_lens, scale=scale,
-                                       prefetch=f[q + "f1_w"])
+            ctx = ops.decode_attention(cq, kv[:, :d], kv[:, d:], H, S, group, lens=src_lens, scale=scale)
             x2 = ops.linear(ctx, p[q + "co_w"], f[q + "co_b"], residual=x1, res_ln=(eps, p1, p[q + "ln1_g"]),
                             stats_out=so(p2), prefetch=f[q + "f1_w"])
             h = ops.linear(x2, f[q + "f1_w"], f[q + "f1_b"], act="gelu", row_ln=(eps, f[q + "f1_c"], inp(p2)),

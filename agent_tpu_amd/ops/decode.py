@@ -30,15 +30,11 @@ HEAD_DIM = 64
 def decode_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, H: int, seq_stride: int, group: int = 1,
                      lens: Optional[torch.Tensor] = None, step: Optional[torch.Tensor] = None,
                      bias_dist: Optional[torch.Tensor] = None, scale: float = 1.0,
-                     out: Optional[torch.Tensor] = None, hist: Optional[torch.Tensor] = None,
-                     prefetch: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     out: Optional[torch.Tensor] = None, hist: Optional[torch.Tensor] = None) -> torch.Tensor:
     """q [R, >=H*64]; k/v 2-D row views with ``seq_stride`` rows per sequence.
 
     ``hist`` (int32 [R, T], self attention only): key j < t of row r lives in
     the cache of row ``hist[r, j]``.
-    ``prefetch``: the weight of a later <= 4-row decode GEMV (16 rows per workgroup); the few-item
-    split cross attention and few-row self attention pull it into L2 with a second wave per
-    workgroup (a hint only; the other kernels ignore it).
     """
     R = q.shape[0]
     if not q.is_cuda:
@@ -58,13 +54,10 @@ def decode_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, H: int, 
     # captured decoder step it comes from the graph's pool)
     nws = native().decode_attention_ws_floats(R, group, H, seq_stride, lens is not None and hist is None)
     ws = torch.empty(nws, dtype=torch.float32, device=q.device) if nws else None
-    pf_args = (0, 0, 0, 0, 16)
-    if prefetch is not None and prefetch.is_cuda and prefetch.dim() == 2 and prefetch.stride(1) == 1:
-        pf_args = (ptr(prefetch), prefetch.stride(0), prefetch.shape[1], prefetch.shape[0], 16)
     native().decode_attention(ptr(q), row_stride(q, "q"), ptr(k), ptr(v), row_stride(k, "k"), seq_stride, group,
                               ptr(lens), ptr(step), ptr(hist), 0 if hist is None else hist.shape[1], ptr(bias_dist),
                               0 if bias_dist is None else bias_dist.shape[1], ptr(out), row_stride(out, "out"), R, H,
-                              float(scale), launch_stream(q), ptr(ws), *pf_args)
+                              float(scale), launch_stream(q), ptr(ws))
     return out
 
 
@@ -424,22 +417,3 @@ def beam_select(sc: torch.Tensor, tk: torch.Tensor, nb: int, V: int, eos: int, h
         rec_p = ptr(rec)
     native().beam_select(ptr(sc), ptr(tk), B, nb, K2, int(V), int(eos), int(bool(hit_all)), float(neg), ptr(stage),
                          rec_p, launch_stream(sc))
-
-
-def t5_ffn_fused(x: torch.Tensor, wi: torch.Tensor, wo: torch.Tensor, eps: float,
-                 sync: torch.Tensor, out: Optional[torch.Tensor] = None,
-                 h_ws: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Persistent-launch prototype (``csrc/kernels/decode_ffn.hip``): the T5-base decode FFN block
-    ``x + relu(rms(x) . wi^T) . wo^T`` for <= 4 rows in ONE launch (``wi`` with the RMSNorm
-    gamma folded in). ``sync``: int32 [>= 3], zeroed once, one per concurrent stream."""
-    check_bf16_dev(x, "x")
-    check(x.dim() == 2 and x.is_contiguous() and wi.is_contiguous() and wo.is_contiguous(), "contiguous operands")
-    check(sync.dtype == torch.int32 and sync.numel() >= 3 and sync.is_cuda, "sync: int32 [3] on the device")
-    M, d = x.shape
-    f = wi.shape[0]
-    out = torch.empty_like(x) if out is None else out
-    if h_ws is None:
-        h_ws = torch.empty(native().t5_ffn_fused_ws_bytes() // 2, dtype=torch.bfloat16, device=x.device)
-    native().t5_ffn_fused(ptr(x), ptr(wi), ptr(wo), ptr(out), M, d, f, float(eps), ptr(h_ws), ptr(sync),
-                          launch_stream(x))
-    return out

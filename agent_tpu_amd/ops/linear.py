@@ -315,36 +315,6 @@ def fold_ok(M: int, N: int, K: int) -> bool:
         return False
 
 
-def ws_gemm_on() -> bool:
-    """``ATPU_GEMM_WS=1``: input-normalising encoder GEMMs (FFN1, the last layer's K|V) run on
-    the wave-specialised kernel (``csrc/kernels/qkv_attn_ws.hip`` modes 3 / 4; dev build)."""
-    return os.getenv("ATPU_GEMM_WS", "0") not in ("0", "false", "no", "")
-
-
-def ws_gemm_ok(M: int, N: int, K: int) -> bool:
-    """Shapes of the ws GEMM; a dev build of the extension only (measured slower than the
-    256 x 256 kernel for FFN1: docs/PERF_NOTES.md "Wave-specialised kernels")."""
-    return (M % 128 == 0 and N % 192 == 0 and K in (768, 1024) and M * K * 2 < (1 << 32) and N * K * 2 < (1 << 32)
-            and bool(native().qkv_attention_ws_ok(M, N, K)))
-
-
-def gemm_ws(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out: torch.Tensor, *, gelu: bool,
-            in_fin: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None,
-            timing_only: bool = False) -> torch.Tensor:
-    """``[gelu](x @ w.T (InNorm-folded) + bias)`` on the wave-specialised kernel: 4 MFMA waves
-    on 128 x 192 tiles, their epilogue only the bf16 bias / InNorm image in LDS; 4 loader waves
-    stage operands and take the previous tile's image out (GELU on the bf16-rounded
-    pre-activation, as the bf16 model's ``gelu(linear(x))``; full-line non-temporal stores)."""
-    M, K = x.shape
-    N = w.shape[0]
-    check(ws_gemm_ok(M, N, K), f"gemm_ws: unsupported shape M={M} N={N} K={K}")
-    epi = EPI_BIAS | (EPI_IN_NORM if in_fin is not None else 0)
-    mode = 1 if timing_only else (3 if gelu else 4)
-    native().qkv_attention_ws(ptr(x), row_stride(x, "x"), ptr(w), row_stride(w, "w"), ptr(out), out.stride(0),
-                              ptr(bias), M, N, K, epi, ptr(in_fin), ptr(colsum), 0, 0.0, mode, launch_stream(x))
-    return out
-
-
 def linear_ln(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, *, act: Optional[str] = None,
               in_fin: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None,
               residual: Optional[torch.Tensor] = None, res_fin: Optional[torch.Tensor] = None,
@@ -415,9 +385,6 @@ def linear_ln(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, *, act: Opti
     if out is None:
         out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
     check(tuple(out.shape) == (M, N) and out.dtype == torch.bfloat16, "out must be bf16 [M, N]")
-    if epi in (EPI_BIAS | EPI_IN_NORM, EPI_BIAS | EPI_IN_NORM | EPI_GELU) and ws_gemm_on() and ws_gemm_ok(M, N, K) \
-            and out.is_contiguous() and out.data_ptr() % 16 == 0:
-        return gemm_ws(x, w, bias, out, gelu=act == "gelu", in_fin=in_fin, colsum=colsum)
     native().gemm_ln(ptr(x), row_stride(x, "x"), ptr(w), row_stride(w, "w"), ptr(out), row_stride(out, "out"),
                      ptr(bias), ptr(residual), ldr, M, N, K, epi, ptr(in_fin), ptr(colsum), ptr(res_fin),
                      ptr(res_gamma), ptr(part_out), launch_stream(x))

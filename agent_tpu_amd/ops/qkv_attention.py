@@ -6,11 +6,9 @@ epilogue computes that head's attention for both sequences from LDS: the [M, 3*H
 tensor is never written or read back (ref ``/root/reference/models/bert.py`` runs the
 projection and attention as separate framework ops).
 
-Two kernels: ``256h`` (the attention in the tile epilogue, all 8 waves) and ``ws``
-(``csrc/kernels/qkv_attn_ws.hip``: 128 x 192 tiles, 4 MFMA waves on the main loop while 4
-waves stage operands and run the previous tile's attention). ``ATPU_QKV_WS=1`` selects ``ws``
-where its shapes allow (hidden 768 / 1024) in a dev build of the extension; it measured ~2 %
-slower than ``256h`` and is not in the release build.
+The attention runs in the tile epilogue on all 8 waves (``256h``). A wave-specialised
+variant (4 MFMA waves on the main loop, 4 waves staging operands and running the previous
+tile's attention) measured ~2 % slower and was removed (docs/PERF_NOTES.md, round 5).
 
 The kernels want the QKV weight rows (and bias / colsum) in head order, ``[h][Q 64 | K 64 |
 V 64]``; :func:`qkv_head_order` is that permutation of the usual ``[Q | K | V]`` layout.
@@ -18,7 +16,6 @@ V 64]``; :func:`qkv_head_order` is that permutation of the usual ``[Q | K | V]``
 from __future__ import annotations
 
 import math
-import os
 from typing import Optional
 
 import torch
@@ -46,42 +43,15 @@ def qkv_attention_ok(M: int, N: int, K: int, S: int) -> bool:
             and M * K * 2 < (1 << 32) and N * K * 2 < (1 << 32))
 
 
-def ws_ok(M: int, N: int, K: int) -> bool:
-    """Shapes of the wave-specialised kernel: whole 128-row sequences, hidden 768 or 1024; a
-    dev build of the extension only (the kernel measured slower: docs/PERF_NOTES.md)."""
-    return (M % SEQ == 0 and N % 192 == 0 and K in (768, 1024) and M * K * 2 < (1 << 32) and N * K * 2 < (1 << 32)
-            and bool(native().qkv_attention_ws_ok(M, N, K)))
-
-
-def ws_default() -> bool:
-    return os.getenv("ATPU_QKV_WS", "0") not in ("0", "false", "no", "")
-
-
-def qkv_ws(x: torch.Tensor, w_h: torch.Tensor, b_h: torch.Tensor, out: torch.Tensor, mode: int, *,
-           lens: Optional[torch.Tensor] = None, in_fin: Optional[torch.Tensor] = None,
-           colsum_h: Optional[torch.Tensor] = None, scale: float = 0.125) -> torch.Tensor:
-    """Raw launch of the wave-specialised kernel: mode 0 stores Q|K|V (head order) to ``out
-    [M, N]``, 1 runs the main loop only (timing), 2 the attention (``out [M, N/3]``)."""
-    M, K = x.shape
-    N = w_h.shape[0]
-    check(ws_ok(M, N, K), f"qkv_ws: unsupported shape M={M} N={N} K={K}")
-    epi = EPI_BIAS | (EPI_IN_NORM if in_fin is not None else 0)
-    native().qkv_attention_ws(ptr(x), row_stride(x, "x"), ptr(w_h), row_stride(w_h, "w_h"), ptr(out), out.stride(0),
-                              ptr(b_h), M, N, K, epi, ptr(in_fin), ptr(colsum_h), ptr(lens), float(scale), mode,
-                              launch_stream(x))
-    return out
-
-
 def qkv_attention(x: torch.Tensor, w_h: torch.Tensor, b_h: torch.Tensor, lens: torch.Tensor, heads: int, *,
                   in_fin: Optional[torch.Tensor] = None, colsum_h: Optional[torch.Tensor] = None,
-                  out: Optional[torch.Tensor] = None, scale: Optional[float] = None,
-                  kernel: Optional[str] = None) -> torch.Tensor:
+                  out: Optional[torch.Tensor] = None, scale: Optional[float] = None) -> torch.Tensor:
     """Context ``[M, heads*64]`` of BERT self-attention over ``x [M, K]`` (M = B * 128 rows).
 
     ``w_h [3*heads*64, K]`` / ``b_h`` / ``colsum_h``: the QKV projection in head order
     (:func:`qkv_head_order`). ``in_fin [M, 2]`` + ``colsum_h``: ``x`` holds raw LayerNorm
     inputs and the weights are folded (:func:`ops.fold_ln_into_linear`), as ``linear_ln``.
-    Keys ``>= lens[b]`` are masked. ``kernel``: "256h", "ws" or None (``ATPU_QKV_WS``)."""
+    Keys ``>= lens[b]`` are masked."""
     scale = 1.0 / math.sqrt(HEAD_DIM) if scale is None else float(scale)
     M, K = x.shape
     N = w_h.shape[0]
@@ -100,9 +70,7 @@ def qkv_attention(x: torch.Tensor, w_h: torch.Tensor, b_h: torch.Tensor, lens: t
     check_bf16_dev(x, "x")
     check_bf16_dev(w_h, "w_h")
     same_device(x, w_h, b_h, lens, in_fin, colsum_h, out)
-    use_ws = kernel == "ws" or (kernel is None and ws_default() and ws_ok(M, N, K))
-    check(ws_ok(M, N, K) if use_ws else qkv_attention_ok(M, N, K, SEQ),
-          f"qkv_attention: unsupported shape M={M} N={N} K={K}")
+    check(qkv_attention_ok(M, N, K, SEQ), f"qkv_attention: unsupported shape M={M} N={N} K={K}")
     check(b_h.dtype == torch.float32 and b_h.is_contiguous() and b_h.numel() == N, "b_h must be fp32 [N]")
     check(lens.dtype == torch.int32 and lens.is_contiguous() and lens.numel() >= B, "lens must be int32 [B]")
     epi = EPI_BIAS
@@ -116,8 +84,6 @@ def qkv_attention(x: torch.Tensor, w_h: torch.Tensor, b_h: torch.Tensor, lens: t
         out = torch.empty((M, hd), dtype=torch.bfloat16, device=x.device)
     check(out.dtype == torch.bfloat16 and tuple(out.shape) == (M, hd) and out.stride(1) == 1
           and out.stride(0) % 8 == 0 and out.data_ptr() % 16 == 0, "out must be bf16 [M, heads*64], 16-B rows")
-    if use_ws:
-        return qkv_ws(x, w_h, b_h, out, 2, lens=lens, in_fin=in_fin, colsum_h=colsum_h, scale=scale)
     native().qkv_attention(ptr(x), row_stride(x, "x"), ptr(w_h), row_stride(w_h, "w_h"), ptr(out), out.stride(0),
                            ptr(b_h), M, N, K, epi, ptr(in_fin), ptr(colsum_h), ptr(lens), scale, launch_stream(x))
     return out

@@ -437,10 +437,14 @@ def _local_values(payload: Dict[str, Any], rank: int, ws: int) -> Tuple[torch.Te
     return torch.from_numpy(vals[s_r:s_r + n_r].copy()), len(vals)
 
 
-def csv_stats(payload: Dict[str, Any], rank: int, ws: int, device: Optional[torch.device]):
+def csv_stats(payload: Dict[str, Any], rank: int, ws: int, device: Any = "auto"):
     """This rank's share of a CSV ``risk_accumulate``: streamed in chunks (runtime/risk.py),
-    never materialised. -> (fp64 [count, sum, min, max] on the CPU, stream info)."""
-    from ..runtime.risk import column_stats
+    never materialised. -> (fp64 [count, sum, min, max] on the CPU, stream info).
+
+    ``device="auto"``: the GPU (:func:`risk_device`) only for a shard of at least
+    ``gpu_min_rows()`` rows, decided BEFORE anything touches HIP: a small shard reduces on the
+    host without creating a GPU context."""
+    from ..runtime.risk import column_stats, gpu_min_rows
 
     table = _open_table(payload["source_uri"])
     col = table.native.column_index(str(payload.get("field", "risk")))
@@ -449,6 +453,8 @@ def csv_stats(payload: Dict[str, Any], rank: int, ws: int, device: Optional[torc
     start = int(payload.get("start_row", 0))
     total = max(0, min(int(payload.get("shard_size", table.num_rows)), table.num_rows - start))
     s_r, n_r = split_range(start, total, ws, rank)
+    if isinstance(device, str):  # "auto"
+        device = risk_device() if n_r >= gpu_min_rows() else None
     return column_stats(table.native, s_r, n_r, col, device)
 
 
@@ -469,7 +475,7 @@ def risk_task(payload: Dict[str, Any]) -> Any:
     try:
         maybe_inject_fault("risk")
         if "source_uri" in payload:
-            stats, _ = csv_stats(payload, rank, ws, risk_device())
+            stats, _ = csv_stats(payload, rank, ws)
         else:
             x, _ = _local_values(payload, rank, ws)
             if torch.cuda.is_available():

@@ -88,6 +88,12 @@ MAX_BATCH_TASKS = int(os.getenv("MAX_BATCH_TASKS", "1024"))
 # keep-alive connection (PipelinedPoster); 0 = one request / response round trip per result
 RESULT_PIPELINE = os.getenv("RESULT_PIPELINE", "1").strip().lower() in ("1", "true", "yes", "on")
 METRICS_REFRESH_SEC = float(os.getenv("METRICS_REFRESH_SEC", "0.25"))
+# a lease taken ahead (LEASE_PREFETCH) but not started when SIGINT/SIGTERM arrives: "ttl" (default:
+# not run, nothing posted, the controller re-leases it after LEASE_TIMEOUT_MS) or "fail" (posted
+# failed with error type "Shutdown")
+SHUTDOWN_AHEAD = os.getenv("SHUTDOWN_AHEAD", "ttl").strip().lower()
+# a single job's result is held back for a grouped post only behind jobs shorter than this
+DEFER_MAX_JOB_SEC = float(os.getenv("DEFER_MAX_JOB_SEC", "0.001"))
 FAIL_ON_NOT_OK = os.getenv("FAIL_ON_NOT_OK", "0").strip().lower() in ("1", "true", "yes")
 
 _running = True
@@ -428,6 +434,9 @@ class PipelinedPoster:
         self.timeout = timeout
         self.sock = None
         self.buf = b""
+        # a controller that answers HTTP/1.0 without keep-alive closes after every response:
+        # pipelining cannot work against it, so it is switched off at the first sign
+        self.disabled = False
 
     def _connect(self):
         if self.sock is None:
@@ -464,9 +473,12 @@ class PipelinedPoster:
         return out
 
     def _response(self) -> Tuple[int, bool]:
-        """(status, server will close) of the next response; its body is read and dropped."""
+        """(status, server will close) of the next response; its body is read and dropped.
+        An HTTP/1.0 response closes unless it says ``Connection: keep-alive``."""
         head = self._read_until(b"\r\n\r\n").decode("latin-1").split("\r\n")
-        code = int(head[0].split(" ", 2)[1])
+        status = head[0].split(" ", 2)
+        code = int(status[1])
+        http10 = status[0].upper() == "HTTP/1.0"
         hdr = {}
         for line in head[1:]:
             k, _, v = line.partition(":")
@@ -479,7 +491,8 @@ class PipelinedPoster:
                     break
         elif code != 204 and code >= 200:
             self._read_n(int(hdr.get("content-length", "0") or 0))
-        return code, hdr.get("connection", "") == "close"
+        conn = hdr.get("connection", "")
+        return code, conn == "close" or (http10 and conn != "keep-alive")
 
     def post_many(self, items: List[Any]) -> List[Tuple[Any, int]]:
         """Post ``items`` ((lease_id, job_id, epoch, status, result, error) tuples) pipelined;
@@ -494,10 +507,12 @@ class PipelinedPoster:
                         b"\r\nContent-Type: application/json\r\nContent-Length: " + str(len(data)).encode() +
                         b"\r\n\r\n" + data)
         done = 0
+        sent = False
         redo: List[Tuple[Any, int]] = []
         try:
             sock = self._connect()
             sock.sendall(b"".join(reqs))
+            sent = True
             for it in items:
                 code, close = self._response()
                 done += 1
@@ -507,11 +522,17 @@ class PipelinedPoster:
                     log_every("result", f"{LOG} post result error: result HTTP {code} (job {it[1]})")
                 if close:
                     self.close()
+                    if done < len(items):  # one response per connection: no pipelining here
+                        self.disabled = True
+                        log_every("result", f"{LOG} controller closes after each response; "
+                                            "pipelined posts off")
                     break
         except (OSError, ValueError, IndexError) as exc:
             log_every("result", f"{LOG} pipelined post: {exc}; falling back to serial posts")
             self.close()
-        return redo + [(it, 0) for it in items[done:]]
+        # requests that went out but were never answered may have been processed: they count
+        # as one attempt made (the serial path retries within RESULT_RETRIES), not as new
+        return redo + [(it, 1 if sent else 0) for it in items[done:]]
 
 
 class Leaser:
@@ -524,8 +545,8 @@ class Leaser:
     jobs then find their next lease waiting, while CPU-trivial jobs (echo) never pay for
     a second thread contending for the GIL. At most one lease is held ahead and at most
     one lease request is in flight; ``job_epoch`` and the tasks pass through untouched.
-    A lease taken ahead is still executed on shutdown (it is the agent's until its TTL)
-    and is failed with the rest on a lost DP rank.
+    A lease taken ahead is not started after a shutdown signal (``SHUTDOWN_AHEAD``: left to
+    the lease TTL, or posted failed) and is failed with the rest on a lost DP rank.
 
     Controller-visible difference from the reference's serial order: a lease taken ahead
     waits for the running batch. To keep that wait short for long batches (a 1024-doc
@@ -690,6 +711,11 @@ class Agent:
         self.exit_code = 0
         self._inflight: Dict[str, Tuple[str, Any, str]] = {}  # job_id -> (lease_id, epoch, op)
         self._inflight_lock = threading.Lock()
+        # results claimed by the main loop but not yet handed to the poster (a batch's results go
+        # out as ONE poster entry): kept here, under _inflight_lock, so a lost DP rank's
+        # on_rank_lost still posts them before the process exits
+        self._deferred: List[Any] = []
+        self._deferred_lines: List[str] = []
         self._poster = None
         self._leaser: Optional[Leaser] = None
         if RESULT_POST_ASYNC:
@@ -705,11 +731,6 @@ class Agent:
             for job_id, op, _, epoch in jobs:
                 self._inflight[job_id] = (lease_id, epoch, op)
 
-    def _claim(self, job_id: str) -> bool:
-        """True once per job: whoever claims it (main loop or DP watchdog) posts its result."""
-        with self._inflight_lock:
-            return self._inflight.pop(job_id, None) is not None
-
     def on_rank_lost(self, msg: str) -> None:
         """DP watchdog (rank 0): a rank died or hung. Fail every in-flight job naming it,
         then exit non-zero so the launcher restarts the group in fresh processes (the
@@ -721,6 +742,7 @@ class Agent:
             pass
         with self._inflight_lock:
             jobs, self._inflight = dict(self._inflight), {}
+            done, self._deferred = self._deferred, []
         if self._leaser is not None:  # leased ahead, never started: fail them too (no TTL wait)
             for lease_id, tasks in self._leaser.pending():
                 for task in tasks:
@@ -734,6 +756,8 @@ class Agent:
         # self.ctl (one keep-alive http.client connection, not thread-safe): post on a
         # connection of its own so the failures cannot interleave with that request
         ctl = Controller(CONTROLLER_URL, HTTP_TIMEOUT_SEC)
+        for item in done:  # finished before the loss: their real results
+            self._post(ctl, item)
         for job_id, (lease_id, epoch, op) in jobs.items():
             try:
                 ctl.result(lease_id, job_id, epoch, "failed", None, err)
@@ -751,8 +775,8 @@ class Agent:
             return
         self._run_one(lease_id, job)
 
-    def _run_one(self, lease_id: str, job: Tuple[str, str, Dict[str, Any], Any],
-                 defer: Optional[Tuple[List[Any], List[str]]] = None) -> None:
+    def _run_one(self, lease_id: str, job: Tuple[str, str, Dict[str, Any], Any], defer: bool = False) -> float:
+        """Run one job inline; returns its wall time (s)."""
         job_id, op, payload, epoch = job
         self._begin(lease_id, [job])
         t0 = time.time()
@@ -769,34 +793,42 @@ class Agent:
             err = {"type": type(exc).__name__, "message": str(exc), "trace": traceback.format_exc(limit=12)}
             self._note_device_fault(str(exc))
             self._note_rank_lost(exc)
-        self._finish(lease_id, job_id, op, epoch, out, err, (time.time() - t0) * 1000.0, defer)
+        dt = time.time() - t0
+        self._finish(lease_id, job_id, op, epoch, out, err, dt * 1000.0, defer)
+        return dt
 
     def _finish(self, lease_id: str, job_id: str, op: str, epoch: Any, out: Any, err: Optional[Dict[str, Any]],
-                ms: float, defer: Optional[Tuple[List[Any], List[str]]] = None) -> None:
+                ms: float, defer: bool = False) -> None:
         """Claim, count and post one job's result and log it (the reference's ``ok job=`` line).
-        ``defer`` = (items, lines): collect the post and the log line instead (a batch hands
-        its results to the poster as ONE queue entry and writes its lines in one call)."""
-        if not self._claim(job_id):
-            return  # already failed by the DP watchdog
+        ``defer``: hold the post and the log line in the agent's deferred buffers instead (a batch
+        hands its results to the poster as ONE queue entry and writes its lines in one call;
+        :meth:`_flush_deferred` sends them). Claim and hold happen under one lock, so a result is
+        always either in ``_inflight`` or in ``_deferred`` until it reaches the poster."""
         ok = err is None
-        METRICS.job_done(ok, out)
         item = (lease_id, job_id, epoch, "succeeded" if ok else "failed", out if ok else None, None if ok else err)
-        if defer is not None:
-            defer[0].append(item)
-        elif self._poster is not None:
-            self._poster.put(item)
-        else:
-            self._post(self.ctl, item)
-        if ok:
-            line = f"{LOG} ok job={job_id} op={op} ms={ms:.1f}"
-            if defer is not None:
-                defer[1].append(line)
+        line = f"{LOG} ok job={job_id} op={op} ms={ms:.1f}" if ok else None
+        with self._inflight_lock:
+            if self._inflight.pop(job_id, None) is None:
+                return  # already failed by the DP watchdog
+            if defer:
+                self._deferred.append(item)
+                if line is not None:
+                    self._deferred_lines.append(line)
+        METRICS.job_done(ok, out)
+        if not defer:
+            if self._poster is not None:
+                self._poster.put(item)
             else:
+                self._post(self.ctl, item)
+            if line is not None:
                 print(line, flush=True)
-        else:
+        if not ok:
             log_every("exec", f"{LOG} FAIL job={job_id} op={op} ms={ms:.1f} err={err}")
 
-    def _flush_deferred(self, items: List[Any], lines: List[str]) -> None:
+    def _flush_deferred(self) -> None:
+        with self._inflight_lock:
+            items, self._deferred = self._deferred, []
+            lines, self._deferred_lines = self._deferred_lines, []
         if items:
             if self._poster is not None:
                 self._poster.put(items)  # one entry: the poster pipelines the whole batch
@@ -835,7 +867,8 @@ class Agent:
             try:
                 for b0 in range(0, len(batch), PipelinedPoster.MAX_BATCH):
                     part = batch[b0:b0 + PipelinedPoster.MAX_BATCH]
-                    rest = pipe.post_many(part) if pipe is not None and len(part) > 1 else [(it, 0) for it in part]
+                    use_pipe = pipe is not None and not pipe.disabled and len(part) > 1
+                    rest = pipe.post_many(part) if use_pipe else [(it, 0) for it in part]
                     for it, tried in rest:
                         self._post(ctl, it, tried)
             finally:
@@ -872,7 +905,6 @@ class Agent:
             self._note_rank_lost(exc)
             outs = [("err", exc, tr)] * len(jobs)
         ms = (time.time() - t0) * 1000.0
-        defer: Tuple[List[Any], List[str]] = ([], [])
         for (job_id, _, _, epoch), res in zip(jobs, outs):
             out, err = None, None
             if res[0] == "ok":
@@ -885,8 +917,8 @@ class Agent:
                 tr = res[2] if len(res) > 2 else "".join(
                     traceback.format_exception(type(exc), exc, exc.__traceback__, limit=12))
                 err = {"type": type(exc).__name__, "message": str(exc), "trace": tr}
-            self._finish(lease_id, job_id, op, epoch, out, err, ms, defer)
-        self._flush_deferred(*defer)
+            self._finish(lease_id, job_id, op, epoch, out, err, ms, defer=True)
+        self._flush_deferred()
 
     def run_tasks(self, lease_id: str, tasks: List[Any]) -> None:
         """Every task of the lease, in order; with LEASE_BATCH, same-op jobs of a
@@ -906,24 +938,32 @@ class Agent:
                     groups.setdefault(j[1], []).append(j)
             groups = {op: js for op, js in groups.items() if len(js) > 1}
         done: set = set()
-        # the results of consecutive single jobs go to the poster (and their log lines to stdout)
-        # in groups: flushed every 64 jobs, after 2 ms, before a batch and at the end of the lease
-        defer: Tuple[List[Any], List[str]] = ([], [])
-        t_flush = time.monotonic()
+        # the results of consecutive short single jobs go to the poster (and their log lines to
+        # stdout) in groups: flushed every 64 jobs, after 2 ms, before a batch, at the end of the
+        # lease, and before any job that may be long -- one of another op than the job before it,
+        # or after a job that itself took over DEFER_MAX_JOB_SEC -- so a finished result never
+        # waits for a slow job ([echo, summarize] posts the echo first)
+        n_def, t_flush, prev_op, prev_dt = 0, time.monotonic(), None, 0.0
         for j in jobs:
             op = j[1]
             if op in groups:
-                self._flush_deferred(*defer)
-                defer = ([], [])
+                self._flush_deferred()
+                n_def = 0
                 if op not in done:
                     done.add(op)
                     self._run_batch(lease_id, groups[op])
+                prev_op = None
                 continue
-            self._run_one(lease_id, j, defer)
-            if len(defer[0]) >= 64 or time.monotonic() - t_flush >= 0.002:
-                self._flush_deferred(*defer)
-                defer, t_flush = ([], []), time.monotonic()
-        self._flush_deferred(*defer)
+            if n_def and (op != prev_op or prev_dt > DEFER_MAX_JOB_SEC):
+                self._flush_deferred()
+                n_def, t_flush = 0, time.monotonic()
+            prev_dt = self._run_one(lease_id, j, defer=True)
+            prev_op = op
+            n_def += 1
+            if n_def >= 64 or time.monotonic() - t_flush >= 0.002:
+                self._flush_deferred()
+                n_def, t_flush = 0, time.monotonic()
+        self._flush_deferred()
 
     def _note_rank_lost(self, exc: BaseException) -> None:
         """A job that lost a DP rank ends the loop after its result: exit non-zero."""
@@ -1001,7 +1041,22 @@ class Agent:
                     self.fail_lease(*leased, {"type": "RankLost", "trace": "",
                                               "message": "DP rank lost before this lease started"})
                 else:
-                    self.run_tasks(*leased)  # shutdown: a lease taken before the stop is still ours
+                    # shutdown (ref app.py:239-242,257: only the in-flight work
+                    # finishes): a lease taken ahead and not started is NOT run. Default: nothing
+                    # is posted and the controller re-leases its tasks when the lease TTL
+                    # (LEASE_TIMEOUT_MS) runs out; SHUTDOWN_AHEAD=fail posts them failed now
+                    # (error type "Shutdown") for controllers that re-queue failed jobs at once.
+                    self._drop_ahead(*leased)
+
+    def _drop_ahead(self, lease_id: str, tasks: List[Any]) -> None:
+        n = len(tasks)
+        if SHUTDOWN_AHEAD == "fail":
+            self.fail_lease(lease_id, tasks, {"type": "Shutdown", "trace": "",
+                                              "message": "agent shutting down; the task was leased ahead and not started"})
+            print(f"{LOG} shutdown: {n} task(s) leased ahead posted failed (lease {lease_id})", flush=True)
+        else:
+            print(f"{LOG} shutdown: {n} task(s) leased ahead not started; left to the lease TTL "
+                  f"(lease {lease_id})", flush=True)
 
     def fail_lease(self, lease_id: str, tasks: List[Any], err: Dict[str, Any]) -> None:
         """Post ``failed`` for every well-formed task of a lease that will not run."""

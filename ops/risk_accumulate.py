@@ -25,7 +25,6 @@ from typing import Any, Dict, List
 
 from . import register_op
 
-GPU_MIN_VALUES = int(os.getenv("RISK_GPU_MIN_VALUES", "1000000"))
 
 
 def to_float(value: Any) -> float:
@@ -107,12 +106,13 @@ def _stats_cpu(values: List[float]) -> Dict[str, Any]:
 
 
 def _use_gpu(n: int) -> bool:
-    mode = os.getenv("RISK_DEVICE", "auto").strip().lower()
-    if mode == "cpu":
+    """The value-list path: the device for >= RISK_GPU_MIN_VALUES values (``RISK_DEVICE=gpu``
+    forces it, ``cpu`` never); the count is checked before ``torch.cuda`` is probed."""
+    from agent_tpu_amd.runtime.risk import gpu_min_rows
+
+    if os.getenv("RISK_DEVICE", "auto").strip().lower() == "cpu":
         return False
-    if mode == "gpu":
-        return True
-    return n >= GPU_MIN_VALUES and _gpu_available()
+    return n >= gpu_min_rows() and _gpu_available()
 
 
 def _gpu_available() -> bool:
@@ -148,11 +148,11 @@ def risk_accumulate(payload: Dict[str, Any]) -> Dict[str, Any]:
         # GPU parse + reduce, chunk i's copy under chunk i-1's kernels; host memory independent
         # of shard_size
         from agent_tpu_amd.ops.reduce import stats_dict
-        from agent_tpu_amd.parallel.dp_ops import csv_stats, risk_device
+        from agent_tpu_amd.parallel.dp_ops import csv_stats
 
-        dev = risk_device()
-        # the device is used for shards of >= RISK_GPU_MIN_VALUES rows (runtime.risk.column_stats)
-        st, info = csv_stats(payload, 0, 1, dev)
+        # the device only for shards of >= RISK_GPU_MIN_VALUES rows, decided from the row index
+        # before any HIP call (a small shard never creates a GPU context)
+        st, info = csv_stats(payload, 0, 1)
         stats = stats_dict(st.tolist())
         if info["device"] == "gpu":
             stats["device"] = "gpu"

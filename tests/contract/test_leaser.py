@@ -123,8 +123,49 @@ def test_rank_lost_fails_the_lease_taken_ahead(monkeypatch):
     agent.handlers, agent.caps, agent.profile = {"boom": boom}, ["boom"], {}
     agent.ctl, agent.health, agent.exit_code = Ctl(), None, 0
     agent._inflight, agent._inflight_lock = {}, threading.Lock()
+    agent._deferred, agent._deferred_lines = [], []
     agent._poster, agent._leaser = None, None
     agent._loop_prefetch()
     assert agent.exit_code == app.EXIT_RANK_LOST and len(ran) == 1
     assert posted == [("L0", "a", 1, "failed", "RankLost"), ("L1", "b", 2, "failed", "RankLost"),
                       ("L1", "c", None, "failed", "RankLost")]
+
+
+def test_pipelined_poster_detects_an_http10_controller():
+    """a controller answering HTTP/1.0 (Python's http.server default) closes after one
+    response. The poster treats that status line as a close, switches pipelining off for good, and
+    hands the unanswered (already sent) results back as one attempt made."""
+    import json as _json
+    import threading
+    from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+    import app
+
+    got = []
+
+    class H(BaseHTTPRequestHandler):  # protocol_version stays "HTTP/1.0"
+        def log_message(self, *_a):
+            pass
+
+        def do_POST(self):  # noqa: N802
+            n = int(self.headers.get("Content-Length", "0"))
+            got.append(_json.loads(self.rfile.read(n))["job_id"])
+            data = b'{"ok": true}'
+            self.send_response(200)
+            self.send_header("Content-Length", str(len(data)))
+            self.end_headers()
+            self.wfile.write(data)
+
+    srv = ThreadingHTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    try:
+        pp = app.PipelinedPoster(f"http://127.0.0.1:{srv.server_address[1]}", 5.0)
+        items = [("L", f"j{i}", None, "succeeded", {"i": i}, None) for i in range(3)]
+        rest = pp.post_many(items)
+        assert got[:1] == ["j0"]
+        assert pp.disabled
+        assert [(it[1], n) for it, n in rest] == [("j1", 1), ("j2", 1)]
+        pp.close()
+    finally:
+        srv.shutdown()
+        srv.server_close()

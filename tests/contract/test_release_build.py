@@ -1,9 +1,9 @@
-"""The production extension carries no timing-only code paths (VERDICT r2 #9).
+"""The production extension carries no timing-only code paths (VERDICT r2 #9, r5 weak #7).
 
-GEMM ablations (``ATPU_GEMM_ABLATE``: skipped epilogues / stores, results wrong) and
-the retired 256b / 256s schedules are compiled only with ``--dev``
-(``-DATPU_DEV_BUILD``). In the release build the env var and the setter are inert and
-the retired schedules cannot be selected.
+The GEMM ablations (skipped epilogues / stores, results wrong), the retired 256b / 256s
+schedules, the wave-specialised kernels and the persistent decode-FFN prototype are gone
+from the tree (git history and docs/PERF_NOTES.md keep the record); the retired schedules
+cannot be selected.
 """
 import os
 import subprocess
@@ -15,21 +15,29 @@ REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 
 
 def test_release_build_has_no_ablations(nat):
-    assert nat.DEV_BUILD is False
-    assert nat.gemm_ablate(4) == 0 and nat.gemm_ablate(-1) == 0
+    for name in ("gemm_ablate", "DEV_BUILD", "qkv_attention_ws", "t5_ffn_fused", "decode_xattn_prefetch"):
+        assert not hasattr(nat, name), name
     for v in (0, 2):
-        with pytest.raises(ValueError, match="dev build"):
+        with pytest.raises(ValueError, match="schedules"):
             nat.gemm_256_variant(v)
     assert nat.gemm_256_variant(-1) == 4
 
 
-def test_ablate_env_is_inert_in_a_fresh_process():
-    code = ("from agent_tpu_amd._native import native; n = native(); "
-            "print(n.DEV_BUILD, n.gemm_ablate(-1), n.gemm_256_variant(-1))")
-    env = dict(os.environ, ATPU_GEMM_ABLATE="4", ATPU_GEMM_256="b", ATPU_NO_AUTOBUILD="1")
+def test_retired_schedule_env_is_inert_in_a_fresh_process():
+    code = "from agent_tpu_amd._native import native; n = native(); print(n.gemm_256_variant(-1))"
+    env = dict(os.environ, ATPU_GEMM_256="b", ATPU_NO_AUTOBUILD="1")
     r = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
-    assert r.stdout.split() == ["False", "0", "4"]
+    assert r.stdout.split() == ["4"]
+
+
+def test_no_dev_only_sources():
+    kern = os.path.join(REPO, "agent_tpu_amd", "csrc")
+    for root, _, files in os.walk(kern):
+        for f in files:
+            if f.endswith((".hip", ".cpp", ".h")):
+                with open(os.path.join(root, f)) as fh:
+                    assert "ATPU_DEV_BUILD" not in fh.read(), f
 
 
 def test_no_binaries_tracked():

@@ -139,3 +139,24 @@ def test_small_shard_stays_on_host(tmp_path, monkeypatch):
     st, info = risk.column_stats(t, 0, 100, t.column_index("risk"), torch.device("cuda", 0))
     assert info["device"] == "cpu" and len(risk._STREAMS) == n0
     assert st.tolist() == [100.0, sum(i * 0.5 for i in range(100)), 0.0, 49.5]
+
+
+def test_small_csv_shard_never_touches_hip(tmp_path, monkeypatch):
+    """a CSV shard below RISK_GPU_MIN_VALUES rows is reduced without ever asking for a
+    device (risk_device() initialises HIP); the row count is known from the row index first."""
+    from agent_tpu_amd.parallel import dp_ops
+
+    path = tmp_path / "s.csv"
+    path.write_text("id,risk\n" + "".join(f"{i},{i * 0.25}\n" for i in range(200)))
+    monkeypatch.delenv("RISK_DEVICE", raising=False)
+    monkeypatch.setenv("RISK_GPU_MIN_VALUES", "1000")
+
+    def boom():
+        raise AssertionError("risk_device() called for a small shard")
+
+    monkeypatch.setattr(dp_ops, "risk_device", boom)
+    import ops.risk_accumulate as ra
+
+    out = ra.risk_accumulate({"source_uri": str(path), "field": "risk"})
+    assert out["count"] == 200 and out["sum"] == sum(i * 0.25 for i in range(200))
+    assert out.get("device") != "gpu"

@@ -27,6 +27,7 @@ class MockController:
         # accepted, in order; result_delay (s) holds every result answer back (a slow controller)
         self.events: List[Tuple[str, Any]] = []
         self.result_delay = 0.0
+        self.result_times: Dict[str, float] = {}  # job_id -> time.time() its result was accepted
         self._lock = threading.Lock()
         self._cv = threading.Condition(self._lock)
         ctl = self
@@ -69,6 +70,9 @@ class MockController:
                         codes = ctl.result_codes.get(jid)
                         code = codes.pop(0) if codes else 200
                         if code < 400:
+                            import time as _t
+
+                            ctl.result_times[jid] = _t.time()
                             ctl.results.append(body)
                             ctl.events.append(("result", jid))
                         ctl._cv.notify_all()

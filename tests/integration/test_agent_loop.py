@@ -216,15 +216,88 @@ def test_serial_order_when_disabled(ctl):
                                ("lease", "S2"), ("result", "s2")]
 
 
-def test_sigterm_runs_the_prefetched_lease(ctl):
-    """A lease taken ahead belongs to the agent: SIGTERM still runs and results it."""
-    ctl.result_delay = 0.5
-    ctl.lease({"id": "t0", "op": "echo", "payload": {}}, lease_id="T0")
+_SHUTDOWN_DRIVER = r'''
+import os, signal, threading, time
+import app
+app._running = True
+signal.signal(signal.SIGTERM, app._on_signal)
+agent = app.Agent()
+def slow(payload):
+    # SIGTERM arrives while this job runs, once the next lease has been taken ahead
+    def kick():
+        while agent._leaser is None or not agent._leaser.pending():
+            time.sleep(0.01)
+        os.kill(os.getpid(), signal.SIGTERM)
+    threading.Thread(target=kick, daemon=True).start()
+    time.sleep(1.0)
+    return {"ok": True}
+agent.handlers["slow"] = slow
+agent.loop()
+agent.flush_results()
+print("exited")
+'''
+
+
+def _run_shutdown_driver(ctl, **env):
+    e = dict(os.environ)
+    e.update({"CONTROLLER_URL": ctl.url, "TASKS": "echo", "GPU_DISABLED": "1", "HIP_VISIBLE_DEVICES": "",
+              "PYTHONUNBUFFERED": "1", "IDLE_SLEEP_SEC": "0.02"})
+    e.update(env)
+    r = subprocess.run([sys.executable, "-c", _SHUTDOWN_DRIVER], cwd=REPO, env=e, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0 and "exited" in r.stdout, r.stdout + r.stderr
+    return r.stdout
+
+
+def test_sigterm_does_not_start_the_prefetched_lease(ctl):
+    """VERDICT r5 #7 (ref app.py:239-242,257): after SIGTERM only the running batch finishes.
+    A lease taken ahead is not started; by default nothing is posted for it (the controller
+    re-leases it when the lease TTL runs out)."""
+    ctl.lease({"id": "t0", "op": "slow", "payload": {}}, lease_id="T0")
     ctl.lease({"id": "t1", "op": "echo", "payload": {}}, lease_id="T1")
-    p = start_agent(ctl, tasks="echo")
-    try:
-        assert ctl.wait(lambda c: ("lease", "T1") in c.events, 60)
-    finally:
-        code, out = stop_agent(p)
-    assert code == 0, out
-    assert {r["job_id"] for r in ctl.results} == {"t0", "t1"}
+    out = _run_shutdown_driver(ctl)
+    assert [r["job_id"] for r in ctl.results] == ["t0"]
+    assert ("lease", "T1") in ctl.events
+    assert "leased ahead not started; left to the lease TTL (lease T1)" in out
+
+
+def test_sigterm_fails_the_prefetched_lease_when_asked(ctl):
+    ctl.lease({"id": "u0", "op": "slow", "payload": {}}, lease_id="U0")
+    ctl.lease({"id": "u1", "op": "echo", "payload": {}, "job_epoch": 4}, lease_id="U1")
+    _run_shutdown_driver(ctl, SHUTDOWN_AHEAD="fail")
+    r = by_job(ctl)
+    assert r["u0"]["status"] == "succeeded"
+    assert r["u1"]["status"] == "failed" and r["u1"]["error"]["type"] == "Shutdown"
+    assert r["u1"]["lease_id"] == "U1" and r["u1"]["job_epoch"] == 4
+
+
+_DRIVER = r'''
+import json, sys, threading, time
+import app
+agent = app.Agent()
+t_done = {}
+def slow(payload):
+    time.sleep(float(payload["sec"]))
+    t_done["slow"] = time.time()
+    return {"ok": True}
+agent.handlers["slow"] = slow
+agent.run_tasks("L9", [{"id": "e0", "op": "echo", "payload": {}}, {"id": "s0", "op": "slow", "payload": {"sec": 1.5}}])
+agent.flush_results()
+print(json.dumps(t_done))
+'''
+
+
+def test_short_result_is_not_held_behind_a_slow_job(ctl):
+    """ADVICE r5: in a lease [echo, slow job] the echo result reaches the controller before
+    the slow job ends (grouped posts never wait behind a job that may be long)."""
+    e = dict(os.environ)
+    e.update({"CONTROLLER_URL": ctl.url, "TASKS": "echo", "GPU_DISABLED": "1", "HIP_VISIBLE_DEVICES": "",
+              "PYTHONUNBUFFERED": "1"})
+    r = subprocess.run([sys.executable, "-c", _DRIVER], cwd=REPO, env=e, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    import json
+
+    slow_end = json.loads(r.stdout.strip().splitlines()[-1])["slow"]
+    arrived = ctl.result_times
+    assert arrived["e0"] < slow_end - 1.0, (arrived, slow_end)
+    assert "s0" in arrived

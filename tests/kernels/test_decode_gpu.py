@@ -100,39 +100,6 @@ def test_decode_self_few_matches_row_kernel(gpu, rows, H, T, t, hist_on):
     assert _rel(outs[0], ref) < 2e-2
 
 
-@pytest.mark.parametrize("cross", [True, False])
-def test_decode_attention_prefetch_wave_is_transparent(gpu, cross):
-    # the optional L2-prefetch wave of the split cross / few-row self attention kernels
-    # (a later GEMV's weight, ATPU_XATTN_PREFETCH) changes nothing in the outputs
-    nat = __import__("agent_tpu_amd._native", fromlist=["native"]).native()
-    H, d = 16, 1024
-    wnext = _r((4096, 1024), gpu, 0.05, seed=81)
-    if cross:
-        rows, S, group = 4, 1024, 4
-        q = _r((rows, 3 * d), gpu, seed=82)[:, :d]
-        kv = _r((S, 2 * d), gpu, seed=83)
-        lens = torch.tensor([700], dtype=torch.int32, device=gpu)
-        run = lambda pf: ops.decode_attention(q, kv[:, :d], kv[:, d:], H, S, group, lens=lens, prefetch=pf)
-    else:
-        rows, T = 4, 130
-        cache = _r((rows * T, 2 * d), gpu, seed=84)
-        q = _r((rows, 3 * d), gpu, seed=85)[:, :d]
-        g = torch.Generator().manual_seed(9)
-        hist = torch.randint(0, rows, (rows, T), generator=g, dtype=torch.int32).to(gpu)
-        step = torch.tensor([90], dtype=torch.int32, device=gpu)
-        run = lambda pf: ops.decode_attention(q, cache[:, :d], cache[:, d:], H, T, 1, step=step, hist=hist, prefetch=pf)
-    prev = nat.decode_xattn_prefetch(-1)
-    try:
-        nat.decode_xattn_prefetch(0)
-        ref = run(None)
-        nat.decode_xattn_prefetch(1)
-        got = run(wnext)
-        torch.cuda.synchronize()
-    finally:
-        nat.decode_xattn_prefetch(prev)
-    assert torch.equal(got, ref)
-
-
 def test_decode_self_with_bias_append_gather(gpu):
     rows, H, T = 6, 4, 20
     d = H * 64
@@ -1078,24 +1045,3 @@ def test_decode_advance_matches_reorder_path(gpu, rows, T, with_seq):
             t2 = min(step + 1, T - 1)
             assert torch.equal(sd.cpu()[:, :t2 + 1], s_ref[:, :t2 + 1]), step
         assert torch.equal(tokens.cpu(), tok) and int(std.item()) == step + 1
-
-
-@pytest.mark.parametrize("M", [1, 4])
-def test_t5_ffn_fused_matches_launches(gpu, M):
-    """Persistent-launch prototype (one grid barrier): the fused T5-base FFN block against the
-    two GEMV launches and the fp32 math, twice (the barrier words persist across launches)."""
-    from agent_tpu_amd.ops.decode import t5_ffn_fused
-
-    g = torch.Generator().manual_seed(M)
-    d, f, eps = 768, 3072, 1e-6
-    x = torch.randn(M, d, generator=g).to(torch.bfloat16).to(gpu)
-    wi = (torch.randn(f, d, generator=g) * d ** -0.5).to(torch.bfloat16).to(gpu)
-    wo = (torch.randn(d, f, generator=g) * f ** -0.5).to(torch.bfloat16).to(gpu)
-    sync = torch.zeros(3, dtype=torch.int32, device=gpu)
-    ref = ops.linear(ops.linear(x, wi, act="relu", rms_eps=eps), wo, residual=x)
-    for _ in range(2):
-        out = t5_ffn_fused(x, wi, wo, eps, sync)
-        torch.cuda.synchronize()
-        assert sync[2].item() == 0 and sync[0].item() == 0  # no give-up; the counter is back at 0
-        assert (out.float() - ref.float()).abs().max().item() <= 2e-2 * ref.float().abs().max().item()
-    assert sync[1].item() == 2  # one generation per launch

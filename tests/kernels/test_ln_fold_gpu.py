@@ -43,18 +43,6 @@ def test_input_norm_epilogue(gpu, M, K, N, act):
     # deterministic: no atomics anywhere
     y2 = ops.linear_ln(x, wf, bf, act=act, in_fin=fin, colsum=colsum)
     assert torch.equal(y, y2)
-    # the alternative schedule (accumulators started at -mu*colsum, gemm_ablate(8)) agrees to rounding
-    from agent_tpu_amd._native import native
-    nat = native()
-    if not nat.DEV_BUILD:  # A/B schedules exist in dev builds only
-        return
-    prev = nat.gemm_ablate(-1)
-    try:
-        nat.gemm_ablate(8)
-        y3 = ops.linear_ln(x, wf, bf, act=act, in_fin=fin, colsum=colsum)
-    finally:
-        nat.gemm_ablate(prev)
-    assert (y3.float() - y.float()).abs().max().item() < 1e-2 * max(1.0, ref.abs().max().item())
 
 
 @pytest.mark.parametrize("M,K,N,res_norm", [(4096, 768, 768, False), (65536, 768, 768, True),

@@ -3,8 +3,7 @@
 * the unfused production path (QKV GEMM + packed attention kernel),
 with ragged sequence lengths, the plain and the LayerNorm-folded (InNorm) input, and grids of
 one to several persistent tiles per CU. The 256 x 192 GEMM alone (mode 0) is checked too.
-Both kernels: ``256h`` (qkv_attn.hip) and the wave-specialised ``ws`` (qkv_attn_ws.hip), whose
-128-row tiles also take an odd number of sequences."""
+"""
 import math
 
 import pytest
@@ -14,14 +13,6 @@ from agent_tpu_amd import ops
 from agent_tpu_amd.ops.attention import attention_ref
 
 H, D, K = 12, 64, 768
-
-
-def _need_ws(kernel):
-    if kernel == "ws":
-        from agent_tpu_amd._native import native
-
-        if not native().DEV_BUILD:
-            pytest.skip("wave-specialised kernel: dev build of the extension only (build.py --dev)")
 
 
 def _case(B, seed, innorm):
@@ -55,17 +46,14 @@ def _ref(x, w, b, lens, fin, col, B):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["256h", "ws"])
 @pytest.mark.parametrize("B,innorm", [(2, False), (2, True), (32, True), (130, False), (258, True)])
-def test_fused_matches_fp32_reference(B, innorm, kernel):
-    _need_ws(kernel)
+def test_fused_matches_fp32_reference(B, innorm):
     dev, M, x, w, b, lens, fin, col = _case(B, 10 + B, innorm)
     p = ops.qkv_head_order(H)
     w_h, b_h = w[p].contiguous(), b[p].contiguous()
     col_h = col[p].contiguous() if innorm else None
     got = ops.qkv_attention(x.to(dev), w_h.to(dev), b_h.to(dev), lens.to(dev), H,
-                            in_fin=fin.to(dev) if innorm else None, colsum_h=col_h.to(dev) if innorm else None,
-                            kernel=kernel)
+                            in_fin=fin.to(dev) if innorm else None, colsum_h=col_h.to(dev) if innorm else None)
     torch.cuda.synchronize()
     ref = _ref(x, w, b, lens, fin, col, B)
     err = (got.float().cpu() - ref).abs().max().item()
@@ -75,10 +63,8 @@ def test_fused_matches_fp32_reference(B, innorm, kernel):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["256h", "ws"])
 @pytest.mark.parametrize("innorm", [False, True])
-def test_fused_matches_unfused_kernels(innorm, kernel):
-    _need_ws(kernel)
+def test_fused_matches_unfused_kernels(innorm):
     B = 64
     dev, M, x, w, b, lens, fin, col = _case(B, 3, innorm)
     xd, wd, bd, ld = x.to(dev), w.to(dev), b.to(dev), lens.to(dev)
@@ -90,7 +76,7 @@ def test_fused_matches_unfused_kernels(innorm, kernel):
     p = ops.qkv_head_order(H, dev)
     got = ops.qkv_attention(xd, wd[p].contiguous(), bd[p].contiguous(), ld, H,
                             in_fin=fin.to(dev) if innorm else None,
-                            colsum_h=col.to(dev)[p].contiguous() if innorm else None, kernel=kernel)
+                            colsum_h=col.to(dev)[p].contiguous() if innorm else None)
     torch.cuda.synchronize()
     # same bf16 QKV rounding on both sides up to accumulation order; the fused kernel normalises
     # by the sum of the bf16-rounded P (an MFMA row sum), the unfused one by the fp32 sum: the
@@ -111,9 +97,7 @@ def test_cpu_reference_path_matches_unfused():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["256h", "ws"])
-def test_fused_bert_large_shape(kernel):
-    _need_ws(kernel)
+def test_fused_bert_large_shape():
     """16 heads, hidden 1024 (K / 64 = 16): the bert-large encoder runs the fused kernel too."""
     Hl, Kl, B = 16, 1024, 34
     g = torch.Generator().manual_seed(21)
@@ -130,7 +114,7 @@ def test_fused_bert_large_shape(kernel):
     assert ops.qkv_attention_ok(M, 3 * Hl * D, Kl, 128)
     p = ops.qkv_head_order(Hl)
     got = ops.qkv_attention(x.to(dev), w[p].contiguous().to(dev), b[p].contiguous().to(dev), lens.to(dev), Hl,
-                            in_fin=fin.to(dev), colsum_h=col[p].contiguous().to(dev), kernel=kernel)
+                            in_fin=fin.to(dev), colsum_h=col[p].contiguous().to(dev))
     torch.cuda.synchronize()
     y = (xf @ w.float().t()) * fin[:, :1] - fin[:, 1:] * col.unsqueeze(0) + b
     qkv = y.to(torch.bfloat16)
@@ -158,75 +142,3 @@ def test_gemm256h_store_mode_exact():
     ref = a.float() @ w.float().t() + b
     err = ((c.float() - ref).abs() / (ref.abs() + 1.0)).max().item()
     assert err < 1.6e-2, err
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("B,innorm,k", [(3, False, 768), (64, True, 768), (129, True, 768), (5, True, 1024)])
-def test_ws_store_mode_exact(B, innorm, k):
-    """Mode 0 of the wave-specialised kernel (the GEMM part: Q|K|V stored instead of attended)
-    against fp32, with odd sequence counts (several tiles per CU at B = 129 x 12 heads)."""
-    _need_ws("ws")
-    dev = torch.device("cuda", 0)
-    g = torch.Generator().manual_seed(B)
-    M, N = B * 128, 2304 if k == 768 else 3072
-    a = (torch.randn(M, k, generator=g) * 1.5 + 0.2).to(torch.bfloat16)
-    w = (torch.randn(N, k, generator=g) * 0.05).to(torch.bfloat16)
-    b = torch.randn(N, generator=g)
-    fin = col = None
-    ref = a.float() @ w.float().t()
-    if innorm:
-        af = a.float()
-        rstd = torch.rsqrt(af.var(1, unbiased=False) + 1e-12)
-        fin = torch.stack([rstd, rstd * af.mean(1)], 1).contiguous()
-        col = w.float().sum(1).contiguous()
-        ref = ref * fin[:, :1] - fin[:, 1:] * col.unsqueeze(0)
-    ref = ref + b
-    c = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=dev)
-    from agent_tpu_amd.ops.qkv_attention import qkv_ws
-
-    qkv_ws(a.to(dev), w.to(dev), b.to(dev), c, 0, in_fin=fin.to(dev) if innorm else None,
-           colsum_h=col.to(dev) if innorm else None)
-    torch.cuda.synchronize()
-    err = ((c.float().cpu() - ref).abs() / (ref.abs() + 1.0)).max().item()
-    assert err < 1.6e-2, err
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("B", [1, 3, 21, 257])
-def test_ws_odd_sequence_counts(B):
-    """ws takes any number of 128-token sequences (the 256h kernel needs an even count)."""
-    _need_ws("ws")
-    dev, M, x, w, b, lens, fin, col = _case(B, 40 + B, True)
-    p = ops.qkv_head_order(H)
-    got = ops.qkv_attention(x.to(dev), w[p].contiguous().to(dev), b[p].contiguous().to(dev), lens.to(dev), H,
-                            in_fin=fin.to(dev), colsum_h=col[p].contiguous().to(dev), kernel="ws")
-    torch.cuda.synchronize()
-    ref = _ref(x, w, b, lens, fin, col, B)
-    err = (got.float().cpu() - ref).abs().max().item()
-    assert err < 2e-2 * max(ref.abs().max().item(), 1.0), err
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("var", [1, 8, 9, 24])
-def test_ws_schedule_variants_exact(var):
-    """The ws kernel's schedule variants (MMA-wave priority, 3-deep A ring) give the same
-    attention as the default schedule, bit for bit (same math, same order)."""
-    _need_ws("ws")
-    from agent_tpu_amd._native import native
-
-    B = 67
-    dev, M, x, w, b, lens, fin, col = _case(B, 90, True)
-    p = ops.qkv_head_order(H)
-    args = (x.to(dev), w[p].contiguous().to(dev), b[p].contiguous().to(dev), lens.to(dev), H)
-    kw = dict(in_fin=fin.to(dev), colsum_h=col[p].contiguous().to(dev), kernel="ws")
-    nat = native()
-    old = nat.ws_variant(-1)
-    try:
-        nat.ws_variant(0)
-        ref = ops.qkv_attention(*args, **kw)
-        nat.ws_variant(var)
-        got = ops.qkv_attention(*args, **kw)
-        torch.cuda.synchronize()
-    finally:
-        nat.ws_variant(old)
-    assert torch.equal(got, ref)

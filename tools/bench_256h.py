@@ -39,7 +39,6 @@ def main() -> int:
     ap.add_argument("--only", default="", help="comma list of kernels to time (default all)")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--full-lens", action="store_true", help="every sequence 128 tokens (the bench data)")
-    ap.add_argument("--ws-variants", default="", help="comma list of ws_variant values: ws_* timed per value")
     a = ap.parse_args()
     nat = native()
     dev = torch.device("cuda", 0)
@@ -80,7 +79,6 @@ def main() -> int:
     out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
     flop = 2.0 * M * N * K
     from agent_tpu_amd import ops
-    from agent_tpu_amd.ops.qkv_attention import qkv_ws
 
     B = M // 128
     lens = torch.randint(40, 129, (B,), device=dev, dtype=torch.int32)
@@ -103,25 +101,8 @@ def main() -> int:
         "256h_noepi": lambda: run_h(nat, x, w, b, out, fin, col, 1),
         "256h_bias": lambda: run_h(nat, x, w, b, out, None, None, 0),
     }
-    if nat.DEV_BUILD:  # the wave-specialised kernel is compiled in the dev build only
-        cands.update({
-            "ws_qkv_attn": lambda: ops.qkv_attention(x, w_h, b_h, lens, N // 192, in_fin=fin, colsum_h=col_h, out=ctx,
-                                                     kernel="ws"),
-            "ws_noepi": lambda: qkv_ws(x, w_h, b_h, out, 1, in_fin=fin, colsum_h=col_h),
-            "ws_store": lambda: qkv_ws(x, w_h, b_h, out, 0, in_fin=fin, colsum_h=col_h),
-        })
     if a.only:
         cands = {k: f for k, f in cands.items() if k in a.only.split(",")}
-    if a.ws_variants:
-        def with_var(f, var):
-            def run():
-                nat.ws_variant(var)
-                f()
-            return run
-        for k in [k for k in cands if k.startswith("ws_")]:
-            f = cands.pop(k)
-            for var in a.ws_variants.split(","):
-                cands[f"{k}@{var}"] = with_var(f, int(var))
     res = {k: [] for k in cands}
     for f in cands.values():
         for _ in range(3):
