@@ -339,13 +339,17 @@ class ClassifyEngine:
         ev = DeviceStages.event
         with span("host_csv_stage_ms", tm):
             st.submit(0, table, start, min(self.B, n), col, self.max_row_bytes, host_threads)
-        for i in range(nb):
-            slot = i % self.n_slots
+        def stage_next(i: int) -> None:
             if i + 1 < nb:
                 b1 = start + (i + 1) * self.B
                 with span("host_csv_stage_ms", tm):
                     st.submit((i + 1) % self.n_slots, table, b1, min(self.B, start + n - b1), col,
                               self.max_row_bytes, host_threads)
+
+        for i in range(nb):
+            slot = i % self.n_slots
+            if self.n_slots > 1:  # batch i+1 stages into the other slot while batch i runs
+                stage_next(i)
             stream = streams[slot]
             ks = int(stream.cuda_stream)
             with torch.cuda.stream(stream):
@@ -355,6 +359,8 @@ class ClassifyEngine:
                 with span("host_launch_ms", tm):
                     _, idx, sc = self.run_slot(slot, int(rows), dst, stream)
                 st.release(slot, ks)
+                if self.n_slots == 1:  # one slot: the next batch stages once this one released it
+                    stage_next(i)
                 r0 = i * self.B
                 c0 = ev(stream) if dst else None
                 out_idx[r0:r0 + rows].copy_(idx[:rows], non_blocking=True)

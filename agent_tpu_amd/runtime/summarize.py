@@ -395,6 +395,17 @@ def _generate_body(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
     top_mask = np.arange(K2) < nb
     rowsB = np.arange(B)[:, None]
     neg = np.float32(NEG)
+    # per-item retirement: an item whose finished hypotheses can no longer change (HF's
+    # BeamHypotheses.is_done with early_stopping, or the early-stop heuristic said no running
+    # beam can beat its worst finished one: every later candidate is pushed down by NEG) is
+    # reported at the search's next yield as (item, sequence, score), before the search ends
+    reported = np.zeros(B, dtype=bool)
+    done_q: List[Tuple[int, List[int], float]] = []
+
+    def take_done() -> List[Tuple[int, List[int], float]]:
+        out = list(done_q)
+        done_q.clear()
+        return out
     # one pinned staging row per step: [parent rows | new tokens | running beam scores]
     # -> ONE async H2D; everything after it (history reorder, token copy, step advance,
     # decoder step) is a single graph replay, and the next top-k finds the beam scores
@@ -508,6 +519,14 @@ def _generate_body(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
         best_run = run_scores[:, :1] / np.float32(float(cur) ** lp)
         worst_fin = np.where(fin_done, fin_scores.min(axis=1, keepdims=True), neg)
         unsat = unsat & (best_run > worst_fin).any(axis=1, keepdims=True)
+        item_done = ~unsat[:, 0]
+        if gen.early_stopping:
+            item_done |= fin_done.all(axis=1)
+        new = np.flatnonzero(item_done & ~reported)
+        if new.size:
+            reported[new] = True
+            for b in new.tolist():
+                done_q.append((b, fin_seq[b, 0, :int(fin_len[b, 0])].tolist(), float(fin_scores[b, 0])))
         open_beam = not (bool(fin_done.all()) and bool(gen.early_stopping))
         return not (bool(unsat.any()) and open_beam and not bool(hits.all()))
 
@@ -523,7 +542,7 @@ def _generate_body(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
     step_dev.fill_(0)
     logits = model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist, logits=not fused)
     if pin and gen.device_select:
-        yield  # let other runs start their encoders / first steps
+        yield []  # let other runs start their encoders / first steps
         on_stream()
         # Device selection: nothing the GPU needs for step t comes from the host (n-gram
         # bans read the device token history, forced tokens the device beam scores), so
@@ -581,7 +600,9 @@ def _generate_body(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
                 logits = launch_next()
             tp1 = time.perf_counter()
             if pending is not None:
-                yield  # other runs enqueue their steps while this one's record is folded in
+                # other runs enqueue their steps while this one's record is folded in; the items
+                # the previous fold retired go to the caller (SummarizeStream posts them)
+                yield take_done()
                 on_stream()
                 rec_ev[pending[1]].synchronize()  # passed already: it precedes the running step
                 steps += 1
@@ -632,6 +653,8 @@ def _generate_body(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
             cur += 1
             if stop:
                 break
+            if done_q:
+                yield take_done()  # retired items (host selection: a caller-paced search too)
     t_dec = time.perf_counter()
     seqs = [fin_seq[b, 0, :int(fin_len[b, 0])].tolist() for b in range(B)]
     scores = [float(fin_scores[b, 0]) for b in range(B)]
@@ -730,7 +753,7 @@ class SummarizeEngine:
             total = 288 * (1 << 30)
         return summarize_batch_docs(total, dims, self.max_src)
 
-    def encode_texts(self, texts: Sequence[str], with_maps: bool = True
+    def encode_texts(self, texts: Sequence[str], with_maps: bool = True, to_device: bool = True
                      ) -> Tuple[torch.Tensor, torch.Tensor, List[Dict[int, str]]]:
         """Hash-tokenize (same spec as K1, the model's vocab), wrap with the
         model's specials (T5: ``toks </s>``; BART: ``<s> toks </s>``), pad to S % 8 == 0.
@@ -757,6 +780,8 @@ class SummarizeEngine:
             arr[np.arange(B), P + ntok + k] = t
         lens_t = torch.from_numpy(L.astype(np.int32))
         vocab_maps = self.word_maps(texts) if with_maps else []
+        if not to_device:
+            return torch.from_numpy(arr), lens_t, vocab_maps
         return torch.from_numpy(arr).to(self.device), lens_t.to(self.device), vocab_maps
 
     def _reverse_map(self, text: str) -> Dict[int, str]:
@@ -871,3 +896,181 @@ def _host_pool():
 
         _POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix="atpu-summ-host")
     return _POOL
+
+
+class SummarizeStream:
+    """Continuous (in-flight) batching for single-document jobs.
+
+    Jobs are :meth:`submit`-ted at any time and :meth:`pump`-ed by the caller's loop. Up to
+    ``max_searches`` beam searches run side by side, each on its own HIP stream (the
+    :func:`generate_concurrent` pairing, generalised): every :meth:`pump` advances each running
+    search by one decode step (their launches interleave, so one search's host bookkeeping runs
+    under another's GPU step), and new documents are ADMITTED at that step boundary as a new
+    search of up to ``part_max`` documents whenever a search slot is free -- they never wait for
+    the running searches to finish. An item is RETIRED (its job completed) the step its
+    hypotheses can no longer change (``_generate_body``'s per-item retirement), not when its
+    whole search ends.
+
+    Documents are grouped by (generation settings, source-length bucket of ``SRC_BUCKET``
+    tokens): a document's padded source length depends on its own length only, never on the
+    documents it is batched with. A job's documents (``texts`` form) stay in one search.
+    ``pump`` returns ``[(tag, sequences, scores, info)]`` for the jobs completed by that call.
+    """
+
+    def __init__(self, engine: "SummarizeEngine", max_searches: Optional[int] = None,
+                 part_max: Optional[int] = None):
+        self.eng = engine
+        self.max_searches = int(max_searches or os.getenv("ATPU_SUMM_STREAMS", "3"))
+        self.part_max = int(part_max or os.getenv("ATPU_INFLIGHT_PART_MAX", "128"))
+        self.part_max = max(1, min(self.part_max, engine.max_batch_docs or self.part_max))
+        self._queues: Dict[tuple, List[tuple]] = {}  # (gen key, bucket) -> [(tag, texts, ids rows, lens, t_submit)]
+        self._active: List[dict] = []
+        self._streams: List[torch.cuda.Stream] = []
+        self.admitted = 0
+        self.searches = 0
+
+    # ------------------------------------------------------------------ admission
+    @staticmethod
+    def _gen_key(gen: GenConfig) -> tuple:
+        return (gen.num_beams, gen.max_length, gen.min_length, gen.length_penalty, gen.early_stopping,
+                gen.no_repeat_ngram_size, gen.forced_bos_id, gen.forced_eos_id, gen.use_graph, gen.device_select)
+
+    def submit(self, tag: Any, texts: Sequence[str], gen: GenConfig) -> None:
+        """Queue one job (``texts``: its documents, at least one)."""
+        ids, lens, _ = self.eng.encode_texts(list(texts), with_maps=False, to_device=False)
+        L = int(lens.max())
+        bucket = -(-L // SRC_BUCKET) * SRC_BUCKET
+        self._queues.setdefault((self._gen_key(gen), bucket), []).append(
+            (tag, list(texts), ids, lens, gen, time.perf_counter()))
+
+    def pending(self) -> int:
+        return sum(len(q) for q in self._queues.values())
+
+    def busy(self) -> bool:
+        return bool(self._active) or self.pending() > 0
+
+    def _stream(self, i: int):
+        while len(self._streams) <= i:
+            self._streams.append(torch.cuda.Stream(self.eng.device))
+        return self._streams[i]
+
+    def _start(self) -> None:
+        """Admit queued jobs as new searches while search slots are free (oldest queue first)."""
+        while len(self._active) < self.max_searches and self._queues:
+            key = min(self._queues, key=lambda k: self._queues[k][0][5])
+            q = self._queues[key]
+            take, ndocs = [], 0
+            while q and (not take or ndocs + len(q[0][1]) <= self.part_max):
+                it = q.pop(0)
+                take.append(it)
+                ndocs += len(it[1])
+            if not q:
+                del self._queues[key]
+            gen = take[0][4]
+            dev = self.eng.device
+            # the part's width: its longest source (<= the bucket); on the device the search pads
+            # every source to the bucket itself (SRC_BUCKET: generate's graph-cache padding)
+            S = max(int(it[2].shape[1]) for it in take)
+            rows = []
+            for _, _, ids, lens, _, _ in take:
+                pad = torch.full((ids.shape[0], S), int(self.eng.cfg.pad_id), dtype=ids.dtype)
+                pad[:, :ids.shape[1]] = ids
+                rows.append((pad, lens))
+            ids = torch.cat([r[0] for r in rows]).to(dev)
+            lens = torch.cat([r[1] for r in rows]).to(dev)
+            texts = [t for it in take for t in it[1]]
+            owners = [(it[0], len(it[1])) for it in take]
+            used = {a["slot"] for a in self._active}
+            slot = next(i for i in range(self.max_searches) if i not in used)
+            on_gpu = dev.type == "cuda"
+            st = self._stream(slot) if on_gpu else None
+            if on_gpu:
+                st.wait_stream(torch.cuda.current_stream(dev))  # the inputs were copied on the caller's stream
+                prep = getattr(self.eng.model, "prepare_decode", None)
+                if prep is not None:
+                    prep(int(ids.shape[1]), int(gen.resolved(self.eng.cfg).max_length))
+            maps = _host_pool().submit(self.eng.word_maps, texts)
+            it = _generate_iter(self.eng.model, ids, lens, gen, stream=st)
+            # per-document result slots; a job completes when all of its documents have
+            starts, pos = [], 0
+            for _, n in owners:
+                starts.append(pos)
+                pos += n
+            self._active.append({"it": it, "slot": slot, "owners": owners, "starts": starts, "maps": maps,
+                                 "texts": texts, "seq": [None] * len(texts), "score": [None] * len(texts),
+                                 "left": [n for _, n in owners], "t0": time.perf_counter(),
+                                 "t_submit": [x[5] for x in take]})
+            self.admitted += len(take)
+            self.searches += 1
+
+    # ------------------------------------------------------------------ stepping
+    def _deliver(self, a: dict, items, out: list, steps: Optional[int] = None) -> None:
+        maps = None
+        for b, seq, score in items:
+            if a["seq"][b] is not None:
+                continue
+            a["seq"][b], a["score"][b] = seq, score
+            # the job owning document b
+            j = max(i for i, s0 in enumerate(a["starts"]) if s0 <= b)
+            a["left"][j] -= 1
+            if a["left"][j] == 0:
+                if maps is None:
+                    maps = a["maps"].result()
+                s0, n = a["starts"][j], a["owners"][j][1]
+                summaries = [self.eng.detokenize(a["seq"][k], maps[k]) for k in range(s0, s0 + n)]
+                info = {"batched_docs": len(a["texts"]), "batched_jobs": len(a["owners"]),
+                        "queue_ms": (a["t0"] - a["t_submit"][j]) * 1e3,
+                        "search_ms": (time.perf_counter() - a["t0"]) * 1e3,
+                        "retired_early": steps is None}
+                if steps is not None:
+                    info["decode_steps"] = steps
+                out.append((a["owners"][j][0], summaries, [a["score"][k] for k in range(s0, s0 + n)], info))
+
+    def pump(self) -> List[tuple]:
+        """Admit what fits, advance every running search one step, return completed jobs."""
+        out: List[tuple] = []
+        self._start()
+        dev = self.eng.device
+        caller = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
+        try:
+            for a in list(self._active):
+                try:
+                    items = next(a["it"])
+                except StopIteration as stop:
+                    res: GenResult = stop.value
+                    self._deliver(a, [(b, s, sc) for b, (s, sc) in enumerate(zip(res.sequences, res.scores))], out,
+                                  steps=res.steps)
+                    self._active.remove(a)
+                    continue
+                if items:
+                    self._deliver(a, items, out)
+        finally:
+            if caller is not None:
+                torch.cuda.set_stream(caller)
+        return out
+
+    def cancel_queued(self) -> List[Any]:
+        """Drop every job not yet admitted to a search; returns their tags."""
+        tags = [it[0] for q in self._queues.values() for it in q]
+        self._queues.clear()
+        return tags
+
+    def abort(self) -> List[Any]:
+        """Forget everything (after a device fault): the tags of every queued and running job."""
+        tags = self.cancel_queued()
+        for a in self._active:
+            done = {j for j, left in enumerate(a["left"]) if left == 0}
+            tags += [o[0] for j, o in enumerate(a["owners"]) if j not in done]
+            try:
+                a["it"].close()
+            except Exception:
+                pass
+        self._active.clear()
+        return tags
+
+    def drain(self) -> List[tuple]:
+        """Run every queued and running search to completion."""
+        out: List[tuple] = []
+        while self.busy():
+            out.extend(self.pump())
+        return out

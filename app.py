@@ -92,6 +92,15 @@ METRICS_REFRESH_SEC = float(os.getenv("METRICS_REFRESH_SEC", "0.25"))
 # not run, nothing posted, the controller re-leases it after LEASE_TIMEOUT_MS) or "fail" (posted
 # failed with error type "Shutdown")
 SHUTDOWN_AHEAD = os.getenv("SHUTDOWN_AHEAD", "ttl").strip().lower()
+# in-flight (continuous) execution: up to this many leased jobs are held at once, leased by a
+# helper thread (pipelined HTTP/1.1 lease requests) while the device runs; batchable ops run the
+# jobs queued so far as the next device batch, map_summarize jobs join the running beam searches
+# at their next decode step (ops.register_stream_op). "auto" (default): sized from the enabled GPU
+# ops' batch sizes and LEASE_TIMEOUT_MS on a GPU agent, 1 (the serial loop) otherwise; 0/1 = the
+# serial lease -> run -> post loop. Controller-visible: the agent holds up to this many leases.
+INFLIGHT_DEPTH_RAW = os.getenv("INFLIGHT_DEPTH", "auto").strip().lower()
+# lease requests sent back to back on one keep-alive connection (at most) per round trip
+LEASE_PIPELINE_MAX = int(os.getenv("LEASE_PIPELINE_MAX", "64"))
 # a single job's result is held back for a grouped post only behind jobs shorter than this
 DEFER_MAX_JOB_SEC = float(os.getenv("DEFER_MAX_JOB_SEC", "0.001"))
 FAIL_ON_NOT_OK = os.getenv("FAIL_ON_NOT_OK", "0").strip().lower() in ("1", "true", "yes")
@@ -535,6 +544,189 @@ class PipelinedPoster:
         return redo + [(it, 1 if sent else 0) for it in items[done:]]
 
 
+class PipelinedLeaser(PipelinedPoster):
+    """``POST /v1/leases`` requests pipelined on one keep-alive connection (the in-flight mode's
+    feeder, :class:`LeaseFeeder`): ``n`` identical lease requests go out in one ``sendall`` and
+    their answers are read in order -- each a lease (its own ``lease_id`` and tasks, exactly the
+    serial loop's) or 204. The controller sees ``n`` ordinary lease requests."""
+
+    def __init__(self, base: str, timeout: float) -> None:
+        super().__init__(base, timeout)
+        import urllib.parse
+
+        u = urllib.parse.urlsplit(base)
+        self.path = (u.path.rstrip("/") + "/v1/leases").encode()
+
+    def _response_body(self) -> Tuple[int, bool, bytes]:
+        head = self._read_until(b"\r\n\r\n").decode("latin-1").split("\r\n")
+        status = head[0].split(" ", 2)
+        code = int(status[1])
+        http10 = status[0].upper() == "HTTP/1.0"
+        hdr = {}
+        for line in head[1:]:
+            k, _, v = line.partition(":")
+            hdr[k.strip().lower()] = v.strip().lower()
+        body = b""
+        if hdr.get("transfer-encoding", "") == "chunked":
+            parts = []
+            while True:
+                n = int(self._read_until(b"\r\n").split(b";")[0], 16)
+                parts.append(self._read_n(n + 2)[:n])
+                if n == 0:
+                    break
+            body = b"".join(parts)
+        elif code != 204 and code >= 200:
+            body = self._read_n(int(hdr.get("content-length", "0") or 0))
+        conn = hdr.get("connection", "")
+        return code, conn == "close" or (http10 and conn != "keep-alive"), body
+
+    def lease_many(self, n: int, body: Dict[str, Any]) -> List[Tuple[str, List[Any]]]:
+        data = _dumps(body)
+        req = (b"POST " + self.path + b" HTTP/1.1\r\nHost: " + self.host.encode() +
+               b"\r\nContent-Type: application/json\r\nContent-Length: " + str(len(data)).encode() +
+               b"\r\n\r\n" + data)
+        out: List[Tuple[str, List[Any]]] = []
+        n = 1 if self.disabled else n
+        try:
+            sock = self._connect()
+            sock.sendall(req * n)
+            for i in range(n):
+                code, close, raw = self._response_body()
+                if code == 200:
+                    resp = json.loads(raw)
+                    lease_id, tasks = resp.get("lease_id"), resp.get("tasks")
+                    if isinstance(lease_id, str) and lease_id and isinstance(tasks, list) and tasks:
+                        out.append((lease_id, tasks))
+                elif code >= 400:
+                    log_every("lease", f"{LOG} lease HTTP {code}: {raw[:200]!r}")
+                if close:
+                    self.close()
+                    if i + 1 < n:
+                        self.disabled = True
+                    break
+        except (OSError, ValueError, IndexError) as exc:
+            log_every("lease", f"{LOG} pipelined lease error: {exc}")
+            self.close()
+        return out
+
+
+class LeaseFeeder:
+    """In-flight mode (``INFLIGHT_DEPTH``): a helper thread keeps up to ``depth`` leased jobs held.
+
+    While fewer are held it sends up to ``LEASE_PIPELINE_MAX`` lease requests at once on its
+    own keep-alive connection (:class:`PipelinedLeaser`); every answered lease's tasks go to
+    the main loop's queue (``take``) and count as held until the main loop reports them
+    finished (``done``). An idle controller (204s) gets one request per ``IDLE_SLEEP_SEC``.
+    Each lease is requested with the agent's ``max_tasks`` / ``timeout_ms``: MAX_TASKS=1 (the
+    reference default) means one job per lease, many leases held."""
+
+    def __init__(self, agent: "Agent", depth: int) -> None:
+        self.agent = agent
+        self.depth = max(1, int(depth))
+        self.cv = threading.Condition()
+        self.q: List[Tuple[str, List[Any]]] = []
+        self.held = 0
+        self.leases = 0
+        self._stop = False
+        self.thread = threading.Thread(target=self._loop, name="atpu-lease-feeder", daemon=True)
+        self.thread.start()
+
+    def _loop(self) -> None:
+        ctl = Controller(CONTROLLER_URL, HTTP_TIMEOUT_SEC)
+        pipe = PipelinedLeaser(CONTROLLER_URL, HTTP_TIMEOUT_SEC) if RESULT_PIPELINE else None
+        if pipe is not None and not pipe.ok:
+            pipe = None
+        idle = False
+        while True:
+            with self.cv:
+                while not self._stop and self.held >= self.depth:
+                    self.cv.wait()
+                if self._stop:
+                    return
+                room = self.depth - self.held
+            per = max(1, MAX_TASKS)
+            n = 1 if idle else max(1, min(LEASE_PIPELINE_MAX, -(-room // per)))
+            got: List[Tuple[str, List[Any]]] = []
+            try:
+                if pipe is not None and n > 1:
+                    body = {"agent": AGENT_NAME, "capabilities": {"ops": self.agent.caps}, "max_tasks": MAX_TASKS,
+                            "timeout_ms": LEASE_TIMEOUT_MS, "labels": BASE_LABELS,
+                            "worker_profile": self.agent.profile, "metrics": METRICS.snapshot()}
+                    got = pipe.lease_many(n, body)
+                else:
+                    one = ctl.lease(self.agent.caps, self.agent.profile)
+                    got = [one] if one else []
+            except Exception as exc:
+                log_every("lease", f"{LOG} lease error: {exc}")
+                time.sleep(ERROR_BACKOFF_SEC)
+                continue
+            if got:
+                with self.cv:
+                    for lease_id, tasks in got:
+                        self.q.append((lease_id, tasks))
+                        self.held += len(tasks)
+                    self.leases += len(got)
+                    self.cv.notify_all()
+            idle = len(got) < n
+            if not got:
+                time.sleep(IDLE_SLEEP_SEC)
+
+    def take(self, timeout: float) -> List[Tuple[str, List[Any]]]:
+        with self.cv:
+            if not self.q and timeout > 0:
+                self.cv.wait_for(lambda: bool(self.q) or self._stop, timeout)
+            out, self.q = self.q, []
+            return out
+
+    def done(self, n: int) -> None:
+        if n:
+            with self.cv:
+                self.held -= n
+                self.cv.notify_all()
+
+    def stop(self) -> List[Tuple[str, List[Any]]]:
+        """Stop leasing; returns the leases taken but not handed to the main loop."""
+        with self.cv:
+            self._stop = True
+            self.cv.notify_all()
+        self.thread.join(timeout=HTTP_TIMEOUT_SEC + 5)
+        with self.cv:
+            out, self.q = self.q, []
+            return out
+
+
+def inflight_depth(caps: List[str], health: Optional[Dict[str, Any]]) -> int:
+    """``INFLIGHT_DEPTH``: an integer, or "auto" -- on an agent with a healthy GPU and a
+    batchable GPU op, the jobs the device serves within half the lease TTL at its batch sizes:
+    two engine batches per batchable op (classify rows, summarize documents from worker_sizing),
+    capped so that the held backlog finishes well inside LEASE_TIMEOUT_MS; 1 otherwise."""
+    raw = INFLIGHT_DEPTH_RAW
+    if raw not in ("", "auto"):
+        try:
+            return max(1, int(raw))
+        except ValueError:
+            return 1
+    gpu_ops = set(caps) & BATCH_OPS
+    if not gpu_ops or health is None or not health.get("ok", False):
+        return 1
+    depth = 0
+    try:
+        from worker_sizing import classify_batch_rows, probe_kfd
+
+        devs = probe_kfd()
+        hbm = devs[0]["total_memory_bytes"] if devs else 288 * (1 << 30)
+        if gpu_ops & {"map_classify", "map_classify_tpu"}:
+            depth = max(depth, 2 * classify_batch_rows(hbm, "bert-base", 128))
+        if "map_summarize" in gpu_ops:
+            # three concurrent searches of ATPU_INFLIGHT_PART_MAX documents each, plus the next round
+            part = int(os.getenv("ATPU_INFLIGHT_PART_MAX", "128"))
+            depth = max(depth, 2 * 3 * part)
+    except Exception:
+        depth = 256
+    # a held job must not sit out its lease TTL: cap by ~ a conservative device rate x TTL/2
+    return max(1, min(depth, max(64, LEASE_TIMEOUT_MS)))
+
+
 class Leaser:
     """``LEASE_PREFETCH``: lease the next task batch while the current one runs.
 
@@ -718,6 +910,7 @@ class Agent:
         self._deferred_lines: List[str] = []
         self._poster = None
         self._leaser: Optional[Leaser] = None
+        self._feeder: Optional[LeaseFeeder] = None
         if RESULT_POST_ASYNC:
             import queue
 
@@ -743,8 +936,12 @@ class Agent:
         with self._inflight_lock:
             jobs, self._inflight = dict(self._inflight), {}
             done, self._deferred = self._deferred, []
-        if self._leaser is not None:  # leased ahead, never started: fail them too (no TTL wait)
-            for lease_id, tasks in self._leaser.pending():
+        pend = list(self._leaser.pending()) if self._leaser is not None else []
+        if self._feeder is not None:
+            with self._feeder.cv:
+                pend += list(self._feeder.q)
+        if pend:  # leased ahead, never started: fail them too (no TTL wait)
+            for lease_id, tasks in pend:
                 for task in tasks:
                     try:
                         job_id, op, _, epoch = extract_task(task)
@@ -884,15 +1081,19 @@ class Agent:
         if self._poster is not None:
             self._poster.join()
 
-    def _run_batch(self, lease_id: str, jobs: List[Tuple[str, str, Dict[str, Any], Any]]) -> None:
-        """Same-op jobs of one lease as ONE device batch. Each job
-        still gets its own result with its own ``job_epoch``; a bad payload fails
-        (or soft-fails) only its own result, exactly as the single-job handler would."""
+    def _run_batch(self, lease_id: str, jobs: List[Tuple[str, str, Dict[str, Any], Any]],
+                   lease_ids: Optional[List[str]] = None) -> None:
+        """Same-op jobs as ONE device batch: the jobs of one lease, or
+        (in-flight mode) of several, ``lease_ids[i]`` naming job i's lease. Each job still
+        gets its own result with its own lease and ``job_epoch``; a bad payload fails (or
+        soft-fails) only its own result, exactly as the single-job handler would."""
         from ops import get_batch_op
 
         op = jobs[0][1]
         fn = get_batch_op(op)
-        self._begin(lease_id, jobs)
+        lids = lease_ids or [lease_id] * len(jobs)
+        if lease_ids is None:
+            self._begin(lease_id, jobs)
         t0 = time.time()
         try:
             with _op_span(f"{op}[x{len(jobs)}]"):
@@ -905,7 +1106,7 @@ class Agent:
             self._note_rank_lost(exc)
             outs = [("err", exc, tr)] * len(jobs)
         ms = (time.time() - t0) * 1000.0
-        for (job_id, _, _, epoch), res in zip(jobs, outs):
+        for (job_id, _, _, epoch), res, lid in zip(jobs, outs, lids):
             out, err = None, None
             if res[0] == "ok":
                 out = res[1]
@@ -917,7 +1118,7 @@ class Agent:
                 tr = res[2] if len(res) > 2 else "".join(
                     traceback.format_exception(type(exc), exc, exc.__traceback__, limit=12))
                 err = {"type": type(exc).__name__, "message": str(exc), "trace": tr}
-            self._finish(lease_id, job_id, op, epoch, out, err, ms, defer=True)
+            self._finish(lid, job_id, op, epoch, out, err, ms, defer=True)
         self._flush_deferred()
 
     def run_tasks(self, lease_id: str, tasks: List[Any]) -> None:
@@ -1002,6 +1203,10 @@ class Agent:
             self.profile = worker_profile(self.health, self.caps)
 
     def loop(self) -> None:
+        depth = inflight_depth(self.caps, self.health)
+        if depth > 1:
+            self._loop_inflight(depth)
+            return
         if LEASE_PREFETCH:
             self._loop_prefetch()
             return
@@ -1047,6 +1252,123 @@ class Agent:
                     # (LEASE_TIMEOUT_MS) runs out; SHUTDOWN_AHEAD=fail posts them failed now
                     # (error type "Shutdown") for controllers that re-queue failed jobs at once.
                     self._drop_ahead(*leased)
+
+    def _loop_inflight(self, depth: int) -> None:
+        """In-flight (continuous) execution, ``INFLIGHT_DEPTH`` > 1 (see :class:`LeaseFeeder`).
+
+        Each turn: take the jobs leased since the last turn; jobs of an op with an in-flight
+        executor (``ops.register_stream_op``: map_summarize) are submitted to it and join its
+        running device work at the next step boundary; jobs of a batchable op are queued and run
+        as ONE batch per op (the next engine batch) together with every other job of that op
+        leased meanwhile, from any number of leases; the rest run inline in arrival order. Then
+        every executor advances one step and the jobs it completed are posted. A job's result is
+        exactly its single-job result (ops contract); its lease and ``job_epoch`` pass through.
+        Shutdown: running device work (admitted searches, the current batch) finishes; jobs
+        held but not started are handled as ``SHUTDOWN_AHEAD`` says (left to the TTL or failed)."""
+        from ops import get_batch_op, get_stream_op
+
+        print(f"{LOG} in-flight mode: up to {depth} leased jobs held (MAX_TASKS={MAX_TASKS})", flush=True)
+        feeder = self._feeder = LeaseFeeder(self, depth)
+        execs: Dict[str, Any] = {}
+        ex_jobs: Dict[Tuple[str, str], Tuple[str, str, Dict[str, Any], Any]] = {}  # executor tag -> job
+        held_back: List[Tuple[str, List[Any]]] = []
+        try:
+            while _running:
+                busy = any(ex.busy() for ex in execs.values() if ex is not None)
+                leases = feeder.take(0.0 if busy else 0.05)
+                batches: Dict[str, List[Tuple[str, Tuple[str, str, Dict[str, Any], Any]]]] = {}
+                for lease_id, tasks in leases:
+                    for task in tasks:
+                        try:
+                            job = extract_task(task)
+                        except Exception as exc:
+                            log_every("task:bad", f"{LOG} bad task: {exc} task={repr(task)[:300]}")
+                            feeder.done(1)
+                            continue
+                        op = job[1]
+                        if op in self.handlers and op not in execs:
+                            factory = get_stream_op(op)
+                            execs[op] = factory() if factory is not None else None
+                        ex = execs.get(op)
+                        if ex is not None:
+                            self._begin(lease_id, [job])
+                            tag = (lease_id, job[0])
+                            try:
+                                early = ex.submit(tag, job[2])
+                            except Exception as exc:
+                                early = ("err", exc, traceback.format_exc(limit=12))
+                            if early is not None:
+                                self._finish_res(lease_id, job, early, 0.0)
+                                feeder.done(1)
+                            else:
+                                ex_jobs[tag] = job
+                        elif op in self.handlers and get_batch_op(op) is not None:
+                            batches.setdefault(op, []).append((lease_id, job))
+                        else:
+                            self._run_one(lease_id, job, defer=True)
+                            feeder.done(1)
+                for op, lst in batches.items():
+                    jobs = [j for _, j in lst]
+                    lids = [lid for lid, _ in lst]
+                    for lid, j in lst:
+                        self._begin(lid, [j])
+                    if len(jobs) == 1:
+                        self._run_one_begun(lids[0], jobs[0])
+                    else:
+                        self._run_batch(lids[0], jobs, lease_ids=lids)
+                    feeder.done(len(jobs))
+                for op, ex in execs.items():
+                    if ex is None or not ex.busy():
+                        continue
+                    t0 = time.time()
+                    try:
+                        done = ex.pump()
+                    except Exception as exc:  # the executor's device work failed: its jobs fail
+                        tr = traceback.format_exc(limit=12)
+                        self._note_device_fault(str(exc))
+                        done = [(tag, ("err", exc, tr)) for tag in ex.abort()]
+                    for tag, res in done:
+                        self._finish_res(tag[0], ex_jobs.pop(tag), res, (time.time() - t0) * 1000.0)
+                    feeder.done(len(done))
+                self._flush_deferred()
+        finally:
+            held_back = feeder.stop()
+            # admitted device work finishes; jobs queued in an executor but not started are not run
+            for op, ex in execs.items():
+                if ex is None:
+                    continue
+                for tag in ex.cancel_queued():
+                    job = ex_jobs.pop(tag)
+                    with self._inflight_lock:
+                        self._inflight.pop(job[0], None)
+                    held_back.append((tag[0], [{"id": job[0], "op": job[1], "payload": job[2], "job_epoch": job[3]}]))
+                while ex.busy():
+                    for tag, res in ex.pump():
+                        self._finish_res(tag[0], ex_jobs.pop(tag), res, 0.0)
+            self._flush_deferred()
+            for lease_id, tasks in held_back:
+                self._drop_ahead(lease_id, tasks)
+
+    def _finish_res(self, lease_id: str, job: Tuple[str, str, Dict[str, Any], Any], res: Any, ms: float) -> None:
+        """Post one job's ``("ok", result) | ("err", exc[, trace])`` (batch / executor form)."""
+        job_id, op, _, epoch = job
+        out, err = None, None
+        if res[0] == "ok":
+            out = res[1]
+            if FAIL_ON_NOT_OK and isinstance(out, dict) and out.get("ok") is False:
+                out, err = None, {"type": "RuntimeError", "message": str(out.get("error", "op returned ok=false")),
+                                  "trace": ""}
+        else:
+            exc = res[1]
+            tr = res[2] if len(res) > 2 else "".join(traceback.format_exception(type(exc), exc, exc.__traceback__,
+                                                                                  limit=12))
+            err = {"type": type(exc).__name__, "message": str(exc), "trace": tr}
+        self._finish(lease_id, job_id, op, epoch, out, err, ms, defer=True)
+
+    def _run_one_begun(self, lease_id: str, job: Tuple[str, str, Dict[str, Any], Any]) -> None:
+        with self._inflight_lock:
+            self._inflight.pop(job[0], None)
+        self._run_one(lease_id, job, defer=True)
 
     def _drop_ahead(self, lease_id: str, tasks: List[Any]) -> None:
         n = len(tasks)

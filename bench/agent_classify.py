@@ -34,6 +34,8 @@ def main() -> int:
                     help="csv: CSV-shard jobs; input: the reference job shape, one pre-tokenized row per job")
     ap.add_argument("--max-tasks", type=int, default=1, help="MAX_TASKS (input form: jobs per lease, batched)")
     ap.add_argument("--batch", default="1", help="LEASE_BATCH")
+    ap.add_argument("--inflight-depth", default="1",
+                    help="INFLIGHT_DEPTH of the agent: 1 = the serial loop, N or auto = in-flight (many leases held)")
     ap.add_argument("--dp", type=int, default=1,
                     help="agent ranks (torch.distributed.run, one process per GPU; rank 0 leases)")
     ap.add_argument("--controller", default="fast", choices=["fast", "mock"],
@@ -135,7 +137,8 @@ def input_form(a) -> int:
     ctl.lease(*[job(-1 - i) for i in range(a.max_tasks)], lease_id="Lwarm")
     nwarm = a.max_tasks
     env = dict(os.environ, CONTROLLER_URL=ctl.url, TASKS="map_classify", IDLE_SLEEP_SEC="0.01",
-               MAX_TASKS=str(a.max_tasks), LEASE_BATCH=a.batch, PYTHONUNBUFFERED="1")
+               MAX_TASKS=str(a.max_tasks), LEASE_BATCH=a.batch, PYTHONUNBUFFERED="1",
+               INFLIGHT_DEPTH=str(a.inflight_depth))
     p = subprocess.Popen([sys.executable, "app.py"], cwd=REPO, env=env, stdout=subprocess.DEVNULL,
                          stderr=subprocess.DEVNULL)
     try:
@@ -155,15 +158,39 @@ def input_form(a) -> int:
         print(json.dumps({"error": "timeout" if not ok else "failed jobs", "results": len(res),
                           "first_bad": bad[:1]}, default=str)[:2000])
         return 1
+    lat = _latencies(ctl, res, nwarm, a.max_tasks)
     print(json.dumps({"metric": f"classified rows/sec end to end through the agent, 1-row input jobs ({a.model}, 1 GPU)",
                       "value": round(a.jobs / el, 1), "unit": "rows/s", "higher_is_better": True,
                       "config": {"jobs": a.jobs, "max_tasks": a.max_tasks, "lease_batch": a.batch, "seq_len": S,
                                  "jobs_per_lease": a.max_tasks, "leases_per_sec": round(a.jobs / a.max_tasks / el, 1),
                                  "result_keys": sorted(res[0]["result"]),
+                                 "inflight_depth": a.inflight_depth, "job_latency_ms": lat,
                                  "controller": a.controller,
                                  "transport": "HTTP/1.1 keep-alive, loopback mock controller",
                                  "data": "synthetic token ids, random-init weights"}}), flush=True)
     return 0
+
+
+def _latencies(ctl, res, nwarm: int, per_lease: int):
+    """Per-job latency (lease answered -> result received at the controller), ms: p50 / p99 / max.
+    Timed job i rode lease 1 + i // per_lease (lease 0 is the warm-up lease)."""
+    lt = list(getattr(ctl, "lease_t", []) or [])
+    rt = list(getattr(ctl, "result_t", []) or [])
+    if lt and rt:
+        out = []
+        for k, r in enumerate(res):
+            i = int(r["job_id"][1:])
+            li = 1 + i // per_lease
+            if li < len(lt) and nwarm + k < len(rt):
+                out.append((rt[nwarm + k] - lt[li]) * 1e3)
+    else:  # the test mock: wall-clock stamps by id
+        out = [(ctl.result_times[r["job_id"]] - ctl.lease_times[f"L{(int(r['job_id'][1:]) // per_lease) * per_lease}"]) * 1e3
+               for r in res if r["job_id"] in ctl.result_times]
+    if not out:
+        return None
+    out.sort()
+    return {"p50": round(out[len(out) // 2], 1), "p99": round(out[min(len(out) - 1, int(0.99 * len(out)))], 1),
+            "max": round(out[-1], 1)}
 
 
 if __name__ == "__main__":

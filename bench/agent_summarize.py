@@ -33,6 +33,9 @@ def main() -> int:
     ap.add_argument("--max-tasks", type=int, default=256)
     ap.add_argument("--src-len", type=int, default=1024)
     ap.add_argument("--batch", default="1", help="LEASE_BATCH (0 = job by job, the reference's shape)")
+    ap.add_argument("--inflight-depth", default="1",
+                    help="INFLIGHT_DEPTH of the agent: 1 = the serial loop, N or auto = in-flight (many leases held; "
+                         "documents join running searches at decode-step boundaries)")
     a = ap.parse_args()
     from agent_tpu_amd.utils.synthetic import make_text_rows
 
@@ -46,7 +49,8 @@ def main() -> int:
     ctl.lease(*warm, lease_id="Lwarm")
     env = dict(os.environ, CONTROLLER_URL=ctl.url, TASKS="map_summarize", IDLE_SLEEP_SEC="0.01",
                MAX_TASKS=str(a.max_tasks), LEASE_BATCH=a.batch, SUMMARIZE_MODEL=a.model,
-               SUMMARIZE_MAX_SOURCE_TOKENS=str(a.src_len), PYTHONUNBUFFERED="1")
+               SUMMARIZE_MAX_SOURCE_TOKENS=str(a.src_len), PYTHONUNBUFFERED="1",
+               INFLIGHT_DEPTH=str(a.inflight_depth))
     p = subprocess.Popen([sys.executable, "app.py"], cwd=REPO, env=env, stdout=subprocess.DEVNULL,
                          stderr=subprocess.DEVNULL)
     try:
@@ -68,12 +72,19 @@ def main() -> int:
         return 1
     epochs_ok = all(r["job_epoch"] == int(r["job_id"][1:]) for r in res)
     per_job_ms = sorted(float(r["result"]["elapsed_ms"]) for r in res)
+    lat = sorted((ctl.result_times[r["job_id"]] - ctl.lease_times[f"L{(int(r['job_id'][1:]) // a.max_tasks) * a.max_tasks}"])
+                 * 1e3 for r in res)
+    lat_ms = {"p50": round(lat[len(lat) // 2], 1), "p99": round(lat[min(len(lat) - 1, int(0.99 * len(lat)))], 1),
+              "max": round(lat[-1], 1)}
     print(json.dumps({"metric": f"summarized docs/sec end to end through the agent, 1-doc jobs ({a.model}, 1 GPU)",
                       "value": round(a.jobs / el, 2), "unit": "docs/s", "higher_is_better": True,
                       "config": {"jobs": a.jobs, "max_tasks": a.max_tasks, "lease_batch": a.batch,
                                  "src_len": a.src_len, "num_beams": 4, "max_length": 130, "min_length": 30,
                                  "batched_docs": res[0]["result"].get("batched_docs", 1),
                                  "median_job_elapsed_ms": round(per_job_ms[len(per_job_ms) // 2], 1),
+                                 "inflight_depth": a.inflight_depth, "job_latency_ms": lat_ms,
+                                 "searches_batched_docs_median": sorted(r["result"].get("batched_docs", 1)
+                                                                         for r in res)[len(res) // 2],
                                  "epochs_passed_through": epochs_ok,
                                  "transport": "HTTP/1.1 keep-alive, loopback mock controller",
                                  "data": "synthetic text documents, random-init weights"}}), flush=True)

@@ -35,6 +35,8 @@ class FastController:
         self.leases: Deque[bytes] = deque()
         self._raw_leases: List[bytes] = []
         self._raw_results: List[bytes] = []
+        self.result_t: List[float] = []  # perf_counter() of each result, in arrival order
+        self.lease_t: List[float] = []   # perf_counter() of each answered (non-idle) lease, in order
         self._results: List[Dict[str, Any]] = []
         self._lease_reqs: List[Dict[str, Any]] = []
         self._cv = threading.Condition()
@@ -92,11 +94,14 @@ class FastController:
                 if path.endswith(b"/v1/results"):
                     with self._cv:
                         self._raw_results.append(body)
+                        self.result_t.append(time.perf_counter())
                     writer.write(_RESULT_OK)
                 elif path.endswith(b"/v1/leases"):
                     with self._cv:
                         self._raw_leases.append(body)
                         out = self.leases.popleft() if self.leases else _IDLE
+                        if out is not _IDLE:
+                            self.lease_t.append(time.perf_counter())
                     writer.write(out)
                 else:
                     writer.write(_answer(404, b'{"error":"not found"}'))

@@ -95,6 +95,27 @@ def get_batch_op(name: str) -> Optional[OpFn]:
     return BATCH_REGISTRY.get(name)
 
 
+#: op name -> factory of a continuous (in-flight) executor: ``factory()`` returns an object
+#: with ``submit(tag, payload)``, ``pump() -> [(tag, ("ok", result) | ("err", exc, trace))]``
+#: and ``busy() -> bool``; jobs join a running device batch at its next step boundary
+STREAM_REGISTRY: Dict[str, Callable[[], Any]] = {}
+
+
+def register_stream_op(name: str) -> Callable[[Callable[[], Any]], Callable[[], Any]]:
+    """Decorator: the in-flight executor factory of op ``name`` (app.py ``INFLIGHT_DEPTH``).
+    As for batch handlers, every result must equal the single-job handler's."""
+
+    def _wrap(fn):
+        STREAM_REGISTRY[name] = fn
+        return fn
+
+    return _wrap
+
+
+def get_stream_op(name: str) -> Optional[Callable[[], Any]]:
+    return STREAM_REGISTRY.get(name)
+
+
 def _enabled_set() -> Optional[Set[str]]:
     """Parse ``TASKS``. ``None`` means "all default ops"; a set is exact names."""
     names = [tok.strip() for tok in os.getenv("TASKS", "").split(",")]

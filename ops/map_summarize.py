@@ -29,7 +29,7 @@ import threading
 import time
 from typing import Any, Dict, List, Optional
 
-from . import register_batch_op, register_op
+from . import register_batch_op, register_op, register_stream_op
 
 
 
@@ -200,3 +200,61 @@ def handle_batch(payloads: List[Dict[str, Any]]) -> List[Any]:
             out[i] = ("ok", result(mode, mine, steps, timing, t0, batched_docs=len(all_texts),
                                    batched_jobs=len(members), **extra))
     return out
+
+
+class _InflightSummarize:
+    """In-flight executor (``ops.register_stream_op``): single-document (or ``texts``) jobs join
+    the running beam searches at their next decode-step boundary and complete the step their
+    hypotheses are final (:class:`agent_tpu_amd.runtime.summarize.SummarizeStream`). The result
+    dict is :func:`result`'s, plus the in-flight ``batched_docs`` / ``queue_ms`` details."""
+
+    def __init__(self):
+        from agent_tpu_amd.runtime.summarize import SummarizeStream
+
+        self.stream = SummarizeStream(_init_engine())
+        self.meta: Dict[Any, tuple] = {}
+
+    def submit(self, tag: Any, payload: Any) -> Optional[tuple]:
+        """Queue a job; a payload that fails validation is answered at once (its soft error)."""
+        v = _validate_one(payload)
+        if isinstance(v, dict):
+            return ("ok", v)
+        texts, mode, gen = v
+        self.meta[tag] = (mode, time.time())
+        try:
+            self.stream.submit(tag, texts, gen)
+        except Exception as exc:  # tokenization / shape errors: this job only
+            self.meta.pop(tag, None)
+            return ("err", exc)
+        return None
+
+    def busy(self) -> bool:
+        return self.stream.busy()
+
+    def cancel_queued(self) -> List[Any]:
+        tags = self.stream.cancel_queued()
+        for t in tags:
+            self.meta.pop(t, None)
+        return tags
+
+    def abort(self) -> List[Any]:
+        tags = self.stream.abort()
+        self.meta.clear()
+        return tags
+
+    def pump(self) -> List[tuple]:
+        out = []
+        for tag, summaries, _, info in self.stream.pump():
+            mode, t0 = self.meta.pop(tag)
+            steps = info.pop("decode_steps", None)
+            out.append((tag, ("ok", result(mode, summaries, steps if steps is not None else -1, {}, t0,
+                                           inflight=True, **info))))
+        return out
+
+
+@register_stream_op("map_summarize")
+def inflight_executor():
+    """None under DP (a DP job is split over the ranks by ``dispatch``; no in-flight form)."""
+    if _dp_world() > 1:
+        return None
+    return _InflightSummarize()

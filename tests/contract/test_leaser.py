@@ -124,7 +124,7 @@ def test_rank_lost_fails_the_lease_taken_ahead(monkeypatch):
     agent.ctl, agent.health, agent.exit_code = Ctl(), None, 0
     agent._inflight, agent._inflight_lock = {}, threading.Lock()
     agent._deferred, agent._deferred_lines = [], []
-    agent._poster, agent._leaser = None, None
+    agent._poster, agent._leaser, agent._feeder = None, None, None
     agent._loop_prefetch()
     assert agent.exit_code == app.EXIT_RANK_LOST and len(ran) == 1
     assert posted == [("L0", "a", 1, "failed", "RankLost"), ("L1", "b", 2, "failed", "RankLost"),

@@ -28,6 +28,7 @@ class MockController:
         self.events: List[Tuple[str, Any]] = []
         self.result_delay = 0.0
         self.result_times: Dict[str, float] = {}  # job_id -> time.time() its result was accepted
+        self.lease_times: Dict[str, float] = {}  # lease_id -> time.time() it was handed out
         self._lock = threading.Lock()
         self._cv = threading.Condition(self._lock)
         ctl = self
@@ -57,6 +58,10 @@ class MockController:
                         item = ctl.leases.popleft() if ctl.leases else (204, None)
                         lid = item[1].get("lease_id") if isinstance(item[1], dict) else None
                         ctl.events.append(("lease", lid))
+                        if lid:
+                            import time as _t
+
+                            ctl.lease_times[lid] = _t.time()
                         ctl._cv.notify_all()
                     self._send(*item)
                 elif self.path == "/v1/results":

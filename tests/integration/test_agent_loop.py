@@ -301,3 +301,30 @@ def test_short_result_is_not_held_behind_a_slow_job(ctl):
     arrived = ctl.result_times
     assert arrived["e0"] < slow_end - 1.0, (arrived, slow_end)
     assert "s0" in arrived
+
+
+def test_inflight_echo_jobs_hold_many_leases(ctl):
+    """INFLIGHT_DEPTH: one job per lease, leases requested pipelined while earlier jobs run;
+    every job resulted once with its lease and epoch."""
+    for i in range(40):
+        ctl.lease({"id": f"f{i}", "op": "echo", "payload": {"i": i}, "job_epoch": i}, lease_id=f"F{i}")
+    p = start_agent(ctl, tasks="echo", MAX_TASKS=1, INFLIGHT_DEPTH=16)
+    try:
+        assert ctl.wait(lambda c: len(c.results) >= 40, 60), ctl.results
+    finally:
+        code, out = stop_agent(p)
+    assert code == 0, out
+    assert "in-flight mode: up to 16 leased jobs held" in out
+    got = sorted((r["job_id"], r["lease_id"], r["job_epoch"], r["result"]["echo"]["i"]) for r in ctl.results)
+    assert got == sorted((f"f{i}", f"F{i}", i, i) for i in range(40))
+    assert all(r["max_tasks"] == 1 for r in ctl.lease_requests)
+
+
+def test_inflight_is_off_for_a_cpu_agent_by_default(ctl):
+    ctl.lease({"id": "g0", "op": "echo", "payload": {}}, lease_id="G0")
+    p = start_agent(ctl, tasks="echo")
+    try:
+        assert ctl.wait(lambda c: len(c.results) >= 1, 60)
+    finally:
+        code, out = stop_agent(p)
+    assert code == 0 and "in-flight mode" not in out

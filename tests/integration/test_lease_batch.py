@@ -122,3 +122,69 @@ def test_summarize_lease_batch_matches_single():
 
 if __name__ == "__main__":
     pytest.main([__file__, "-q"])
+
+
+def _run_inflight(jobs, tasks, depth, **env):
+    """Every job in a lease of its own (MAX_TASKS=1, the reference's shape), in-flight mode."""
+    ctl = MockController().start()
+    try:
+        for j in jobs:
+            ctl.lease(j, lease_id="L-" + j["id"])
+        p = start_agent(ctl, tasks=tasks, MAX_TASKS=1, INFLIGHT_DEPTH=depth, CLASSIFY_DEVICE="cpu",
+                        OMP_NUM_THREADS="2", **env)
+        try:
+            want = {j["id"] for j in jobs}
+            assert ctl.wait(lambda c: want <= {r["job_id"] for r in c.results}, 240), ctl.results
+        finally:
+            rc, out = stop_agent(p, timeout=60)
+        assert rc == 0, out[-3000:]
+        assert "in-flight mode" in out
+        return {r["job_id"]: r for r in ctl.results}, list(ctl.events)
+    finally:
+        ctl.stop()
+
+
+def test_classify_inflight_matches_single():
+    """one job per lease, many leases held; the jobs leased meanwhile run as
+    one batch, each result equal to the job-by-job run and carrying its own lease and epoch."""
+    jobs = _classify_jobs()
+    got, events = _run_inflight(jobs, "echo,map_classify", 32)
+    single, _ = _run(jobs, "echo,map_classify", "0")
+    for j in jobs:
+        assert got[j["id"]]["lease_id"] == "L-" + j["id"]
+        assert got[j["id"]]["job_epoch"] == j.get("job_epoch")
+        assert got[j["id"]]["status"] == single[j["id"]]["status"]
+    for jid in ("a", "b", "c"):
+        tb, ts = got[jid]["result"]["topk"], single[jid]["result"]["topk"]
+        assert [t["index"] for t in tb] == [t["index"] for t in ts]
+        assert all(abs(x["score"] - y["score"]) < 1e-5 for x, y in zip(tb, ts))
+    for jid in ("t1", "t2"):
+        assert got[jid]["result"]["row_count"] == single[jid]["result"]["row_count"]
+    assert got["bad"]["result"]["reason"] == single["bad"]["result"]["reason"]
+    assert got["strict"]["status"] == "failed"
+    # several leases were held at once: more than one lease was answered before the first result
+    first_result = next(i for i, e in enumerate(events) if e[0] == "result")
+    assert sum(1 for e in events[:first_result] if e[0] == "lease" and e[1]) > 1, events[:first_result + 1]
+
+
+def test_summarize_inflight_matches_single():
+    doc = "alpha beta gamma delta epsilon zeta eta theta iota kappa lambda mu "
+    jobs = [
+        {"id": "s1", "op": "map_summarize", "job_epoch": 9, "payload": {"text": doc * 3, "max_length": 10,
+                                                                      "min_length": 3}},
+        {"id": "s2", "op": "map_summarize", "payload": {"text": (doc[::-1] + " nu xi") * 2, "max_length": 10,
+                                                        "min_length": 3}},
+        {"id": "bad", "op": "map_summarize", "payload": {"text": "   "}},
+        {"id": "s3", "op": "map_summarize", "payload": {"texts": [doc, doc * 2], "max_length": 10, "min_length": 3}},
+        {"id": "s4", "op": "map_summarize", "payload": {"text": doc, "max_length": 8, "min_length": 2}},
+    ]
+    env = dict(SUMMARIZE_MODEL="t5-tiny", SUMMARIZE_FORCE_CPU="1")
+    got, _ = _run_inflight(jobs, "map_summarize", 16, **env)
+    single, _ = _run(jobs, "map_summarize", "0", **env)
+    assert got["bad"]["result"] == single["bad"]["result"] == {"ok": False, "error": "no text provided"}
+    for jid in ("s1", "s2", "s4"):
+        assert got[jid]["status"] == "succeeded", got[jid]
+        assert got[jid]["result"]["summary"] == single[jid]["result"]["summary"]
+        assert got[jid]["result"]["inflight"] is True
+    assert got["s1"]["job_epoch"] == 9 and got["s1"]["lease_id"] == "L-s1"
+    assert got["s3"]["result"]["summaries"] == single["s3"]["result"]["summaries"]
