@@ -161,6 +161,8 @@ PYBIND11_MODULE(_atpu, m) {
       py::arg("scale1"), py::arg("threads") = 8, "CPU twin of rand_fill (bit-identical values)");
   m.def("gemv_selected", &gemv_selected, py::arg("M"), py::arg("N"), py::arg("epi"),
         "true when gemm_bf16 runs this [M, N] problem / epilogue on the <= 4-row GEMV");
+  m.def("batch_invariant", &batch_invariant, py::arg("set") = -1,
+        "batch-invariant kernel selection (ATPU_BATCH_INVARIANT): 1 on, 0 off, -1 reads; returns the current");
   m.def("gemm_force_tile", &gemm_force_tile, py::arg("set") = -1, "GEMM kernel family override: 0 auto, 64, 128, 256");
   m.def("gemm_dec_mode", &gemm_dec_mode, py::arg("set") = -1,
         "skinny-M GEMM path: 1 = 64x64 multi-stage dec kernel, 0 = 128x128 split-K; returns the current");

@@ -274,60 +274,23 @@ __device__ __forceinline__ void gelu_poly16(float (&v)[16]) {
   }
 }
 
-// A/B variants of gelu_poly16 (gemm_ablate 9-11, ffn1 only): MODE & 1 = scalar
-// v_fma_f32 instead of packed pairs (a v_pk_fma_f32 issued beside another wave's
-// MFMAs costs more than its two scalar halves); MODE & 2 = degree 8 on
-// |x/sqrt2| <= 3 (max |err| 5.2e-5, tools/gelu_fit.py --deg 8 --a 3.0).
-template <int MODE>
-__device__ __forceinline__ void gelu_poly16_v(float (&v)[16]) {
-  if constexpr (MODE == 0) {
-    gelu_poly16(v);
-  } else {
-    constexpr bool kD8 = MODE & 2;
-    constexpr int kDeg = kD8 ? 8 : 10;
-    constexpr float kQ10[11] = {1.536687613e-01f,  -7.178471889e-03f, 4.856055602e-04f, -3.426085095e-05f,
-                                2.347781901e-06f,  -1.526724844e-07f, 8.713541888e-09f, -4.079194205e-10f,
-                                2.366933385e-11f,  -1.725522828e-12f, 5.926992431e-14f};
-    constexpr float kQ8[11] = {1.662152261e-01f, -8.985635825e-03f, 6.880812580e-04f, -5.386176053e-05f,
-                               3.873941750e-06f, -2.390964369e-07f, 1.633439162e-08f, -1.310694664e-09f,
-                               5.403365602e-11f, 0.f, 0.f};
-    constexpr float kClamp = kD8 ? 4.242640495e+00f : 4.596194267e+00f;
-    constexpr float kH = kD8 ? 9.0f : 1.056250000e+01f;
-    if constexpr (MODE & 1) {
-      float xc[16], w[16], p[16];
+// gelu_poly16's arithmetic on ONE value, operation for operation (a v_pk_fma_f32 lane is the
+// same correctly rounded fp32 FMA as v_fma_f32; the clamp is the same [0, 1] output modifier):
+// every GEMM family (64x64 dec, 128x128, 256x256, GEMV, split-K reduce) applies this GELU, so
+// a row's FFN output does not depend on which kernel the batch size selected (batch invariance).
+__device__ __forceinline__ float gelu_poly1(float x) {
+  constexpr int kDeg = 10;
+  constexpr float kQ[kDeg + 1] = {1.536687613e-01f,  -7.178471889e-03f, 4.856055602e-04f, -3.426085095e-05f,
+                                  2.347781901e-06f,  -1.526724844e-07f, 8.713541888e-09f, -4.079194205e-10f,
+                                  2.366933385e-11f,  -1.725522828e-12f, 5.926992431e-14f};
+  constexpr float kH = 1.056250000e+01f;
+  const float w = fmaf(x, x, -kH);
+  float p = kQ[kDeg];
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        xc[e] = __builtin_amdgcn_fmed3f(v[e], -kClamp, kClamp);
-        w[e] = fmaf(xc[e], xc[e], -kH);
-        p[e] = kD8 ? kQ8[kDeg] : kQ10[kDeg];
-      }
-#pragma unroll
-      for (int k = kDeg - 1; k >= 0; --k)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) p[e] = fmaf(p[e], w[e], kD8 ? kQ8[k] : kQ10[k]);
-#pragma unroll
-      for (int e = 0; e < 16; ++e) v[e] = v[e] * fmaf(xc[e], p[e], 0.5f);
-    } else {
-      f32x2 xc[8], w[8], p[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        xc[e] = f32x2{__builtin_amdgcn_fmed3f(v[2 * e], -kClamp, kClamp),
-                      __builtin_amdgcn_fmed3f(v[2 * e + 1], -kClamp, kClamp)};
-        w[e] = __builtin_elementwise_fma(xc[e], xc[e], f32x2{-kH, -kH});
-        p[e] = f32x2{kQ8[kDeg], kQ8[kDeg]};
-      }
-#pragma unroll
-      for (int k = kDeg - 1; k >= 0; --k)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) p[e] = __builtin_elementwise_fma(p[e], w[e], f32x2{kQ8[k], kQ8[k]});
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const f32x2 g = f32x2{v[2 * e], v[2 * e + 1]} * __builtin_elementwise_fma(xc[e], p[e], f32x2{0.5f, 0.5f});
-        v[2 * e] = g[0];
-        v[2 * e + 1] = g[1];
-      }
-    }
-  }
+  for (int k = kDeg - 1; k >= 0; --k) p = fmaf(p, w, kQ[k]);
+  float phi;
+  asm("v_fma_f32 %0, %1, %2, %3 clamp" : "=v"(phi) : "v"(x), "v"(p), "v"(0.5f));
+  return x * phi;
 }
 
 __device__ __forceinline__ float bf2f(bf16 x) { return static_cast<float>(x); }

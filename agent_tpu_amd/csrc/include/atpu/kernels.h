@@ -91,6 +91,9 @@ bool gemv_selected(int M, int N, int epi);
 int gemm_splitk_splits(int M, int N, int K);
 // skinny-M selector (benchmarks): 1 = 64x64 multi-stage dec kernel, 0 = 128x128 split-K
 int gemm_dec_mode(int set);
+// batch-invariant kernel selection (ATPU_BATCH_INVARIANT): no GEMV / split-K GEMMs, no split
+// cross attention / few-row self attention, no few-row LM head or merge; set 0/1, -1 reads
+int batch_invariant(int set);
 // kernel family override (benchmarks/tests): 0 auto, 64 dec, 128, 256; -1 reads
 int gemm_force_tile(int set);
 // 256x256 schedule selector (benchmarks): set >= 0 switches; returns the current

@@ -1026,7 +1026,7 @@ int decode_self_few(int set) {
 int decode_attention_splits(int rows, int group, int H, int seq_stride, bool cross) {
   // key chunks of the split cross attention, 0 = the per-(item, head) kernel: split while
   // the unsplit grid (items x heads) cannot cover the chip twice
-  if (!cross || group < 1 || group > 8 || seq_stride < 2 * kSplitKeys) return 0;
+  if (!cross || group < 1 || group > 8 || seq_stride < 2 * kSplitKeys || batch_invariant(-1)) return 0;
   const int nseq = (rows + group - 1) / group;
   if (nseq * H >= 512) return 0;
   return (seq_stride + kSplitKeys - 1) / kSplitKeys;
@@ -1056,7 +1056,7 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
     ATPU_CHECK(!hist || hist_stride >= seq_stride, "decode_attention: hist rows shorter than the cache");
     ATPU_CHECK(ldo % 8 == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 && (reinterpret_cast<uintptr_t>(q) & 15) == 0,
                "decode_attention: q / out need 16-B rows");
-    if (rows * H <= num_cus() && seq_stride <= 192 && decode_self_few(-1)) {
+    if (rows * H <= num_cus() && seq_stride <= 192 && decode_self_few(-1) && !batch_invariant(-1)) {
 #define ATPU_SF(KC)                                                                                                \
   hipLaunchKernelGGL((decode_self_few_kernel<KC>), dim3(rows, H), dim3(64), 0, stream, q, ldq, k, v, ldkv, seq_stride, \
                      step_dev, hist, hist_stride, bias_dist, bias_stride, out, ldo, scale)

@@ -294,7 +294,7 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_bf16_kernel(
       }
       if constexpr (EPI & kEpiGelu) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = gelu_fast(v[e]);
+        for (int e = 0; e < 4; ++e) v[e] = gelu_poly1(v[e]);
       }
       if constexpr (EPI & kEpiTanh) {
 #pragma unroll
@@ -468,7 +468,10 @@ __device__ __forceinline__ void epilogue_256(const f32x4 (&acc)[8][4], int m0, i
       const f32x4 lo4 = acc[2 * pp][j] + b4[j], hi4 = acc[2 * pp + 1][j] + b4[j];
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = lo4[e], v[4 + e] = hi4[e];
-      if constexpr (EPI & kEpiGelu) gelu_fast8(v);
+      if constexpr (EPI & kEpiGelu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = gelu_poly1(v[e]);
+      }
       if constexpr (EPI & kEpiTanh) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = tanhf(v[e]);
@@ -828,7 +831,7 @@ __device__ __forceinline__ void epilogue_256_line(const f32x4 (&acc)[8][4], int 
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[j][e] = t[e];
     }
-    if constexpr (EPI & kEpiGelu) gelu_poly16_v<GM>(*reinterpret_cast<float(*)[16]>(&v[0][0]));
+    if constexpr (EPI & kEpiGelu) gelu_poly16(*reinterpret_cast<float(*)[16]>(&v[0][0]));
     if constexpr (EPI & kEpiTanh) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -1591,7 +1594,7 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
       if constexpr (EPI & kEpiBias) v += *reinterpret_cast<const f32x4*>(bias + n);
       if constexpr (EPI & kEpiGelu) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = gelu_fast(v[e]);
+        for (int e = 0; e < 4; ++e) v[e] = gelu_poly1(v[e]);
       }
       if constexpr (EPI & kEpiTanh) {
 #pragma unroll
@@ -1703,7 +1706,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     if constexpr (EPI & kEpiBias) v += *reinterpret_cast<const f32x4*>(bias + n);
     if constexpr (EPI & kEpiGelu) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = gelu_fast(v[e]);
+      for (int e = 0; e < 4; ++e) v[e] = gelu_poly1(v[e]);
     }
     if constexpr (EPI & kEpiTanh) {
 #pragma unroll
@@ -1859,6 +1862,22 @@ bool skinny(int M, int N) { return ((M + 127) / 128) * ((N + 127) / 128) < (M <=
 bool big_fills(int M, int N) { return 2 * ((M + 255) / 256) * (N / 256) > num_cus(); }
 }  // namespace
 
+int batch_invariant(int set) {
+  // Batch-invariant kernel selection (ATPU_BATCH_INVARIANT=1, the agent's default): a row's
+  // result must not depend on how many rows share its launch. Off: the <= 4-row GEMV (v_dot2
+  // partial sums) and split-K (fp32 slices summed by a second kernel) run where they are faster;
+  // both change a row's K-summation order with the batch's row count. On: every GEMM row is one
+  // MFMA 16x16x32 chain over K in ascending order on the 64x64 / 128x128 / 256x256 kernels,
+  // which compute a row identically (the same chain, the same epilogue arithmetic and GELU);
+  // decode attention and the LM head likewise keep their per-row kernels (decode.hip, lm_head.hip).
+  static int v = [] {
+    const char* f = std::getenv("ATPU_BATCH_INVARIANT");
+    return (f && f[0] == '1') ? 1 : 0;
+  }();
+  if (set == 0 || set == 1) v = set;
+  return v;
+}
+
 int gemm_splitk_splits(int M, int N, int K) {
   // Skinny problems (decode: M = beams x docs) leave most of the 256 CUs idle.
   // dec kernel: split K only when even 64x64 tiles give < 64 blocks AND the
@@ -1872,6 +1891,7 @@ int gemm_splitk_splits(int M, int N, int K) {
     return f ? std::atoi(f) : -1;
   }();
   const int nk = K / kBK;
+  if (batch_invariant(-1)) return 1;
   int want;
   if (gemm_dec_mode(-1) == 1 && skinny(M, N)) {
     const int tiles = ((M + 63) / 64) * ((N + 63) / 64);
@@ -2119,7 +2139,7 @@ __global__ __launch_bounds__((NWV * KS + PF) * 64) void gemv_kernel(const bf16* 
     if constexpr (EPI & kEpiRowRms) v *= __builtin_amdgcn_rsqf(rs * (1.f / K) + rms_eps);
     if constexpr (EPI & kEpiRowLn) v = fmaf(v, lnst.x, -lnst.y * e_col);
     if constexpr (EPI & kEpiBias) v += e_bias;
-    if constexpr (EPI & kEpiGelu) v = gelu_fast(v);
+    if constexpr (EPI & kEpiGelu) v = gelu_poly1(v);
     if constexpr (EPI & kEpiRelu) v = fmaxf(v, 0.f);
     if constexpr (EPI & kEpiResidual) {
       if constexpr (EPI & kEpiResLn) v = fmaf(fmaf(e_res, lnst.x, -lnst.y), e_gam, v);
@@ -2166,7 +2186,8 @@ bool gemv_ok(const GemmArgs& g) {
     const char* f = std::getenv("ATPU_GEMV");
     return !(f && f[0] == '0');
   }();
-  return on && g.M <= kGemvRows && g.N % 16 == 0 && !(g.epi & ~kGemvEpis) && gemm_force_tile(-1) == 0;
+  return on && !batch_invariant(-1) && g.M <= kGemvRows && g.N % 16 == 0 && !(g.epi & ~kGemvEpis) &&
+         gemm_force_tile(-1) == 0;
 }
 
 void launch_gemv(const GemmArgs& g, hipStream_t s) {

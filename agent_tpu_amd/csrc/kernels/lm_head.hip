@@ -597,8 +597,10 @@ void lm_head_topk(const bf16* A, int lda, const bf16* W, int ldw, const float* b
   ATPU_CHECK(!(rms && has_bias), "lm_head_topk: RMSNorm folding and a bias together are not instantiated");
   // few rows, and one workgroup per CU covers the vocabulary (T5's 251 panels; BART's 393 would
   // run in two rounds at one 8-wave workgroup per CU: 44 vs 40 us per call, measured)
-  const bool few = M <= kFewRows && K % (32 * kFewWaves) == 0 && K <= 32 * kFewWaves * kFewKs && wc == kBN &&
-                   ntn <= num_cus();
+  // (batch_invariant: the per-row tiles of lm_head_topk_kernel and the one merge kernel for every M)
+  const bool inv = batch_invariant(-1) != 0;
+  const bool few = !inv && M <= kFewRows && K % (32 * kFewWaves) == 0 && K <= 32 * kFewWaves * kFewKs &&
+                   wc == kBN && ntn <= num_cus();
   if (few) {
 #define ATPU_LMF(R, B, X)                                                                                             \
   hipLaunchKernelGGL((lm_head_few_kernel<R, B, X>), dim3(ntn), dim3(kFewWaves * 64), 0, stream, A, lda, W, ldw, bias, \
@@ -635,7 +637,7 @@ void lm_head_topk(const bf16* A, int lda, const bf16* W, int ldw, const float* b
 #undef ATPU_LM_CFG
 #undef ATPU_LM
   }
-  if (M <= kMergeFewRows)
+  if (M <= kMergeFewRows && !inv)
     hipLaunchKernelGGL(lm_head_merge_few_kernel, dim3(M), dim3(kMergeFewThreads), 0, stream, hdr, cand, nslab,
                        beam_scores, topk, out_score, out_token);
   else

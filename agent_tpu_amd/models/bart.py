@@ -249,7 +249,10 @@ class BartModel:
 
     def _enc_fold_ok(self, M: int) -> bool:
         d, ff = self.cfg.d_model, self.cfg.d_ff
-        return (self.enc_ln_fold and self.cfg.enc_layers >= 2 and ops.fold_ok(M, 3 * d, d) and ops.fold_ok(M, ff, d)
+        # not under batch invariance: the fold applies from M >= 2048 rows only, so a short batch
+        # would take the LayerNorm-pass encoder and round differently
+        return (self.enc_ln_fold and not ops.batch_invariant() and self.cfg.enc_layers >= 2
+                and ops.fold_ok(M, 3 * d, d) and ops.fold_ok(M, ff, d)
                 and ops.fold_ok(M, d, ff))
 
     def _encode_folded(self, ids: torch.Tensor, lens: torch.Tensor, ckv_out: Optional[torch.Tensor] = None):

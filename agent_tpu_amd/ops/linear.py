@@ -87,8 +87,30 @@ def linear_ref(x, w, bias=None, act=None, residual=None, out_f32=False, rms_eps=
 
 
 @functools.lru_cache(maxsize=4096)
-def _splits(M: int, N: int, K: int) -> int:
+def _splits_cached(M: int, N: int, K: int, inv: bool) -> int:
     return native().gemm_splitk_splits(M, N, K)
+
+
+def _splits(M: int, N: int, K: int) -> int:
+    return _splits_cached(M, N, K, batch_invariant())
+
+
+def batch_invariant() -> bool:
+    """Batch-invariant kernel selection (``ATPU_BATCH_INVARIANT``; the agent turns it on): a
+    row's result never depends on how many rows share its launch -- no GEMV / split-K GEMMs,
+    no split cross attention or few-row self attention, no few-row LM head, and the engines
+    keep batches on their folded / padded paths (docs/ARCHITECTURE.md "Batch invariance")."""
+    try:
+        return bool(native().batch_invariant(-1))
+    except Exception:  # no extension (CPU-only oracle paths): nothing to select
+        return False
+
+
+def set_batch_invariant(on: bool) -> bool:
+    """Switch batch-invariant selection; returns the previous setting."""
+    prev = batch_invariant()
+    native().batch_invariant(1 if on else 0)
+    return prev
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: Optional[str] = None,

@@ -189,7 +189,9 @@ class ClassifyEngine:
     # so a job costs one H2D from pinned staging, one graph launch and one D2H instead
     # of ~100 eager launches (padding rows are empty and their results dropped).
     def _bucket(self, n: int) -> int:
-        b = 8
+        # batch invariance: at least 16 rows (2048 tokens), so every bucket takes the LayerNorm-
+        # folded encoder (ops.fold_ok: M >= 2048, whole 256-row tiles) that the big batches take
+        b = 16 if ops.batch_invariant() else 8
         while b < n:
             b *= 2
         return min(b, self.B)

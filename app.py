@@ -58,6 +58,9 @@ LOG = "[agent-mi355x]"
 from agent_tpu_amd.parallel.launch import ensure_rank_env  # noqa: E402
 
 ensure_rank_env()
+# a job's result must not depend on which other jobs share its device batch (lease batching,
+# in-flight batching, DP shards): batch-invariant kernel selection unless the operator opts out
+os.environ.setdefault("ATPU_BATCH_INVARIANT", "1")
 
 # ------------------------------------------------------------------ config
 # identical names and defaults to the reference (app.py:21-41)

@@ -2,7 +2,7 @@
 sharing the one GPU (gloo rehearsal of the RCCL process model), leasing
 map_classify CSV-shard jobs from the mock controller: C1 weight broadcast,
 per-rank shard classification on the HIP path, C2 all-gather of top-k, and
-the single-rank result equal to the 2-rank one."""
+the single-rank result bit-identical to the 2-rank one (batch invariance)."""
 import os
 import signal
 import socket
@@ -73,6 +73,6 @@ def test_dp_agent_classify_csv(gpu, tmp_path):
     assert [x["row"] for x in r2["rows"]] == list(range(7, 308))
     for a, b in zip(r2["rows"], r1["rows"]):
         assert [t["index"] for t in a["topk"]] == [t["index"] for t in b["topk"]]
-        # the ranks' batches have other row counts than the single rank's, so they can take
-        # other (equally accurate) kernel paths, e.g. LayerNorm folding needs rows*S % 256 == 0
-        assert abs(a["topk"][0]["score"] - b["topk"][0]["score"]) < 2e-3
+        # batch invariance (the agent's ATPU_BATCH_INVARIANT default): a rank's shard takes other
+        # row counts than the single rank's batches, and every score is still bit-identical
+        assert [t["score"] for t in a["topk"]] == [t["score"] for t in b["topk"]]
