@@ -162,6 +162,13 @@ class ClassifyEngine:
         return self._staged[slot]
 
     def run_slot(self, slot: int, rows: int, stages: Optional[DeviceStages] = None, stream=None):
+        if rows < self.B and ops.batch_invariant():
+            # batch invariance: a partial batch (a shard's tail) runs the full-batch step like every
+            # other batch -- an M-sized eager step could take other kernels (the folded encoder needs
+            # M >= 2048 and whole 256-row tiles) -- its extra rows empty strings, their results unused
+            offs = self.offs[slot]
+            offs[rows + 1:].copy_(offs[rows:rows + 1].expand(self.B - rows))
+            rows = self.B
         if stages is None:
             if self.use_graph and rows == self.B:
                 return self._graph_step(slot)
