@@ -161,8 +161,6 @@ PYBIND11_MODULE(_atpu, m) {
       py::arg("scale1"), py::arg("threads") = 8, "CPU twin of rand_fill (bit-identical values)");
   m.def("gemv_selected", &gemv_selected, py::arg("M"), py::arg("N"), py::arg("epi"),
         "true when gemm_bf16 runs this [M, N] problem / epilogue on the <= 4-row GEMV");
-  m.def("gemm_w4_mode", &gemm_w4_mode, py::arg("set") = -1,
-        "4-wave persistent GEMM for plain big-M epilogues: 0 off, 1 on, 2 timing-only (no epilogue); -1 reads");
   m.def("batch_invariant", &batch_invariant, py::arg("set") = -1,
         "batch-invariant kernel selection (ATPU_BATCH_INVARIANT): 1 on, 0 off, -1 reads; returns the current");
   m.def("gemm_force_tile", &gemm_force_tile, py::arg("set") = -1, "GEMM kernel family override: 0 auto, 64, 128, 256");

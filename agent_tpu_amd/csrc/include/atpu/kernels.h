@@ -94,8 +94,6 @@ int gemm_dec_mode(int set);
 // batch-invariant kernel selection (ATPU_BATCH_INVARIANT): no GEMV / split-K GEMMs, no split
 // cross attention / few-row self attention, no few-row LM head or merge; set 0/1, -1 reads
 int batch_invariant(int set);
-// 4-wave persistent GEMM (benchmarks / A-B): 0 off, 1 on for the plain big-M epilogues, 2 timing-only
-int gemm_w4_mode(int set);
 // kernel family override (benchmarks/tests): 0 auto, 64 dec, 128, 256; -1 reads
 int gemm_force_tile(int set);
 // 256x256 schedule selector (benchmarks): set >= 0 switches; returns the current

@@ -1349,173 +1349,6 @@ __global__ __launch_bounds__(512, 1) void gemm256s_kernel(
 }
 
 
-// ============================================================================
-// 4-wave persistent GEMM ("w4"): one wave per SIMD, 256 x 128 tiles,
-// each wave a 128 x 64 block (the same per-wave tile and fragment / epilogue layout as the
-// 8-wave kernels: acc[8][4], epilogue_256_line), a 3-slot LDS ring of [384 rows x 128 B]
-// K-tile images (A rows 0-255, B rows 256-383; 48 KiB each) fed by LDS-DMA one K-tile ahead,
-// and the k-step fragment reads software-pipelined one k-step ahead of the MFMAs (two
-// register sets, F0 / F1). Per K-tile t (gk = the workgroup's running K-tile count):
-//   A  ds_read k-step 1 of t            -> F1
-//   B  lgkmcnt(12)                      (F0 = k-step 0 of t landed)
-//   C  32 MFMAs on F0
-//   D  vmcnt: this wave's DMA of K-tile t+1 landed
-//   E  s_barrier                        (every wave's DMA of t+1 landed; every wave's reads of
-//                                        slot (gk-1)%3 retired at its G of the last K-tile)
-//   F  DMA K-tile t+2 (or the next tile's K-tile 0 / 1) -> slot (gk+2)%3
-//   G  lgkmcnt(0)                       (F1 landed)
-//   H  ds_read k-step 0 of t+1 (or of the next tile's K-tile 0) -> F0
-//   I  32 MFMAs on F1
-// The next tile's first two K-tiles are staged (and its first k-step read) under the last
-// K-tiles of this one, so a tile starts without a memory latency; its epilogue runs after.
-// ABL (timing-only, results WRONG): 1 = no epilogue (accumulators kept live).
-// ============================================================================
-constexpr int kW4Slots = 3;
-constexpr int kW4Img = 384 * 128;                  // one K-tile image: 256 A rows + 128 B rows
-constexpr int kW4EpiOff = kW4Slots * kW4Img;       // 4 waves x 2 KiB line-epilogue scratch
-constexpr int kW4BiasOff = kW4EpiOff + 4 * 2048;   // [2 tile parities][128] fp32 bias
-constexpr int kW4Lds = kW4BiasOff + 2 * 128 * 4;
-static_assert(kW4Lds <= 160 * 1024, "w4 LDS budget");
-
-template <int EPI, int ABL = 0>
-__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16* __restrict__ A, int lda,
-                                                         const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C,
-                                                         int ldc, const float* __restrict__ bias,
-                                                         const bf16* __restrict__ R, int ldr, int M, int N, int K) {
-  using namespace g2;
-  static_assert(!(EPI & (kEpiInNorm | kEpiResNorm | kEpiStatsOut | kEpiRowRms | kEpiKvScatter | kEpiOutF32)),
-                "w4: plain epilogues only");
-  __shared__ __attribute__((aligned(16))) char lds[kW4Lds];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int ntn = N / 128, ntm = M / 256, ntiles = ntm * ntn;
-  const int G = gridDim.x;
-  int v = blockIdx.x;
-  if (v >= ntiles) return;
-  const int fr = lane & 15, fc = lane >> 4;
-
-  // staging: instruction i (0..11) of this wave fills image rows rb*8..+8, rb = i*4 + wave
-  // (rb < 32: A rows, else B rows), lane = (row srow, 16-B chunk spos), source chunk swizzled
-  const bf16* src[12];
-  auto set_src = [&](int tm0, int tn0) {
-    const int srow = lane >> 3, spos = lane & 7;
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-      const int r = (i * 4 + wave) * 8 + srow;  // image row 0..383
-      src[i] = r < 256 ? A + (size_t)(tm0 + r) * lda + sw(r, spos) * 8
-                       : Bt + (size_t)(tn0 + r - 256) * ldb + sw(r - 256, spos) * 8;
-    }
-  };
-  auto stage = [&](int kt, int slot) {
-    char* base = lds + slot * kW4Img;
-#pragma unroll
-    for (int i = 0; i < 12; ++i) glds16(src[i] + kt * 64, base + (i * 4 + wave) * 1024);
-  };
-  auto stage_bias = [&](int tn0, int par) {  // every wave one 4-B DMA (waves w, w+2 the same 256 B)
-    if constexpr (EPI & kEpiBias)
-      __builtin_amdgcn_global_load_lds((const ATPU_GLOBAL_AS void*)(bias + tn0 + (wave & 1) * 64 + lane),
-                                       (ATPU_LDS_AS void*)(lds + kW4BiasOff + (par * 128 + (wave & 1) * 64) * 4), 4, 0,
-                                       0);
-  };
-  bf16x8 af0[8], bf0[4], af1[8], bf1[4];
-  auto read_k = [&](bf16x8 (&af)[8], bf16x8 (&bf)[4], int slot, int ks) {
-    const char* img = lds + slot * kW4Img;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int r = wm * 128 + i * 16 + fr;
-      af[i] = *reinterpret_cast<const bf16x8*>(img + r * 128 + sw(r, ks * 4 + fc) * 16);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int r = wn * 64 + j * 16 + fr;
-      bf[j] = *reinterpret_cast<const bf16x8*>(img + 256 * 128 + r * 128 + sw(r, ks * 4 + fc) * 16);
-    }
-  };
-  f32x4 acc[8][4];
-  auto mma = [&](const bf16x8 (&af)[8], const bf16x8 (&bf)[4]) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
-  };
-
-  const int nk = K / 64;
-  int tile = xcd_remap(v, ntiles);
-  int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 128;
-  set_src(m0, n0);
-  stage_bias(n0, 0);
-  stage(0, 0);
-  stage(1, 1);
-  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // bias + K-tile 0 landed (K-tile 1 may fly)
-  __builtin_amdgcn_s_barrier();
-  read_k(af0, bf0, 0, 0);
-  int gk = 0;    // running K-tile count: slot = gk % 3
-  int par = 0;   // bias parity of the current tile
-  for (;;) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int vn = v + G;
-    const bool has_next = vn < ntiles;
-    const int cm0 = m0, cn0 = n0;
-    for (int t = 0; t < nk; ++t) {
-      const int slot = gk % kW4Slots;
-      const bool more = t + 1 < nk || has_next;  // a K-tile (this tile's or the next one's) follows
-      read_k(af1, bf1, slot, 1);                                   // A
-      asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");         // B
-      __builtin_amdgcn_sched_barrier(0);
-      mma(af0, bf0);                                               // C
-      __builtin_amdgcn_sched_barrier(0);
-      if (more) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // D
-        __builtin_amdgcn_s_barrier();                              // E
-        const int kn = t + 2;                                      // F
-        if (kn == nk && has_next) {  // the stream runs on into the next tile
-          tile = xcd_remap(vn, ntiles);
-          m0 = (tile / ntn) * 256;
-          n0 = (tile % ntn) * 128;
-          set_src(m0, n0);
-        }
-        if (kn < nk) stage(kn, (gk + 2) % kW4Slots);
-        else if (has_next && kn - nk < nk) {
-          if (kn == nk + 1) stage_bias(n0, par ^ 1);
-          stage(kn - nk, (gk + 2) % kW4Slots);
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          // G
-      __builtin_amdgcn_sched_barrier(0);
-      if (more) read_k(af0, bf0, (gk + 1) % kW4Slots, 0);           // H
-      mma(af1, bf1);                                               // I
-      __builtin_amdgcn_sched_barrier(0);
-      ++gk;
-    }
-    if constexpr (ABL & 1) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
-    } else {
-      u32x4 pre[2][2];
-      if constexpr (EPI & kEpiResidual) {
-        const int lr = lane >> 3, lc = lane & 7;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int h = 0; h < 2; ++h)
-            pre[i][h] = load16_untracked(R + (size_t)(cm0 + wm * 128 + i * 16 + h * 8 + lr) * ldr + cn0 + wn * 64 + lc * 8);
-      }
-      epilogue_256_line<EPI, true>(acc, cm0, cn0, wm, wn, lane, C, ldc, R, ldr,
-                                   reinterpret_cast<const float*>(lds + kW4BiasOff) + par * 128,
-                                   lds + kW4EpiOff + wave * 2048, pre);
-    }
-    if (!has_next) break;
-    v = vn;
-    par ^= 1;
-  }
-}
-
 }  // namespace
 
 static int g_cu_budget = 0;
@@ -1549,39 +1382,6 @@ int64_t make_cu_mask_stream(int first_bit, int nbits) {
 }
 
 namespace {
-
-int w4_epi_ok(int epi) {
-  return epi == 0 || epi == kEpiBias || epi == (kEpiBias | kEpiGelu) || epi == (kEpiBias | kEpiResidual) ||
-         epi == kEpiResidual || epi == (kEpiBias | kEpiRelu);
-}
-
-void launch_w4(const GemmArgs& g, hipStream_t s, int abl) {
-  ATPU_CHECK(g.M % 256 == 0 && g.N % 128 == 0 && g.K % 64 == 0 && g.K >= 128, "w4: M % 256, N % 128, K % 64, K >= 128");
-  ATPU_CHECK(g.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(g.C) & 15) == 0, "w4: 16-B output rows");
-  const int tiles = (g.M / 256) * (g.N / 128);
-  int nb = std::min(tiles, num_cus());
-  if (nb >= 8) nb &= ~7;
-#define ATPU_W4(E)                                                                                              \
-  case E:                                                                                                       \
-    if (abl)                                                                                                    \
-      hipLaunchKernelGGL((gemm_w4_kernel<E, 1>), dim3(nb), dim3(256), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, \
-                         g.bias, g.R, g.ldr, g.M, g.N, g.K);                                                    \
-    else                                                                                                        \
-      hipLaunchKernelGGL((gemm_w4_kernel<E, 0>), dim3(nb), dim3(256), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, \
-                         g.bias, g.R, g.ldr, g.M, g.N, g.K);                                                    \
-    break;
-  switch (g.epi) {
-    ATPU_W4(0)
-    ATPU_W4(kEpiBias)
-    ATPU_W4(kEpiBias | kEpiGelu)
-    ATPU_W4(kEpiBias | kEpiResidual)
-    ATPU_W4(kEpiResidual)
-    ATPU_W4(kEpiBias | kEpiRelu)
-    default:
-      throw std::invalid_argument("atpu: w4 GEMM: unsupported epilogue " + std::to_string(g.epi));
-  }
-#undef ATPU_W4
-}
 
 template <bool NT, bool LINE = false>
 void launch_256s(const GemmArgs& g, hipStream_t s) {
@@ -2029,17 +1829,6 @@ int gemm_256_variant(int set) {
     ATPU_CHECK(set == 1 || set == 3 || set == 4, "gemm_256_variant: schedules 1 (256p), 3 (256l), 4 (256n)");
     v = set;
   }
-  return v;
-}
-
-int gemm_w4_mode(int set) {
-  // 4-wave persistent GEMM for the plain (non-LN-folding) big-M epilogues: 0 off (default),
-  // 1 on, 2 = timing-only ablation without the epilogue (results WRONG); ATPU_GEMM_W4
-  static int v = [] {
-    const char* f = std::getenv("ATPU_GEMM_W4");
-    return f ? std::atoi(f) : 0;
-  }();
-  if (set >= 0) v = set;
   return v;
 }
 
@@ -2617,11 +2406,6 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
                        (forced ? (forced == 256 && big_ok) : (g.M >= 2048 && big_ok && big_fills(g.M, g.N)));
   // 256s counts its epilogue's stores in the next tile's waits: whole row tiles only
   const bool persistent_ok = g.M % 256 == 0;
-  if (gemm_w4_mode(-1) && use_big && persistent_ok && g.N % 128 == 0 && w4_epi_ok(g.epi) && g.K >= 128) {
-    launch_w4(g, stream, gemm_w4_mode(-1) == 2);
-    ATPU_HIP_CHECK(hipGetLastError());
-    return;
-  }
   if (use_big && persistent_ok && kernel256 >= 2) {
     if (kernel256 == 3) launch_256s<false, true>(g, stream);
     else launch_256s<true, true>(g, stream);
