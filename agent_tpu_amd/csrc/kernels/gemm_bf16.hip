@@ -1444,6 +1444,85 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// One row's share of a 64x64 "dec" tile epilogue (also the exact few-row kernel's): the lane holds
+// row m, columns nb + j*16 + fchunk*4 .. +3 of fragments j < NJ (nb = the wave's first column;
+// with RowStats NJ = 2, nb a 32-column slab). Every operation and its order are shared, so the
+// two kernels produce the same bits for a row (batch invariance).
+template <int EPI, int NJ>
+__device__ __forceinline__ void dec_row_out(const f32x4 (&acc)[NJ], int m, int nb, int fchunk, int M, int N,
+                                            float rstd, float rmu, float2 rf, bf16* __restrict__ C, int ldc,
+                                            const float* __restrict__ bias, const bf16* __restrict__ R, int ldr,
+                                            const KvOut& kvo, const LnDec& ln, int kv_pos) {
+  static_assert(!(EPI & kEpiRowStats) || NJ == 2, "RowStats: a 32-column slab per wave");
+  if (m >= M) return;
+  float ps = 0.f, pss = 0.f;  // RowStats: this lane's share of the wave's 32-column slab
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int n = nb + j * 16 + fchunk * 4;
+    if (n >= N) continue;
+    f32x4 v = acc[j];
+    if constexpr (EPI & kEpiRowRms) v *= rstd;
+    if constexpr (EPI & kEpiRowLn) {
+      const f32x4 cs = *reinterpret_cast<const f32x4*>(ln.colsum + n);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaf(v[e], rstd, -rmu * cs[e]);
+    }
+    if constexpr (EPI & kEpiBias) v += *reinterpret_cast<const f32x4*>(bias + n);
+    if constexpr (EPI & kEpiGelu) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = gelu_poly1(v[e]);
+    }
+    if constexpr (EPI & kEpiTanh) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
+    }
+    if constexpr (EPI & kEpiRelu) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    if constexpr (EPI & kEpiResidual) {
+      const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + n);
+      if constexpr (EPI & kEpiResLn) {
+        const f32x4 g = *reinterpret_cast<const f32x4*>(ln.gamma + n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaf(fmaf(bf2f(r[e]), rf.x, -rf.y), g[e], v[e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += bf2f(r[e]);
+      }
+    }
+    if constexpr (EPI & kEpiOutF32) {
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + (size_t)m * ldc + n) = v;
+    } else {
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+      if (EPI & kEpiKvScatter) {
+        // the tile is all Q or all K|V (host: kv_col0 % 128 == 0)
+        // a step past the cache (caller bug) drops the K|V write instead of writing out of bounds
+        if (n < kvo.col0)
+          *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
+        else if (kv_pos < kvo.T)
+          *reinterpret_cast<bf16x4*>(kvo.cache + ((size_t)m * kvo.T + kv_pos) * kvo.ld + (n - kvo.col0)) = o;
+      } else {
+        *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
+      }
+      if constexpr (EPI & kEpiRowStats) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float f = bf2f(o[e]);
+          ps += f;
+          pss = fmaf(f, f, pss);
+        }
+      }
+    }
+  }
+  if constexpr (EPI & kEpiRowStats) {
+    const float S = lane_rows_sum(ps), Q = lane_rows_sum(pss);
+    if (fchunk == 0 && nb < N) *reinterpret_cast<float2*>(ln.part_out + 2 * ((size_t)(nb / 32) * M + m)) = float2{S, Q};
+  }
+}
+
 template <int EPI, int NST, int SPLIT>
 __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict__ A, int lda,
                                                           const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C,
@@ -1576,78 +1655,128 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
     if constexpr (EPI & kEpiResLn) rfs[i] = part_ln(pv[i], pslots, fchunk, rms_eps);
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int m = m0 + wm * 32 + i * 16 + frow;
-    if (m >= M) continue;
-    const float2 rf = rfs[i];
-    float ps = 0.f, pss = 0.f;  // RowStats: this lane's share of the wave's 32-column slab
+  for (int i = 0; i < 2; ++i)
+    dec_row_out<EPI, 2>(acc[i], m0 + wm * 32 + i * 16 + frow, n0 + wn * 32, fchunk, M, N, rstd[i], rmu[i], rfs[i],
+                        C, ldc, bias, R, ldr, kvo, ln, kv_pos);
+}
+
+// ============================================================================
+// Exact few-row GEMM (M <= 16, batch-invariant mode: ATPU_BATCH_INVARIANT). The <= 4-row GEMV
+// sums K with v_dot2 partials spread over lanes, so a 1-document decode step would round
+// differently from the same document inside a batch (the dec / 128 / 256 kernels). This kernel
+// computes each output exactly as gemm_dec_kernel does -- ONE v_mfma_f32_16x16x32_bf16 chain over
+// K in ascending 32-wide k-steps with the same fragment layout (lane (fr, fc): row fr, k fc*8..+8),
+// the RowRms sum of squares in the same lane order, and the shared epilogue (dec_row_out) -- but
+// with no LDS ring: one wave owns 16 x (16 NJ) outputs and streams its operands straight into MFMA
+// fragment registers, RD k-steps per round, the next round's loads in flight under this round's
+// MFMAs (two register sets). N / (16 NJ) single-wave workgroups (NJ = 2 for RowStats slabs).
+// ============================================================================
+template <int EPI, int NJ, int RD>
+__global__ __launch_bounds__(64) void gemm_few_exact_kernel(const bf16* __restrict__ A, int lda,
+                                                            const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C,
+                                                            int ldc, const float* __restrict__ bias,
+                                                            const bf16* __restrict__ R, int ldr, int M, int N, int K,
+                                                            float rms_eps, KvOut kvo, LnDec ln) {
+  const int lane = threadIdx.x, fr = lane & 15, fc = lane >> 4;
+  const int nb = blockIdx.x * 16 * NJ;  // this wave's first column
+  const bf16* ar = A + (size_t)min(fr, M - 1) * lda + fc * 8;
+  const bf16* br[NJ];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wn * 32 + j * 16 + fchunk * 4;
-      if (n >= N) continue;
-      f32x4 v = acc[i][j];
-      if constexpr (EPI & kEpiRowRms) v *= rstd[i];
-      if constexpr (EPI & kEpiRowLn) {
-        const f32x4 cs = *reinterpret_cast<const f32x4*>(ln.colsum + n);
+  for (int j = 0; j < NJ; ++j) br[j] = Bt + (size_t)min(nb + j * 16 + fr, N - 1) * ldb + fc * 8;
+  constexpr bool kPart = EPI & (kEpiRowLn | kEpiResLn);
+  float2 pv[kPartPerLane];
+  const int pslots = (EPI & kEpiRowLn) ? K / 32 : N / 32;
+  if constexpr (kPart) part_prefetch(pv, (EPI & kEpiRowLn) ? ln.in_part : ln.res_part, pslots, M, fr, fc);
+  f32x4 acc[NJ];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = fmaf(v[e], rstd[i], -rmu[i] * cs[e]);
-      }
-      if constexpr (EPI & kEpiBias) v += *reinterpret_cast<const f32x4*>(bias + n);
-      if constexpr (EPI & kEpiGelu) {
+  for (int j = 0; j < NJ; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ssq = 0.f;
+  const int nks = K / 32;
+  bf16x8 a0[RD], b0[RD][NJ], a1[RD], b1[RD][NJ];
+  auto load = [&](bf16x8 (&a)[RD], bf16x8 (&b)[RD][NJ], int r0) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = gelu_poly1(v[e]);
-      }
-      if constexpr (EPI & kEpiTanh) {
+    for (int u = 0; u < RD; ++u) {
+      const int ks = min(r0 + u, nks - 1);  // clamped: a tail round's extra k-steps are never used
+      a[u] = *reinterpret_cast<const bf16x8*>(ar + ks * 32);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
-      }
-      if constexpr (EPI & kEpiRelu) {
+      for (int j = 0; j < NJ; ++j) b[u][j] = *reinterpret_cast<const bf16x8*>(br[j] + ks * 32);
+    }
+  };
+  auto mma = [&](const bf16x8 (&a)[RD], const bf16x8 (&b)[RD][NJ], int r0) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-      }
-      if constexpr (EPI & kEpiResidual) {
-        const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * ldr + n);
-        if constexpr (EPI & kEpiResLn) {
-          const f32x4 g = *reinterpret_cast<const f32x4*>(ln.gamma + n);
+    for (int u = 0; u < RD; ++u) {
+      if (r0 + u < nks) {  // uniform
+        if constexpr (EPI & kEpiRowRms) ssq = sumsq_bf16x8(a[u], ssq);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = fmaf(fmaf(bf2f(r[e]), rf.x, -rf.y), g[e], v[e]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += bf2f(r[e]);
-        }
-      }
-      if constexpr (EPI & kEpiOutF32) {
-        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + (size_t)m * ldc + n) = v;
-      } else {
-        bf16x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
-        if (EPI & kEpiKvScatter) {
-          // the tile is all Q or all K|V (host: kv_col0 % 128 == 0)
-          // a step past the cache (caller bug) drops the K|V write instead of writing out of bounds
-          if (n < kvo.col0)
-            *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
-          else if (kv_pos < kvo.T)
-            *reinterpret_cast<bf16x4*>(kvo.cache + ((size_t)m * kvo.T + kv_pos) * kvo.ld + (n - kvo.col0)) = o;
-        } else {
-          *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
-        }
-        if constexpr (EPI & kEpiRowStats) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float f = bf2f(o[e]);
-            ps += f;
-            pss = fmaf(f, f, pss);
-          }
-        }
+        for (int j = 0; j < NJ; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[u][j], a[u], acc[j], 0, 0, 0);
       }
     }
-    if constexpr (EPI & kEpiRowStats) {
-      const float S = lane_rows_sum(ps), Q = lane_rows_sum(pss);
-      const int col = n0 + wn * 32;
-      if (fchunk == 0 && col < N) *reinterpret_cast<float2*>(ln.part_out + 2 * ((size_t)(col / 32) * M + m)) = float2{S, Q};
+  };
+  load(a0, b0, 0);
+  for (int r0 = 0; r0 < nks; r0 += 2 * RD) {
+    if (r0 + RD < nks) load(a1, b1, r0 + RD);
+    mma(a0, b0, r0);
+    if (r0 + RD < nks) {
+      if (r0 + 2 * RD < nks) load(a0, b0, r0 + 2 * RD);
+      mma(a1, b1, r0 + RD);
     }
   }
+  const int kv_pos = (EPI & kEpiKvScatter) ? max(*kvo.step, 0) : 0;
+  float rstd = (EPI & kEpiRowRms) ? __builtin_amdgcn_rsqf(lane_rows_sum(ssq) * (1.f / K) + rms_eps) : 1.f;
+  float rmu = 0.f;
+  float2 rf = float2{1.f, 0.f};
+  if constexpr (EPI & kEpiRowLn) {
+    const float2 st = part_ln(pv, pslots, fc, rms_eps);
+    rstd = st.x;
+    rmu = st.y;
+  }
+  if constexpr (EPI & kEpiResLn) rf = part_ln(pv, pslots, fc, rms_eps);
+  dec_row_out<EPI, NJ>(acc, fr, nb, fc, M, N, rstd, rmu, rf, C, ldc, bias, R, ldr, kvo, ln, kv_pos);
+}
+
+bool few_exact_ok(const GemmArgs& g) {
+  return batch_invariant(-1) && g.M <= 16 && g.N % 32 == 0 && g.K % 32 == 0 && gemm_force_tile(-1) == 0 &&
+         !(g.epi & (kEpiInNorm | kEpiResNorm | kEpiStatsOut));
+}
+
+void launch_few_exact(const GemmArgs& g, hipStream_t s) {
+  const KvOut kvo{g.kv_cache, g.kv_ld, g.kv_T, g.kv_col0, g.kv_step};
+  const LnDec ln{g.colsum, g.in_part, g.res_part, g.gamma, g.part_out};
+#define ATPU_FEW_GO(E, NJ)                                                                                           \
+  hipLaunchKernelGGL((gemm_few_exact_kernel<E, NJ, 8>), dim3(g.N / (16 * (NJ))), dim3(64), 0, s, g.A, g.lda, g.Bt,   \
+                     g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, g.rms_eps, kvo, ln)
+#define ATPU_FEW_CASE(E)                                 \
+  case E:                                                \
+    if constexpr (((E) & kEpiRowStats) != 0) ATPU_FEW_GO(E, 2); \
+    else ATPU_FEW_GO(E, 1);                              \
+    break;
+  switch (g.epi) {
+    ATPU_FEW_CASE(kEpiRowLn | kEpiBias | kEpiKvScatter)
+    ATPU_FEW_CASE(kEpiRowLn | kEpiBias)
+    ATPU_FEW_CASE(kEpiRowLn | kEpiBias | kEpiGelu)
+    ATPU_FEW_CASE(kEpiBias | kEpiResidual | kEpiResLn | kEpiRowStats)
+    ATPU_FEW_CASE(kEpiBias | kEpiResidual | kEpiRowStats)
+    ATPU_FEW_CASE(kEpiBias | kEpiResidual | kEpiResLn)
+    ATPU_FEW_CASE(kEpiRowRms | kEpiKvScatter)
+    ATPU_FEW_CASE(kEpiBias | kEpiKvScatter)
+    ATPU_FEW_CASE(kEpiRowRms)
+    ATPU_FEW_CASE(kEpiRowRms | kEpiRelu)
+    ATPU_FEW_CASE(kEpiRowRms | kEpiOutF32)
+    ATPU_FEW_CASE(0)
+    ATPU_FEW_CASE(kEpiBias)
+    ATPU_FEW_CASE(kEpiBias | kEpiGelu)
+    ATPU_FEW_CASE(kEpiBias | kEpiTanh)
+    ATPU_FEW_CASE(kEpiBias | kEpiResidual)
+    ATPU_FEW_CASE(kEpiResidual)
+    ATPU_FEW_CASE(kEpiGelu)
+    ATPU_FEW_CASE(kEpiRelu)
+    ATPU_FEW_CASE(kEpiOutF32)
+    ATPU_FEW_CASE(kEpiBias | kEpiOutF32)
+    default:
+      throw std::invalid_argument("atpu: unsupported GEMM epilogue " + std::to_string(g.epi));
+  }
+#undef ATPU_FEW_CASE
+#undef ATPU_FEW_GO
 }
 
 // Ring depth 4 (64 KiB LDS, 2 blocks/CU). 8 stages measured the same on the
@@ -2322,6 +2451,20 @@ void gemm_bf16(const GemmArgs& g, hipStream_t stream) {
   // times over; the 128x128 kernel (2 blocks/CU) covers small M and odd N.
   // ATPU_GEMM_TILE=128|256 forces one (benchmarks/tests).
   const int forced = gemm_force_tile(-1);
+  if (few_exact_ok(g) && !(g.epi & kEpiRowLn && !(g.epi & kEpiRowStats) && g.part_out)) {
+    // batch-invariant mode, <= 16 rows: the dec kernel's exact arithmetic without its LDS ring
+    if (g.epi & kEpiKvScatter)
+      ATPU_CHECK(g.kv_cache && g.kv_step && g.kv_T > 0 && g.kv_col0 % 128 == 0 && g.kv_col0 > 0 && g.kv_col0 < g.N &&
+                     g.kv_ld >= g.N - g.kv_col0 && g.kv_ld % 4 == 0,
+                 "gemm: KvScatter needs a cache, a device step, kv_col0 % 128 == 0 and kv_ld >= N - kv_col0");
+    ATPU_CHECK(!(g.epi & (kEpiRowRms | kEpiRowLn | kEpiResLn)) || g.rms_eps > 0.f, "gemm: RowRms / RowLn / ResLn need eps > 0");
+    ATPU_CHECK(!(g.epi & kEpiRowLn) || (g.colsum && g.in_part && g.K <= 1024), "gemm: RowLn needs colsum, in_part, K <= 1024");
+    ATPU_CHECK(!(g.epi & kEpiResLn) || (g.res_part && g.gamma && g.N <= 1024), "gemm: ResLn needs res_part, gamma, N <= 1024");
+    ATPU_CHECK(!(g.epi & kEpiRowStats) || g.part_out, "gemm: RowStats needs part_out");
+    launch_few_exact(g, stream);
+    ATPU_HIP_CHECK(hipGetLastError());
+    return;
+  }
   if (gemv_ok(g) && gemv_has_case(g.epi)) {  // <= 4 rows: weight-streaming GEMV (no split-K)
     launch_gemv(g, stream);
     return;

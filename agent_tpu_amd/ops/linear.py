@@ -95,6 +95,9 @@ def _splits(M: int, N: int, K: int) -> int:
     return _splits_cached(M, N, K, batch_invariant())
 
 
+_splits.cache_clear = _splits_cached.cache_clear  # (tools and tests re-read the split rule)
+
+
 def batch_invariant() -> bool:
     """Batch-invariant kernel selection (``ATPU_BATCH_INVARIANT``; the agent turns it on): a
     row's result never depends on how many rows share its launch -- no GEMV / split-K GEMMs,

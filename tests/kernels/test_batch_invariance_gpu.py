@@ -188,3 +188,53 @@ def test_classify_single_rows_equal_stacked(gpu, invariant):
     for i in (0, 5, 36):
         one = eng.classify_ids(ids[i:i + 1], lens[i:i + 1], 4)
         assert torch.equal(one.idx[0], stacked.idx[i]) and torch.equal(one.score[0], stacked.score[i]), i
+
+
+@pytest.mark.parametrize("epi", ["rms_kv", "rms_relu", "bias_res", "bias_gelu", "row_ln", "res_ln_stats", "out_f32"])
+@pytest.mark.parametrize("M,K", [(1, 768), (4, 3072), (16, 1024)])
+def test_few_row_exact_kernel_equals_dec(gpu, nat, invariant, epi, M, K):
+    """Under batch invariance <= 16 rows run gemm_few_exact_kernel (no LDS ring); it must give
+    the dec kernel's bits (ATPU_GEMM_TILE=64 forces the dec kernel on the same rows)."""
+    from agent_tpu_amd.ops.linear import row_parts_ref
+
+    N = 1024 if epi in ("row_ln", "res_ln_stats") else 768
+    x = _r((M, K), gpu, 1.0, 61)
+    w = _r((N, K), gpu, K ** -0.5, 62)
+    b = (torch.randn(N, generator=torch.Generator().manual_seed(63)) * 0.1).to(gpu)
+    res = _r((M, N), gpu, 1.0, 64)
+
+    def run():
+        if epi == "rms_kv":
+            T = 8
+            cache = torch.zeros((M * T, 2 * N), dtype=torch.bfloat16, device=gpu)
+            w3 = _r((3 * N, K), gpu, K ** -0.5, 65)
+            q = ops.linear(x, w3, rms_eps=1e-6, kv_cache=(cache, T, torch.tensor([3], dtype=torch.int32,
+                                                                                   device=gpu), N))
+            return [q, cache]
+        if epi == "rms_relu":
+            return [ops.linear(x, w, act="relu", rms_eps=1e-6)]
+        if epi == "bias_res":
+            return [ops.linear(x, w, b, residual=res)]
+        if epi == "bias_gelu":
+            return [ops.linear(x, w, b, act="gelu")]
+        if epi == "out_f32":
+            return [ops.linear(x, w, out_f32=True, rms_eps=1e-6)]
+        if epi == "row_ln":
+            if K > 1024:
+                pytest.skip("RowLn rows are <= 1024 wide")
+            part = row_parts_ref(x).contiguous()
+            return [ops.linear(x, w, b, act="gelu", row_ln=(1e-5, w.float().sum(1).contiguous(), part))]
+        part = torch.empty((N // 32, M, 2), dtype=torch.float32, device=gpu)
+        gam = (1 + 0.1 * torch.randn(N, generator=torch.Generator().manual_seed(66))).to(gpu)
+        y = ops.linear(x, w, b, residual=res, res_ln=(1e-5, row_parts_ref(res).contiguous(), gam), stats_out=part)
+        return [y, part]
+
+    got = run()
+    prev = _tile(nat, 64)
+    try:
+        ref = run()
+    finally:
+        nat.gemm_force_tile(prev)
+    torch.cuda.synchronize()
+    for a_, b_ in zip(got, ref):
+        assert torch.equal(a_, b_), epi
