@@ -187,15 +187,13 @@ PYBIND11_MODULE(_atpu, m) {
   m.def("decode_attention", [](uintptr_t q, int ldq, uintptr_t k, uintptr_t v, int ldkv, int seq_stride, int group,
                                uintptr_t lens, uintptr_t step_dev, uintptr_t hist, int hist_stride, uintptr_t bias,
                                int bias_stride, uintptr_t out, int ldo, int rows, int H, float scale, uintptr_t stream,
-                               uintptr_t ws, uintptr_t tickets) {
+                               uintptr_t ws) {
     decode_attention(P<const bf16>(q), ldq, P<const bf16>(k), P<const bf16>(v), ldkv, seq_stride, group,
                      P<const int32_t>(lens), P<const int32_t>(step_dev), P<const int32_t>(hist), hist_stride,
-                     P<const float>(bias), bias_stride, P<bf16>(out), ldo, rows, H, scale, S(stream), P<float>(ws),
-                     P<int32_t>(tickets));
+                     P<const float>(bias), bias_stride, P<bf16>(out), ldo, rows, H, scale, S(stream), P<float>(ws));
   }, py::arg("q"), py::arg("ldq"), py::arg("k"), py::arg("v"), py::arg("ldkv"), py::arg("seq_stride"), py::arg("group"),
      py::arg("lens"), py::arg("step_dev"), py::arg("hist"), py::arg("hist_stride"), py::arg("bias"), py::arg("bias_stride"),
-     py::arg("out"), py::arg("ldo"), py::arg("rows"), py::arg("H"), py::arg("scale"), py::arg("stream"), py::arg("ws") = 0,
-     py::arg("tickets") = 0);
+     py::arg("out"), py::arg("ldo"), py::arg("rows"), py::arg("H"), py::arg("scale"), py::arg("stream"), py::arg("ws") = 0);
   m.def("decode_attention_ws_floats", [](int rows, int group, int H, int seq_stride, bool cross) {
     return decode_attention_ws_floats(rows, group, H, seq_stride, cross);
   });
@@ -265,7 +263,6 @@ PYBIND11_MODULE(_atpu, m) {
   m.def("lm_head_ws_bytes", &lm_head_ws_bytes);
   m.def("lm_head_stages", &lm_head_stages, py::arg("set") = -1);
   m.def("decode_self_few", &decode_self_few, py::arg("set") = -1);
-  m.def("decode_cross_fuse", &decode_cross_fuse, py::arg("set") = -1);
   m.def(
       "lm_head_topk",
       [](uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t bias, float rms_eps, int M, int V, int K, int topk,

@@ -121,12 +121,11 @@ int64_t make_cu_mask_stream(int first_bit, int nbits);  // hipStream_t over CU-m
 void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int ldkv, int seq_stride, int group,
                       const int32_t* lens, const int32_t* step_dev, const int32_t* hist, int hist_stride,
                       const float* bias_dist, int bias_stride, bf16* out, int ldo, int rows, int H, float scale,
-                      hipStream_t stream, float* ws = nullptr, int32_t* tickets = nullptr);
+                      hipStream_t stream, float* ws = nullptr);
 // Cross attention (lens) over a grid of few items splits the keys into 64-key chunks
 // (flash decoding) when given a workspace of this many floats (0: no split for the shape).
 int decode_attention_splits(int rows, int group, int H, int seq_stride, bool cross);
 size_t decode_attention_ws_floats(int rows, int group, int H, int seq_stride, bool cross);
-int decode_cross_fuse(int set);  // 1: split cross attention combined by the last chunk when given tickets (default)
 int decode_self_few(int set);  // 1: few-row self attention one wave per (row, head), T <= 192 (default); -1 reads
 // one-workgroup state advance of a small beam search (rows x stride x 4 B x (seq ? 2 : 1) <= 64 KiB):
 // hist / seq reordered in place by par (as beam_reorder_hist, seq with last = tok, off 1),

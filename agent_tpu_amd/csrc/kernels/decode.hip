@@ -332,66 +332,28 @@ __global__ __launch_bounds__(NW * 64) void decode_self_attention_kernel(
 // ----------------------------------------------------------------------------
 constexpr int kSplitKeys = 64;
 constexpr int kSplitRec = 2 + kD;  // floats per (row, head, chunk): max, sum, o[64]
-constexpr int kMaxSplits = kMaxKeys / kSplitKeys;
-
-// out[row][h*64 + d] = sum_c o_c[d] e^(m_c - M) / sum_c l_c e^(m_c - M), M = max_c m_c, for
-// rows row0 .. row0+G-1 (G <= GM) of head h, one wave: lane c < NS loads chunk c's (max, sum)
-// and the weights are reduced across lanes; then lane = dimension sums the chunks' o. Every
-// load of every row is issued before the first reduction (a loop of dependent rounds took
-// 8 us per call); NSM >= NS chunk slots per row. decode_attn_combine_kernel and the split
-// kernel's last arriving workgroup both run this, so the one- and two-launch forms give the
-// same bits.
-template <int GM, int NSM>
-__device__ __forceinline__ void attn_combine_rows(const float* __restrict__ ws, int NS, int H, int row0, int G, int h,
-                                                  bf16* __restrict__ out, int ldo) {
-  const int lane = threadIdx.x & 63;
-  float ov[GM][NSM], m[GM], l[GM];
-#pragma unroll
-  for (int g = 0; g < GM; ++g) {
-    if (g < G) {
-      const float* r = ws + ((size_t)(row0 + g) * H + h) * NS * kSplitRec;
-#pragma unroll
-      for (int c = 0; c < NSM; ++c) ov[g][c] = r[min(c, NS - 1) * kSplitRec + 2 + lane];
-      m[g] = lane < NS ? r[lane * kSplitRec] : -FLT_MAX;
-      l[g] = lane < NS ? r[lane * kSplitRec + 1] : 0.f;
-    }
-  }
-#pragma unroll
-  for (int g = 0; g < GM; ++g) {
-    if (g < G) {
-      const float M = wave_max(m[g]);
-      const float w = lane < NS ? __expf(m[g] - M) : 0.f;  // 0 for an empty chunk (max -FLT_MAX)
-      const float L = wave_sum(w * l[g]);
-      float o = 0.f;
-#pragma unroll
-      for (int c = 0; c < NSM; ++c)
-        o += (c < NS ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), c)) : 0.f) * ov[g][c];
-      out[(size_t)(row0 + g) * ldo + h * kD + lane] = f2bf(L > 0.f ? o / L : 0.f);
-    }
-  }
-}
 
 template <int GM>
-__device__ __forceinline__ void attn_combine_any(const float* __restrict__ ws, int NS, int H, int row0, int G, int h,
-                                                 bf16* __restrict__ out, int ldo) {
-  if (NS <= 16)
-    attn_combine_rows<GM, 16>(ws, NS, H, row0, G, h, out, ldo);
-  else
-    attn_combine_rows<GM, kMaxSplits>(ws, NS, H, row0, G, h, out, ldo);
-}
-
-// One (item, head, 64-key chunk) of the split cross attention: scores, softmax partials and
-// the unnormalised P.V of the chunk's n >= 1 keys for the item's G beam rows, into rec(g).
-template <int GM, class Rec>
-__device__ __forceinline__ void cross_split_chunk(const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k,
-                                                  const bf16* __restrict__ v, int ldkv, int seq_stride, int group,
-                                                  int seq, int h, int G, int len, int jb, int n,
-                                                  const float* __restrict__ bias_dist, int bias_stride, Rec rec,
-                                                  float scale) {
+__global__ __launch_bounds__(64) void decode_cross_split_kernel(
+    const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k, const bf16* __restrict__ v, int ldkv,
+    int seq_stride, int group, int nrows, const int32_t* __restrict__ lens, const float* __restrict__ bias_dist,
+    int bias_stride, float* __restrict__ ws, int H, float scale) {
   typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
   __shared__ float pl[GM][kSplitKeys];
+  const int seq = blockIdx.x, h = blockIdx.y, c = blockIdx.z, NS = gridDim.z;
   const int lane = threadIdx.x;
+  const int G = min(group, nrows - seq * group);
+  const int len = min(lens[seq], seq_stride);
+  const int jb = c * kSplitKeys, n = max(0, min(kSplitKeys, len - jb));
   auto at = [&](int j) -> size_t { return ((size_t)seq * seq_stride + j) * ldkv + h * kD; };
+  auto rec = [&](int g) { return ws + (((size_t)(seq * group + g) * H + h) * NS + c) * kSplitRec; };
+  if (n == 0) {  // a chunk past this item's source length contributes nothing
+    for (int i = lane; i < G * kSplitRec; i += 64) {
+      const int g = i / kSplitRec, e = i % kSplitRec;
+      rec(g)[e] = e == 0 ? -FLT_MAX : 0.f;
+    }
+    return;
+  }
   // every load before any use: the beams' queries (lane = (beam, 16-B chunk); through
   // LDS, as per-beam scalar loads they cost one round trip per beam), the bias, the K
   // row of key jb + lane and the V slabs of P.V
@@ -473,51 +435,28 @@ __device__ __forceinline__ void cross_split_chunk(const bf16* __restrict__ q, in
   }
 }
 
-template <int GM>
-__global__ __launch_bounds__(64) void decode_cross_split_kernel(
-    const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k, const bf16* __restrict__ v, int ldkv,
-    int seq_stride, int group, int nrows, const int32_t* __restrict__ lens, const float* __restrict__ bias_dist,
-    int bias_stride, float* __restrict__ ws, int H, float scale, int* __restrict__ tickets, bf16* __restrict__ out,
-    int ldo) {
-  const int seq = blockIdx.x, h = blockIdx.y, c = blockIdx.z, NS = gridDim.z;
-  const int lane = threadIdx.x;
-  const int G = min(group, nrows - seq * group);
-  const int len = min(lens[seq], seq_stride);
-  const int jb = c * kSplitKeys, n = max(0, min(kSplitKeys, len - jb));
-  auto rec = [&](int g) { return ws + (((size_t)(seq * group + g) * H + h) * NS + c) * kSplitRec; };
-  if (n == 0) {  // a chunk past this item's source length contributes nothing
-    for (int i = lane; i < G * kSplitRec; i += 64) {
-      const int g = i / kSplitRec, e = i % kSplitRec;
-      rec(g)[e] = e == 0 ? -FLT_MAX : 0.f;
-    }
-  } else {
-    cross_split_chunk<GM>(q, ldq, k, v, ldkv, seq_stride, group, seq, h, G, len, jb, n, bias_dist, bias_stride, rec,
-                          scale);
-  }
-  if (tickets == nullptr) return;  // decode_attn_combine_kernel follows
-  // last arriver: the (item, head)'s NS chunk workgroups each take a ticket after their records
-  // are out (release); the one that draws NS - 1 sees every record (acquire), combines the
-  // item's rows and puts the counter back to 0 for the next launch. No workgroup waits.
-  const int slot = seq * H + h;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  int t = 0;
-  if (lane == 0) t = __hip_atomic_fetch_add(tickets + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  t = __builtin_amdgcn_readfirstlane(t);
-  if (t != NS - 1) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  if (lane == 0) tickets[slot] = 0;
-  const int row0 = seq * group;
-  if constexpr (GM == 1) {
-    attn_combine_any<1>(ws, NS, H, row0, G, h, out, ldo);
-  } else {
-    for (int g0 = 0; g0 < G; g0 += 4) attn_combine_any<4>(ws, NS, H, row0 + g0, min(4, G - g0), h, out, ldo);
-  }
-}
-
-// one wave per (row, head); the split kernel does the same in its last arriver when given tickets
+// out[row][h*64 + d] = sum_c o_c[d] e^(m_c - M) / sum_c l_c e^(m_c - M), M = max_c m_c
+// (one wave per (row, head)): lane c < NS loads chunk c's (max, sum) and the weights are
+// reduced across lanes; then lane = dimension sums the chunks' o with every load issued
+// before the first add (a loop of dependent rounds took 8 us per call)
+constexpr int kMaxSplits = kMaxKeys / kSplitKeys;
 __global__ __launch_bounds__(64) void decode_attn_combine_kernel(const float* __restrict__ ws, int NS, int H,
                                                                  bf16* __restrict__ out, int ldo) {
-  attn_combine_any<1>(ws, NS, H, blockIdx.x, 1, blockIdx.y, out, ldo);
+  const int row = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
+  const float* r = ws + ((size_t)row * H + h) * NS * kSplitRec;
+  float ov[kMaxSplits];
+#pragma unroll
+  for (int c = 0; c < kMaxSplits; ++c) ov[c] = r[min(c, NS - 1) * kSplitRec + 2 + lane];
+  const float m = lane < NS ? r[lane * kSplitRec] : -FLT_MAX;
+  const float l = lane < NS ? r[lane * kSplitRec + 1] : 0.f;
+  const float M = wave_max(m);
+  const float w = lane < NS ? __expf(m - M) : 0.f;  // 0 for an empty chunk (max -FLT_MAX)
+  const float L = wave_sum(w * l);
+  float o = 0.f;
+#pragma unroll
+  for (int c = 0; c < kMaxSplits; ++c)
+    o += (c < NS ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), c)) : 0.f) * ov[c];
+  out[(size_t)row * ldo + h * kD + lane] = f2bf(L > 0.f ? o / L : 0.f);
 }
 
 // ----------------------------------------------------------------------------
@@ -1084,20 +1023,8 @@ int decode_self_few(int set) {
   return v;
 }
 
-int decode_cross_fuse(int set) {
-  // split cross attention combined by each (item, head)'s last arriving chunk workgroup when the
-  // caller passes tickets (one launch instead of two); ATPU_DEC_XFUSE=0 keeps the combine kernel
-  static int v = [] {
-    const char* f = std::getenv("ATPU_DEC_XFUSE");
-    return (f && f[0] == '0') ? 0 : 1;
-  }();
-  if (set == 0 || set == 1) v = set;
-  return v;
-}
-
 int decode_attention_splits(int rows, int group, int H, int seq_stride, bool cross) {
-  // key chunks of the split cross attention, 0 = the per-(item, head) kernel: split while
-  // the unsplit grid (items x heads) cannot cover the chip twice
+  // key chunks of the split cross attention, 0 = the per-(item, head) kernel
   if (!cross || group < 1 || group > 8 || seq_stride < 2 * kSplitKeys) return 0;
   const int nseq = (rows + group - 1) / group;
   // batch invariance: the split form for every item count (an item's keys always go through the
@@ -1115,7 +1042,7 @@ size_t decode_attention_ws_floats(int rows, int group, int H, int seq_stride, bo
 void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int ldkv, int seq_stride, int group,
                       const int32_t* lens, const int32_t* step_dev, const int32_t* hist, int hist_stride,
                       const float* bias_dist, int bias_stride, bf16* out, int ldo, int rows, int H, float scale,
-                      hipStream_t stream, float* ws, int32_t* tickets) {
+                      hipStream_t stream, float* ws) {
   ATPU_CHECK(rows > 0 && H > 0 && group >= 1, "decode_attention: bad shape");
   ATPU_CHECK(lens || step_dev, "decode_attention: need lens or a device step");
   ATPU_CHECK(!hist || (step_dev && group == 1), "decode_attention: hist is for self attention (group 1)");
@@ -1164,12 +1091,9 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
     static_assert(kMaxSplits * kSplitKeys >= kMaxKeys, "combine kernel chunk count");
     ATPU_CHECK(ldq % 8 == 0 && (reinterpret_cast<uintptr_t>(q) & 15) == 0, "decode_attention: q needs 16-B rows");
     ATPU_CHECK((reinterpret_cast<uintptr_t>(ws) & 15) == 0, "decode_attention: ws must be 16-byte aligned");
-    // tickets (nseq x H zeroed counters, left zeroed): the last chunk of each (item, head) combines
-    int* tk = decode_cross_fuse(-1) ? reinterpret_cast<int*>(tickets) : nullptr;
-    ATPU_CHECK(!tk || (ldo % 8 == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0), "decode_attention: out needs 16-B rows");
 #define ATPU_DS(GM)                                                                                               \
   hipLaunchKernelGGL((decode_cross_split_kernel<GM>), dim3(nseq, H, ns), dim3(64), 0, stream, q, ldq, k, v, ldkv, \
-                     seq_stride, group, rows, lens, bias_dist, bias_stride, ws, H, scale, tk, out, ldo)
+                     seq_stride, group, rows, lens, bias_dist, bias_stride, ws, H, scale)
     if (group == 1) {
       ATPU_DS(1);
     } else if (group <= 4) {
@@ -1179,10 +1103,8 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
     }
 #undef ATPU_DS
     ATPU_HIP_CHECK(hipGetLastError());
-    if (!tk) {
-      hipLaunchKernelGGL(decode_attn_combine_kernel, dim3(rows, H), dim3(64), 0, stream, ws, ns, H, out, ldo);
-      ATPU_HIP_CHECK(hipGetLastError());
-    }
+    hipLaunchKernelGGL(decode_attn_combine_kernel, dim3(rows, H), dim3(64), 0, stream, ws, ns, H, out, ldo);
+    ATPU_HIP_CHECK(hipGetLastError());
     return;
   }
 #define ATPU_DA(GM, NW)                                                                                          \

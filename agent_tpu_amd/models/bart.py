@@ -336,7 +336,7 @@ class BartModel:
 
     def step(self, tokens: torch.Tensor, step: torch.Tensor, cache: torch.Tensor, T: int, ckv: torch.Tensor,
              src_lens: torch.Tensor, S: int, group: int, hist: Optional[torch.Tensor] = None, logits: bool = True,
-             x0: Optional[torch.Tensor] = None, tickets: Optional[torch.Tensor] = None):
+             x0: Optional[torch.Tensor] = None):
         """One decoder position for ``rows`` sequences -> fp32 logits [rows, V] (see T5Model.step)."""
         cfg, p = self.cfg, self.p
         d, H = cfg.d_model, cfg.heads
@@ -346,7 +346,7 @@ class BartModel:
         x = x0 if x0 is not None else ops.embed_pos_layernorm(tokens, p["shared"], p["dec.pos"], step, POS_OFFSET,
                                                               p["dec.ln_emb_g"], p["dec.ln_emb_b"], cfg.eps)
         if self.ln_fold:
-            return self._step_folded(x, step, cache, T, ckv, src_lens, S, group, hist, logits, tickets)
+            return self._step_folded(x, step, cache, T, ckv, src_lens, S, group, hist, logits)
         for i in range(cfg.dec_layers):
             q = f"dec.l{i}."
             c = cache[i]
@@ -361,7 +361,7 @@ class BartModel:
                               p[q + "ln1_b"], cfg.eps)
             cq = ops.linear(x, p[q + "cq_w"], p[q + "cq_b"])
             kv = ckv[:, i * 2 * d:(i + 1) * 2 * d]
-            ctx = ops.decode_attention(cq, kv[:, :d], kv[:, d:], H, S, group, lens=src_lens, scale=scale, tickets=tickets)
+            ctx = ops.decode_attention(cq, kv[:, :d], kv[:, d:], H, S, group, lens=src_lens, scale=scale)
             x = ops.layernorm(ops.linear(ctx, p[q + "co_w"], p[q + "co_b"], residual=x), p[q + "lnc_g"],
                               p[q + "lnc_b"], cfg.eps)
             f = ops.linear(x, p[q + "f1_w"], p[q + "f1_b"], act="gelu")
@@ -382,7 +382,7 @@ class BartModel:
                 and nat.gemv_selected(rows, cfg.d_ff, EPI_ROW_LN | EPI_BIAS | EPI_GELU)
                 and nat.gemv_selected(rows, d, EPI_BIAS | EPI_RESIDUAL | EPI_RES_LN))
 
-    def _step_folded(self, x, step, cache, T, ckv, src_lens, S, group, hist, logits=True, tickets=None):
+    def _step_folded(self, x, step, cache, T, ckv, src_lens, S, group, hist, logits=True):
         """:meth:`step` with the decoder LayerNorms folded into the GEMMs (only the last one
         runs as a pass). The GEMM producing a pre-LN row writes its partial (sum, sumsq) per
         32-column slab; the GEMM reading LN(x) as input and the one adding LN(x) as its
@@ -426,7 +426,7 @@ class BartModel:
             cq = ops.linear(x1, f[q + "cq_w"], f[q + "cq_b"], row_ln=(eps, f[q + "cq_c"], inp(p1)), row_ln_out=ro(p1),
                             prefetch=(p[q + "co_w"], rpb))
             kv = ckv[:, i * 2 * d:(i + 1) * 2 * d]
-            ctx = ops.decode_attention(cq, kv[:, :d], kv[:, d:], H, S, group, lens=src_lens, scale=scale, tickets=tickets)
+            ctx = ops.decode_attention(cq, kv[:, :d], kv[:, d:], H, S, group, lens=src_lens, scale=scale)
             x2 = ops.linear(ctx, p[q + "co_w"], f[q + "co_b"], residual=x1, res_ln=(eps, p1, p[q + "ln1_g"]),
                             stats_out=so(p2), prefetch=f[q + "f1_w"])
             h = ops.linear(x2, f[q + "f1_w"], f[q + "f1_b"], act="gelu", row_ln=(eps, f[q + "f1_c"], inp(p2)),

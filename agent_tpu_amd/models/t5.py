@@ -288,7 +288,7 @@ class T5Model:
 
     def step(self, tokens: torch.Tensor, step: torch.Tensor, cache: torch.Tensor, T: int, ckv: torch.Tensor,
              src_lens: torch.Tensor, S: int, group: int, hist: Optional[torch.Tensor] = None, logits: bool = True,
-             x0: Optional[torch.Tensor] = None, tickets: Optional[torch.Tensor] = None):
+             x0: Optional[torch.Tensor] = None):
         """One decoder position for ``rows`` sequences -> fp32 logits [rows, V]
         (``logits=False``: the :class:`ops.LmHead` input for the fused LM head + top-k).
 
@@ -296,9 +296,7 @@ class T5Model:
         cache rows of sequence r are r*T .. r*T+T-1; encoder rows of batch item
         r // group are (r//group)*S ... ``hist`` (int32 [rows, T]) are beam
         backpointers: position j < step of row r was computed by row hist[r, j].
-        Every argument is a device tensor, so the step is hipGraph-capturable. ``tickets``
-        (``ops.new_tickets``, one per search): the split cross attention combines in its last
-        arriving workgroup (one launch per layer instead of two, same bits).
+        Every argument is a device tensor, so the step is hipGraph-capturable.
         """
         cfg, p = self.cfg, self.p
         d, H = cfg.d_model, cfg.heads
@@ -308,7 +306,7 @@ class T5Model:
         if x.dtype != p["dec.l0.qkv"].dtype:
             x = x.to(p["dec.l0.qkv"].dtype)
         if self.rms_fold:
-            return self._step_folded(x, step, cache, T, ckv, src_lens, S, group, hist, dbias, logits, tickets)
+            return self._step_folded(x, step, cache, T, ckv, src_lens, S, group, hist, dbias, logits)
         for i in range(cfg.dec_layers):
             q = f"dec.l{i}."
             c = cache[i]
@@ -320,7 +318,7 @@ class T5Model:
             y = ops.rmsnorm(x, p[q + "ln2"], cfg.eps)
             cq = ops.linear(y, p[q + "cq"])
             kv = ckv[:, i * 2 * d:(i + 1) * 2 * d]
-            ctx = ops.decode_attention(cq, kv[:, :d], kv[:, d:], H, S, group, lens=src_lens, tickets=tickets)
+            ctx = ops.decode_attention(cq, kv[:, :d], kv[:, d:], H, S, group, lens=src_lens)
             x = ops.linear(ctx, p[q + "co"], residual=x)
             y = ops.rmsnorm(x, p[q + "ln3"], cfg.eps)
             f = ops.linear(y, p[q + "wi"], act="relu")
@@ -328,7 +326,7 @@ class T5Model:
         y = ops.rmsnorm(x, p["dec.ln_f"], cfg.eps)
         return ops.lm_head(y, p["lm"], None, 0.0, logits)
 
-    def _step_folded(self, x, step, cache, T, ckv, src_lens, S, group, hist, dbias, logits=True, tickets=None):
+    def _step_folded(self, x, step, cache, T, ckv, src_lens, S, group, hist, dbias, logits=True):
         """:meth:`step` with each RMSNorm folded into its consumer GEMM (37 fewer launches
         per step, no normalised copy of x); logits equal the unfolded step to bf16 rounding."""
         cfg, p, f = self.cfg, self.p, self.rms_folded()
@@ -349,7 +347,7 @@ class T5Model:
             x = ops.linear(ctx, p[q + "o"], residual=x, prefetch=f[q + "cq"])
             cq = ops.linear(x, f[q + "cq"], rms_eps=eps, prefetch=p[q + "co"])
             kv = ckv[:, i * 2 * d:(i + 1) * 2 * d]
-            ctx = ops.decode_attention(cq, kv[:, :d], kv[:, d:], H, S, group, lens=src_lens, tickets=tickets)
+            ctx = ops.decode_attention(cq, kv[:, :d], kv[:, d:], H, S, group, lens=src_lens)
             x = ops.linear(ctx, p[q + "co"], residual=x, prefetch=f[q + "wi"])
             h = ops.linear(x, f[q + "wi"], act="relu", rms_eps=eps, prefetch=p[q + "wo"])
             x = ops.linear(h, p[q + "wo"], residual=x, prefetch=nxt_qkv[i])

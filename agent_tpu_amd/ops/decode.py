@@ -30,16 +30,11 @@ HEAD_DIM = 64
 def decode_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, H: int, seq_stride: int, group: int = 1,
                      lens: Optional[torch.Tensor] = None, step: Optional[torch.Tensor] = None,
                      bias_dist: Optional[torch.Tensor] = None, scale: float = 1.0,
-                     out: Optional[torch.Tensor] = None, hist: Optional[torch.Tensor] = None,
-                     tickets: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     out: Optional[torch.Tensor] = None, hist: Optional[torch.Tensor] = None) -> torch.Tensor:
     """q [R, >=H*64]; k/v 2-D row views with ``seq_stride`` rows per sequence.
 
     ``hist`` (int32 [R, T], self attention only): key j < t of row r lives in
     the cache of row ``hist[r, j]``.
-    ``tickets`` (cross attention): a zeroed int32 buffer of at least items x H counters that
-    only this stream uses (:func:`new_tickets`); the split cross attention then combines its
-    key chunks in the last arriving workgroup of each (item, head) instead of a second
-    launch (same bits), and leaves the counters zeroed for the next call.
     """
     R = q.shape[0]
     if not q.is_cuda:
@@ -59,22 +54,11 @@ def decode_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, H: int, 
     # captured decoder step it comes from the graph's pool)
     nws = native().decode_attention_ws_floats(R, group, H, seq_stride, lens is not None and hist is None)
     ws = torch.empty(nws, dtype=torch.float32, device=q.device) if nws else None
-    if tickets is not None and nws:
-        check(tickets.dtype == torch.int32 and tickets.is_contiguous() and tickets.device == q.device
-              and tickets.numel() >= -(-R // group) * H, "tickets must be int32 [>= items * H] on q's device")
-    else:
-        tickets = None
     native().decode_attention(ptr(q), row_stride(q, "q"), ptr(k), ptr(v), row_stride(k, "k"), seq_stride, group,
                               ptr(lens), ptr(step), ptr(hist), 0 if hist is None else hist.shape[1], ptr(bias_dist),
                               0 if bias_dist is None else bias_dist.shape[1], ptr(out), row_stride(out, "out"), R, H,
-                              float(scale), launch_stream(q), ptr(ws), ptr(tickets))
+                              float(scale), launch_stream(q), ptr(ws))
     return out
-
-
-def new_tickets(rows: int, H: int, device) -> torch.Tensor:
-    """Zeroed last-arriver counters for :func:`decode_attention` (``rows * H`` covers any group);
-    one buffer per stream of decoder steps (a search's slot), reused by every layer and step."""
-    return torch.zeros(rows * H, dtype=torch.int32, device=device)
 
 
 def _decode_attention_ref(q, k, v, H, seq_stride, group, lens, step, bias_dist, scale, out, hist=None):

@@ -365,18 +365,15 @@ def _generate_body(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
     if slot is not None:
         b = slot.bufs
         cache, hist, hist_alt, step_dev = b["cache"], b["hist"], b["hist_alt"], b["step"]
-        tickets = b["tickets"]
         hist.zero_()
         hist_alt.zero_()
     else:
         cache = model.new_cache(rows, T)
-        # the cross attention's last-arriver counters: this search's stream only
-        tickets = ops.new_tickets(rows, model.cfg.heads, dev) if dev.type == "cuda" else None
         hist = torch.zeros((rows, T), dtype=torch.int32, device=dev)
         hist_alt = torch.zeros_like(hist)
         step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
         if new_slot is not None:
-            new_slot.bufs.update(ckv=ckv, cache=cache, hist=hist, hist_alt=hist_alt, step=step_dev, tickets=tickets)
+            new_slot.bufs.update(ckv=ckv, cache=cache, hist=hist, hist_alt=hist_alt, step=step_dev)
 
     # Host beam state lives in numpy: the per-step bookkeeping is ~40 tiny
     # array ops, ~4x cheaper than torch CPU ops, and everything that is not
@@ -455,7 +452,7 @@ def _generate_body(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
             ops.decode_advance(hist, seq_dev, par_dev, tok_dev, tokens, step_dev, embed=emb, out=x0)
             if x0 is not None:
                 return model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist, logits=not fused,
-                                  x0=x0, tickets=tickets)
+                                  x0=x0)
         else:
             ops.beam_reorder_hist(hist, hist_alt, par_dev, step_dev)
             hist.copy_(hist_alt)  # keep the captured buffer address
@@ -464,8 +461,7 @@ def _generate_body(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
                 seq_dev.copy_(seq_alt)
             tokens.copy_(tok_dev)
             step_dev.add_(1)
-        return model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist, logits=not fused,
-                          tickets=tickets)
+        return model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist, logits=not fused)
 
     def launch_next() -> torch.Tensor:
         nonlocal graph, g_logits
@@ -544,8 +540,7 @@ def _generate_body(model, src_ids: torch.Tensor, src_lens: torch.Tensor, gen: Ge
     cur = 1  # sequence length so far (decoder start token included)
     steps = 0
     step_dev.fill_(0)
-    logits = model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist, logits=not fused,
-                        tickets=tickets)
+    logits = model.step(tokens, step_dev, cache, T, ckv, src_lens, S, nb, hist=hist, logits=not fused)
     if pin and gen.device_select:
         yield []  # let other runs start their encoders / first steps
         on_stream()

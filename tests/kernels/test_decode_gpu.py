@@ -55,29 +55,6 @@ def test_decode_cross_split_keys(gpu, lens, group, S, H, scale):
         assert _rel(out, ref) < 2e-2
 
 
-@pytest.mark.parametrize("lens,group,S,H,scale", [([1, 63, 64, 65, 128, 1024], 4, 1024, 12, 1.0),
-                                                   ([1000], 4, 1024, 12, 0.125), ([130, 7], 1, 130, 16, 1.0),
-                                                   ([700, 3, 640], 8, 704, 12, 1.0), ([200, 199], 3, 256, 12, 1.0),
-                                                   ([2048, 1500, 9], 4, 2048, 16, 1.0), ([1024] * 40, 4, 1024, 12, 1.0)])
-def test_decode_cross_last_arriver_combine(gpu, lens, group, S, H, scale):
-    """Split cross attention given tickets: each (item, head)'s last arriving chunk workgroup
-    combines (one launch). Bit-identical to the split + combine kernels, the counters are back
-    at zero after every call, and the same tickets serve call after call."""
-    nseq = len(lens)
-    rows = nseq * group - (1 if group > 2 else 0)
-    q = _r((rows, 3 * H * 64), gpu, seed=44)[:, :H * 64]
-    kv = _r((nseq * S, 2 * H * 64), gpu, seed=45)
-    lt = torch.tensor(lens, dtype=torch.int32).to(gpu)
-    tickets = ops.new_tickets(rows, H, gpu)
-    for bias in (None, _r((H, S), gpu, 1.0, torch.float32, seed=46)):
-        two = ops.decode_attention(q, kv[:, :H * 64], kv[:, H * 64:], H, S, group, lens=lt, bias_dist=bias, scale=scale)
-        for _ in range(3):
-            one = ops.decode_attention(q, kv[:, :H * 64], kv[:, H * 64:], H, S, group, lens=lt, bias_dist=bias,
-                                       scale=scale, tickets=tickets)
-            assert torch.equal(one, two)
-        assert not tickets.any()
-
-
 @pytest.mark.parametrize("rows,H,T,t", [(4, 12, 130, 70), (1, 12, 130, 0), (8, 16, 300, 299)])
 def test_decode_self_head_groups(gpu, rows, H, T, t):
     # few rows: the per-row self-attention kernel spreads the heads over grid.y
