@@ -319,61 +319,78 @@ __global__ __launch_bounds__(NW * 64) void decode_self_attention_kernel(
 }
 
 // ----------------------------------------------------------------------------
-// Cross attention with the keys split over workgroups ("flash decoding"), for grids
-// the per-(item, head) kernel leaves idle: 1 document x 12 heads is 12 workgroups on
-// 256 CUs, each walking 1024 keys through dependent load rounds (23 us per call where
-// the K/V bytes take < 1 us). Here one wave per (item, head, 64-key chunk):
+// Cross attention in 64-key chunks ("flash decoding"). The split kernel runs one wave per
+// (item, head, chunk) for grids the per-(item, head) kernel leaves idle: 1 document x 12
+// heads is 12 workgroups on 256 CUs, each walking 1024 keys through dependent load rounds
+// (23 us per call where the K/V bytes take < 1 us). Per chunk:
 //   scores : lane = key, its 128-B K row in 8 x 16-B loads, v_dot2 with each of the
-//            item's G beam queries (registers), wave max / sum per query;
+//            item's G beam queries (LDS), butterfly max / sum over the beams;
 //   P.V    : lane = (key sub 0..7, 8 dims), all 8 V slabs' loads in flight at once,
 //            probabilities through LDS, xor-reduce over the key subs;
-//   output : per (row, head, chunk) {max, sum, o[64]} (o unnormalised) into ws.
-// decode_attn_combine_kernel rescales the chunks to the global max and divides.
+//   record : per (row, chunk) {max, sum, o[64]} (o unnormalised).
+// decode_attn_combine_kernel rescales a row's chunks to the global max and divides. The
+// chunked kernel runs the SAME chunk and combine code with the records in LDS, one workgroup
+// per (item, head) (no record traffic; for many items), so both forms give the same bits
+// and batch-invariant mode can pick either by the grid size.
 // ----------------------------------------------------------------------------
 constexpr int kSplitKeys = 64;
 constexpr int kSplitRec = 2 + kD;  // floats per (row, head, chunk): max, sum, o[64]
+constexpr int kMaxSplits = kMaxKeys / kSplitKeys;
+
+struct XsArgs {  // one (item, head) of the cross attention
+  const bf16* q;
+  const bf16* k;
+  const bf16* v;
+  const float* bias_dist;
+  int ldq, ldkv, seq_stride, group, bias_stride, seq, h, G, len;
+  float scale;
+};
+
+struct XsRegs {  // one chunk's operands: the K row of key jb + lane, the V slabs, the bias
+  bf16x8 kk[8];
+  bf16x8 vv[kSplitKeys / 8];
+  float bj;
+};
+
+// the item's G beam queries (lane = (beam, 16-B chunk)) -> LDS; the caller syncs. The row is
+// clamped, not the load predicated: a load under `qg < G` merged with an undefined value may be
+// speculated for every lane by the compiler, i.e. read past the last item's rows (it was, and
+// faulted on a small q).
+__device__ __forceinline__ bf16x8 xs_query_load(const XsArgs& a) {
+  const int lane = threadIdx.x & 63, qg = min(lane >> 3, a.G - 1), qe = lane & 7;
+  return *reinterpret_cast<const bf16x8*>(a.q + (size_t)(a.seq * a.group + qg) * a.ldq + a.h * kD + qe * 8);
+}
 
 template <int GM>
-__global__ __launch_bounds__(64) void decode_cross_split_kernel(
-    const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k, const bf16* __restrict__ v, int ldkv,
-    int seq_stride, int group, int nrows, const int32_t* __restrict__ lens, const float* __restrict__ bias_dist,
-    int bias_stride, float* __restrict__ ws, int H, float scale) {
-  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-  __shared__ float pl[GM][kSplitKeys];
-  const int seq = blockIdx.x, h = blockIdx.y, c = blockIdx.z, NS = gridDim.z;
-  const int lane = threadIdx.x;
-  const int G = min(group, nrows - seq * group);
-  const int len = min(lens[seq], seq_stride);
-  const int jb = c * kSplitKeys, n = max(0, min(kSplitKeys, len - jb));
-  auto at = [&](int j) -> size_t { return ((size_t)seq * seq_stride + j) * ldkv + h * kD; };
-  auto rec = [&](int g) { return ws + (((size_t)(seq * group + g) * H + h) * NS + c) * kSplitRec; };
-  if (n == 0) {  // a chunk past this item's source length contributes nothing
-    for (int i = lane; i < G * kSplitRec; i += 64) {
-      const int g = i / kSplitRec, e = i % kSplitRec;
-      rec(g)[e] = e == 0 ? -FLT_MAX : 0.f;
-    }
-    return;
-  }
-  // every load before any use: the beams' queries (lane = (beam, 16-B chunk); through
-  // LDS, as per-beam scalar loads they cost one round trip per beam), the bias, the K
-  // row of key jb + lane and the V slabs of P.V
-  __shared__ bf16x8 qsh[GM][8];
-  const int qg = lane >> 3, qe = lane & 7;
-  bf16x8 qv;
-  if (qg < G) qv = *reinterpret_cast<const bf16x8*>(q + (size_t)(seq * group + qg) * ldq + h * kD + qe * 8);
+__device__ __forceinline__ void xs_query_store(const XsArgs& a, const bf16x8& qv, bf16x8 (&qsh)[GM][8]) {
+  const int lane = threadIdx.x & 63, qg = lane >> 3, qe = lane & 7;
+  if (qg < a.G) qsh[qg][qe] = qv;
+}
+
+// every load of chunk [jb, jb + n), n >= 1, issued at once
+__device__ __forceinline__ void xs_load(const XsArgs& a, int jb, int n, XsRegs& r) {
+  const int lane = threadIdx.x & 63;
+  auto at = [&](int j) -> size_t { return ((size_t)a.seq * a.seq_stride + j) * a.ldkv + a.h * kD; };
   const int jk = jb + min(lane, n - 1);
-  const float bj = bias_dist ? bias_dist[h * bias_stride + (len - 1 - jk)] : 0.f;
-  bf16x8 kk[8];
-  const bf16* kr = k + at(jk);
+  r.bj = a.bias_dist ? a.bias_dist[a.h * a.bias_stride + (a.len - 1 - jk)] : 0.f;
+  const bf16* kr = a.k + at(jk);
 #pragma unroll
-  for (int e = 0; e < 8; ++e) kk[e] = *reinterpret_cast<const bf16x8*>(kr + e * 8);
+  for (int e = 0; e < 8; ++e) r.kk[e] = *reinterpret_cast<const bf16x8*>(kr + e * 8);
   const int ksub = lane >> 3, dc = (lane & 7) * 8;
-  bf16x8 vv[kSplitKeys / 8];
 #pragma unroll
   for (int u = 0; u < kSplitKeys / 8; ++u)
-    vv[u] = *reinterpret_cast<const bf16x8*>(v + at(jb + min(u * 8 + ksub, n - 1)) + dc);
-  if (qg < G) qsh[qg][qe] = qv;
-  __syncthreads();
+    r.vv[u] = *reinterpret_cast<const bf16x8*>(a.v + at(jb + min(u * 8 + ksub, n - 1)) + dc);
+}
+
+// chunk [jb, jb + n) of the loaded operands -> the G rows' records rec(g) (one wave; pl is
+// the wave's own probability rows). Every multiply-add here and in xs_combine is an explicit
+// fma or an unfusable product, so the split and chunked kernels (different surrounding code)
+// cannot differ in the compiler's contraction choices.
+template <int GM, class Rec>
+__device__ __forceinline__ void xs_compute(const XsArgs& a, int n, const XsRegs& r, const bf16x8 (&qsh)[GM][8],
+                                           float (&pl)[GM][kSplitKeys], Rec rec) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  const int lane = threadIdx.x & 63, G = a.G;
   // every beam's score first, then ONE butterfly max and ONE butterfly sum over the beams
   // (wave_bfly: lane l ends with beam l >> kSh) instead of a wave max and sum per beam
   constexpr int kSh = GM == 1 ? 6 : GM == 4 ? 4 : 3;
@@ -388,10 +405,10 @@ __global__ __launch_bounds__(64) void decode_cross_split_kernel(
         const bf16x8 qq = qsh[g][e];
 #pragma unroll
         for (int t = 0; t < 4; ++t)
-          d[t] = __builtin_amdgcn_fdot2_f32_bf16(bf16x2_t{kk[e][2 * t], kk[e][2 * t + 1]},
+          d[t] = __builtin_amdgcn_fdot2_f32_bf16(bf16x2_t{r.kk[e][2 * t], r.kk[e][2 * t + 1]},
                                                  bf16x2_t{qq[2 * t], qq[2 * t + 1]}, d[t], false);
       }
-      sjv[g] = lane < n ? ((d[0] + d[1]) + (d[2] + d[3])) * scale + bj : -FLT_MAX;
+      sjv[g] = lane < n ? __builtin_fmaf((d[0] + d[1]) + (d[2] + d[3]), a.scale, r.bj) : -FLT_MAX;
     }
   }
   const float mxl = wave_bfly<GM>(sjv, OpMax{});
@@ -403,7 +420,8 @@ __global__ __launch_bounds__(64) void decode_cross_split_kernel(
     if (g < G) pl[g][lane] = pv[g];
   }
   const float sml = wave_bfly<GM>(pv, OpAdd{});  // beam lane >> kSh
-  __syncthreads();
+  __builtin_amdgcn_wave_barrier();  // (one wave: LDS ops complete in order)
+  const int ksub = lane >> 3, dc = (lane & 7) * 8;
   float o[GM][8];
 #pragma unroll
   for (int g = 0; g < GM; ++g)
@@ -417,46 +435,145 @@ __global__ __launch_bounds__(64) void decode_cross_split_kernel(
       if (g < G) {
         const float pj = jl < n ? pl[g][jl] : 0.f;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[g][e] += pj * bf2f(vv[u][e]);
+        for (int e = 0; e < 8; ++e) o[g][e] = __builtin_fmaf(pj, bf2f(r.vv[u][e]), o[g][e]);
       }
     }
   }
 #pragma unroll
   for (int g = 0; g < GM; ++g) {
     if (g < G) {
-      float* r = rec(g);
+      float* rp = rec(g);
       // the 8 dims over the key subs (lane bits 3-5) by butterfly: lane l ends with dim dc + ksub
-      r[2 + dc + ksub] = wave_bfly_rows8(o[g]);
+      rp[2 + dc + ksub] = wave_bfly_rows8(o[g]);
       if (lane == (g << kSh)) {
-        r[0] = mxg[g];
-        r[1] = sml;
+        rp[0] = mxg[g];
+        rp[1] = sml;
       }
     }
   }
+  __builtin_amdgcn_wave_barrier();  // pl is rewritten by the wave's next chunk
 }
 
-// out[row][h*64 + d] = sum_c o_c[d] e^(m_c - M) / sum_c l_c e^(m_c - M), M = max_c m_c
-// (one wave per (row, head)): lane c < NS loads chunk c's (max, sum) and the weights are
-// reduced across lanes; then lane = dimension sums the chunks' o with every load issued
-// before the first add (a loop of dependent rounds took 8 us per call)
-constexpr int kMaxSplits = kMaxKeys / kSplitKeys;
-__global__ __launch_bounds__(64) void decode_attn_combine_kernel(const float* __restrict__ ws, int NS, int H,
-                                                                 bf16* __restrict__ out, int ldo) {
-  const int row = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
-  const float* r = ws + ((size_t)row * H + h) * NS * kSplitRec;
-  float ov[kMaxSplits];
+// a chunk past the item's source length contributes nothing
+template <class Rec>
+__device__ __forceinline__ void xs_empty(int G, Rec rec) {
+  for (int i = threadIdx.x & 63; i < G * kSplitRec; i += 64) {
+    const int g = i / kSplitRec, e = i % kSplitRec;
+    rec(g)[e] = e == 0 ? -FLT_MAX : 0.f;
+  }
+}
+
+// out[h*64 + d] of one row = sum_c o_c[d] e^(m_c - M) / sum_c l_c e^(m_c - M), M = max_c m_c,
+// from the row's NS records r[c * kSplitRec] (one wave): lane c < NS takes chunk c's (max, sum)
+// and the weights are reduced across lanes; then lane = dimension sums the chunks' o with
+// every load issued before the first add (a loop of dependent rounds took 8 us per call).
+// NSM >= NS record slots are read (16 covers 1024-token sources).
+template <int NSM>
+__device__ __forceinline__ void xs_combine(const float* r, int NS, bf16* __restrict__ out_row) {
+  const int lane = threadIdx.x & 63;
+  float ov[NSM];
 #pragma unroll
-  for (int c = 0; c < kMaxSplits; ++c) ov[c] = r[min(c, NS - 1) * kSplitRec + 2 + lane];
-  const float m = lane < NS ? r[lane * kSplitRec] : -FLT_MAX;
-  const float l = lane < NS ? r[lane * kSplitRec + 1] : 0.f;
+  for (int c = 0; c < NSM; ++c) ov[c] = r[min(c, NS - 1) * kSplitRec + 2 + lane];
+  const float mr = r[min(lane, NS - 1) * kSplitRec], lr = r[min(lane, NS - 1) * kSplitRec + 1];  // (in bounds)
+  const float m = lane < NS ? mr : -FLT_MAX;
+  const float l = lane < NS ? lr : 0.f;
   const float M = wave_max(m);
   const float w = lane < NS ? __expf(m - M) : 0.f;  // 0 for an empty chunk (max -FLT_MAX)
-  const float L = wave_sum(w * l);
+  float wl = w * l;
+  asm volatile("" : "+v"(wl));  // a rounded product: never fused into the reduction's first add
+  const float L = wave_sum(wl);
   float o = 0.f;
 #pragma unroll
-  for (int c = 0; c < kMaxSplits; ++c)
-    o += (c < NS ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), c)) : 0.f) * ov[c];
-  out[(size_t)row * ldo + h * kD + lane] = f2bf(L > 0.f ? o / L : 0.f);
+  for (int c = 0; c < NSM; ++c)
+    o = __builtin_fmaf(c < NS ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), c)) : 0.f, ov[c], o);
+  out_row[lane] = f2bf(L > 0.f ? o / L : 0.f);
+}
+
+__device__ __forceinline__ void xs_combine_any(const float* r, int NS, bf16* __restrict__ out_row) {
+  if (NS <= 16)
+    xs_combine<16>(r, NS, out_row);
+  else
+    xs_combine<kMaxSplits>(r, NS, out_row);
+}
+
+template <int GM>
+__global__ __launch_bounds__(64) void decode_cross_split_kernel(
+    const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k, const bf16* __restrict__ v, int ldkv,
+    int seq_stride, int group, int nrows, const int32_t* __restrict__ lens, const float* __restrict__ bias_dist,
+    int bias_stride, float* __restrict__ ws, int H, float scale) {
+  __shared__ float pl[GM][kSplitKeys];
+  __shared__ bf16x8 qsh[GM][8];
+  const int seq = blockIdx.x, h = blockIdx.y, c = blockIdx.z, NS = gridDim.z;
+  const int G = min(group, nrows - seq * group);
+  const int len = min(lens[seq], seq_stride);
+  const XsArgs a{q, k, v, bias_dist, ldq, ldkv, seq_stride, group, bias_stride, seq, h, G, len, scale};
+  const int jb = c * kSplitKeys, n = max(0, min(kSplitKeys, len - jb));
+  auto rec = [&](int g) { return ws + (((size_t)(seq * group + g) * H + h) * NS + c) * kSplitRec; };
+  if (n == 0) {
+    xs_empty(G, rec);
+    return;
+  }
+  // every load before any use: the beams' queries (through LDS: as per-beam scalar loads they
+  // cost one round trip per beam), the bias, the K row of key jb + lane and the V slabs
+  XsRegs r;
+  const bf16x8 qv = xs_query_load(a);
+  xs_load(a, jb, n, r);
+  xs_query_store<GM>(a, qv, qsh);
+  __syncthreads();
+  xs_compute<GM>(a, n, r, qsh, pl, rec);
+}
+
+// one wave per (row, head)
+__global__ __launch_bounds__(64) void decode_attn_combine_kernel(const float* __restrict__ ws, int NS, int H,
+                                                                 bf16* __restrict__ out, int ldo) {
+  const int row = blockIdx.x, h = blockIdx.y;
+  xs_combine_any(ws + ((size_t)row * H + h) * NS * kSplitRec, NS, out + (size_t)row * ldo + h * kD);
+}
+
+// One workgroup per (item, head): wave w takes chunks w, w + NW, ..., the next chunk's loads in
+// flight under the current one's arithmetic, records into LDS ([GM][NSX] x kSplitRec floats,
+// NS <= NSX), then wave g % NW combines beam row g.
+template <int GM, int NW, int NSX>
+__global__ __launch_bounds__(NW * 64) void decode_cross_chunked_kernel(
+    const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k, const bf16* __restrict__ v, int ldkv,
+    int seq_stride, int group, int nrows, const int32_t* __restrict__ lens, const float* __restrict__ bias_dist,
+    int bias_stride, bf16* __restrict__ out, int ldo, int NS, float scale) {
+  __shared__ float recs[GM][NSX][kSplitRec];
+  __shared__ float pl[NW][GM][kSplitKeys];
+  __shared__ bf16x8 qsh[GM][8];
+  const int seq = blockIdx.x, h = blockIdx.y, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int G = min(group, nrows - seq * group);
+  const int len = min(lens[seq], seq_stride);
+  const XsArgs a{q, k, v, bias_dist, ldq, ldkv, seq_stride, group, bias_stride, seq, h, G, len, scale};
+  const int nch = min(NS, (len + kSplitKeys - 1) / kSplitKeys);  // chunks holding keys
+  auto nkeys = [&](int c) { return min(kSplitKeys, len - c * kSplitKeys); };
+  bf16x8 qv;
+  if (w == 0) qv = xs_query_load(a);
+  XsRegs r0, r1;
+  {  // (unconditional on a clamped chunk: see xs_query_load)
+    const int c0 = min(w, max(nch - 1, 0));
+    xs_load(a, c0 * kSplitKeys, max(1, nkeys(c0)), r0);
+  }
+  if (w == 0) xs_query_store<GM>(a, qv, qsh);
+  for (int c = nch + w; c < NS; c += NW) {  // chunks past the source length
+    auto rec = [&](int g) { return &recs[g][c][0]; };
+    xs_empty(G, rec);
+  }
+  __syncthreads();
+  // two register sets: chunk c + NW's loads are in flight under chunk c's arithmetic
+  for (int c = w; c < nch; c += 2 * NW) {
+    if (c + NW < nch) xs_load(a, (c + NW) * kSplitKeys, nkeys(c + NW), r1);
+    auto rec0 = [&](int g) { return &recs[g][c][0]; };
+    xs_compute<GM>(a, nkeys(c), r0, qsh, pl[w], rec0);
+    if (c + NW < nch) {
+      if (c + 2 * NW < nch) xs_load(a, (c + 2 * NW) * kSplitKeys, nkeys(c + 2 * NW), r0);
+      auto rec1 = [&](int g) { return &recs[g][c + NW][0]; };
+      xs_compute<GM>(a, nkeys(c + NW), r1, qsh, pl[w], rec1);
+    }
+  }
+  __syncthreads();
+  for (int g = w; g < G; g += NW)
+    xs_combine_any(&recs[g][0][0], NS, out + (size_t)(seq * group + g) * ldo + h * kD);
 }
 
 // ----------------------------------------------------------------------------
@@ -1024,13 +1141,12 @@ int decode_self_few(int set) {
 }
 
 int decode_attention_splits(int rows, int group, int H, int seq_stride, bool cross) {
-  // key chunks of the split cross attention, 0 = the per-(item, head) kernel
+  // key chunks of the split cross attention while the per-(item, head) grid (items x heads)
+  // cannot cover the chip twice, else 0 (decode_cross_chunked_kernel under batch invariance: the
+  // same bits; decode_attention_kernel otherwise)
   if (!cross || group < 1 || group > 8 || seq_stride < 2 * kSplitKeys) return 0;
   const int nseq = (rows + group - 1) / group;
-  // batch invariance: the split form for every item count (an item's keys always go through the
-  // same 64-key chunks and combine, whatever else shares the launch); else only while the
-  // unsplit grid (items x heads) cannot cover the chip twice
-  if (nseq * H >= 512 && !batch_invariant(-1)) return 0;
+  if (nseq * H >= 512) return 0;
   return (seq_stride + kSplitKeys - 1) / kSplitKeys;
 }
 
@@ -1104,6 +1220,37 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
 #undef ATPU_DS
     ATPU_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(decode_attn_combine_kernel, dim3(rows, H), dim3(64), 0, stream, ws, ns, H, out, ldo);
+    ATPU_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  // batch invariance (or ATPU_DEC_XCHUNK=1): a grid too large to split runs the split form's chunk
+  // and combine arithmetic in one workgroup per (item, head), so an item rounds the same in a
+  // launch of any size
+  static const bool xchunk_env = [] {
+    const char* f = std::getenv("ATPU_DEC_XCHUNK");
+    return f && f[0] == '1';
+  }();
+  if (lens && !hist && group <= 8 && seq_stride >= 2 * kSplitKeys && (batch_invariant(-1) || xchunk_env)) {
+    ATPU_CHECK(ldq % 8 == 0 && (reinterpret_cast<uintptr_t>(q) & 15) == 0, "decode_attention: q needs 16-B rows");
+    const int ns = (seq_stride + kSplitKeys - 1) / kSplitKeys;
+#define ATPU_DC(GM, NSX)                                                                                         \
+  hipLaunchKernelGGL((decode_cross_chunked_kernel<GM, 4, NSX>), dim3(nseq, H), dim3(256), 0, stream, q, ldq, k, v, \
+                     ldkv, seq_stride, group, rows, lens, bias_dist, bias_stride, out, ldo, ns, scale)
+#define ATPU_DC_NS(GM)  \
+  if (ns <= 16) {       \
+    ATPU_DC(GM, 16);    \
+  } else {              \
+    ATPU_DC(GM, 32);    \
+  }
+    if (group == 1) {
+      ATPU_DC_NS(1)
+    } else if (group <= 4) {
+      ATPU_DC_NS(4)
+    } else {
+      ATPU_DC_NS(8)
+    }
+#undef ATPU_DC_NS
+#undef ATPU_DC
     ATPU_HIP_CHECK(hipGetLastError());
     return;
   }

@@ -1669,14 +1669,21 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
 // the RowRms sum of squares in the same lane order, and the shared epilogue (dec_row_out) -- but
 // with no LDS ring: one wave owns 16 x (16 NJ) outputs and streams its operands straight into MFMA
 // fragment registers, RD k-steps per round, the next round's loads in flight under this round's
-// MFMAs (two register sets). N / (16 NJ) single-wave workgroups (NJ = 2 for RowStats slabs).
+// MFMAs (two register sets). N / (16 NJ) workgroups of one compute wave (NJ = 2 for RowStats
+// slabs), plus (PF) the GEMV's L2 prefetch wave for the next decoder GEMM's weight rows.
 // ============================================================================
-template <int EPI, int NJ, int RD>
-__global__ __launch_bounds__(64) void gemm_few_exact_kernel(const bf16* __restrict__ A, int lda,
-                                                            const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C,
-                                                            int ldc, const float* __restrict__ bias,
-                                                            const bf16* __restrict__ R, int ldr, int M, int N, int K,
-                                                            float rms_eps, KvOut kvo, LnDec ln) {
+template <int EPI, int NJ, int RD, bool PF>
+__global__ __launch_bounds__(64 * (1 + PF)) void gemm_few_exact_kernel(
+    const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C, int ldc,
+    const float* __restrict__ bias, const bf16* __restrict__ R, int ldr, int M, int N, int K, float rms_eps, KvOut kvo,
+    LnDec ln, L2Pf pf) {
+  if constexpr (PF) {
+    __shared__ __attribute__((aligned(16))) char pf_scratch[256];
+    if (threadIdx.x >= 64) {
+      l2_prefetch_rows<0>(pf, threadIdx.x & 63, pf_scratch, blockIdx.x, gridDim.x);
+      return;
+    }
+  }
   const int lane = threadIdx.x, fr = lane & 15, fc = lane >> 4;
   const int nb = blockIdx.x * 16 * NJ;  // this wave's first column
   const bf16* ar = A + (size_t)min(fr, M - 1) * lda + fc * 8;
@@ -1742,13 +1749,27 @@ bool few_exact_ok(const GemmArgs& g) {
 void launch_few_exact(const GemmArgs& g, hipStream_t s) {
   const KvOut kvo{g.kv_cache, g.kv_ld, g.kv_T, g.kv_col0, g.kv_step};
   const LnDec ln{g.colsum, g.in_part, g.res_part, g.gamma, g.part_out};
-#define ATPU_FEW_GO(E, NJ)                                                                                           \
-  hipLaunchKernelGGL((gemm_few_exact_kernel<E, NJ, 8>), dim3(g.N / (16 * (NJ))), dim3(64), 0, s, g.A, g.lda, g.Bt,   \
-                     g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, g.rms_eps, kvo, ln)
+  // the GEMV's prefetch rule (ATPU_GEMV_PREFETCH, not from RowStats launches)
+  static const bool pf_on = [] {
+    const char* f = std::getenv("ATPU_GEMV_PREFETCH");
+    return !(f && f[0] == '0');
+  }();
+  const bool pf = pf_on && g.pf_w && g.pf_n > 0 && g.pf_k > 0 && !(g.epi & kEpiRowStats);
+  const L2Pf pfa{g.pf_w, g.pf_ld, g.pf_k, g.pf_n, g.pf_rpb > 0 ? g.pf_rpb : 16};
+#define ATPU_FEW_GO(E, NJ)                                                                                         \
+  if (pf)                                                                                                          \
+    hipLaunchKernelGGL((gemm_few_exact_kernel<E, NJ, 8, true>), dim3(g.N / (16 * (NJ))), dim3(128), 0, s, g.A,    \
+                       g.lda, g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, g.rms_eps, kvo, ln, pfa); \
+  else                                                                                                             \
+    hipLaunchKernelGGL((gemm_few_exact_kernel<E, NJ, 8, false>), dim3(g.N / (16 * (NJ))), dim3(64), 0, s, g.A,    \
+                       g.lda, g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, g.rms_eps, kvo, ln, pfa)
 #define ATPU_FEW_CASE(E)                                 \
   case E:                                                \
-    if constexpr (((E) & kEpiRowStats) != 0) ATPU_FEW_GO(E, 2); \
-    else ATPU_FEW_GO(E, 1);                              \
+    if constexpr (((E) & kEpiRowStats) != 0) {           \
+      ATPU_FEW_GO(E, 2);                                 \
+    } else {                                             \
+      ATPU_FEW_GO(E, 1);                                 \
+    }                                                    \
     break;
   switch (g.epi) {
     ATPU_FEW_CASE(kEpiRowLn | kEpiBias | kEpiKvScatter)

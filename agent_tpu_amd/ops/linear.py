@@ -144,8 +144,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     producer needs ``stats_out`` (its 8-wave, 32-column-slab workgroups).
 
     ``prefetch``: the weight of the NEXT linear of a decode chain (or ``(weight, 32)`` when that
-    linear writes ``stats_out``: 32 weight rows per workgroup). A <= 4-row GEMV pulls it into the
-    L2 of the XCDs that will read it while it runs (a hint; ignored elsewhere and on CPU)."""
+    linear writes ``stats_out``: 32 weight rows per workgroup). A <= 4-row GEMV (or, batch-invariant,
+    the <= 16-row exact kernel) pulls it into the L2 of the XCDs that will read it while it runs
+    (a hint; ignored elsewhere and on CPU)."""
     check(act in _ACTS, f"unknown activation {act!r}")
     M0, N0 = x.shape[0], w.shape[0]
 
@@ -267,7 +268,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     if not kv_args:
         kv_args = (0, 0, 0, 0, 0)
     pf_args = (0, 0, 0, 0, 16)
-    if prefetch is not None and M <= 4:
+    if prefetch is not None and M <= 16:  # the <= 4-row GEMV and the batch-invariant few-row kernel
         pw, rpb = prefetch if isinstance(prefetch, tuple) else (prefetch, 16)
         if pw.is_cuda and pw.dim() == 2 and pw.stride(1) == 1:
             pf_args = (ptr(pw), pw.stride(0), pw.shape[1], pw.shape[0], int(rpb))

@@ -134,6 +134,33 @@ def test_decode_attention_one_item_vs_many(gpu, invariant):
     assert torch.equal(big[:4], small)
 
 
+@pytest.mark.parametrize("group,S,H,items", [(4, 1024, 12, 64), (8, 2048, 16, 40), (1, 700, 12, 50),
+                                              (3, 256, 12, 200)])
+def test_cross_attention_chunked_equals_split(gpu, invariant, group, S, H, items):
+    """Past the split grid (items x heads >= 512) batch-invariant mode runs decode_cross_chunked_kernel
+    (the split form's chunk and combine code, one workgroup per (item, head), records in LDS):
+    every item equals its own one-item split launch bit for bit, and the reference to rounding."""
+    from agent_tpu_amd.ops.decode import _decode_attention_ref
+
+    d = H * 64
+    rows = items * group
+    q = _r((rows, 3 * d), gpu, 1.0, 81)[:, :d]  # strided like the fused QKV output
+    kv = _r((items * S, 2 * d), gpu, 1.0, 82)
+    lens = torch.randint(1, S + 1, (items,), generator=torch.Generator().manual_seed(83), dtype=torch.int32)
+    lens[0], lens[-1] = S, 37  # a full source and one shorter than a chunk
+    lens = lens.to(gpu)
+    bias = _r((H, S), gpu, 1.0, 84, torch.float32)
+    many = ops.decode_attention(q, kv[:, :d], kv[:, d:], H, S, group, lens=lens, bias_dist=bias, scale=0.125)
+    for i in (0, 1, items // 2, items - 1):
+        one = ops.decode_attention(q[i * group:(i + 1) * group], kv[i * S:(i + 1) * S, :d], kv[i * S:(i + 1) * S, d:],
+                                   H, S, group, lens=lens[i:i + 1], bias_dist=bias, scale=0.125)
+        assert torch.equal(many[i * group:(i + 1) * group], one), i
+    sub = slice(0, 3 * group)
+    ref = _decode_attention_ref(q[sub].cpu(), kv[:3 * S, :d].cpu(), kv[:3 * S, d:].cpu(), H, S, group, lens[:3].cpu(),
+                                None, bias.cpu(), 0.125, None)
+    assert (many[sub].float().cpu() - ref.float()).abs().max().item() < 2e-2 * max(1.0, ref.float().abs().max().item())
+
+
 @pytest.mark.parametrize("V,d,rms,bias", [(32128, 768, True, False), (50264, 1024, False, True)])
 def test_lm_head_topk_rows_4_vs_64(gpu, invariant, V, d, rms, bias):
     w = _r((V, d), gpu, d ** -0.5, 31)
@@ -198,6 +225,8 @@ def test_few_row_exact_kernel_equals_dec(gpu, nat, invariant, epi, M, K):
     from agent_tpu_amd.ops.linear import row_parts_ref
 
     N = 1024 if epi in ("row_ln", "res_ln_stats") else 768
+    if epi == "row_ln":
+        K = min(K, 1024)  # RowLn rows are <= 1024 wide
     x = _r((M, K), gpu, 1.0, 61)
     w = _r((N, K), gpu, K ** -0.5, 62)
     b = (torch.randn(N, generator=torch.Generator().manual_seed(63)) * 0.1).to(gpu)
@@ -220,8 +249,6 @@ def test_few_row_exact_kernel_equals_dec(gpu, nat, invariant, epi, M, K):
         if epi == "out_f32":
             return [ops.linear(x, w, out_f32=True, rms_eps=1e-6)]
         if epi == "row_ln":
-            if K > 1024:
-                pytest.skip("RowLn rows are <= 1024 wide")
             part = row_parts_ref(x).contiguous()
             return [ops.linear(x, w, b, act="gelu", row_ln=(1e-5, w.float().sum(1).contiguous(), part))]
         part = torch.empty((N // 32, M, 2), dtype=torch.float32, device=gpu)
