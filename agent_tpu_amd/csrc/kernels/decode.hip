@@ -346,80 +346,99 @@ struct XsArgs {  // one (item, head) of the cross attention
   float scale;
 };
 
-struct XsRegs {  // one chunk's operands: the K row of key jb + lane, the V slabs, the bias
-  bf16x8 kk[8];
+template <bool B>
+struct XsRegs {  // one chunk's operands: K (MFMA A fragments of the 4 16-key tiles), V slabs, bias
+  bf16x8 ka[4], kb[4];  // tile t: key jb + 16 t + (lane & 15), dims (lane >> 4) * 8 (+32 in kb)
   bf16x8 vv[kSplitKeys / 8];
-  float bj;
+  float bj[B ? 4 : 1][4];  // (B) T5-style distance bias of key jb + 16 t + 4 (lane >> 4) + e
 };
 
-// the item's G beam queries (lane = (beam, 16-B chunk)) -> LDS; the caller syncs. The row is
-// clamped, not the load predicated: a load under `qg < G` merged with an undefined value may be
-// speculated for every lane by the compiler, i.e. read past the last item's rows (it was, and
-// faulted on a small q).
-__device__ __forceinline__ bf16x8 xs_query_load(const XsArgs& a) {
-  const int lane = threadIdx.x & 63, qg = min(lane >> 3, a.G - 1), qe = lane & 7;
-  return *reinterpret_cast<const bf16x8*>(a.q + (size_t)(a.seq * a.group + qg) * a.ldq + a.h * kD + qe * 8);
-}
+struct XsQ {  // the item's beam queries as the MFMA B operand: query lane & 15 (zero past G)
+  bf16x8 q0, q1;
+};
 
-template <int GM>
-__device__ __forceinline__ void xs_query_store(const XsArgs& a, const bf16x8& qv, bf16x8 (&qsh)[GM][8]) {
-  const int lane = threadIdx.x & 63, qg = lane >> 3, qe = lane & 7;
-  if (qg < a.G) qsh[qg][qe] = qv;
-}
-
-// every load of chunk [jb, jb + n), n >= 1, issued at once
-__device__ __forceinline__ void xs_load(const XsArgs& a, int jb, int n, XsRegs& r) {
-  const int lane = threadIdx.x & 63;
-  auto at = [&](int j) -> size_t { return ((size_t)a.seq * a.seq_stride + j) * a.ldkv + a.h * kD; };
-  const int jk = jb + min(lane, n - 1);
-  r.bj = a.bias_dist ? a.bias_dist[a.h * a.bias_stride + (a.len - 1 - jk)] : 0.f;
-  const bf16* kr = a.k + at(jk);
+// The row is clamped and the padding zeroed by a select, not a predicated load: a load under
+// `li < G` merged with an undefined value may be speculated for every lane by the compiler,
+// i.e. read past the last item's rows (it was, and faulted on a small q).
+__device__ __forceinline__ XsQ xs_q(const XsArgs& a) {
+  const int lane = threadIdx.x & 63, li = lane & 15, kq = (lane >> 4) * 8;
+  const bf16* qr = a.q + (size_t)(a.seq * a.group + min(li, a.G - 1)) * a.ldq + a.h * kD;
+  XsQ r{*reinterpret_cast<const bf16x8*>(qr + kq), *reinterpret_cast<const bf16x8*>(qr + 32 + kq)};
+  if (li >= a.G) {
 #pragma unroll
-  for (int e = 0; e < 8; ++e) r.kk[e] = *reinterpret_cast<const bf16x8*>(kr + e * 8);
+    for (int e = 0; e < 8; ++e) r.q0[e] = r.q1[e] = f2bf(0.f);
+  }
+  return r;
+}
+
+// every load of chunk [jb, jb + n), n >= 1, issued at once (B: with the distance bias)
+template <bool B>
+__device__ __forceinline__ void xs_load(const XsArgs& a, int jb, int n, XsRegs<B>& r) {
+  const int lane = threadIdx.x & 63, li = lane & 15, kq = (lane >> 4) * 8;
+  auto at = [&](int j) -> size_t { return ((size_t)a.seq * a.seq_stride + j) * a.ldkv + a.h * kD; };
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const bf16* kr = a.k + at(jb + min(t * 16 + li, n - 1));
+    r.ka[t] = *reinterpret_cast<const bf16x8*>(kr + kq);
+    r.kb[t] = *reinterpret_cast<const bf16x8*>(kr + 32 + kq);
+  }
   const int ksub = lane >> 3, dc = (lane & 7) * 8;
 #pragma unroll
   for (int u = 0; u < kSplitKeys / 8; ++u)
     r.vv[u] = *reinterpret_cast<const bf16x8*>(a.v + at(jb + min(u * 8 + ksub, n - 1)) + dc);
+  if constexpr (B) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = jb + min(t * 16 + (lane >> 4) * 4 + e, n - 1);
+        r.bj[t][e] = a.bias_dist[a.h * a.bias_stride + (a.len - 1 - j)];
+      }
+  }
 }
 
-// chunk [jb, jb + n) of the loaded operands -> the G rows' records rec(g) (one wave; pl is
-// the wave's own probability rows). Every multiply-add here and in xs_combine is an explicit
-// fma or an unfusable product, so the split and chunked kernels (different surrounding code)
-// cannot differ in the compiler's contraction choices.
-template <int GM, class Rec>
-__device__ __forceinline__ void xs_compute(const XsArgs& a, int n, const XsRegs& r, const bf16x8 (&qsh)[GM][8],
+// chunk [jb, jb + n) of the loaded operands -> the G rows' records rec(g) (one wave; pl is the
+// wave's own probability rows):
+//   scores : S^T[16 keys x 16 queries] per 16-key tile on MFMA (2 x 16x16x32 each); lane l
+//            holds keys 4 (l >> 4) + e of each tile for query l & 15; max and sum of the query
+//            over its lanes l, l^16, l^32, l^48 (lane_rows_*), in a fixed order;
+//   P.V    : lane = (key sub 0..7, 8 dims), probabilities through LDS, xor-reduce over the subs.
+// Every multiply-add here and in xs_combine is an explicit fma or an unfusable product, so the
+// split and chunked kernels (different surrounding code) cannot differ in contraction.
+template <int GM, bool B, class Rec>
+__device__ __forceinline__ void xs_compute(const XsArgs& a, int n, const XsRegs<B>& r, const XsQ& q,
                                            float (&pl)[GM][kSplitKeys], Rec rec) {
-  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-  const int lane = threadIdx.x & 63, G = a.G;
-  // every beam's score first, then ONE butterfly max and ONE butterfly sum over the beams
-  // (wave_bfly: lane l ends with beam l >> kSh) instead of a wave max and sum per beam
-  constexpr int kSh = GM == 1 ? 6 : GM == 4 ? 4 : 3;
-  float sjv[GM];
+  const int lane = threadIdx.x & 63, li = lane & 15, kg = lane >> 4, G = a.G;
+  f32x4 acc[4];
 #pragma unroll
-  for (int g = 0; g < GM; ++g) {
-    sjv[g] = -FLT_MAX;
-    if (g < G) {  // G is uniform: no divergence
-      float d[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < 4; ++t) {
+    acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(r.ka[t], q.q0, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(r.kb[t], q.q1, acc[t], 0, 0, 0);
+  }
+  float sv[4][4], m = -FLT_MAX;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const bf16x8 qq = qsh[g][e];
+  for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-          d[t] = __builtin_amdgcn_fdot2_f32_bf16(bf16x2_t{r.kk[e][2 * t], r.kk[e][2 * t + 1]},
-                                                 bf16x2_t{qq[2 * t], qq[2 * t + 1]}, d[t], false);
-      }
-      sjv[g] = lane < n ? __builtin_fmaf((d[0] + d[1]) + (d[2] + d[3]), a.scale, r.bj) : -FLT_MAX;
+    for (int e = 0; e < 4; ++e) {
+      const int j = t * 16 + kg * 4 + e;
+      sv[t][e] = j < n ? __builtin_fmaf(acc[t][e], a.scale, B ? r.bj[B ? t : 0][e] : 0.f) : -FLT_MAX;
+      m = fmaxf(m, sv[t][e]);
     }
-  }
-  const float mxl = wave_bfly<GM>(sjv, OpMax{});
-  float pv[GM], mxg[GM];
+  m = lane_rows_max(m);
+  float sum = 0.f;
+  f32x4 pv[4];
 #pragma unroll
-  for (int g = 0; g < GM; ++g) {
-    mxg[g] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mxl), g << kSh));
-    pv[g] = (g < G && lane < n) ? __expf(sjv[g] - mxg[g]) : 0.f;
-    if (g < G) pl[g][lane] = pv[g];
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      pv[t][e] = t * 16 + kg * 4 + e < n ? __expf(sv[t][e] - m) : 0.f;
+      sum += pv[t][e];
+    }
+  sum = lane_rows_sum(sum);
+  if (li < G) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) *reinterpret_cast<f32x4*>(&pl[li][t * 16 + kg * 4]) = pv[t];
   }
-  const float sml = wave_bfly<GM>(pv, OpAdd{});  // beam lane >> kSh
   __builtin_amdgcn_wave_barrier();  // (one wave: LDS ops complete in order)
   const int ksub = lane >> 3, dc = (lane & 7) * 8;
   float o[GM][8];
@@ -445,9 +464,9 @@ __device__ __forceinline__ void xs_compute(const XsArgs& a, int n, const XsRegs&
       float* rp = rec(g);
       // the 8 dims over the key subs (lane bits 3-5) by butterfly: lane l ends with dim dc + ksub
       rp[2 + dc + ksub] = wave_bfly_rows8(o[g]);
-      if (lane == (g << kSh)) {
-        rp[0] = mxg[g];
-        rp[1] = sml;
+      if (lane == g) {  // query g's max and sum (lanes l & 15 == g hold them)
+        rp[0] = m;
+        rp[1] = sum;
       }
     }
   }
@@ -496,13 +515,12 @@ __device__ __forceinline__ void xs_combine_any(const float* r, int NS, bf16* __r
     xs_combine<kMaxSplits>(r, NS, out_row);
 }
 
-template <int GM>
+template <int GM, bool B>
 __global__ __launch_bounds__(64) void decode_cross_split_kernel(
     const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k, const bf16* __restrict__ v, int ldkv,
     int seq_stride, int group, int nrows, const int32_t* __restrict__ lens, const float* __restrict__ bias_dist,
     int bias_stride, float* __restrict__ ws, int H, float scale) {
-  __shared__ float pl[GM][kSplitKeys];
-  __shared__ bf16x8 qsh[GM][8];
+  __shared__ __attribute__((aligned(16))) float pl[GM][kSplitKeys];
   const int seq = blockIdx.x, h = blockIdx.y, c = blockIdx.z, NS = gridDim.z;
   const int G = min(group, nrows - seq * group);
   const int len = min(lens[seq], seq_stride);
@@ -513,14 +531,11 @@ __global__ __launch_bounds__(64) void decode_cross_split_kernel(
     xs_empty(G, rec);
     return;
   }
-  // every load before any use: the beams' queries (through LDS: as per-beam scalar loads they
-  // cost one round trip per beam), the bias, the K row of key jb + lane and the V slabs
-  XsRegs r;
-  const bf16x8 qv = xs_query_load(a);
-  xs_load(a, jb, n, r);
-  xs_query_store<GM>(a, qv, qsh);
-  __syncthreads();
-  xs_compute<GM>(a, n, r, qsh, pl, rec);
+  // every load before any use: the beams' queries, the K tiles, the V slabs (and the bias)
+  const XsQ qr = xs_q(a);
+  XsRegs<B> r;
+  xs_load<B>(a, jb, n, r);
+  xs_compute<GM, B>(a, n, r, qr, pl, rec);
 }
 
 // one wave per (row, head)
@@ -533,42 +548,38 @@ __global__ __launch_bounds__(64) void decode_attn_combine_kernel(const float* __
 // One workgroup per (item, head): wave w takes chunks w, w + NW, ..., the next chunk's loads in
 // flight under the current one's arithmetic, records into LDS ([GM][NSX] x kSplitRec floats,
 // NS <= NSX), then wave g % NW combines beam row g.
-template <int GM, int NW, int NSX>
+template <int GM, int NW, int NSX, bool B>
 __global__ __launch_bounds__(NW * 64) void decode_cross_chunked_kernel(
     const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k, const bf16* __restrict__ v, int ldkv,
     int seq_stride, int group, int nrows, const int32_t* __restrict__ lens, const float* __restrict__ bias_dist,
     int bias_stride, bf16* __restrict__ out, int ldo, int NS, float scale) {
   __shared__ float recs[GM][NSX][kSplitRec];
-  __shared__ float pl[NW][GM][kSplitKeys];
-  __shared__ bf16x8 qsh[GM][8];
+  __shared__ __attribute__((aligned(16))) float pl[NW][GM][kSplitKeys];
   const int seq = blockIdx.x, h = blockIdx.y, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int G = min(group, nrows - seq * group);
   const int len = min(lens[seq], seq_stride);
   const XsArgs a{q, k, v, bias_dist, ldq, ldkv, seq_stride, group, bias_stride, seq, h, G, len, scale};
   const int nch = min(NS, (len + kSplitKeys - 1) / kSplitKeys);  // chunks holding keys
   auto nkeys = [&](int c) { return min(kSplitKeys, len - c * kSplitKeys); };
-  bf16x8 qv;
-  if (w == 0) qv = xs_query_load(a);
-  XsRegs r0, r1;
-  {  // (unconditional on a clamped chunk: see xs_query_load)
+  const XsQ qr = xs_q(a);
+  XsRegs<B> r0, r1;
+  {  // (unconditional on a clamped chunk: see xs_q)
     const int c0 = min(w, max(nch - 1, 0));
-    xs_load(a, c0 * kSplitKeys, max(1, nkeys(c0)), r0);
+    xs_load<B>(a, c0 * kSplitKeys, max(1, nkeys(c0)), r0);
   }
-  if (w == 0) xs_query_store<GM>(a, qv, qsh);
   for (int c = nch + w; c < NS; c += NW) {  // chunks past the source length
     auto rec = [&](int g) { return &recs[g][c][0]; };
     xs_empty(G, rec);
   }
-  __syncthreads();
   // two register sets: chunk c + NW's loads are in flight under chunk c's arithmetic
   for (int c = w; c < nch; c += 2 * NW) {
-    if (c + NW < nch) xs_load(a, (c + NW) * kSplitKeys, nkeys(c + NW), r1);
+    if (c + NW < nch) xs_load<B>(a, (c + NW) * kSplitKeys, nkeys(c + NW), r1);
     auto rec0 = [&](int g) { return &recs[g][c][0]; };
-    xs_compute<GM>(a, nkeys(c), r0, qsh, pl[w], rec0);
+    xs_compute<GM, B>(a, nkeys(c), r0, qr, pl[w], rec0);
     if (c + NW < nch) {
-      if (c + 2 * NW < nch) xs_load(a, (c + 2 * NW) * kSplitKeys, nkeys(c + 2 * NW), r0);
+      if (c + 2 * NW < nch) xs_load<B>(a, (c + 2 * NW) * kSplitKeys, nkeys(c + 2 * NW), r0);
       auto rec1 = [&](int g) { return &recs[g][c + NW][0]; };
-      xs_compute<GM>(a, nkeys(c + NW), r1, qsh, pl[w], rec1);
+      xs_compute<GM, B>(a, nkeys(c + NW), r1, qr, pl[w], rec1);
     }
   }
   __syncthreads();
@@ -1207,9 +1218,15 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
     static_assert(kMaxSplits * kSplitKeys >= kMaxKeys, "combine kernel chunk count");
     ATPU_CHECK(ldq % 8 == 0 && (reinterpret_cast<uintptr_t>(q) & 15) == 0, "decode_attention: q needs 16-B rows");
     ATPU_CHECK((reinterpret_cast<uintptr_t>(ws) & 15) == 0, "decode_attention: ws must be 16-byte aligned");
-#define ATPU_DS(GM)                                                                                               \
-  hipLaunchKernelGGL((decode_cross_split_kernel<GM>), dim3(nseq, H, ns), dim3(64), 0, stream, q, ldq, k, v, ldkv, \
-                     seq_stride, group, rows, lens, bias_dist, bias_stride, ws, H, scale)
+#define ATPU_DS1(GM, B)                                                                                         \
+  hipLaunchKernelGGL((decode_cross_split_kernel<GM, B>), dim3(nseq, H, ns), dim3(64), 0, stream, q, ldq, k, v,  \
+                     ldkv, seq_stride, group, rows, lens, bias_dist, bias_stride, ws, H, scale)
+#define ATPU_DS(GM)          \
+  if (bias_dist) {           \
+    ATPU_DS1(GM, true);      \
+  } else {                   \
+    ATPU_DS1(GM, false);     \
+  }
     if (group == 1) {
       ATPU_DS(1);
     } else if (group <= 4) {
@@ -1218,6 +1235,7 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
       ATPU_DS(8);
     }
 #undef ATPU_DS
+#undef ATPU_DS1
     ATPU_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(decode_attn_combine_kernel, dim3(rows, H), dim3(64), 0, stream, ws, ns, H, out, ldo);
     ATPU_HIP_CHECK(hipGetLastError());
@@ -1233,9 +1251,15 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
   if (lens && !hist && group <= 8 && seq_stride >= 2 * kSplitKeys && (batch_invariant(-1) || xchunk_env)) {
     ATPU_CHECK(ldq % 8 == 0 && (reinterpret_cast<uintptr_t>(q) & 15) == 0, "decode_attention: q needs 16-B rows");
     const int ns = (seq_stride + kSplitKeys - 1) / kSplitKeys;
-#define ATPU_DC(GM, NSX)                                                                                         \
-  hipLaunchKernelGGL((decode_cross_chunked_kernel<GM, 4, NSX>), dim3(nseq, H), dim3(256), 0, stream, q, ldq, k, v, \
-                     ldkv, seq_stride, group, rows, lens, bias_dist, bias_stride, out, ldo, ns, scale)
+#define ATPU_DC1(GM, NSX, B)                                                                                    \
+  hipLaunchKernelGGL((decode_cross_chunked_kernel<GM, 4, NSX, B>), dim3(nseq, H), dim3(256), 0, stream, q, ldq, k, \
+                     v, ldkv, seq_stride, group, rows, lens, bias_dist, bias_stride, out, ldo, ns, scale)
+#define ATPU_DC(GM, NSX)        \
+  if (bias_dist) {              \
+    ATPU_DC1(GM, NSX, true);    \
+  } else {                      \
+    ATPU_DC1(GM, NSX, false);   \
+  }
 #define ATPU_DC_NS(GM)  \
   if (ns <= 16) {       \
     ATPU_DC(GM, 16);    \
@@ -1251,6 +1275,7 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
     }
 #undef ATPU_DC_NS
 #undef ATPU_DC
+#undef ATPU_DC1
     ATPU_HIP_CHECK(hipGetLastError());
     return;
   }

@@ -1756,13 +1756,18 @@ void launch_few_exact(const GemmArgs& g, hipStream_t s) {
   }();
   const bool pf = pf_on && g.pf_w && g.pf_n > 0 && g.pf_k > 0 && !(g.epi & kEpiRowStats);
   const L2Pf pfa{g.pf_w, g.pf_ld, g.pf_k, g.pf_n, g.pf_rpb > 0 ? g.pf_rpb : 16};
-#define ATPU_FEW_GO(E, NJ)                                                                                         \
-  if (pf)                                                                                                          \
-    hipLaunchKernelGGL((gemm_few_exact_kernel<E, NJ, 8, true>), dim3(g.N / (16 * (NJ))), dim3(128), 0, s, g.A,    \
-                       g.lda, g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, g.rms_eps, kvo, ln, pfa); \
-  else                                                                                                             \
-    hipLaunchKernelGGL((gemm_few_exact_kernel<E, NJ, 8, false>), dim3(g.N / (16 * (NJ))), dim3(64), 0, s, g.A,    \
-                       g.lda, g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, g.rms_eps, kvo, ln, pfa)
+  // K >= 2048 (T5 wo, BART fc2): 16 k-steps per round, half the dependent load rounds
+#define ATPU_FEW_GO1(E, NJ, RD, P)                                                                                 \
+  hipLaunchKernelGGL((gemm_few_exact_kernel<E, NJ, RD, P>), dim3(g.N / (16 * (NJ))), dim3(64 * (1 + (P))), 0, s,  \
+                     g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, g.rms_eps, kvo, ln, pfa)
+#define ATPU_FEW_GO(E, NJ)              \
+  if (pf && g.K >= 2048) {              \
+    ATPU_FEW_GO1(E, NJ, 16, true);      \
+  } else if (pf) {                      \
+    ATPU_FEW_GO1(E, NJ, 8, true);       \
+  } else {                              \
+    ATPU_FEW_GO1(E, NJ, 8, false);      \
+  }
 #define ATPU_FEW_CASE(E)                                 \
   case E:                                                \
     if constexpr (((E) & kEpiRowStats) != 0) {           \
@@ -1798,6 +1803,7 @@ void launch_few_exact(const GemmArgs& g, hipStream_t s) {
   }
 #undef ATPU_FEW_CASE
 #undef ATPU_FEW_GO
+#undef ATPU_FEW_GO1
 }
 
 // Ring depth 4 (64 KiB LDS, 2 blocks/CU). 8 stages measured the same on the
