@@ -1449,13 +1449,10 @@ __device__ __forceinline__ void wait_vmcnt() {
 // with RowStats NJ = 2, nb a 32-column slab). Every operation and its order are shared, so the
 // two kernels produce the same bits for a row (batch invariance).
 template <int EPI, int NJ>
-__device__ __forceinline__ void dec_row_out(const f32x4 (&acc)[NJ], int m, int nb, int fchunk, int M, int N,
-                                            float rstd, float rmu, float2 rf, bf16* __restrict__ C, int ldc,
-                                            const float* __restrict__ bias, const bf16* __restrict__ R, int ldr,
-                                            const KvOut& kvo, const LnDec& ln, int kv_pos) {
-  static_assert(!(EPI & kEpiRowStats) || NJ == 2, "RowStats: a 32-column slab per wave");
-  if (m >= M) return;
-  float ps = 0.f, pss = 0.f;  // RowStats: this lane's share of the wave's 32-column slab
+__device__ __forceinline__ void dec_row_vals(const f32x4 (&acc)[NJ], int m, int nb, int fchunk, int N, float rstd,
+                                             float rmu, float2 rf, bf16* __restrict__ C, int ldc,
+                                             const float* __restrict__ bias, const bf16* __restrict__ R, int ldr,
+                                             const KvOut& kvo, const LnDec& ln, int kv_pos, bf16x4 (&ov)[NJ]) {
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int n = nb + j * 16 + fchunk * 4;
@@ -1497,6 +1494,7 @@ __device__ __forceinline__ void dec_row_out(const f32x4 (&acc)[NJ], int m, int n
       bf16x4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+      ov[j] = o;
       if (EPI & kEpiKvScatter) {
         // the tile is all Q or all K|V (host: kv_col0 % 128 == 0)
         // a step past the cache (caller bug) drops the K|V write instead of writing out of bounds
@@ -1507,20 +1505,43 @@ __device__ __forceinline__ void dec_row_out(const f32x4 (&acc)[NJ], int m, int n
       } else {
         *reinterpret_cast<bf16x4*>(C + (size_t)m * ldc + n) = o;
       }
-      if constexpr (EPI & kEpiRowStats) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float f = bf2f(o[e]);
-          ps += f;
-          pss = fmaf(f, f, pss);
-        }
-      }
     }
   }
-  if constexpr (EPI & kEpiRowStats) {
-    const float S = lane_rows_sum(ps), Q = lane_rows_sum(pss);
-    if (fchunk == 0 && nb < N) *reinterpret_cast<float2*>(ln.part_out + 2 * ((size_t)(nb / 32) * M + m)) = float2{S, Q};
+}
+
+// RowStats: the (sum, sum of squares) of the row's stored (bf16) outputs over the 32-column slab
+// at nb, this lane's 2 x 4 values in column order, then over the slab's 4 lanes of the row
+__device__ __forceinline__ void dec_row_stats(const bf16x4 (&ov)[2], int m, int nb, int fchunk, int M, int N,
+                                              const LnDec& ln) {
+  float ps = 0.f, pss = 0.f;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if (nb + j * 16 + fchunk * 4 >= N) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float f = bf2f(ov[j][e]);
+      ps += f;
+      pss = fmaf(f, f, pss);
+    }
   }
+  const float S = lane_rows_sum(ps), Q = lane_rows_sum(pss);
+  if (fchunk == 0 && nb < N) *reinterpret_cast<float2*>(ln.part_out + 2 * ((size_t)(nb / 32) * M + m)) = float2{S, Q};
+}
+
+// One row's share of a 64x64 "dec" tile epilogue (also the exact few-row kernel's): the lane holds
+// row m, columns nb + j*16 + fchunk*4 .. +3 of fragments j < NJ (nb = the wave's first column;
+// with RowStats NJ = 2, nb a 32-column slab). Every operation and its order are shared, so the
+// two kernels produce the same bits for a row (batch invariance).
+template <int EPI, int NJ>
+__device__ __forceinline__ void dec_row_out(const f32x4 (&acc)[NJ], int m, int nb, int fchunk, int M, int N,
+                                            float rstd, float rmu, float2 rf, bf16* __restrict__ C, int ldc,
+                                            const float* __restrict__ bias, const bf16* __restrict__ R, int ldr,
+                                            const KvOut& kvo, const LnDec& ln, int kv_pos) {
+  static_assert(!(EPI & kEpiRowStats) || NJ == 2, "RowStats: a 32-column slab per wave");
+  if (m >= M) return;
+  bf16x4 ov[NJ];
+  dec_row_vals<EPI, NJ>(acc, m, nb, fchunk, N, rstd, rmu, rf, C, ldc, bias, R, ldr, kvo, ln, kv_pos, ov);
+  if constexpr (EPI & kEpiRowStats) dec_row_stats(ov, m, nb, fchunk, M, N, ln);
 }
 
 template <int EPI, int NST, int SPLIT>
@@ -1667,55 +1688,54 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
 // computes each output exactly as gemm_dec_kernel does -- ONE v_mfma_f32_16x16x32_bf16 chain over
 // K in ascending 32-wide k-steps with the same fragment layout (lane (fr, fc): row fr, k fc*8..+8),
 // the RowRms sum of squares in the same lane order, and the shared epilogue (dec_row_out) -- but
-// with no LDS ring: one wave owns 16 x (16 NJ) outputs and streams its operands straight into MFMA
+// with no LDS ring: one wave owns 16 x 16 outputs and streams its operands straight into MFMA
 // fragment registers, RD k-steps per round, the next round's loads in flight under this round's
-// MFMAs (two register sets). N / (16 NJ) workgroups of one compute wave (NJ = 2 for RowStats
-// slabs), plus (PF) the GEMV's L2 prefetch wave for the next decoder GEMM's weight rows.
+// MFMAs (two register sets). N / 16 compute waves, one per workgroup (two per workgroup for
+// RowStats: a 32-column slab whose statistics wave 0 forms from both halves' stored outputs, in
+// the 64x64 kernel's order), plus (PF) the GEMV's L2 prefetch wave for the next GEMM's weight rows.
 // ============================================================================
-template <int EPI, int NJ, int RD, bool PF>
-__global__ __launch_bounds__(64 * (1 + PF)) void gemm_few_exact_kernel(
+template <int EPI, int RD, bool PF>
+__global__ __launch_bounds__(64 * (((EPI & kEpiRowStats) ? 2 : 1) + PF)) void gemm_few_exact_kernel(
     const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C, int ldc,
     const float* __restrict__ bias, const bf16* __restrict__ R, int ldr, int M, int N, int K, float rms_eps, KvOut kvo,
     LnDec ln, L2Pf pf) {
+  // compute waves, one 16-column fragment each: 2 for RowStats (a 32-column slab, whose statistics
+  // wave 0 forms from both halves in dec_row_out's order)
+  constexpr int NCW = (EPI & kEpiRowStats) ? 2 : 1;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if constexpr (PF) {
     __shared__ __attribute__((aligned(16))) char pf_scratch[256];
-    if (threadIdx.x >= 64) {
-      l2_prefetch_rows<0>(pf, threadIdx.x & 63, pf_scratch, blockIdx.x, gridDim.x);
+    if (w == NCW) {  // (takes the compute waves' barriers)
+      l2_prefetch_rows<NCW - 1>(pf, threadIdx.x & 63, pf_scratch, blockIdx.x, gridDim.x);
       return;
     }
   }
-  const int lane = threadIdx.x, fr = lane & 15, fc = lane >> 4;
-  const int nb = blockIdx.x * 16 * NJ;  // this wave's first column
+  const int lane = threadIdx.x & 63, fr = lane & 15, fc = lane >> 4;
+  const int nb = (blockIdx.x * NCW + w) * 16;  // this wave's first column
   const bf16* ar = A + (size_t)min(fr, M - 1) * lda + fc * 8;
-  const bf16* br[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) br[j] = Bt + (size_t)min(nb + j * 16 + fr, N - 1) * ldb + fc * 8;
+  const bf16* br = Bt + (size_t)min(nb + fr, N - 1) * ldb + fc * 8;
   constexpr bool kPart = EPI & (kEpiRowLn | kEpiResLn);
   float2 pv[kPartPerLane];
   const int pslots = (EPI & kEpiRowLn) ? K / 32 : N / 32;
   if constexpr (kPart) part_prefetch(pv, (EPI & kEpiRowLn) ? ln.in_part : ln.res_part, pslots, M, fr, fc);
-  f32x4 acc[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
   float ssq = 0.f;
   const int nks = K / 32;
-  bf16x8 a0[RD], b0[RD][NJ], a1[RD], b1[RD][NJ];
-  auto load = [&](bf16x8 (&a)[RD], bf16x8 (&b)[RD][NJ], int r0) {
+  bf16x8 a0[RD], b0[RD], a1[RD], b1[RD];
+  auto load = [&](bf16x8 (&a)[RD], bf16x8 (&b)[RD], int r0) {
 #pragma unroll
     for (int u = 0; u < RD; ++u) {
       const int ks = min(r0 + u, nks - 1);  // clamped: a tail round's extra k-steps are never used
       a[u] = *reinterpret_cast<const bf16x8*>(ar + ks * 32);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) b[u][j] = *reinterpret_cast<const bf16x8*>(br[j] + ks * 32);
+      b[u] = *reinterpret_cast<const bf16x8*>(br + ks * 32);
     }
   };
-  auto mma = [&](const bf16x8 (&a)[RD], const bf16x8 (&b)[RD][NJ], int r0) {
+  auto mma = [&](const bf16x8 (&a)[RD], const bf16x8 (&b)[RD], int r0) {
 #pragma unroll
     for (int u = 0; u < RD; ++u) {
       if (r0 + u < nks) {  // uniform
         if constexpr (EPI & kEpiRowRms) ssq = sumsq_bf16x8(a[u], ssq);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[u][j], a[u], acc[j], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[u], a[u], acc[0], 0, 0, 0);
       }
     }
   };
@@ -1738,7 +1758,21 @@ __global__ __launch_bounds__(64 * (1 + PF)) void gemm_few_exact_kernel(
     rmu = st.y;
   }
   if constexpr (EPI & kEpiResLn) rf = part_ln(pv, pslots, fc, rms_eps);
-  dec_row_out<EPI, NJ>(acc, fr, nb, fc, M, N, rstd, rmu, rf, C, ldc, bias, R, ldr, kvo, ln, kv_pos);
+  if constexpr (NCW == 1) {
+    dec_row_out<EPI, 1>(acc, fr, nb, fc, M, N, rstd, rmu, rf, C, ldc, bias, R, ldr, kvo, ln, kv_pos);
+  } else {
+    __shared__ bf16x4 xch[64];  // wave 1's stored outputs, for wave 0's slab statistics
+    bf16x4 ov[1];
+    if (fr < M) {
+      dec_row_vals<EPI & ~kEpiRowStats, 1>(acc, fr, nb, fc, N, rstd, rmu, rf, C, ldc, bias, R, ldr, kvo, ln, kv_pos, ov);
+      if (w == 1) xch[lane] = ov[0];
+    }
+    __syncthreads();
+    if (w == 0 && fr < M) {
+      const bf16x4 both[2] = {ov[0], xch[lane]};
+      dec_row_stats(both, fr, nb, fc, M, N, ln);
+    }
+  }
 }
 
 bool few_exact_ok(const GemmArgs& g) {
@@ -1757,25 +1791,21 @@ void launch_few_exact(const GemmArgs& g, hipStream_t s) {
   const bool pf = pf_on && g.pf_w && g.pf_n > 0 && g.pf_k > 0 && !(g.epi & kEpiRowStats);
   const L2Pf pfa{g.pf_w, g.pf_ld, g.pf_k, g.pf_n, g.pf_rpb > 0 ? g.pf_rpb : 16};
   // K >= 2048 (T5 wo, BART fc2): 16 k-steps per round, half the dependent load rounds
-#define ATPU_FEW_GO1(E, NJ, RD, P)                                                                                 \
-  hipLaunchKernelGGL((gemm_few_exact_kernel<E, NJ, RD, P>), dim3(g.N / (16 * (NJ))), dim3(64 * (1 + (P))), 0, s,  \
+#define ATPU_FEW_GO1(E, RD, P)                                                                                    \
+  hipLaunchKernelGGL((gemm_few_exact_kernel<E, RD, P>), dim3(g.N / (16 * kNcw)), dim3(64 * (kNcw + (P))), 0, s,   \
                      g.A, g.lda, g.Bt, g.ldb, g.C, g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, g.rms_eps, kvo, ln, pfa)
-#define ATPU_FEW_GO(E, NJ)              \
-  if (pf && g.K >= 2048) {              \
-    ATPU_FEW_GO1(E, NJ, 16, true);      \
-  } else if (pf) {                      \
-    ATPU_FEW_GO1(E, NJ, 8, true);       \
-  } else {                              \
-    ATPU_FEW_GO1(E, NJ, 8, false);      \
+#define ATPU_FEW_CASE(E)                                    \
+  case E: {                                                 \
+    constexpr int kNcw = ((E) & kEpiRowStats) ? 2 : 1;      \
+    if (pf && g.K >= 2048) {                                \
+      ATPU_FEW_GO1(E, 16, true);                            \
+    } else if (pf) {                                        \
+      ATPU_FEW_GO1(E, 8, true);                             \
+    } else {                                                \
+      ATPU_FEW_GO1(E, 8, false);                            \
+    }                                                       \
+    break;                                                  \
   }
-#define ATPU_FEW_CASE(E)                                 \
-  case E:                                                \
-    if constexpr (((E) & kEpiRowStats) != 0) {           \
-      ATPU_FEW_GO(E, 2);                                 \
-    } else {                                             \
-      ATPU_FEW_GO(E, 1);                                 \
-    }                                                    \
-    break;
   switch (g.epi) {
     ATPU_FEW_CASE(kEpiRowLn | kEpiBias | kEpiKvScatter)
     ATPU_FEW_CASE(kEpiRowLn | kEpiBias)
@@ -1802,7 +1832,6 @@ void launch_few_exact(const GemmArgs& g, hipStream_t s) {
       throw std::invalid_argument("atpu: unsupported GEMM epilogue " + std::to_string(g.epi));
   }
 #undef ATPU_FEW_CASE
-#undef ATPU_FEW_GO
 #undef ATPU_FEW_GO1
 }
 
