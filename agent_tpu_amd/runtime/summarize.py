@@ -920,8 +920,10 @@ class SummarizeStream:
     def __init__(self, engine: "SummarizeEngine", max_searches: Optional[int] = None,
                  part_max: Optional[int] = None):
         self.eng = engine
-        self.max_searches = int(max_searches or os.getenv("ATPU_SUMM_STREAMS", "3"))
-        self.part_max = int(part_max or os.getenv("ATPU_INFLIGHT_PART_MAX", "128"))
+        # two searches of up to 256 documents measured best through the agent (T5-base 1-doc jobs:
+        # 513 docs/s vs 388 at three of 128; docs/PERF_NOTES.md "In-flight search shape")
+        self.max_searches = int(max_searches or os.getenv("ATPU_INFLIGHT_SEARCHES", "2"))
+        self.part_max = int(part_max or os.getenv("ATPU_INFLIGHT_PART_MAX", "256"))
         self.part_max = max(1, min(self.part_max, engine.max_batch_docs or self.part_max))
         self._queues: Dict[tuple, List[tuple]] = {}  # (gen key, bucket) -> [(tag, texts, ids rows, lens, t_submit)]
         self._active: List[dict] = []

@@ -721,9 +721,11 @@ def inflight_depth(caps: List[str], health: Optional[Dict[str, Any]]) -> int:
         if gpu_ops & {"map_classify", "map_classify_tpu"}:
             depth = max(depth, 2 * classify_batch_rows(hbm, "bert-base", 128))
         if "map_summarize" in gpu_ops:
-            # three concurrent searches of ATPU_INFLIGHT_PART_MAX documents each, plus the next round
-            part = int(os.getenv("ATPU_INFLIGHT_PART_MAX", "128"))
-            depth = max(depth, 2 * 3 * part)
+            # the concurrent searches of ATPU_INFLIGHT_PART_MAX documents each, plus the next search
+            # (runtime.summarize.SummarizeStream's defaults)
+            part = int(os.getenv("ATPU_INFLIGHT_PART_MAX", "256"))
+            searches = int(os.getenv("ATPU_INFLIGHT_SEARCHES", "2"))
+            depth = max(depth, (searches + 1) * part)
     except Exception:
         depth = 256
     # a held job must not sit out its lease TTL: cap by ~ a conservative device rate x TTL/2
