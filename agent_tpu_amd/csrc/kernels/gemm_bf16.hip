@@ -1775,6 +1775,82 @@ __global__ __launch_bounds__(64 * (((EPI & kEpiRowStats) ? 2 : 1) + PF)) void ge
   }
 }
 
+// The long-K few-row case (K = 2048 / 3072: T5's FF-out, M <= 8): the register kernel above needs K / 512
+// dependent load rounds per wave (8.1 us for T5 wo against the GEMV's 5). Here the workgroup's 4 waves
+// put the wave's whole B slab (16 weight rows x K) and the M activation rows into LDS with LDS-DMA, every
+// load in flight at once, and wave 0 runs the same MFMA chain (same fragments, same order, same epilogue)
+// from LDS; wave 3 then issues the next GEMM's L2 prefetch. Bit-identical to gemm_few_exact_kernel.
+template <int EPI, int NKS>
+__global__ __launch_bounds__(256) void gemm_few_dma_kernel(const bf16* __restrict__ A, int lda,
+                                                           const bf16* __restrict__ Bt, int ldb, bf16* __restrict__ C,
+                                                           int ldc, const float* __restrict__ bias,
+                                                           const bf16* __restrict__ R, int ldr, int M, int N, int K,
+                                                           KvOut kvo, LnDec ln, L2Pf pf, int pf_on) {
+  static_assert(!(EPI & (kEpiRowStats | kEpiRowLn | kEpiResLn | kEpiRowRms)), "plain / bias / residual epilogues");
+  constexpr int kApitch = NKS * 64 + 16;  // bytes per staged A row (padded: rows land 4 banks apart)
+  constexpr int kApieces = NKS / 16;      // 1-KiB DMA pieces per A row
+  __shared__ __attribute__((aligned(16))) char sB[NKS * 1024];  // k-step ks: lane (fr, fc)'s 16 B at ks*1024 + 16*lane
+  __shared__ __attribute__((aligned(16))) char sA[8 * kApitch];
+  __shared__ __attribute__((aligned(16))) char pf_scratch[256];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int fr = lane & 15, fc = lane >> 4;
+  const int nb = blockIdx.x * 16;
+  const bf16* br = Bt + (size_t)min(nb + fr, N - 1) * ldb + fc * 8;
+  for (int ks = w; ks < NKS; ks += 4) glds16(br + ks * 32, sB + ks * 1024);
+  for (int p = w; p < M * kApieces; p += 4) {
+    const int r = p / kApieces, i = p - r * kApieces;
+    glds16(A + (size_t)r * lda + i * 512 + lane * 8, sA + r * kApitch + i * 1024);
+  }
+  wait_vmcnt0();
+  __syncthreads();
+  if (w != 0) {
+    if (w == 3 && pf_on) l2_prefetch_rows<0>(pf, lane, pf_scratch, blockIdx.x, gridDim.x);
+    return;
+  }
+  const char* ap = sA + min(fr, M - 1) * kApitch + fc * 16;
+  const char* bp = sB + lane * 16;
+  f32x4 acc[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll 8
+  for (int ks = 0; ks < NKS; ++ks) {
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(ap + ks * 64);
+    const bf16x8 b = *reinterpret_cast<const bf16x8*>(bp + ks * 1024);
+    acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, acc[0], 0, 0, 0);
+  }
+  dec_row_out<EPI, 1>(acc, fr, nb, fc, M, N, 1.f, 0.f, float2{1.f, 0.f}, C, ldc, bias, R, ldr, kvo, ln, 0);
+}
+
+// the DMA form's cases (launch_few_exact); false: the register kernel
+bool launch_few_dma(const GemmArgs& g, hipStream_t s, bool pf, const L2Pf& pfa) {
+  static const bool on = [] {
+    const char* f = std::getenv("ATPU_FEW_DMA");
+    return !(f && f[0] == '0');
+  }();
+  if (!on || g.M > 8 || (g.K != 2048 && g.K != 3072) || g.N % 16) return false;
+  const KvOut kvo{g.kv_cache, g.kv_ld, g.kv_T, g.kv_col0, g.kv_step};
+  const LnDec ln{g.colsum, g.in_part, g.res_part, g.gamma, g.part_out};
+#define ATPU_FD(E, NKS)                                                                                          \
+  hipLaunchKernelGGL((gemm_few_dma_kernel<E, NKS>), dim3(g.N / 16), dim3(256), 0, s, g.A, g.lda, g.Bt, g.ldb, g.C, \
+                     g.ldc, g.bias, g.R, g.ldr, g.M, g.N, g.K, kvo, ln, pfa, pf ? 1 : 0)
+#define ATPU_FD_CASE(E)   \
+  case E:                 \
+    if (g.K == 2048) {    \
+      ATPU_FD(E, 64);     \
+    } else {              \
+      ATPU_FD(E, 96);     \
+    }                     \
+    return true;
+  switch (g.epi) {
+    ATPU_FD_CASE(0)
+    ATPU_FD_CASE(kEpiBias)
+    ATPU_FD_CASE(kEpiResidual)
+    ATPU_FD_CASE(kEpiBias | kEpiResidual)
+    default:
+      return false;
+  }
+#undef ATPU_FD_CASE
+#undef ATPU_FD
+}
+
 bool few_exact_ok(const GemmArgs& g) {
   return batch_invariant(-1) && g.M <= 16 && g.N % 32 == 0 && g.K % 32 == 0 && gemm_force_tile(-1) == 0 &&
          !(g.epi & (kEpiInNorm | kEpiResNorm | kEpiStatsOut));
@@ -1790,6 +1866,7 @@ void launch_few_exact(const GemmArgs& g, hipStream_t s) {
   }();
   const bool pf = pf_on && g.pf_w && g.pf_n > 0 && g.pf_k > 0 && !(g.epi & kEpiRowStats);
   const L2Pf pfa{g.pf_w, g.pf_ld, g.pf_k, g.pf_n, g.pf_rpb > 0 ? g.pf_rpb : 16};
+  if (launch_few_dma(g, s, pf, pfa)) return;
   // K >= 2048 (T5 wo, BART fc2): 16 k-steps per round, half the dependent load rounds
 #define ATPU_FEW_GO1(E, RD, P)                                                                                    \
   hipLaunchKernelGGL((gemm_few_exact_kernel<E, RD, P>), dim3(g.N / (16 * kNcw)), dim3(64 * (kNcw + (P))), 0, s,   \

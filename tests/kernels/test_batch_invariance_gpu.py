@@ -217,11 +217,13 @@ def test_classify_single_rows_equal_stacked(gpu, invariant):
         assert torch.equal(one.idx[0], stacked.idx[i]) and torch.equal(one.score[0], stacked.score[i]), i
 
 
-@pytest.mark.parametrize("epi", ["rms_kv", "rms_relu", "bias_res", "bias_gelu", "row_ln", "res_ln_stats", "out_f32"])
-@pytest.mark.parametrize("M,K", [(1, 768), (4, 3072), (16, 1024)])
+@pytest.mark.parametrize("epi", ["rms_kv", "rms_relu", "bias_res", "res", "plain", "bias_gelu", "row_ln", "res_ln_stats",
+                                 "out_f32"])
+@pytest.mark.parametrize("M,K", [(1, 768), (4, 3072), (8, 2048), (16, 1024)])
 def test_few_row_exact_kernel_equals_dec(gpu, nat, invariant, epi, M, K):
-    """Under batch invariance <= 16 rows run gemm_few_exact_kernel (no LDS ring); it must give
-    the dec kernel's bits (ATPU_GEMM_TILE=64 forces the dec kernel on the same rows)."""
+    """Under batch invariance <= 16 rows run gemm_few_exact_kernel (no LDS ring; K = 2048 / 3072 at
+    <= 8 rows: gemm_few_dma_kernel); it must give the dec kernel's bits (ATPU_GEMM_TILE=64 forces the
+    dec kernel on the same rows)."""
     from agent_tpu_amd.ops.linear import row_parts_ref
 
     N = 1024 if epi in ("row_ln", "res_ln_stats") else 768
@@ -244,6 +246,10 @@ def test_few_row_exact_kernel_equals_dec(gpu, nat, invariant, epi, M, K):
             return [ops.linear(x, w, act="relu", rms_eps=1e-6)]
         if epi == "bias_res":
             return [ops.linear(x, w, b, residual=res)]
+        if epi == "res":  # T5's FF-out (K = 3072: the LDS-DMA form at <= 8 rows)
+            return [ops.linear(x, w, residual=res)]
+        if epi == "plain":
+            return [ops.linear(x, w)]
         if epi == "bias_gelu":
             return [ops.linear(x, w, b, act="gelu")]
         if epi == "out_f32":
