@@ -1878,6 +1878,8 @@ void launch_few_exact(const GemmArgs& g, hipStream_t s) {
       ATPU_FEW_GO1(E, 16, true);                            \
     } else if (pf) {                                        \
       ATPU_FEW_GO1(E, 8, true);                             \
+    } else if (g.K >= 2048) {                               \
+      ATPU_FEW_GO1(E, 16, false);                           \
     } else {                                                \
       ATPU_FEW_GO1(E, 8, false);                            \
     }                                                       \
