@@ -1852,8 +1852,16 @@ bool launch_few_dma(const GemmArgs& g, hipStream_t s, bool pf, const L2Pf& pfa) 
 }
 
 bool few_exact_ok(const GemmArgs& g) {
-  return batch_invariant(-1) && g.M <= 16 && g.N % 32 == 0 && g.K % 32 == 0 && gemm_force_tile(-1) == 0 &&
-         !(g.epi & (kEpiInNorm | kEpiResNorm | kEpiStatsOut));
+  // batch-invariant mode: every <= 16-row GEMM; otherwise the 5-16-row ones (2-4 documents x 4 beams), where
+  // it replaces the 64x64 kernel's few-workgroup grid with the same bits (ATPU_FEW_ROWS=0: off). <= 4 rows
+  // keep the GEMV there.
+  static const bool rows_on = [] {
+    const char* f = std::getenv("ATPU_FEW_ROWS");
+    return !(f && f[0] == '0');
+  }();
+  const bool inv = batch_invariant(-1) != 0;
+  return (inv || (rows_on && g.M > 4)) && g.M <= 16 && g.N % 32 == 0 && g.K % 32 == 0 &&
+         gemm_force_tile(-1) == 0 && !(g.epi & (kEpiInNorm | kEpiResNorm | kEpiStatsOut));
 }
 
 void launch_few_exact(const GemmArgs& g, hipStream_t s) {
