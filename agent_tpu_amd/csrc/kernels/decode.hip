@@ -562,7 +562,7 @@ __global__ __launch_bounds__(NW * 64) void decode_cross_chunked_kernel(
   const int nch = min(NS, (len + kSplitKeys - 1) / kSplitKeys);  // chunks holding keys
   auto nkeys = [&](int c) { return min(kSplitKeys, len - c * kSplitKeys); };
   const XsQ qr = xs_q(a);
-  XsRegs<B> r0, r1;
+  XsRegs<B> r0;
   {  // (unconditional on a clamped chunk: see xs_q)
     const int c0 = min(w, max(nch - 1, 0));
     xs_load<B>(a, c0 * kSplitKeys, max(1, nkeys(c0)), r0);
@@ -571,16 +571,12 @@ __global__ __launch_bounds__(NW * 64) void decode_cross_chunked_kernel(
     auto rec = [&](int g) { return &recs[g][c][0]; };
     xs_empty(G, rec);
   }
-  // two register sets: chunk c + NW's loads are in flight under chunk c's arithmetic
-  for (int c = w; c < nch; c += 2 * NW) {
-    if (c + NW < nch) xs_load<B>(a, (c + NW) * kSplitKeys, nkeys(c + NW), r1);
+  // one register set (168 VGPRs: three waves per SIMD) -- the other resident waves hide a chunk's
+  // load latency; two sets (236 VGPRs, two waves per SIMD) ran 256-doc T5 at 542 vs 593 docs/s
+  for (int c = w; c < nch; c += NW) {
+    if (c != w) xs_load<B>(a, c * kSplitKeys, nkeys(c), r0);
     auto rec0 = [&](int g) { return &recs[g][c][0]; };
     xs_compute<GM, B>(a, nkeys(c), r0, qr, pl[w], rec0);
-    if (c + NW < nch) {
-      if (c + 2 * NW < nch) xs_load<B>(a, (c + 2 * NW) * kSplitKeys, nkeys(c + 2 * NW), r0);
-      auto rec1 = [&](int g) { return &recs[g][c + NW][0]; };
-      xs_compute<GM, B>(a, nkeys(c + NW), r1, qr, pl[w], rec1);
-    }
   }
   __syncthreads();
   for (int g = w; g < G; g += NW)
@@ -1241,14 +1237,9 @@ void decode_attention(const bf16* q, int ldq, const bf16* k, const bf16* v, int 
     ATPU_HIP_CHECK(hipGetLastError());
     return;
   }
-  // batch invariance (or ATPU_DEC_XCHUNK=1): a grid too large to split runs the split form's chunk
-  // and combine arithmetic in one workgroup per (item, head), so an item rounds the same in a
-  // launch of any size
-  static const bool xchunk_env = [] {
-    const char* f = std::getenv("ATPU_DEC_XCHUNK");
-    return f && f[0] == '1';
-  }();
-  if (lens && !hist && group <= 8 && seq_stride >= 2 * kSplitKeys && (batch_invariant(-1) || xchunk_env)) {
+  // batch invariance: a grid too large to split runs the split form's chunk and combine arithmetic
+  // in one workgroup per (item, head), so an item rounds the same in a launch of any size
+  if (lens && !hist && group <= 8 && seq_stride >= 2 * kSplitKeys && batch_invariant(-1)) {
     ATPU_CHECK(ldq % 8 == 0 && (reinterpret_cast<uintptr_t>(q) & 15) == 0, "decode_attention: q needs 16-B rows");
     const int ns = (seq_stride + kSplitKeys - 1) / kSplitKeys;
 #define ATPU_DC1(GM, NSX, B)                                                                                    \
