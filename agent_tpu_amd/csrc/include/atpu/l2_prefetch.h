@@ -26,14 +26,22 @@ template <int BARRIERS>
 __device__ __forceinline__ void l2_prefetch_rows(const L2Pf& pf, int lane, char* scratch, int bid, int nblk) {
   const int lpr = (pf.k * 2 + 127) / 128;  // 128-B lines per row
   const int blocks = (pf.n + pf.rpb - 1) / pf.rpb;
-  for (int bb = bid; bb < blocks; bb += nblk) {
+  // fewer next blocks than workgroups here (e.g. 32 RowStats slabs of an 8 MB weight behind 256
+  // workgroups): the `share` workgroups bid = bb (mod blocks) -- the same XCD as block bb when
+  // blocks % 8 == 0 -- split block bb's lines, instead of 32 waves streaming 256 KB each while
+  // the kernel waits for them to end
+  const int share = (blocks < nblk && nblk % blocks == 0) ? nblk / blocks : 1;
+  for (int bb = (share > 1 ? bid % blocks : bid); bb < blocks; bb += (share > 1 ? blocks : nblk)) {
     const int r0 = bb * pf.rpb, nl = min(pf.rpb, pf.n - r0) * lpr;
-    for (int i0 = 0; i0 < nl; i0 += 64) {  // wave-uniform trip count: every lane issues the DMA
-      const int i = min(i0 + lane, nl - 1);
+    const int part = share > 1 ? bid / blocks : 0;
+    const int l0 = (int)((long)nl * part / share), l1 = (int)((long)nl * (part + 1) / share);
+    for (int i0 = l0; i0 < l1; i0 += 64) {  // wave-uniform trip count: every lane issues the DMA
+      const int i = min(i0 + lane, l1 - 1);
       const int r = r0 + i / lpr, l = i - (i / lpr) * lpr;
       const char* p = reinterpret_cast<const char*>(pf.w + (size_t)r * pf.ld) + l * 128;
       __builtin_amdgcn_global_load_lds((const ATPU_GLOBAL_AS void*)p, (ATPU_LDS_AS void*)scratch, 4, 0, 0);
     }
+    if (share > 1) break;  // one block per workgroup
   }
 #pragma unroll
   for (int b = 0; b < BARRIERS; ++b) asm volatile("s_barrier" ::: "memory");
