@@ -38,7 +38,8 @@ import sys
 import threading
 import time
 import traceback
-from typing import Any, Dict, List, Optional, Tuple
+from collections import deque
+from typing import Any, Deque, Dict, List, Optional, Tuple
 
 try:
     import requests
@@ -104,6 +105,10 @@ SHUTDOWN_AHEAD = os.getenv("SHUTDOWN_AHEAD", "ttl").strip().lower()
 INFLIGHT_DEPTH_RAW = os.getenv("INFLIGHT_DEPTH", "auto").strip().lower()
 # lease requests sent back to back on one keep-alive connection (at most) per round trip
 LEASE_PIPELINE_MAX = int(os.getenv("LEASE_PIPELINE_MAX", "64"))
+# auto in-flight depth: hold at most what the measured completion rate finishes within this fraction of
+# the lease TTL (never less than a third of the sized depth, nor more than all of it; all of it until
+# completions are measured)
+INFLIGHT_TTL_FRACTION = float(os.getenv("INFLIGHT_TTL_FRACTION", "0.6"))
 # a single job's result is held back for a grouped post only behind jobs shorter than this
 DEFER_MAX_JOB_SEC = float(os.getenv("DEFER_MAX_JOB_SEC", "0.001"))
 FAIL_ON_NOT_OK = os.getenv("FAIL_ON_NOT_OK", "0").strip().lower() in ("1", "true", "yes")
@@ -623,9 +628,15 @@ class LeaseFeeder:
     Each lease is requested with the agent's ``max_tasks`` / ``timeout_ms``: MAX_TASKS=1 (the
     reference default) means one job per lease, many leases held."""
 
-    def __init__(self, agent: "Agent", depth: int) -> None:
+    RATE_WINDOW_SEC = 3.0
+
+    def __init__(self, agent: "Agent", depth: int, adaptive: bool = False) -> None:
         self.agent = agent
         self.depth = max(1, int(depth))
+        # adaptive (auto depth): the sized depth until completions are measured, then the completion rate
+        self.adaptive = bool(adaptive)
+        self.floor = max(1, self.depth // 3)
+        self._done_log: Deque[Tuple[float, int]] = deque()
         self.cv = threading.Condition()
         self.q: List[Tuple[str, List[Any]]] = []
         self.held = 0
@@ -642,11 +653,11 @@ class LeaseFeeder:
         idle = False
         while True:
             with self.cv:
-                while not self._stop and self.held >= self.depth:
-                    self.cv.wait()
+                while not self._stop and self.held >= self.limit():
+                    self.cv.wait(0.2 if self.adaptive else None)
                 if self._stop:
                     return
-                room = self.depth - self.held
+                room = self.limit() - self.held
             per = max(1, MAX_TASKS)
             n = 1 if idle else max(1, min(LEASE_PIPELINE_MAX, -(-room // per)))
             got: List[Tuple[str, List[Any]]] = []
@@ -681,10 +692,29 @@ class LeaseFeeder:
             out, self.q = self.q, []
             return out
 
+    def limit(self) -> int:
+        """Jobs to hold now (call with ``cv`` held): the depth, or -- adaptive -- what the jobs
+        completed in the last RATE_WINDOW_SEC finish within INFLIGHT_TTL_FRACTION of the lease TTL,
+        clamped to [depth / 3, depth] (the depth until a rate is measured), so held jobs do not
+        outlive their leases on a slower device or model."""
+        if not self.adaptive:
+            return self.depth
+        now = time.monotonic()
+        log = self._done_log
+        while log and now - log[0][0] > self.RATE_WINDOW_SEC:
+            log.popleft()
+        if len(log) < 2 or now - log[0][0] < 0.25:
+            return self.depth
+        rate = sum(n for _, n in log) / (now - log[0][0])
+        cap = int(rate * LEASE_TIMEOUT_MS / 1000.0 * INFLIGHT_TTL_FRACTION)
+        return max(self.floor, min(self.depth, cap))
+
     def done(self, n: int) -> None:
         if n:
             with self.cv:
                 self.held -= n
+                if self.adaptive:
+                    self._done_log.append((time.monotonic(), n))
                 self.cv.notify_all()
 
     def stop(self) -> List[Tuple[str, List[Any]]]:
@@ -1273,7 +1303,7 @@ class Agent:
         from ops import get_batch_op, get_stream_op
 
         print(f"{LOG} in-flight mode: up to {depth} leased jobs held (MAX_TASKS={MAX_TASKS})", flush=True)
-        feeder = self._feeder = LeaseFeeder(self, depth)
+        feeder = self._feeder = LeaseFeeder(self, depth, adaptive=INFLIGHT_DEPTH_RAW in ("", "auto"))
         execs: Dict[str, Any] = {}
         ex_jobs: Dict[Tuple[str, str], Tuple[str, str, Dict[str, Any], Any]] = {}  # executor tag -> job
         held_back: List[Tuple[str, List[Any]]] = []

@@ -169,3 +169,33 @@ def test_pipelined_poster_detects_an_http10_controller():
     finally:
         srv.shutdown()
         srv.server_close()
+
+
+def test_feeder_adaptive_limit_follows_rate_and_ttl(monkeypatch):
+    """Auto in-flight depth: the sized depth until completions are measured, then what the completion
+    rate finishes within INFLIGHT_TTL_FRACTION of the lease TTL, clamped to [depth/3, depth]."""
+    import collections
+
+    import app
+
+    f = app.LeaseFeeder.__new__(app.LeaseFeeder)  # the limit rule alone (no thread)
+    f.depth, f.adaptive, f.floor = 768, True, 256
+    f._done_log = collections.deque()
+    assert f.limit() == 768
+    monkeypatch.setattr(app, "LEASE_TIMEOUT_MS", 3000)
+    monkeypatch.setattr(app, "INFLIGHT_TTL_FRACTION", 0.6)
+    now = [100.0]
+    monkeypatch.setattr(app.time, "monotonic", lambda: now[0])
+    # 396 jobs over the last second -> 396 x 3 s x 0.6 = 712 held at most
+    for i in range(11):
+        f._done_log.append((99.0 + i * 0.1, 36))
+    assert f.limit() == 712
+    # a slow device: 50 jobs/s -> 90, clamped up to the floor
+    f._done_log = collections.deque((99.0 + i * 0.1, 5) for i in range(11))
+    assert f.limit() == 256
+    # a fast one: clamped down to the depth
+    f._done_log = collections.deque((99.0 + i * 0.1, 1000) for i in range(11))
+    assert f.limit() == 768
+    # fixed depth (an explicit INFLIGHT_DEPTH) ignores the rate
+    f.adaptive = False
+    assert f.limit() == 768
